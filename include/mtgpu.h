@@ -1,0 +1,136 @@
+/*
+ * mtgpu.h -- C-ABI of the MI355X batched merge-tree engine (libmtgpu.so).
+ *
+ * Drop-in boundary for the reference's op-apply surface:
+ *   Client.applyMsg(msg: ISequencedDocumentMessage)       packages/dds/merge-tree/src/client.ts:797-819
+ *   new Client(...) + startOrUpdateCollaboration(longId)  client.ts:74-83, 1051-1071
+ *   Client.getLength()                                    client.ts:1049
+ *   TestClient.getText() / MergeTreeTextHelper.getText    src/test/testClient.ts:102-104, textSegment.ts:154-172
+ * One engine owns many independent documents (one reference `Client` observer per document);
+ * a batch of sequenced ops from many documents is applied in one submit.  The host shim
+ * (js/batchClient.js over the N-API addon, or fluidframework_amd/client.py over ctypes) turns
+ * ISequencedDocumentMessage JSON into mt_op_rec rows: long client ids are interned per document
+ * in first-appearance order with the observer as short id 0 (client.ts:636-660, 1057-1062);
+ * property keys/values are interned per document (properties.ts; ids are opaque, equality only).
+ *
+ * Plain pointers and sizes only; no torch or HIP types.  All functions return mt_status.
+ */
+#ifndef MTGPU_H
+#define MTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- op record: one merge-tree delta op of one sequenced message (32 bytes) -------------- */
+enum mt_op_type {
+    MT_OP_INSERT = 0,   /* ops.ts:29-34 MergeTreeDeltaType.INSERT   (client.ts:393-441)      */
+    MT_OP_REMOVE = 1,   /* MergeTreeDeltaType.REMOVE                (client.ts:320-351)      */
+    MT_OP_ANNOTATE = 2, /* MergeTreeDeltaType.ANNOTATE              (client.ts:358-386)      */
+    MT_OP_NOOP = 3      /* non-op message: only updateSeqNumbers(msn, seq) (client.ts:818)  */
+};
+enum mt_op_flags {
+    MT_F_REWRITE = 1u << 0,    /* annotate with combiningOp {name:"rewrite"} (properties.ts:118-124) */
+    MT_F_PROPS = 1u << 1,      /* insert spec carries a props object (TextSegment.make, textSegment.ts:24-30) */
+    MT_F_GROUP_MORE = 1u << 2  /* GROUP member: next record is the next member of the same message
+                                  (client.ts:782-790); the window update waits for the last member */
+};
+#define MT_F_NPAIRS_SHIFT 3    /* bits 3..7: number of (key,value) property pairs in the payload */
+
+typedef struct mt_op_rec {
+    int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */
+    int32_t ref_seq;      /* referenceSequenceNumber                                            */
+    int32_t msn;          /* minimumSequenceNumber                                              */
+    uint16_t client;      /* per-document short client id (observer = 0, never in ops)          */
+    uint8_t type;         /* mt_op_type                                                         */
+    uint8_t flags;        /* mt_op_flags | npairs << MT_F_NPAIRS_SHIFT                          */
+    int32_t pos1;         /* insert position / range start                                      */
+    int32_t pos2;         /* range end (remove, annotate)                                       */
+    uint32_t payload_off; /* byte offset into the batch payload                                 */
+    uint32_t payload_len; /* text bytes + 2*npairs: [text][key u8, value u8]*; value 0 = null   */
+} mt_op_rec;
+
+/* ---- limits of the device representation (checked; violations become per-doc errors) ------ */
+#define MT_MAX_CLIENTS 64      /* short client ids 0..63 (overlap set is a u64 bitmask)          */
+#define MT_MAX_KEYS 8          /* property keys per document (u8 value id per key)              */
+#define MT_MAX_VALUES 255      /* property value ids 1..255 per document (0 = absent/null)      */
+
+typedef enum mt_status {
+    MT_OK = 0,
+    MT_ERR_ARG = 1,
+    MT_ERR_HIP = 2,
+    MT_ERR_NOMEM = 3,
+    MT_ERR_STATE = 4,
+    MT_ERR_DOC = 5          /* at least one document has a sticky error (see mt_doc_error) */
+} mt_status;
+
+/* per-document sticky error codes (mirror the reference's assert/throw sites) */
+enum mt_doc_err {
+    MT_DERR_NONE = 0,
+    MT_DERR_SEQ_ORDER = 1,      /* "Incoming remote op sequence# <= local collabWindow's currentSequence#" client.ts:461-462 */
+    MT_DERR_MSN_ORDER = 2,      /* "Incoming remote op minSequence# < local collabWindow's minSequence#"  client.ts:463-464 */
+    MT_DERR_INSERT_FAILED = 3,  /* "MergeTree insert failed" mergeTree.ts:2210-2216                      */
+    MT_DERR_CAPACITY = 4,       /* segment/block/heap capacity of the device representation exceeded    */
+    MT_DERR_TEXT_ARENA = 5,     /* per-document text arena exhausted                                    */
+    MT_DERR_LIMITS = 6,         /* client id / property key / value id outside MT_MAX_* */
+    MT_DERR_BAD_OP = 7          /* malformed record (type, payload bounds, negative positions) */
+};
+
+typedef struct mt_cfg {
+    int32_t device;             /* HIP device ordinal                                             */
+    uint32_t max_docs;          /* documents this engine can hold                                 */
+    uint32_t seg_capacity;      /* max linked segments per document (device slot pool)            */
+    uint32_t text_capacity;     /* text arena bytes per document                                  */
+    uint32_t heap_capacity;     /* zamboni LRU heap entries per document                          */
+    uint32_t ops_per_launch;    /* b: ops per document per kernel launch (0 = whole batch)        */
+} mt_cfg;
+
+typedef struct mt_engine mt_engine;
+typedef struct mt_batch mt_batch;
+
+mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out);
+mt_status mt_engine_destroy(mt_engine* eng);
+
+/* Start `n_docs` empty documents: Client + startOrUpdateCollaboration(observer, 0, 0)
+ * (client.ts:1051-1071, mergeTree.ts:1254-1271). */
+mt_status mt_docs_init(mt_engine* eng, uint32_t n_docs);
+
+/* Host -> device staging of a CSR op batch.  Ops are grouped by document (doc_row_ptr has
+ * n_docs+1 entries) and seq-ascending within a document.  Buffers are caller-owned and copied
+ * before return. */
+mt_status mt_batch_upload(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops,
+                          const uint8_t* payload, uint64_t payload_bytes,
+                          const uint32_t* doc_row_ptr, mt_batch** out);
+/* Apply a staged batch (asynchronous on the engine's stream; = applyMsg for every op). */
+mt_status mt_batch_apply(mt_engine* eng, const mt_batch* batch);
+mt_status mt_batch_free(mt_engine* eng, mt_batch* batch);
+/* upload + apply + free (the synchronous drop-in for a loop of applyMsg calls) */
+mt_status mt_submit(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops,
+                    const uint8_t* payload, uint64_t payload_bytes, const uint32_t* doc_row_ptr);
+mt_status mt_sync(mt_engine* eng);
+
+/* Readout (synchronises).  Text = MergeTreeTextHelper.getText for the observer. */
+mt_status mt_get_length(mt_engine* eng, uint32_t doc, uint32_t* len);
+mt_status mt_get_text(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uint64_t* len);
+/* Canonical state (JSON, see DESIGN.md "Canonical state"): L1 text, L2 linked leaves,
+ * L3 block shape, currentSeq/minSeq. */
+mt_status mt_get_state(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uint64_t* len);
+/* Per-document 64-bit checksum of the canonical state (DESIGN.md "Checksum"). */
+mt_status mt_checksums(mt_engine* eng, uint64_t* out, uint32_t n_docs);
+mt_status mt_doc_error(mt_engine* eng, uint32_t doc, int32_t* code, int32_t* seq);
+
+/* Measurement hooks for bench.py: device time of the last mt_batch_apply (ms, HIP events on
+ * the engine stream), kernel launches it issued, and the algorithmic bytes it moved. */
+mt_status mt_last_apply_stats(mt_engine* eng, float* ms, uint32_t* launches, uint64_t* alg_bytes);
+/* Segment count of every document (after sync). */
+mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
+
+const char* mt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTGPU_H */

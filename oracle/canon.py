@@ -1,0 +1,59 @@
+"""Canonical-state checksum computed from the canonical JSON (third, independent statement of
+the checksum definition in DESIGN.md; checks the C++ oracle and device checksums).
+TEST INFRASTRUCTURE ONLY."""
+
+M64 = (1 << 64) - 1
+
+
+def mix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def fnv1a(b):
+    h = 0xCBF29CE484222325
+    for c in b:
+        h ^= c
+        h = (h * 0x100000001B3) & M64
+    return h
+
+
+def seg_hash(idx, text_hash, seq, client, rseq, rclient, overlap, props_lo, props_defined):
+    b = (seq & 0xFFFFFFFF) | ((client & 0xFFFFFFFF) << 32)
+    c = (rseq & 0xFFFFFFFF) | ((rclient & 0xFFFFFFFF) << 32)
+    h = mix64(text_hash ^ ((idx * 0xD6E8FEB86659FD93) & M64))
+    h = mix64(h ^ b)
+    h = mix64(h ^ c)
+    h = mix64(h ^ overlap)
+    h = mix64(h ^ props_lo ^ ((1 if props_defined else 0) << 63))
+    return h
+
+
+def checksum(state):
+    """state: canonical JSON dict {"seq","msn","segs":[[text,seq,client,rseq,rclient,[ov],props]],"tree"}"""
+    seg_sum = 0
+    for i, (text, seq, client, rseq, rclient, ov, props) in enumerate(state['segs']):
+        overlap = 0
+        for o in ov:
+            overlap |= 1 << o
+        props_lo = 0
+        if props is not None:
+            for k, v in props.items():
+                kid = int(k[1:])
+                if kid < 8:
+                    props_lo |= (int(v) & 0xFF) << (8 * kid)
+        seg_sum = (seg_sum + seg_hash(i, fnv1a(text.encode()), seq, client, rseq, rclient, overlap, props_lo,
+                                      props is not None)) & M64
+    tree_sum = 0
+    for level, counts in enumerate(state['tree']):
+        for b, cnt in enumerate(counts):
+            tree_sum = (tree_sum + mix64(cnt ^ (b << 8) ^ (level << 56))) & M64
+    s = mix64(seg_sum) ^ mix64(tree_sum ^ 0x5851F42D4C957F2D)
+    s ^= mix64((state['seq'] & 0xFFFFFFFF) | ((state['msn'] & 0xFFFFFFFF) << 32))
+    return mix64(s ^ len(state['segs']))
+
+
+def text_of(state):
+    return ''.join(s[0] for s in state['segs'] if s[3] == -1)

@@ -1,0 +1,33 @@
+/* mtcpu.h -- C ABI of the CPU oracle (oracle/mtcpu.cpp).  TEST INFRASTRUCTURE ONLY:
+ * loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; never by the
+ * product library. */
+#ifndef MTCPU_H
+#define MTCPU_H
+#include <stdint.h>
+#include "../include/mtgpu.h"
+#include "../fluidframework_amd/csrc/mt_synth.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mto_engine mto_engine;
+
+mto_engine* mto_create(uint32_t n_docs);
+void mto_destroy(mto_engine* e);
+int mto_apply(mto_engine* e, const mt_op_rec* ops, const uint8_t* payload, const uint32_t* row_ptr,
+              uint32_t n_docs, int n_threads);
+void mto_checksums(mto_engine* e, uint64_t* out, uint32_t n_docs);
+int mto_doc_error(mto_engine* e, uint32_t doc, int32_t* seq);
+uint64_t mto_doc_state(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
+uint64_t mto_doc_text(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
+uint32_t mto_doc_nsegs(mto_engine* e, uint32_t doc);
+int mto_generate(const mt_synth_cfg* cfg, uint32_t d0, uint32_t n_docs, mt_op_rec* ops, uint8_t* payload,
+                 uint32_t* row_ptr, uint64_t* pay_ptr, int n_threads);
+uint64_t mto_seg_hash(uint64_t idx, uint64_t text_hash, int32_t seq, int32_t client, int32_t rseq,
+                      int32_t rclient, uint64_t overlap, uint64_t props_lo, uint32_t props_defined);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,120 @@
+"""ctypes wrapper of the CPU oracle (oracle/mtcpu.cpp -> oracle/libmtoracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product path (fluidframework_amd) never imports this module.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+from fluidframework_amd.oplog import OP_DTYPE, OpBatch, synth_cfg_array
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libmtoracle.so')
+SRC = os.path.join(HERE, 'mtcpu.cpp')
+
+_lib = None
+
+
+def build(force=False):
+    """Compile the oracle (g++, no GPU needed)."""
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(
+            os.path.getmtime(SRC), os.path.getmtime(os.path.join(HERE, 'mtcpu.h')),
+            os.path.getmtime(os.path.join(HERE, '..', 'fluidframework_amd', 'csrc', 'mt_synth.h'))):
+        subprocess.check_call(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-Wall', '-o', LIB_PATH, SRC,
+                               '-lpthread'])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+        L.mto_create.restype = vp
+        L.mto_create.argtypes = [u32]
+        L.mto_destroy.argtypes = [vp]
+        L.mto_apply.restype = ctypes.c_int
+        L.mto_apply.argtypes = [vp, vp, vp, vp, u32, ctypes.c_int]
+        L.mto_checksums.argtypes = [vp, vp, u32]
+        L.mto_doc_error.restype = ctypes.c_int
+        L.mto_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32)]
+        L.mto_doc_state.restype = u64
+        L.mto_doc_state.argtypes = [vp, u32, ctypes.c_char_p, u64]
+        L.mto_doc_text.restype = u64
+        L.mto_doc_text.argtypes = [vp, u32, ctypes.c_char_p, u64]
+        L.mto_doc_nsegs.restype = u32
+        L.mto_doc_nsegs.argtypes = [vp, u32]
+        L.mto_generate.restype = ctypes.c_int
+        L.mto_generate.argtypes = [vp, u32, u32, vp, vp, vp, vp, ctypes.c_int]
+        L.mto_seg_hash.restype = u64
+        L.mto_seg_hash.argtypes = [u64, u64, i32, i32, i32, i32, u64, u64, u32]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def generate(n_docs, d0=0, threads=os.cpu_count(), **cfg):
+    """Synthetic observer-driven op log (mt_synth.h spec) for documents [d0, d0+n_docs)."""
+    L = lib()
+    c = ctypes.create_string_buffer(synth_cfg_array(**cfg))
+    row_ptr = np.zeros(n_docs + 1, dtype=np.uint32)
+    pay_ptr = np.zeros(n_docs + 1, dtype=np.uint64)
+    L.mto_generate(c, d0, n_docs, None, None, _ptr(row_ptr), _ptr(pay_ptr), threads)
+    ops = np.zeros(int(row_ptr[-1]), dtype=OP_DTYPE)
+    payload = np.zeros(int(pay_ptr[-1]), dtype=np.uint8)
+    L.mto_generate(c, d0, n_docs, _ptr(ops), _ptr(payload), _ptr(row_ptr), _ptr(pay_ptr), threads)
+    return OpBatch(ops, payload, row_ptr)
+
+
+class Oracle:
+    """Observer replay of a batch on the CPU oracle."""
+
+    def __init__(self, n_docs):
+        self.n_docs = n_docs
+        self.h = lib().mto_create(n_docs)
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            lib().mto_destroy(self.h)
+            self.h = None
+
+    def apply(self, batch, threads=1):
+        assert batch.n_docs <= self.n_docs
+        rc = lib().mto_apply(self.h, _ptr(batch.ops), _ptr(batch.payload), _ptr(batch.row_ptr), batch.n_docs,
+                             threads)
+        assert rc == 0
+        return self
+
+    def checksums(self):
+        out = np.zeros(self.n_docs, dtype=np.uint64)
+        lib().mto_checksums(self.h, _ptr(out), self.n_docs)
+        return out
+
+    def error(self, doc):
+        s = ctypes.c_int32(0)
+        code = lib().mto_doc_error(self.h, doc, ctypes.byref(s))
+        return code, s.value
+
+    def state(self, doc):
+        n = lib().mto_doc_state(self.h, doc, None, 0)
+        buf = ctypes.create_string_buffer(int(n))
+        lib().mto_doc_state(self.h, doc, buf, n)
+        return json.loads(buf.value.decode())
+
+    def text(self, doc):
+        n = lib().mto_doc_text(self.h, doc, None, 0)
+        buf = ctypes.create_string_buffer(int(n))
+        lib().mto_doc_text(self.h, doc, buf, n)
+        return buf.value.decode()
+
+    def nsegs(self, doc):
+        return lib().mto_doc_nsegs(self.h, doc)

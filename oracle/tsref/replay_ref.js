@@ -1,0 +1,205 @@
+"use strict";
+// Replays an MTLOG op log through the REFERENCE merge-tree (type-stripped into oracle/_tsref by
+// build_ref.py) with one observer Client per document -- exactly the reference's own observer
+// pattern (clientReplayTool.ts:193-255; mergeTreeOperationRunner.ts:163-178 client 0) -- and
+// prints one canonical-state JSON line per document (DESIGN.md "Canonical state").
+// TEST INFRASTRUCTURE ONLY (this container; the reference never travels to the GPU box).
+//
+//   node replay_ref.js state <log.mtlog> [d0 d1]     -> JSON lines {doc, err, state}
+//   node replay_ref.js bench <log.mtlog> <threads>   -> ops/sec over all docs (worker_threads)
+const fs = require("fs");
+const path = require("path");
+const { Worker, isMainThread, parentPort, workerData } = require("worker_threads");
+
+const ROOT = path.join(__dirname, "..", "_tsref", "merge-tree", "src");
+const { Client } = require(path.join(ROOT, "client.js"));
+const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
+const { MergeTree } = require(path.join(ROOT, "mergeTree.js"));
+
+function loadLog(file) {
+    const buf = fs.readFileSync(file);
+    if (buf.toString("latin1", 0, 8) !== "MTLOG001") throw new Error("not an MTLOG file");
+    const nDocs = buf.readUInt32LE(8);
+    const nOps = Number(buf.readBigUInt64LE(16));
+    const nBytes = Number(buf.readBigUInt64LE(24));
+    let off = 32;
+    const rowPtr = new Uint32Array(nDocs + 1);
+    for (let i = 0; i <= nDocs; i++) rowPtr[i] = buf.readUInt32LE(off + 4 * i);
+    off += 4 * (nDocs + 1);
+    const opsOff = off;
+    const payOff = off + 32 * nOps;
+    return { buf, nDocs, nOps, nBytes, rowPtr, opsOff, payOff };
+}
+
+function readOp(log, i) {
+    const b = log.buf, o = log.opsOff + 32 * i;
+    return {
+        seq: b.readInt32LE(o), ref: b.readInt32LE(o + 4), msn: b.readInt32LE(o + 8),
+        client: b.readUInt16LE(o + 12), type: b.readUInt8(o + 14), flags: b.readUInt8(o + 15),
+        pos1: b.readInt32LE(o + 16), pos2: b.readInt32LE(o + 20),
+        poff: b.readUInt32LE(o + 24), plen: b.readUInt32LE(o + 28),
+    };
+}
+
+function propsOf(log, r) {
+    const np = r.flags >> 3;
+    const start = log.payOff + r.poff + r.plen - 2 * np;
+    const props = {};
+    for (let q = 0; q < np; q++) {
+        const k = log.buf.readUInt8(start + 2 * q), v = log.buf.readUInt8(start + 2 * q + 1);
+        props["k" + k] = v === 0 ? null : v;
+    }
+    return props;
+}
+
+// op record -> IMergeTreeOp JSON (ops.ts:63-110; opBuilder.ts:49-134)
+function toOp(log, r) {
+    const np = r.flags >> 3;
+    if (r.type === 0) {
+        const text = log.buf.toString("latin1", log.payOff + r.poff, log.payOff + r.poff + r.plen - 2 * np);
+        const seg = (r.flags & 2) ? { text, props: propsOf(log, r) } : text;
+        return { type: 0, pos1: r.pos1, seg };
+    }
+    if (r.type === 1) return { type: 1, pos1: r.pos1, pos2: r.pos2 };
+    if (r.type === 2) {
+        const op = { type: 2, pos1: r.pos1, pos2: r.pos2, props: propsOf(log, r) };
+        if (r.flags & 1) op.combiningOp = { name: "rewrite" };
+        return op;
+    }
+    return undefined;
+}
+
+function* messages(log, d) {
+    let group = null;
+    for (let i = log.rowPtr[d]; i < log.rowPtr[d + 1]; i++) {
+        const r = readOp(log, i);
+        const op = toOp(log, r);
+        if (group || (r.flags & 4)) {
+            if (!group) group = { r, ops: [] };
+            if (op) group.ops.push(op);
+            if (r.flags & 4) continue;
+            const g = group; group = null;
+            yield msgOf(g.r, { type: 3, ops: g.ops });
+            continue;
+        }
+        yield msgOf(r, op);
+    }
+}
+
+function msgOf(r, op) {
+    return {
+        clientId: "c" + r.client, clientSequenceNumber: 1, contents: op, metadata: undefined,
+        minimumSequenceNumber: r.msn, origin: undefined, referenceSequenceNumber: r.ref,
+        sequenceNumber: r.seq, timestamp: 0, term: 1, traces: [], type: op ? "op" : "noop",
+    };
+}
+
+function specToSegment(spec) { return TextSegment.fromJSONObject(spec); }
+
+function newObserver() {
+    const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+    const c = new Client(specToSegment, logger);
+    c.startOrUpdateCollaboration("observer");
+    return c;
+}
+
+function logId(client, shortId) {
+    const long = client.getLongClientId(shortId);
+    return long === "observer" ? 0 : parseInt(long.slice(1), 10);
+}
+
+function canonical(client) {
+    const mt = client.mergeTree;
+    const segs = [];
+    const walk = (b) => {
+        for (let i = 0; i < b.childCount; i++) {
+            const ch = b.children[i];
+            if (!ch.isLeaf()) { walk(ch); continue; }
+            const removed = ch.removedSeq !== undefined;
+            const ov = (ch.removedClientOverlap || []).map((x) => logId(client, x)).sort((a, b) => a - b);
+            let props = null;
+            if (ch.properties) {
+                props = {};
+                for (const k of Object.keys(ch.properties).sort((a, b) => parseInt(a.slice(1)) - parseInt(b.slice(1)))) {
+                    props[k] = ch.properties[k];
+                }
+            }
+            segs.push([ch.text, ch.seq, logId(client, ch.clientId), removed ? ch.removedSeq : -1,
+                removed ? logId(client, ch.removedClientId) : -1, ov, props]);
+        }
+    };
+    walk(mt.root);
+    const tree = [];
+    let lvl = [mt.root];
+    while (lvl.length) {
+        tree.push(lvl.map((b) => b.childCount));
+        const nxt = [];
+        for (const b of lvl) for (let i = 0; i < b.childCount; i++) if (!b.children[i].isLeaf()) nxt.push(b.children[i]);
+        lvl = nxt;
+    }
+    const w = mt.getCollabWindow();
+    return { seq: w.currentSeq, msn: w.minSeq, segs, tree };
+}
+
+function replayDoc(log, d) {
+    const c = newObserver();
+    let err = null;
+    try {
+        for (const m of messages(log, d)) c.applyMsg(m);
+    } catch (e) {
+        err = String(e.message || e);
+    }
+    return { c, err };
+}
+
+function main() {
+    const mode = process.argv[2];
+    const log = loadLog(process.argv[3]);
+    if (mode === "state") {
+        const d0 = process.argv[4] ? parseInt(process.argv[4], 10) : 0;
+        const d1 = process.argv[5] ? parseInt(process.argv[5], 10) : log.nDocs;
+        const out = [];
+        for (let d = d0; d < d1; d++) {
+            const { c, err } = replayDoc(log, d);
+            out.push(JSON.stringify({ doc: d, err, state: canonical(c), text: c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId()) }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
+    if (mode === "bench") {
+        const threads = parseInt(process.argv[4] || "1", 10);
+        const file = process.argv[3];
+        const t0 = process.hrtime.bigint();
+        let done = 0, ops = 0;
+        for (let t = 0; t < threads; t++) {
+            const w = new Worker(__filename, { workerData: { file, t, threads } });
+            w.on("message", (m) => {
+                ops += m.ops;
+                if (++done === threads) {
+                    const dt = Number(process.hrtime.bigint() - t0) / 1e9;
+                    console.log(JSON.stringify({ threads, ops, seconds: dt, ops_per_sec: ops / dt }));
+                }
+            });
+        }
+        return;
+    }
+    throw new Error("mode: state | bench");
+}
+
+if (isMainThread) {
+    main();
+} else {
+    // worker: docs round-robin (replayMultipleFiles.ts:123-190 pattern); messages pre-built
+    // outside the timed loop, as DeltaManager parses JSON upstream (deltaManager.ts:1283-1290)
+    const log = loadLog(workerData.file);
+    let ops = 0, apply = 0;
+    for (let d = workerData.t; d < log.nDocs; d += workerData.threads) {
+        const msgs = Array.from(messages(log, d));
+        const c = newObserver();
+        const t0 = process.hrtime.bigint();
+        for (const m of msgs) c.applyMsg(m);
+        apply += Number(process.hrtime.bigint() - t0);
+        ops += log.rowPtr[d + 1] - log.rowPtr[d];
+    }
+    parentPort.postMessage({ ops, apply_ns: apply });
+}

@@ -1,0 +1,33 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs on the GPU box via gpurun)')
+    config.addinivalue_line('markers', 'reference: needs /root/reference + node (build container only)')
+
+
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+GOLDEN_SETS = ['scenarios', 'synth_c1', 'synth_c2', 'synth_c3', 'synth_c4', 'synth_tiny']
+
+
+def load_golden(name):
+    import json
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    with open(os.path.join(GOLDEN, name + '.expected.jsonl')) as f:
+        exp = [json.loads(line) for line in f if line.strip()]
+    return batch, exp
+
+
+@pytest.fixture(scope='session')
+def oracle_lib():
+    from oracle import oracle
+    oracle.build()
+    return oracle

@@ -1,0 +1,914 @@
+// mt_apply.hip -- the MI355X batched merge-tree apply engine (gfx950 / CDNA4).
+//
+// One wave64 per document.  A launch stages each document's compact state (HBM, document
+// order, structure-of-arrays; mt_state.h) into the wave's slice of LDS, applies that
+// document's next ops in seq order -- the observer Client.applyMsg of the reference
+// (client.ts:797-828) -- and writes the state back compacted.  Per op, lanes cooperate:
+//   * visibility of every segment for (refSeq R, client C) and the position prefix sums are
+//     lane-parallel over the document order (DPP scan, mt_wave.h): this is what
+//     PartialSequenceLengths caches on the CPU (partialLengths.ts:433-487);
+//   * the B-tree shape (arity 8, split 4/4, pack, needsScour) is kept as per-level child-count
+//     arrays beside the ordered segment array, so the shape-dependent placement and zamboni
+//     rules (mergeTree.ts:2248-2277, 2345-2489, 1273-1478) are reproduced exactly;
+//   * split / insert / remove / annotate become shifts of the order array plus per-slot
+//     field writes; zamboni scour/pack are compactions of the order array + count edits.
+// Nothing here is a dense contraction: no MFMA.  The wave's LDS footprint sets occupancy.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtgpu.h"
+#include "mt_state.h"
+#include "mt_wave.h"
+
+namespace mt {
+
+constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
+constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
+
+template <int CAP>
+struct Lds {
+    static constexpr int LB = CAP / 2;      // leaf blocks
+    static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
+    static constexpr int H = CAP / 2 + 64;  // heap entries (1-based)
+    uint64_t ovl[CAP];
+    uint64_t props[CAP];
+    int32_t seq[CAP];
+    int32_t rseq[CAP];
+    uint32_t len[CAP];
+    uint32_t toff[CAP];
+    int32_t cum[CAP];       // scratch: inclusive prefix of visible length per position
+    int32_t bst[LB + 1];    // scratch: leaf-block start positions
+    int32_t hseq[H];
+    uint16_t hslot[H];
+    uint16_t order[CAP];    // document order -> slot
+    uint16_t freel[CAP];
+    uint8_t client[CAP];
+    uint8_t rclient[CAP];
+    uint8_t flags[CAP];
+    uint8_t lbcnt[LB];
+    uint8_t lbscour[LB];
+    uint8_t ibcnt[MT_MAXLEV - 1][IB];
+    int32_t n, nlev, heap_n, cur_seq, min_seq, err, err_seq, nfree, next_slot;
+    int32_t nb[MT_MAXLEV];
+    uint32_t text_top;
+};
+
+template <int CAP>
+struct Wave {
+    using L = Lds<CAP>;
+    L& s;
+    const int lane;
+    uint8_t* arena;
+    const uint32_t textcap;
+
+    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc) : s(lds), lane(lane_id()), arena(a), textcap(tc) {}
+
+    MT_DEV void fail(int code, int32_t seq) {
+        if (s.err == 0) {
+            s.err = code;
+            s.err_seq = seq;
+        }
+        wave_sync();
+    }
+
+    // -------------------------------------------------------------- visibility
+    // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697)
+    MT_DEV int vis(int slot, int32_t R, int C) const {
+        const bool seen = (s.client[slot] == C) || (s.seq[slot] <= R);
+        if (!seen) return 0;
+        if (s.flags[slot] & MT_SF_REMOVED) {
+            if (s.rclient[slot] == C || ((s.ovl[slot] >> C) & 1ull) || s.rseq[slot] <= R) return 0;
+        }
+        return (int)s.len[slot];
+    }
+
+    // cum[i] = sum of vis over positions 0..i; returns the total (getLength(R, C))
+    MT_DEV int scan(int32_t R, int C) {
+        const int n = s.n;
+        int carry = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const int v = i < n ? vis(s.order[i], R, C) : 0;
+            const int incl = wave_incl_scan(v) + carry;
+            if (i < n) s.cum[i] = incl;
+            carry = wave_last(incl);
+        }
+        wave_sync();
+        return carry;
+    }
+    MT_DEV int cstart(int k) const { return k > 0 ? s.cum[k - 1] : 0; }
+
+    // ------------------------------------------------------------- array shifts
+    template <class T>
+    MT_DEV void shift_right(T* a, int from, int count_end) {  // a[from..end) -> a[from+1..end+1)
+        for (int hi = count_end; hi > from; hi -= 64) {
+            const int i = hi - 1 - lane;
+            T v{};
+            const bool ok = i >= from;
+            if (ok) v = a[i];
+            wave_sync();
+            if (ok) a[i + 1] = v;
+            wave_sync();
+        }
+    }
+    template <class T>
+    MT_DEV void shift_left(T* a, int from, int count_end, int by) {  // a[from..end) -> a[from-by..)
+        for (int lo = from; lo < count_end; lo += 64) {
+            const int i = lo + lane;
+            T v{};
+            const bool ok = i < count_end;
+            if (ok) v = a[i];
+            wave_sync();
+            if (ok) a[i - by] = v;
+            wave_sync();
+        }
+    }
+
+    // ----------------------------------------------------------------- blocks
+    MT_DEV uint8_t* lvl(int L) { return L == 0 ? s.lbcnt : s.ibcnt[L - 1]; }
+    MT_DEV int lvlcap(int L) const { return L == 0 ? Lds<CAP>::LB : Lds<CAP>::IB; }
+
+    // bst[b] = first position of leaf block b (bst[nb0] = n)
+    MT_DEV void block_starts() {
+        const int nb = s.nb[0];
+        int carry = 0;
+        for (int base = 0; base < nb; base += 64) {
+            const int b = base + lane;
+            const int c = b < nb ? (int)s.lbcnt[b] : 0;
+            const int incl = wave_incl_scan(c) + carry;
+            if (b < nb) s.bst[b] = incl - c;
+            carry = wave_last(incl);
+        }
+        if (lane == 0) s.bst[nb] = carry;
+        wave_sync();
+    }
+
+    // leaf block containing position k (first non-empty block whose range holds k); needs bst
+    MT_DEV int block_of_pos(int k) {
+        const int nb = s.nb[0];
+        for (int base = 0; base < nb; base += 64) {
+            const int b = base + lane;
+            const bool hit = b < nb && s.bst[b] <= k && k < s.bst[b] + (int)s.lbcnt[b];
+            const uint64_t m = wave_ballot(hit);
+            if (m) return base + first_lane(m);
+        }
+        return -1;
+    }
+
+    // parent index (level L+1) of block b at level L, and the first child index of that parent
+    MT_DEV int parent_of(int L, int b, int* first_child) {
+        const uint8_t* pc = lvl(L + 1);
+        const int np = s.nb[L + 1];
+        int carry = 0;
+        for (int base = 0; base < np; base += 64) {
+            const int p = base + lane;
+            const int c = p < np ? (int)pc[p] : 0;
+            const int incl = wave_incl_scan(c) + carry;
+            const uint64_t m = wave_ballot(p < np && incl - c <= b && b < incl);
+            if (m) {
+                const int fl = first_lane(m);
+                if (first_child) *first_child = wave_bcast(incl - c, fl);
+                return base + fl;
+            }
+            carry = wave_last(incl);
+        }
+        return -1;
+    }
+
+    // insert a new block with `cnt` children right after block b at level L
+    MT_DEV bool insert_block_after(int L, int b, int cnt) {
+        const int nb = s.nb[L];
+        if (nb + 1 > lvlcap(L)) return false;
+        uint8_t* a = lvl(L);
+        shift_right(a, b + 1, nb);
+        if (L == 0) shift_right(s.lbscour, b + 1, nb);
+        if (lane == 0) {
+            a[b + 1] = (uint8_t)cnt;
+            if (L == 0) s.lbscour[b + 1] = MT_SC_UNDEF;
+        }
+        s.nb[L] = nb + 1;
+        wave_sync();
+        return true;
+    }
+
+    // block b at level L has reached kMaxNodes children: split 4/4 upward (split +
+    // insertingWalk's parent insert + updateRoot, mergeTree.ts:2446-2489, 1876-1887)
+    MT_DEV bool split_up(int L, int b, int32_t seq) {
+        for (;;) {
+            const int half = kMaxNodes / 2;
+            int parent = -1;
+            if (L < s.nlev - 1) parent = parent_of(L, b, nullptr);
+            if (lane == 0) lvl(L)[b] = (uint8_t)half;
+            wave_sync();
+            if (!insert_block_after(L, b, half)) return fail(MT_DERR_CAPACITY, seq), false;
+            if (L == s.nlev - 1) {  // split the root: new root with 2 children
+                if (s.nlev + 1 > MT_MAXLEV) return fail(MT_DERR_CAPACITY, seq), false;
+                const int nl = s.nlev;
+                if (lane == 0) lvl(nl)[0] = 2;
+                s.nb[nl] = 1;
+                s.nlev = nl + 1;
+                wave_sync();
+                return true;
+            }
+            uint8_t* pc = lvl(L + 1);
+            const int c = (int)pc[parent] + 1;
+            if (lane == 0) pc[parent] = (uint8_t)c;
+            wave_sync();
+            if (c < kMaxNodes) return true;
+            L = L + 1;
+            b = parent;
+        }
+    }
+
+    // ------------------------------------------------------------------ slots
+    MT_DEV int alloc_slot(int32_t seq) {
+        int sl;
+        if (s.nfree > 0) {
+            sl = s.freel[s.nfree - 1];
+            wave_sync();
+            s.nfree = s.nfree - 1;
+        } else {
+            sl = s.next_slot;
+            if (sl >= CAP) {
+                fail(MT_DERR_CAPACITY, seq);
+                return -1;
+            }
+            s.next_slot = sl + 1;
+        }
+        wave_sync();
+        return sl;
+    }
+    // unlink: free the slot and kill heap entries that still point at it
+    MT_DEV void free_slot(int sl) {
+        const int hn = s.heap_n;
+        for (int base = 1; base <= hn; base += 64) {
+            const int i = base + lane;
+            if (i <= hn && s.hslot[i] == sl) s.hslot[i] = MT_DEAD_SLOT;
+        }
+        if (lane == 0) s.freel[s.nfree] = (uint16_t)sl;
+        wave_sync();
+        s.nfree = s.nfree + 1;
+        wave_sync();
+    }
+
+    // insert slot `sl` at document position k of leaf block b; splits blocks as needed.
+    // `cum_val` >= 0 also keeps the cum[] scratch aligned (for a second boundary split).
+    MT_DEV bool insert_at(int k, int b, int sl, int cum_val, int32_t seq) {
+        const int n = s.n;
+        if (n + 1 > CAP) return fail(MT_DERR_CAPACITY, seq), false;
+        shift_right(s.order, k, n);
+        if (cum_val >= 0) shift_right(s.cum, k, n);
+        if (lane == 0) {
+            s.order[k] = (uint16_t)sl;
+            if (cum_val >= 0) s.cum[k] = cum_val;
+        }
+        s.n = n + 1;
+        const int c = (int)s.lbcnt[b] + 1;
+        wave_sync();
+        if (lane == 0) s.lbcnt[b] = (uint8_t)c;
+        wave_sync();
+        if (c >= kMaxNodes) return split_up(0, b, seq);
+        return true;
+    }
+
+    // ------------------------------------------------------------------- text
+    MT_DEV void arena_copy(uint32_t dst, uint32_t src, uint32_t n) {
+        for (uint32_t base = 0; base < n; base += 64) {
+            const uint32_t i = base + lane;
+            uint8_t v = 0;
+            if (i < n) v = arena[src + i];
+            __threadfence_block();
+            if (i < n) arena[dst + i] = v;
+        }
+        __threadfence_block();
+    }
+
+    // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245): split the segment visible to
+    // (R, C) that strictly contains pos.  Keeps cum[] valid for the same view.
+    MT_DEV bool boundary(int pos, int32_t R, int C, int32_t seq) {
+        const int n = s.n;
+        int k = -1;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const bool hit = i < n && cstart(i) < pos && pos < s.cum[i];
+            const uint64_t m = wave_ballot(hit);
+            if (m) {
+                k = base + first_lane(m);
+                break;
+            }
+        }
+        if (k < 0) return true;
+        const int sl = s.order[k];
+        const int off = pos - cstart(k);
+        const int t = alloc_slot(seq);
+        if (t < 0) return false;
+        block_starts();
+        const int b = block_of_pos(k);
+        // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
+        if (lane == 0) {
+            s.seq[t] = s.seq[sl];
+            s.client[t] = s.client[sl];
+            s.rseq[t] = s.rseq[sl];
+            s.rclient[t] = s.rclient[sl];
+            s.ovl[t] = s.ovl[sl];
+            s.props[t] = s.props[sl];
+            s.flags[t] = s.flags[sl];
+            s.len[t] = s.len[sl] - (uint32_t)off;
+            s.toff[t] = s.toff[sl] + (uint32_t)off;
+            s.len[sl] = (uint32_t)off;
+            const uint8_t last = arena[s.toff[sl] + (uint32_t)off - 1];
+            s.flags[sl] = (uint8_t)((s.flags[sl] & ~MT_SF_NL) | (last == '\n' ? MT_SF_NL : 0));
+        }
+        const int old_end = s.cum[k];
+        wave_sync();
+        if (lane == 0) s.cum[k] = pos;
+        wave_sync();
+        return insert_at(k + 1, b, t, old_end, seq);
+    }
+
+    // ------------------------------------------------------------------- heap
+    // Heap<LRUSegment> (collections.ts:213-265), comparer maxSeq (mergeTree.ts:923-926)
+    MT_DEV bool heap_push(int32_t key, int sl, int32_t seq) {
+        if (s.heap_n + 1 >= Lds<CAP>::H) return fail(MT_DERR_CAPACITY, seq), false;
+        if (lane == 0) {
+            int k = s.heap_n + 1;
+            s.hseq[k] = key;
+            s.hslot[k] = (uint16_t)sl;
+            while (k > 1 && s.hseq[k >> 1] - s.hseq[k] > 0) {
+                const int32_t ts = s.hseq[k >> 1];
+                const uint16_t tl = s.hslot[k >> 1];
+                s.hseq[k >> 1] = s.hseq[k];
+                s.hslot[k >> 1] = s.hslot[k];
+                s.hseq[k] = ts;
+                s.hslot[k] = tl;
+                k >>= 1;
+            }
+        }
+        const int hn = s.heap_n + 1;
+        wave_sync();
+        s.heap_n = hn;
+        wave_sync();
+        return true;
+    }
+    MT_DEV int heap_pop() {
+        int sl = 0;
+        if (lane == 0) {
+            sl = s.hslot[1];
+            const int cnt = s.heap_n - 1;
+            s.hseq[1] = s.hseq[s.heap_n];
+            s.hslot[1] = s.hslot[s.heap_n];
+            int k = 1;
+            while ((k << 1) <= cnt) {
+                int j = k << 1;
+                if (j < cnt && s.hseq[j] - s.hseq[j + 1] > 0) j++;
+                if (s.hseq[k] - s.hseq[j] <= 0) break;
+                const int32_t ts = s.hseq[k];
+                const uint16_t tl = s.hslot[k];
+                s.hseq[k] = s.hseq[j];
+                s.hslot[k] = s.hslot[j];
+                s.hseq[j] = ts;
+                s.hslot[j] = tl;
+                k = j;
+            }
+        }
+        sl = wave_bcast(sl, 0);
+        wave_sync();
+        s.heap_n = s.heap_n - 1;
+        wave_sync();
+        return sl;
+    }
+
+    // addToLRUSet (mergeTree.ts:1273-1283) for a segment in leaf block b
+    MT_DEV bool add_lru(int b, int sl, int32_t seq) {
+        if (s.lbscour[b] != MT_SC_TRUE && seq > s.cur_seq) {
+            wave_sync();
+            if (lane == 0) s.lbscour[b] = MT_SC_TRUE;
+            wave_sync();
+            return heap_push(seq, sl, seq);
+        }
+        return true;
+    }
+
+    // ---------------------------------------------------------------- zamboni
+    static MT_DEV bool props_match(uint8_t fa, uint64_t pa, uint8_t fb, uint64_t pb) {
+        return ((fa ^ fb) & MT_SF_PDEF) == 0 && pa == pb;  // matchProperties, properties.ts:62-93
+    }
+
+    // scourNode on leaf block b (mergeTree.ts:1289-1365).  Unlinks removed segments at or
+    // below minSeq, appends acked segments into their predecessor, compacts the order array.
+    // Returns the block's new child count.
+    MT_DEV int scour(int b) {
+        const int st = s.bst[b];
+        const int cnt = s.lbcnt[b];
+        const int32_t minSeq = s.min_seq;
+        int kept = 0, prev = -1;
+        uint16_t keep[kMaxNodes];
+        for (int q = 0; q < cnt; q++) {
+            const int sl = s.order[st + q];
+            const uint8_t f = s.flags[sl];
+            if (f & MT_SF_REMOVED) {
+                if (s.rseq[sl] > minSeq) keep[kept++] = (uint16_t)sl;
+                else free_slot(sl);  // UNLINK
+                prev = -1;
+            } else if (s.seq[sl] <= minSeq) {
+                bool app = false;
+                if (prev >= 0) {
+                    const uint32_t pl = s.len[prev], ql = s.len[sl];
+                    app = !(s.flags[prev] & MT_SF_NL) && (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
+                          props_match(s.flags[prev], s.props[prev], f, s.props[sl]) && ql > 0;
+                }
+                if (app) {
+                    append_text(prev, sl);
+                    free_slot(sl);  // APPEND: segment.parent = undefined
+                } else {
+                    keep[kept++] = (uint16_t)sl;
+                    prev = s.len[sl] > 0 ? sl : -1;
+                }
+            } else {
+                keep[kept++] = (uint16_t)sl;
+                prev = -1;
+            }
+        }
+        if (kept < cnt) {
+            wave_sync();
+            if (lane < kept) s.order[st + lane] = keep[lane];
+            wave_sync();
+            shift_left(s.order, st + cnt, s.n, cnt - kept);
+            s.n = s.n - (cnt - kept);
+            wave_sync();
+            if (lane == 0) s.lbcnt[b] = (uint8_t)kept;
+            // later block starts move left
+            const int nb = s.nb[0];
+            for (int base = b + 1; base <= nb; base += 64) {
+                const int j = base + lane;
+                if (j <= nb) s.bst[j] -= (cnt - kept);
+            }
+            wave_sync();
+        }
+        return kept;
+    }
+
+    // TextSegment.append (textSegment.ts:76-85): prev.text += seg.text
+    MT_DEV void append_text(int prev, int sl) {
+        const uint32_t pt = s.toff[prev], pl = s.len[prev], qt = s.toff[sl], ql = s.len[sl];
+        uint32_t top = s.text_top;
+        if (pt + pl == qt) {
+            // views are adjacent in the arena: nothing to copy
+        } else if (pt + pl == top) {
+            if (top + ql > textcap) return (void)fail(MT_DERR_TEXT_ARENA, s.cur_seq);
+            arena_copy(top, qt, ql);
+            top += ql;
+        } else {
+            if (top + pl + ql > textcap) return (void)fail(MT_DERR_TEXT_ARENA, s.cur_seq);
+            arena_copy(top, pt, pl);
+            arena_copy(top + pl, qt, ql);
+            if (lane == 0) s.toff[prev] = top;
+            top += pl + ql;
+        }
+        wave_sync();
+        if (lane == 0) {
+            s.len[prev] = pl + ql;
+            s.flags[prev] = (uint8_t)((s.flags[prev] & ~MT_SF_NL) | (s.flags[sl] & MT_SF_NL));
+        }
+        s.text_top = top;
+        wave_sync();
+    }
+
+    // pack (mergeTree.ts:1368-1420): repack the children of block P at level L+1, recursing up
+    MT_DEV void pack(int L, int P, int first_child) {
+        for (;;) {
+            const int m = lvl(L + 1)[P];
+            int total = 0;
+            if (L == 0) {
+                for (int j = first_child; j < first_child + m; j++) total += scour(j);
+            } else {
+                const uint8_t* c = lvl(L);
+                for (int j = first_child; j < first_child + m; j++) total += c[j];
+            }
+            const int half = kMaxNodes / 2;
+            int cc = min(kMaxNodes - 1, total / half);
+            if (cc < 1) cc = 1;
+            const int base = total / cc, extra = total % cc;
+            uint8_t* a = lvl(L);
+            const int nb = s.nb[L];
+            wave_sync();
+            if (cc < m) {
+                shift_left(a, first_child + m, nb, m - cc);
+                if (L == 0) shift_left(s.lbscour, first_child + m, nb, m - cc);
+            } else if (cc > m) {
+                for (int q = 0; q < cc - m; q++) {
+                    shift_right(a, first_child + m, nb + q);
+                    if (L == 0) shift_right(s.lbscour, first_child + m, nb + q);
+                }
+            }
+            if (lane < cc) {
+                a[first_child + lane] = (uint8_t)(base + (lane < extra ? 1 : 0));
+                if (L == 0) s.lbscour[first_child + lane] = MT_SC_UNDEF;
+            }
+            s.nb[L] = nb + cc - m;
+            wave_sync();
+            if (lane == 0) lvl(L + 1)[P] = (uint8_t)cc;
+            wave_sync();
+            if (L == 0) block_starts();
+            // underflow(parent) && parent.parent
+            if (cc < kMaxNodes / 2 && (L + 1) < s.nlev - 1) {
+                int fc = 0;
+                const int PP = parent_of(L + 1, P, &fc);
+                L = L + 1;
+                P = PP;
+                first_child = fc;
+                continue;
+            }
+            return;
+        }
+    }
+
+    // find the current position of slot sl (segment identity of a heap entry)
+    MT_DEV int pos_of_slot(int sl) {
+        const int n = s.n;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const uint64_t m = wave_ballot(i < n && s.order[i] == sl);
+            if (m) return base + first_lane(m);
+        }
+        return -1;
+    }
+
+    // zamboniSegments (mergeTree.ts:1422-1478), zamboniSegmentsMaxCount = 2
+    MT_DEV void zamboni() {
+        for (int it = 0; it < 2; it++) {
+            if (s.heap_n == 0 || s.hseq[1] > s.min_seq) break;
+            wave_sync();
+            const int sl = heap_pop();
+            if (sl == (int)MT_DEAD_SLOT) continue;
+            const int k = pos_of_slot(sl);
+            if (k < 0) continue;
+            block_starts();
+            const int b = block_of_pos(k);
+            if (s.lbscour[b] == MT_SC_FALSE) continue;
+            const int cnt = s.lbcnt[b];
+            const int kept = scour(b);
+            wave_sync();
+            if (lane == 0) s.lbscour[b] = MT_SC_FALSE;
+            wave_sync();
+            if (kept < cnt && kept < kMaxNodes / 2 && s.nlev > 1) {
+                int fc = 0;
+                const int P = parent_of(0, b, &fc);
+                pack(0, P, fc);
+            }
+            if (s.err) return;
+        }
+    }
+
+    // -------------------------------------------------------------------- ops
+    // props: apply (key, value) pairs; value 0 = null = delete (properties.ts:95-116)
+    static MT_DEV uint64_t apply_pairs(uint64_t p, const uint8_t* pairs, int np) {
+        for (int q = 0; q < np; q++) {
+            const int k = pairs[2 * q];
+            const uint64_t v = pairs[2 * q + 1];
+            p = (p & ~(0xFFull << (8 * k))) | (v << (8 * k));
+        }
+        return p;
+    }
+
+    MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np) {
+        const int32_t S = op.seq, R = op.ref_seq;
+        const int C = op.client, pos = op.pos1;
+        scan(R, C);
+        if (!boundary(pos, R, C, S)) return;
+        if (tlen > 0) {  // blockInsert (mergeTree.ts:2141-2224)
+            block_starts();
+            const int nb = s.nb[0];
+            // first leaf block whose cumulative visible end >= pos (insertingWalk descent)
+            int b = -1;
+            for (int base = 0; base < nb; base += 64) {
+                const int j = base + lane;
+                bool hit = false;
+                if (j < nb) {
+                    const int st = s.bst[j], c = s.lbcnt[j];
+                    const int bend = c > 0 ? s.cum[st + c - 1] : cstart(st);
+                    hit = bend >= pos;
+                }
+                const uint64_t m = wave_ballot(hit);
+                if (m) {
+                    b = base + first_lane(m);
+                    break;
+                }
+            }
+            if (b < 0) return fail(MT_DERR_INSERT_FAILED, S);
+            const int st = s.bst[b], c = s.lbcnt[b];
+            // leaf placement: first child with pos < len, or pos == len == 0 and breakTie
+            bool hit = false;
+            if (lane < c) {
+                const int k = st + lane;
+                const int ce = s.cum[k], cs = cstart(k);
+                const int sl = s.order[k];
+                const bool rm_before = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] <= R;
+                hit = ce > pos || (ce == pos && cs == pos && !rm_before);
+            }
+            const uint64_t m = wave_ballot(hit);
+            // not found: append at the end of block b (pos_rem == 0 there, mergeTree.ts:2431-2444)
+            const int k = m ? st + first_lane(m) : st + c;
+            const int t = alloc_slot(S);
+            if (t < 0) return;
+            const uint32_t top = s.text_top;
+            if (top + (uint32_t)tlen > textcap) return fail(MT_DERR_TEXT_ARENA, S);
+            for (int base = 0; base < tlen; base += 64) {
+                const int i = base + lane;
+                if (i < tlen) arena[top + i] = pay[i];
+            }
+            __threadfence_block();
+            if (lane == 0) {
+                s.seq[t] = S;
+                s.client[t] = (uint8_t)C;
+                s.rseq[t] = 0;
+                s.rclient[t] = 0;
+                s.ovl[t] = 0;
+                s.len[t] = (uint32_t)tlen;
+                s.toff[t] = top;
+                uint8_t f = pay[tlen - 1] == '\n' ? MT_SF_NL : 0;
+                uint64_t p = 0;
+                if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
+                    f |= MT_SF_PDEF;
+                    p = apply_pairs(0, pairs, np);
+                }
+                s.flags[t] = f;
+                s.props[t] = p;
+            }
+            s.text_top = top + (uint32_t)tlen;
+            wave_sync();
+            const int idx = k - st;  // index inside block b before a possible split
+            const int before_nb = s.nb[0];
+            if (!insert_at(k, b, t, -1, S)) return;
+            const int bb = (s.nb[0] > before_nb && idx >= kMaxNodes / 2) ? b + 1 : b;
+            if (S > s.min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
+                if (!add_lru(bb, t, S)) return;
+            }
+        }
+        zamboni();
+    }
+
+    MT_DEV void op_range(const mt_op_rec& op, const uint8_t* pairs, int np) {
+        const int32_t S = op.seq, R = op.ref_seq;
+        const int C = op.client, start = op.pos1, end = op.pos2;
+        const bool is_remove = op.type == MT_OP_REMOVE;
+        scan(R, C);
+        if (!boundary(start, R, C, S)) return;
+        if (!boundary(end, R, C, S)) return;
+        // markRangeRemoved / annotateRange leaf actions over mapRange (mergeTree.ts:2903-2965)
+        const int n = s.n;
+        const uint64_t cbit = 1ull << C;
+        const bool rewrite = op.flags & MT_F_REWRITE;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            if (i < n) {
+                const int ce = s.cum[i], cs = cstart(i);
+                if (ce > cs && cs < end && ce > start) {
+                    const int sl = s.order[i];
+                    if (is_remove) {
+                        if (s.flags[sl] & MT_SF_REMOVED) {
+                            s.ovl[sl] |= cbit;  // addOverlappingClient (first remover wins)
+                        } else {
+                            s.flags[sl] |= MT_SF_REMOVED;
+                            s.rseq[sl] = S;
+                            s.rclient[sl] = (uint8_t)C;
+                        }
+                    } else {  // SegmentPropertiesManager.addProperties (remote, no combining op)
+                        uint64_t p = (s.flags[sl] & MT_SF_PDEF) ? s.props[sl] : 0;
+                        if (rewrite) p = 0;
+                        s.props[sl] = apply_pairs(p, pairs, np);
+                        s.flags[sl] |= MT_SF_PDEF;
+                    }
+                }
+            }
+        }
+        wave_sync();
+        // addToLRUSet for touched segments in document order: one heap push per leaf block
+        // whose needsScour is not already true, for its first touched segment
+        block_starts();
+        const int nb = s.nb[0];
+        for (int base = 0; base < nb; base += 64) {
+            const int j = base + lane;
+            int first = -1;
+            if (j < nb) {
+                const int st = s.bst[j], c = s.lbcnt[j];
+                for (int q = 0; q < c; q++) {
+                    const int k = st + q;
+                    const int ce = s.cum[k], cs = cstart(k);
+                    if (ce > cs && cs < end && ce > start) {
+                        first = k;
+                        break;
+                    }
+                }
+            }
+            uint64_t m = wave_ballot(first >= 0);
+            while (m) {
+                const int fl = first_lane(m);
+                m &= m - 1;
+                const int k = wave_bcast(first, fl);
+                if (!add_lru(base + fl, s.order[k], S)) return;
+            }
+        }
+        zamboni();
+    }
+
+    // Client.updateSeqNumbers + MergeTree.setMinSeq (client.ts:821-828, mergeTree.ts:1718-1736)
+    MT_DEV void update_seq(int32_t msn, int32_t seq) {
+        if (!(s.cur_seq <= seq)) return fail(MT_DERR_SEQ_ORDER, seq);
+        wave_sync();
+        s.cur_seq = seq;
+        wave_sync();
+        if (!(msn <= seq) || !(s.min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, seq);
+        if (msn > s.min_seq) {
+            wave_sync();
+            s.min_seq = msn;
+            wave_sync();
+            zamboni();
+        }
+    }
+
+    MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
+        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        const int32_t S = op.seq;
+        if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
+        if (op.type != MT_OP_NOOP) {
+            if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
+            if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+            if (!(s.cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);   // client.ts:461-462
+            if (!(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // client.ts:463-464
+        }
+        const uint8_t* pay = payload + op.payload_off;
+        const int tlen = (int)op.payload_len - 2 * np;
+        const uint8_t* pairs = pay + tlen;
+        for (int q = 0; q < np; q++)
+            if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
+        if (op.type == MT_OP_INSERT) {
+            if (op.pos1 < 0) return fail(MT_DERR_BAD_OP, S);
+            op_insert(op, pay, tlen, pairs, np);
+        } else if (op.type != MT_OP_NOOP) {
+            if (op.pos1 < 0 || op.pos2 < 0) return fail(MT_DERR_BAD_OP, S);
+            op_range(op, pairs, np);
+        }
+        if (s.err) return;
+        if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
+    }
+
+    // ------------------------------------------------------------ load / store
+    MT_DEV void load(const mt_gstate& g, uint32_t d) {
+        const mt_doc_scalars& sc = g.sc[d];
+        const int n = sc.nseg;
+        const size_t so = (size_t)d * g.segcap;
+        for (int i = lane; i < n; i += 64) {
+            s.seq[i] = g.seq[so + i];
+            s.rseq[i] = g.rseq[so + i];
+            s.len[i] = g.len[so + i];
+            s.toff[i] = g.toff[so + i];
+            s.ovl[i] = g.ovl[so + i];
+            s.props[i] = g.props[so + i];
+            s.client[i] = g.client[so + i];
+            s.rclient[i] = g.rclient[so + i];
+            s.flags[i] = g.flags[so + i];
+            s.order[i] = (uint16_t)i;
+        }
+        const size_t lo = (size_t)d * g.lbcap;
+        for (int i = lane; i < sc.nb[0]; i += 64) {
+            s.lbcnt[i] = g.lbcnt[lo + i];
+            s.lbscour[i] = g.lbscour[lo + i];
+        }
+        for (int L = 1; L < sc.nlev; L++) {
+            const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
+            for (int i = lane; i < sc.nb[L]; i += 64) s.ibcnt[L - 1][i] = g.ibcnt[io + i];
+        }
+        const size_t ho = (size_t)d * g.hcap;
+        for (int i = 1 + lane; i <= sc.heap_n; i += 64) {
+            s.hseq[i] = g.hseq[ho + i];
+            s.hslot[i] = g.hslot[ho + i];
+        }
+        if (lane == 0) {
+            s.n = n;
+            s.nlev = sc.nlev;
+            for (int L = 0; L < MT_MAXLEV; L++) s.nb[L] = sc.nb[L];
+            s.heap_n = sc.heap_n;
+            s.cur_seq = sc.cur_seq;
+            s.min_seq = sc.min_seq;
+            s.err = sc.err;
+            s.err_seq = sc.err_seq;
+            s.nfree = 0;
+            s.next_slot = n;
+            s.text_top = sc.text_top;
+        }
+        wave_sync();
+    }
+
+    MT_DEV void store(const mt_gstate& g, uint32_t d) {
+        const int n = s.n;
+        const size_t so = (size_t)d * g.segcap;
+        if ((uint32_t)n > g.segcap || s.nb[0] > (int)g.lbcap || s.heap_n >= (int)g.hcap) fail(MT_DERR_CAPACITY, s.cur_seq);
+        const int nn = min(n, (int)g.segcap);
+        for (int i = lane; i < nn; i += 64) {
+            const int sl = s.order[i];
+            g.seq[so + i] = s.seq[sl];
+            g.rseq[so + i] = s.rseq[sl];
+            g.len[so + i] = s.len[sl];
+            g.toff[so + i] = s.toff[sl];
+            g.ovl[so + i] = s.ovl[sl];
+            g.props[so + i] = s.props[sl];
+            g.client[so + i] = s.client[sl];
+            g.rclient[so + i] = s.rclient[sl];
+            g.flags[so + i] = s.flags[sl];
+            s.cum[sl] = i;  // slot -> position for the heap remap
+        }
+        wave_sync();
+        const size_t lo = (size_t)d * g.lbcap;
+        for (int i = lane; i < min(s.nb[0], (int)g.lbcap); i += 64) {
+            g.lbcnt[lo + i] = s.lbcnt[i];
+            g.lbscour[lo + i] = s.lbscour[i];
+        }
+        for (int L = 1; L < s.nlev; L++) {
+            const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
+            for (int i = lane; i < min(s.nb[L], (int)g.ibcap); i += 64) g.ibcnt[io + i] = s.ibcnt[L - 1][i];
+        }
+        const size_t ho = (size_t)d * g.hcap;
+        for (int i = 1 + lane; i <= min(s.heap_n, (int)g.hcap - 1); i += 64) {
+            g.hseq[ho + i] = s.hseq[i];
+            const uint16_t sl = s.hslot[i];
+            g.hslot[ho + i] = sl == MT_DEAD_SLOT ? MT_DEAD_SLOT : (uint16_t)s.cum[sl];
+        }
+        if (lane == 0) {
+            mt_doc_scalars& sc = g.sc[d];
+            sc.nseg = nn;
+            sc.nlev = s.nlev;
+            for (int L = 0; L < MT_MAXLEV; L++) sc.nb[L] = s.nb[L];
+            sc.heap_n = s.heap_n;
+            sc.cur_seq = s.cur_seq;
+            sc.min_seq = s.min_seq;
+            sc.err = s.err;
+            sc.err_seq = s.err_seq;
+            sc.text_top = s.text_top;
+        }
+    }
+};
+
+template <int CAP>
+__global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+                                                   const uint8_t* __restrict__ payload,
+                                                   const uint32_t* __restrict__ row_ptr,
+                                                   const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
+                                                   uint32_t op_lo, uint32_t op_cnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t w = blockIdx.x;
+    if (w >= n_docs) return;
+    const uint32_t d = doc_ids ? doc_ids[w] : w;
+    Lds<CAP>& lds = *reinterpret_cast<Lds<CAP>*>(smem);
+    Wave<CAP> wv(lds, g.text + (size_t)d * g.textcap, g.textcap);
+    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+    const uint32_t a = min(r1, r0 + op_lo);
+    const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
+    if (a >= b) return;
+    wv.load(g, d);
+    for (uint32_t i = a; i < b; i++) {
+        if (lds.err) break;
+        const mt_op_rec op = ops[i];
+        wv.apply(op, payload);
+    }
+    wv.store(g, d);
+}
+
+}  // namespace mt
+
+// ------------------------------------------------------------------------------------------
+// host-side launchers (called from mt_engine.cpp)
+extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+                                      const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
+                                      uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    dim3 grid(n_docs), block(64);
+#define MT_LAUNCH(CAPV)                                                                                      \
+    case CAPV: {                                                                                             \
+        const size_t lds = sizeof(mt::Lds<CAPV>);                                                            \
+        hipLaunchKernelGGL(mt::apply_kernel<CAPV>, grid, block, lds, stream, *g, ops, payload, row_ptr,       \
+                           doc_ids, n_docs, op_lo, op_cnt);                                                  \
+        return hipGetLastError();                                                                            \
+    }
+    switch (cap_class) {
+        MT_LAUNCH(128)
+        MT_LAUNCH(256)
+        MT_LAUNCH(512)
+        MT_LAUNCH(1024)
+        MT_LAUNCH(2048)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef MT_LAUNCH
+}
+
+extern "C" size_t mt_lds_bytes(int cap_class) {
+    switch (cap_class) {
+        case 128: return sizeof(mt::Lds<128>);
+        case 256: return sizeof(mt::Lds<256>);
+        case 512: return sizeof(mt::Lds<512>);
+        case 1024: return sizeof(mt::Lds<1024>);
+        case 2048: return sizeof(mt::Lds<2048>);
+        default: return 0;
+    }
+}

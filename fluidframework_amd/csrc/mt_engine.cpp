@@ -1,0 +1,443 @@
+// mt_engine.cpp -- host side of libmtgpu.so: the C-ABI declared in include/mtgpu.h.
+//
+// Owns the device-resident document states (mt_state.h), stages CSR op batches into HBM and
+// drives the apply kernels on one HIP stream.  A batch is applied as a sequence of launches of
+// at most `ops_per_launch` ops per document (the serving tick; 0 = the whole batch in one
+// launch).  Before every launch the documents with work are binned by the LDS capacity class
+// they need (mt_bin_kernel), so small documents run at high occupancy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mtgpu.h"
+#include "mt_checksum.h"
+#include "mt_state.h"
+
+extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+                                      const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
+                                      uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
+extern "C" size_t mt_lds_bytes(int cap_class);
+extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
+extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
+                                    uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
+                                    uint32_t* ids, hipStream_t st);
+extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+
+namespace {
+const int32_t kClasses[] = {128, 256, 512, 1024, 2048};
+constexpr int kNumClasses = 5;
+// {CAP, LB, IB, H} per class: must match mt::Lds<CAP> in mt_apply.hip
+const int32_t kClassParams[kNumClasses * 4] = {
+    128, 64, 24, 128, 256, 128, 40, 192, 512, 256, 72, 320, 1024, 512, 136, 576, 2048, 1024, 264, 1088};
+}  // namespace
+
+struct mt_batch {
+    mt_op_rec* ops = nullptr;
+    uint8_t* payload = nullptr;
+    uint32_t* row_ptr = nullptr;
+    uint64_t n_ops = 0, payload_bytes = 0;
+    uint32_t n_docs = 0;
+    uint32_t max_ops_per_doc = 0;
+};
+
+struct mt_engine {
+    mt_cfg cfg{};
+    hipStream_t stream = nullptr;
+    mt_gstate g{};
+    uint32_t n_docs = 0;
+    std::vector<void*> allocs;
+    int32_t* d_classes = nullptr;
+    uint32_t* d_counts = nullptr;
+    uint32_t* d_ids = nullptr;
+    uint32_t* h_counts = nullptr;  // pinned
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;
+    uint32_t last_launches = 0;
+    uint64_t last_bytes = 0;
+};
+
+#define HIP_OK(x)                                                                                            \
+    do {                                                                                                     \
+        hipError_t e_ = (x);                                                                                 \
+        if (e_ != hipSuccess) {                                                                              \
+            fprintf(stderr, "libmtgpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return MT_ERR_HIP;                                                                               \
+        }                                                                                                    \
+    } while (0)
+
+template <class T>
+static mt_status dalloc(mt_engine* e, T** p, size_t count) {
+    void* q = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(&q, count * sizeof(T)) != hipSuccess) return MT_ERR_NOMEM;
+    e->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return MT_OK;
+}
+
+extern "C" {
+
+const char* mt_version(void) { return "libmtgpu 0.1 (gfx950)"; }
+
+mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
+    if (!cfg || !out || cfg->max_docs == 0) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(cfg->device));
+    auto* e = new mt_engine();
+    e->cfg = *cfg;
+    if (e->cfg.seg_capacity == 0) e->cfg.seg_capacity = 2048;
+    if (e->cfg.text_capacity == 0) e->cfg.text_capacity = 64 * 1024;
+    if (e->cfg.heap_capacity == 0) e->cfg.heap_capacity = 1088;
+    e->cfg.seg_capacity = std::min<uint32_t>(e->cfg.seg_capacity, 2048);
+    mt_gstate& g = e->g;
+    const size_t D = cfg->max_docs;
+    g.segcap = e->cfg.seg_capacity;
+    g.lbcap = g.segcap / 2;
+    g.ibcap = g.segcap / 8 + 8;
+    g.hcap = e->cfg.heap_capacity;
+    g.textcap = e->cfg.text_capacity;
+    mt_status st = MT_OK;
+    const size_t S = D * g.segcap;
+    if ((st = dalloc(e, &g.seq, S)) || (st = dalloc(e, &g.rseq, S)) || (st = dalloc(e, &g.len, S)) ||
+        (st = dalloc(e, &g.toff, S)) || (st = dalloc(e, &g.ovl, S)) || (st = dalloc(e, &g.props, S)) ||
+        (st = dalloc(e, &g.client, S)) || (st = dalloc(e, &g.rclient, S)) || (st = dalloc(e, &g.flags, S)) ||
+        (st = dalloc(e, &g.lbcnt, D * g.lbcap)) || (st = dalloc(e, &g.lbscour, D * g.lbcap)) ||
+        (st = dalloc(e, &g.ibcnt, D * (MT_MAXLEV - 1) * g.ibcap)) || (st = dalloc(e, &g.hseq, D * g.hcap)) ||
+        (st = dalloc(e, &g.hslot, D * g.hcap)) || (st = dalloc(e, &g.sc, D)) ||
+        (st = dalloc(e, &g.text, D * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
+        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
+        mt_engine_destroy(e);
+        return st;
+    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_counts, kNumClasses * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+        mt_engine_destroy(e);
+        return MT_ERR_HIP;
+    }
+    HIP_OK(hipMemcpy(e->d_classes, kClassParams, sizeof(kClassParams), hipMemcpyHostToDevice));
+    *out = e;
+    return MT_OK;
+}
+
+mt_status mt_engine_destroy(mt_engine* e) {
+    if (!e) return MT_ERR_ARG;
+    hipSetDevice(e->cfg.device);
+    if (e->stream) hipStreamSynchronize(e->stream);
+    for (void* p : e->allocs) hipFree(p);
+    if (e->h_counts) hipHostFree(e->h_counts);
+    if (e->ev0) hipEventDestroy(e->ev0);
+    if (e->ev1) hipEventDestroy(e->ev1);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+    return MT_OK;
+}
+
+mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
+    if (!e || n_docs > e->cfg.max_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    e->n_docs = n_docs;
+    HIP_OK(mt_launch_init(&e->g, n_docs, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
+                          uint64_t payload_bytes, const uint32_t* doc_row_ptr, mt_batch** out) {
+    if (!e || !out || !doc_row_ptr) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    auto* b = new mt_batch();
+    b->n_docs = e->n_docs;
+    b->n_ops = n_ops;
+    b->payload_bytes = payload_bytes;
+    if (doc_row_ptr[b->n_docs] != n_ops) {
+        delete b;
+        return MT_ERR_ARG;
+    }
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+        if (doc_row_ptr[d + 1] < doc_row_ptr[d]) {
+            delete b;
+            return MT_ERR_ARG;
+        }
+        b->max_ops_per_doc = std::max(b->max_ops_per_doc, doc_row_ptr[d + 1] - doc_row_ptr[d]);
+    }
+    for (uint64_t i = 0; i < n_ops; i++) {  // payload bounds: the kernels trust these
+        if ((uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes) {
+            delete b;
+            return MT_ERR_ARG;
+        }
+    }
+    if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
+        hipMalloc(&b->payload, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||
+        hipMalloc(&b->row_ptr, (b->n_docs + 1) * sizeof(uint32_t)) != hipSuccess) {
+        mt_batch_free(e, b);
+        return MT_ERR_NOMEM;
+    }
+    HIP_OK(hipMemcpyAsync(b->ops, ops, n_ops * sizeof(mt_op_rec), hipMemcpyHostToDevice, e->stream));
+    if (payload_bytes) HIP_OK(hipMemcpyAsync(b->payload, payload, payload_bytes, hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(b->row_ptr, doc_row_ptr, (b->n_docs + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    *out = b;
+    return MT_OK;
+}
+
+mt_status mt_batch_free(mt_engine* e, mt_batch* b) {
+    if (!e || !b) return MT_ERR_ARG;
+    hipSetDevice(e->cfg.device);
+    hipStreamSynchronize(e->stream);
+    if (b->ops) hipFree(b->ops);
+    if (b->payload) hipFree(b->payload);
+    if (b->row_ptr) hipFree(b->row_ptr);
+    delete b;
+    return MT_OK;
+}
+
+mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
+    if (!e || !b || b->n_docs != e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
+    const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
+    e->last_launches = 0;
+    HIP_OK(hipEventRecord(e->ev0, e->stream));
+    for (uint32_t t = 0; t < ticks; t++) {
+        const uint32_t lo = t * per;
+        HIP_OK(hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream));
+        HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
+                             e->stream));
+        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        for (int c = 0; c < kNumClasses; c++) {
+            const uint32_t cnt = e->h_counts[c];
+            if (!cnt) continue;
+            HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                   e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
+            e->last_launches++;
+        }
+    }
+    HIP_OK(hipEventRecord(e->ev1, e->stream));
+    HIP_OK(hipEventSynchronize(e->ev1));
+    HIP_OK(hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
+    return MT_OK;
+}
+
+mt_status mt_submit(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
+                    uint64_t payload_bytes, const uint32_t* doc_row_ptr) {
+    mt_batch* b = nullptr;
+    mt_status st = mt_batch_upload(e, ops, n_ops, payload, payload_bytes, doc_row_ptr, &b);
+    if (st) return st;
+    st = mt_batch_apply(e, b);
+    mt_batch_free(e, b);
+    return st;
+}
+
+mt_status mt_sync(mt_engine* e) {
+    if (!e) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+mt_status mt_last_apply_stats(mt_engine* e, float* ms, uint32_t* launches, uint64_t* alg_bytes) {
+    if (!e) return MT_ERR_ARG;
+    if (ms) *ms = e->last_ms;
+    if (launches) *launches = e->last_launches;
+    if (alg_bytes) *alg_bytes = e->last_bytes;
+    return MT_OK;
+}
+
+mt_status mt_checksums(mt_engine* e, uint64_t* out, uint32_t n_docs) {
+    if (!e || !out || n_docs > e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    uint64_t* d = nullptr;
+    HIP_OK(hipMalloc(&d, std::max<uint32_t>(1, n_docs) * sizeof(uint64_t)));
+    hipError_t r = mt_launch_checksum(&e->g, n_docs, d, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(out, d, n_docs * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    hipFree(d);
+    return r == hipSuccess ? MT_OK : MT_ERR_HIP;
+}
+
+mt_status mt_seg_counts(mt_engine* e, uint32_t* out, uint32_t n_docs) {
+    if (!e || !out || n_docs > e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    std::vector<mt_doc_scalars> sc(n_docs);
+    HIP_OK(hipMemcpyAsync(sc.data(), e->g.sc, n_docs * sizeof(mt_doc_scalars), hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (uint32_t d = 0; d < n_docs; d++) out[d] = (uint32_t)sc[d].nseg;
+    return MT_OK;
+}
+
+mt_status mt_doc_error(mt_engine* e, uint32_t doc, int32_t* code, int32_t* seq) {
+    if (!e || doc >= e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    mt_doc_scalars sc;
+    HIP_OK(hipMemcpyAsync(&sc, e->g.sc + doc, sizeof sc, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (code) *code = sc.err;
+    if (seq) *seq = sc.err_seq;
+    return MT_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------- canonical readout
+namespace {
+struct HostDoc {
+    mt_doc_scalars sc;
+    std::vector<int32_t> seq, rseq;
+    std::vector<uint32_t> len, toff;
+    std::vector<uint64_t> ovl, props;
+    std::vector<uint8_t> client, rclient, flags, text;
+    std::vector<std::vector<uint8_t>> levels;  // per level child counts (level 0 = leaf blocks)
+};
+
+template <class T>
+hipError_t fetch(std::vector<T>& v, const T* base, size_t off, size_t n, hipStream_t st) {
+    v.resize(n);
+    if (!n) return hipSuccess;
+    return hipMemcpyAsync(v.data(), base + off, n * sizeof(T), hipMemcpyDeviceToHost, st);
+}
+
+mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
+    const mt_gstate& g = e->g;
+    HIP_OK(hipMemcpyAsync(&h.sc, g.sc + d, sizeof h.sc, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const size_t so = (size_t)d * g.segcap, n = (size_t)h.sc.nseg;
+    HIP_OK(fetch(h.seq, g.seq, so, n, e->stream));
+    HIP_OK(fetch(h.rseq, g.rseq, so, n, e->stream));
+    HIP_OK(fetch(h.len, g.len, so, n, e->stream));
+    HIP_OK(fetch(h.toff, g.toff, so, n, e->stream));
+    HIP_OK(fetch(h.ovl, g.ovl, so, n, e->stream));
+    HIP_OK(fetch(h.props, g.props, so, n, e->stream));
+    HIP_OK(fetch(h.client, g.client, so, n, e->stream));
+    HIP_OK(fetch(h.rclient, g.rclient, so, n, e->stream));
+    HIP_OK(fetch(h.flags, g.flags, so, n, e->stream));
+    HIP_OK(fetch(h.text, g.text, (size_t)d * g.textcap, h.sc.text_top, e->stream));
+    h.levels.resize(h.sc.nlev);
+    for (int L = 0; L < h.sc.nlev; L++) {
+        if (L == 0) HIP_OK(fetch(h.levels[0], g.lbcnt, (size_t)d * g.lbcap, h.sc.nb[0], e->stream));
+        else HIP_OK(fetch(h.levels[L], g.ibcnt, ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap, h.sc.nb[L], e->stream));
+    }
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+void json_str(std::string& o, const uint8_t* p, size_t n) {
+    o += '"';
+    for (size_t i = 0; i < n; i++) {
+        unsigned char c = p[i];
+        if (c == '"' || c == '\\') {
+            o += '\\';
+            o += (char)c;
+        } else if (c < 0x20) {
+            char buf[8];
+            snprintf(buf, sizeof buf, "\\u%04x", c);
+            o += buf;
+        } else {
+            o += (char)c;
+        }
+    }
+    o += '"';
+}
+
+std::string state_json(const HostDoc& h) {
+    std::string o = "{\"seq\":" + std::to_string(h.sc.cur_seq) + ",\"msn\":" + std::to_string(h.sc.min_seq) + ",\"segs\":[";
+    for (int i = 0; i < h.sc.nseg; i++) {
+        if (i) o += ',';
+        o += '[';
+        json_str(o, h.text.data() + h.toff[i], h.len[i]);
+        const bool rm = h.flags[i] & MT_SF_REMOVED;
+        o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(h.client[i]) + ',';
+        o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient[i]) : "-1") + ",[";
+        bool f = true;
+        for (int c = 0; c < 64; c++)
+            if ((h.ovl[i] >> c) & 1) {
+                if (!f) o += ',';
+                f = false;
+                o += std::to_string(c);
+            }
+        o += "],";
+        if (!(h.flags[i] & MT_SF_PDEF)) {
+            o += "null";
+        } else {
+            o += '{';
+            bool f2 = true;
+            for (int k = 0; k < MT_MAX_KEYS; k++) {
+                const unsigned v = (unsigned)((h.props[i] >> (8 * k)) & 0xFF);
+                if (!v) continue;
+                if (!f2) o += ',';
+                f2 = false;
+                o += "\"k" + std::to_string(k) + "\":" + std::to_string(v);
+            }
+            o += '}';
+        }
+        o += ']';
+    }
+    o += "],\"tree\":[";
+    for (int depth = 0; depth < h.sc.nlev; depth++) {
+        const auto& lv = h.levels[h.sc.nlev - 1 - depth];
+        if (depth) o += ',';
+        o += '[';
+        for (size_t b = 0; b < lv.size(); b++) {
+            if (b) o += ',';
+            o += std::to_string(lv[b]);
+        }
+        o += ']';
+    }
+    o += "]}";
+    return o;
+}
+
+mt_status copy_out(const std::string& s, char* buf, uint64_t cap, uint64_t* len) {
+    if (len) *len = s.size();
+    if (buf && cap) {
+        const uint64_t n = std::min<uint64_t>(cap - 1, s.size());
+        memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return MT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+mt_status mt_get_state(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint64_t* len) {
+    if (!e || doc >= e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HostDoc h;
+    mt_status st = read_doc(e, doc, h);
+    if (st) return st;
+    return copy_out(state_json(h), buf, cap, len);
+}
+
+mt_status mt_get_text(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint64_t* len) {
+    if (!e || doc >= e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HostDoc h;
+    mt_status st = read_doc(e, doc, h);
+    if (st) return st;
+    std::string t;
+    for (int i = 0; i < h.sc.nseg; i++)
+        if (!(h.flags[i] & MT_SF_REMOVED)) t.append((const char*)h.text.data() + h.toff[i], h.len[i]);
+    return copy_out(t, buf, cap, len);
+}
+
+mt_status mt_get_length(mt_engine* e, uint32_t doc, uint32_t* len) {
+    if (!e || doc >= e->n_docs || !len) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HostDoc h;
+    mt_status st = read_doc(e, doc, h);
+    if (st) return st;
+    uint32_t n = 0;
+    for (int i = 0; i < h.sc.nseg; i++)
+        if (!(h.flags[i] & MT_SF_REMOVED)) n += h.len[i];
+    *len = n;
+    return MT_OK;
+}
+
+}  // extern "C"

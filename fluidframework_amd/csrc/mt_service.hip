@@ -1,0 +1,102 @@
+// mt_service.hip -- small device kernels around the apply engine: document init, per-launch
+// capacity binning, canonical-state checksums.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtgpu.h"
+#include "mt_checksum.h"
+#include "mt_state.h"
+#include "mt_wave.h"
+
+// Client + startOrUpdateCollaboration: an empty root block, collab window (0, 0)
+// (mergeTree.ts:1125-1129, 1254-1271)
+__global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n_docs) return;
+    mt_doc_scalars sc{};
+    sc.nseg = 0;
+    sc.nlev = 1;
+    sc.nb[0] = 1;
+    g.sc[d] = sc;
+    g.lbcnt[(size_t)d * g.lbcap] = 0;
+    g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
+}
+
+// Bin the documents that have ops in this launch by the LDS capacity class they need.
+// Each op adds at most 2 segments (a boundary split + an insert, or two boundary splits),
+// at most 2 leaf blocks, and a handful of heap entries.  classes[k] = {CAP, LB, IB, H}.
+__global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
+                              uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes,
+                              uint32_t* __restrict__ counts, uint32_t* __restrict__ ids) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n_docs) return;
+    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+    const uint32_t a = min(r1, r0 + op_lo);
+    const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
+    const mt_doc_scalars sc = g.sc[d];
+    if (a >= b || sc.err) return;
+    const int ops = (int)(b - a);
+    int ib_need = 0;
+    for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
+    int c = n_classes - 1;
+    for (int k = 0; k < n_classes; k++) {
+        const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2], h = classes[4 * k + 3];
+        if (sc.nseg + 2 * ops + 1 <= cap && sc.nb[0] + 2 * ops + 1 <= lb && ib_need + ops + 1 <= ib &&
+            sc.heap_n + 4 * ops + 16 <= h) {
+            c = k;
+            break;
+        }
+    }
+    const uint32_t at = atomicAdd(&counts[c], 1u);
+    ids[(size_t)c * n_docs + at] = d;
+}
+
+// checksum of the canonical state (mt_checksum.h), one wave per document
+__global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n_docs, uint64_t* __restrict__ out) {
+    const uint32_t d = blockIdx.x;
+    if (d >= n_docs) return;
+    const int lane = lane_id();
+    const mt_doc_scalars sc = g.sc[d];
+    const size_t so = (size_t)d * g.segcap;
+    const uint8_t* text = g.text + (size_t)d * g.textcap;
+    uint64_t seg_sum = 0;
+    for (int i = lane; i < sc.nseg; i += 64) {
+        uint64_t h = MT_FNV_INIT;
+        const uint32_t t0 = g.toff[so + i], tl = g.len[so + i];
+        for (uint32_t q = 0; q < tl; q++) h = mt_fnv1a_step(h, text[t0 + q]);
+        const uint8_t f = g.flags[so + i];
+        const bool rm = f & MT_SF_REMOVED;
+        seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], g.client[so + i], rm ? g.rseq[so + i] : -1,
+                               rm ? (int32_t)g.rclient[so + i] : -1, g.ovl[so + i], g.props[so + i],
+                               (f & MT_SF_PDEF) ? 1u : 0u);
+    }
+    uint64_t tree_sum = 0;
+    for (int L = 0; L < sc.nlev; L++) {
+        const uint64_t depth = (uint64_t)(sc.nlev - 1 - L);
+        const uint8_t* cnt = L == 0 ? g.lbcnt + (size_t)d * g.lbcap
+                                    : g.ibcnt + ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
+        for (int b = lane; b < sc.nb[L]; b += 64) tree_sum += mt_tree_term(cnt[b], (uint64_t)b, depth);
+    }
+    // wave sums of 64-bit values
+    for (int o = 1; o < 64; o <<= 1) {
+        seg_sum += (uint64_t)__shfl_xor((unsigned long long)seg_sum, o, 64);
+        tree_sum += (uint64_t)__shfl_xor((unsigned long long)tree_sum, o, 64);
+    }
+    if (lane == 0) out[d] = mt_finish_checksum(seg_sum, tree_sum, sc.cur_seq, sc.min_seq, (uint32_t)sc.nseg);
+}
+
+extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st) {
+    hipLaunchKernelGGL(mt_init_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, n_docs);
+    return hipGetLastError();
+}
+extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
+                                    uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
+                                    uint32_t* ids, hipStream_t st) {
+    hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
+                       classes, n_classes, counts, ids);
+    return hipGetLastError();
+}
+extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(mt_checksum_kernel, dim3(n_docs), dim3(64), 0, st, *g, n_docs, out);
+    return hipGetLastError();
+}

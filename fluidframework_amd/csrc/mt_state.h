@@ -1,0 +1,53 @@
+// mt_state.h -- device-resident per-document merge-tree state (HBM layout) shared by the
+// kernels and the host side of libmtgpu.so.  See DESIGN.md "Data layout in HBM".
+//
+// Between launches a document is stored COMPACT and IN DOCUMENT ORDER: entry i of every
+// segment array is the i-th linked leaf (what walkAllSegments visits, mergeTree.ts:2969-2983).
+// Arrays are structure-of-arrays with a fixed per-document stride so a wave loads/stores a
+// document's first N entries with coalesced accesses.
+#pragma once
+#include <stdint.h>
+
+#define MT_MAXLEV 7          // block levels incl. leaf blocks: 8^7 leaves
+#define MT_DEAD_SLOT 0xFFFFu // heap entry whose segment was unlinked (segment.parent === undefined)
+
+// segment flag bits
+#define MT_SF_REMOVED 1u     // removedSeq !== undefined
+#define MT_SF_PDEF 2u        // properties !== undefined (possibly empty)
+#define MT_SF_NL 4u          // text ends with "\n" (TextSegment.canAppend, textSegment.ts:63-68)
+
+// needsScour tri-state (mergeTree.ts:63, 1279, 1438, 1445)
+#define MT_SC_UNDEF 0
+#define MT_SC_TRUE 1
+#define MT_SC_FALSE 2
+
+struct mt_doc_scalars {      // 64 bytes
+    int32_t nseg;            // linked segments
+    int32_t nlev;            // block levels (1 = the root is the only, leaf, block)
+    int32_t nb[MT_MAXLEV];   // blocks per level (level 0 = leaf blocks)
+    int32_t heap_n;          // zamboni LRU heap size (entries 1..heap_n)
+    int32_t cur_seq, min_seq;// collabWindow.currentSeq / minSeq
+    int32_t err, err_seq;    // sticky per-document error (mt_doc_err) and the seq that raised it
+    uint32_t text_top;       // bytes used in the document's text arena
+};
+
+// Device pointers + capacities (one allocation per array, [n_docs][capacity]).
+struct mt_gstate {
+    int32_t* seq;      // [doc][segcap]
+    int32_t* rseq;
+    uint32_t* len;
+    uint32_t* toff;    // text view: arena offset
+    uint64_t* ovl;     // removedClientOverlap as a bitmask over short client ids
+    uint64_t* props;   // 8 keys x u8 value id
+    uint8_t* client;
+    uint8_t* rclient;
+    uint8_t* flags;
+    uint8_t* lbcnt;    // [doc][lbcap]       leaf-block child counts, in order
+    uint8_t* lbscour;  // [doc][lbcap]       leaf-block needsScour
+    uint8_t* ibcnt;    // [doc][MT_MAXLEV-1][ibcap] interior-level child counts
+    int32_t* hseq;     // [doc][hcap]        heap maxSeq (1-based, entry 0 unused)
+    uint16_t* hslot;   // [doc][hcap]        heap segment (position between launches)
+    mt_doc_scalars* sc;// [doc]
+    uint8_t* text;     // [doc][textcap]     text arena
+    uint32_t segcap, lbcap, ibcap, hcap, textcap;
+};

@@ -10,6 +10,8 @@
 
 #include <stdint.h>
 
+#include "../../include/mtgpu.h"
+
 #if defined(__HIPCC__)
 #define MT_HD __host__ __device__
 #else

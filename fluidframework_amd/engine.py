@@ -1,0 +1,183 @@
+"""Python host binding of libmtgpu.so (ctypes over the C-ABI in include/mtgpu.h).
+
+`MergeEngine` owns many independent documents on one MI355X; `apply(batch)` is the batched
+drop-in for calling `Client.applyMsg` (client.ts:797-819) on every op of every document.
+The HIP library is required: there is no CPU fallback, and a missing/unbuilt library raises.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+from .oplog import OpBatch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libmtgpu.so')
+
+MT_ERRORS = {0: 'ok', 1: 'bad argument', 2: 'HIP error', 3: 'out of device memory', 4: 'bad state',
+             5: 'document error'}
+DOC_ERRORS = {0: None,
+              1: "Incoming remote op sequence# <= local collabWindow's currentSequence#",
+              2: "Incoming remote op minSequence# < local collabWindow's minSequence#",
+              3: 'MergeTree insert failed',
+              4: 'device capacity exceeded',
+              5: 'text arena exhausted',
+              6: 'client id / property key / value id out of range',
+              7: 'malformed op record'}
+
+
+class MtError(RuntimeError):
+    pass
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [('device', ctypes.c_int32), ('max_docs', ctypes.c_uint32), ('seg_capacity', ctypes.c_uint32),
+                ('text_capacity', ctypes.c_uint32), ('heap_capacity', ctypes.c_uint32),
+                ('ops_per_launch', ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libmtgpu.so (built in-tree by fluidframework_amd/build.py); raise if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MtError(f'{LIB_PATH} is missing: build it with `python fluidframework_amd/build.py` '
+                          '(there is no CPU fallback)')
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+        L.mt_engine_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(vp)]
+        L.mt_engine_destroy.argtypes = [vp]
+        L.mt_docs_init.argtypes = [vp, u32]
+        L.mt_batch_upload.argtypes = [vp, vp, u64, vp, u64, vp, ctypes.POINTER(vp)]
+        L.mt_batch_apply.argtypes = [vp, vp]
+        L.mt_batch_free.argtypes = [vp, vp]
+        L.mt_submit.argtypes = [vp, vp, u64, vp, u64, vp]
+        L.mt_sync.argtypes = [vp]
+        L.mt_get_length.argtypes = [vp, u32, ctypes.POINTER(u32)]
+        L.mt_get_text.argtypes = [vp, u32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
+        L.mt_get_state.argtypes = [vp, u32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
+        L.mt_checksums.argtypes = [vp, vp, u32]
+        L.mt_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32),
+                                          ctypes.POINTER(u64)]
+        L.mt_seg_counts.argtypes = [vp, vp, u32]
+        L.mt_version.restype = ctypes.c_char_p
+        for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
+                     'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
+                     'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts'):
+            getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise MtError(f'{what}: {MT_ERRORS.get(rc, rc)}')
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class DeviceBatch:
+    """An op batch staged in HBM (mt_batch_upload); apply it with MergeEngine.apply_staged."""
+
+    def __init__(self, engine, batch):
+        self.engine = engine
+        self.n_ops = batch.n_ops
+        self.h = ctypes.c_void_p()
+        _check(lib().mt_batch_upload(engine.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload),
+                                     len(batch.payload), _ptr(batch.row_ptr), ctypes.byref(self.h)),
+               'mt_batch_upload')
+
+    def free(self):
+        if self.h:
+            lib().mt_batch_free(self.engine.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class MergeEngine:
+    def __init__(self, n_docs, device=0, seg_capacity=2048, text_capacity=64 * 1024, heap_capacity=1088,
+                 ops_per_launch=0):
+        cfg = _Cfg(device, n_docs, seg_capacity, text_capacity, heap_capacity, ops_per_launch)
+        self.h = ctypes.c_void_p()
+        _check(lib().mt_engine_create(ctypes.byref(cfg), ctypes.byref(self.h)), 'mt_engine_create')
+        self.n_docs = n_docs
+        _check(lib().mt_docs_init(self.h, n_docs), 'mt_docs_init')
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().mt_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- apply --------------------------------------------------------------------------
+    def apply(self, batch: OpBatch):
+        """Synchronous drop-in for applyMsg over every op of the batch."""
+        assert batch.n_docs == self.n_docs, 'a batch covers every document of the engine'
+        _check(lib().mt_submit(self.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload), len(batch.payload),
+                               _ptr(batch.row_ptr)), 'mt_submit')
+        return self
+
+    def stage(self, batch: OpBatch):
+        assert batch.n_docs == self.n_docs
+        return DeviceBatch(self, batch)
+
+    def apply_staged(self, dbatch: DeviceBatch):
+        _check(lib().mt_batch_apply(self.h, dbatch.h), 'mt_batch_apply')
+        return self
+
+    def last_stats(self):
+        ms, launches, nbytes = ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
+        _check(lib().mt_last_apply_stats(self.h, ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(nbytes)),
+               'mt_last_apply_stats')
+        return ms.value, launches.value, nbytes.value
+
+    # -- readout -------------------------------------------------------------------------
+    def checksums(self):
+        out = np.zeros(self.n_docs, dtype=np.uint64)
+        _check(lib().mt_checksums(self.h, _ptr(out), self.n_docs), 'mt_checksums')
+        return out
+
+    def seg_counts(self):
+        out = np.zeros(self.n_docs, dtype=np.uint32)
+        _check(lib().mt_seg_counts(self.h, _ptr(out), self.n_docs), 'mt_seg_counts')
+        return out
+
+    def error(self, doc):
+        code, seq = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().mt_doc_error(self.h, doc, ctypes.byref(code), ctypes.byref(seq)), 'mt_doc_error')
+        return code.value, seq.value
+
+    def _string(self, fn, doc):
+        n = ctypes.c_uint64()
+        _check(fn(self.h, doc, None, 0, ctypes.byref(n)), fn.__name__)
+        buf = ctypes.create_string_buffer(n.value + 1)
+        _check(fn(self.h, doc, buf, n.value + 1, ctypes.byref(n)), fn.__name__)
+        return buf.raw[:n.value].decode('latin-1')
+
+    def state(self, doc):
+        return json.loads(self._string(lib().mt_get_state, doc))
+
+    def text(self, doc):
+        return self._string(lib().mt_get_text, doc)
+
+    def length(self, doc):
+        n = ctypes.c_uint32()
+        _check(lib().mt_get_length(self.h, doc, ctypes.byref(n)), 'mt_get_length')
+        return n.value

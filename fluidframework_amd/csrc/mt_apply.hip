@@ -18,6 +18,7 @@
 
 #include "../../include/mtgpu.h"
 #include "mt_state.h"
+#include "mt_synth.h"
 #include "mt_wave.h"
 
 namespace mt {
@@ -50,7 +51,10 @@ struct Lds {
     uint8_t ibcnt[MT_MAXLEV - 1][IB];
     int32_t n, nlev, heap_n, cur_seq, min_seq, err, err_seq, nfree, next_slot;
     int32_t nb[MT_MAXLEV];
-    uint32_t text_top;
+    uint32_t text_top, text_half;
+    int32_t gcref[64];      // generator: latest refSeq per client (deli clientSeqManager)
+    int32_t gstall;         // generator: client 1 holds its refSeq until this seq
+    uint32_t gpay;          // generator: payload bytes used in this document's region
 };
 
 template <int CAP>
@@ -58,10 +62,11 @@ struct Wave {
     using L = Lds<CAP>;
     L& s;
     const int lane;
-    uint8_t* arena;
+    uint8_t* const abase;   // document's double-buffered arena: [2][textcap]
+    uint8_t* arena;         // current half
     const uint32_t textcap;
 
-    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc) : s(lds), lane(lane_id()), arena(a), textcap(tc) {}
+    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc) : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc) {}
 
     MT_DEV void fail(int code, int32_t seq) {
         if (s.err == 0) {
@@ -283,6 +288,41 @@ struct Wave {
         __threadfence_block();
     }
 
+    // Copy every linked segment's text, in document order, into the other half of the arena
+    // (TextSegment text has no identity; only its content is state).  Afterwards adjacent
+    // segments are adjacent in the arena, so later appends are free.
+    MT_DEV void compact_text() {
+        uint8_t* dst = abase + (size_t)(s.text_half ^ 1u) * textcap;
+        const int n = s.n;
+        uint32_t carry = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const int sl = i < n ? s.order[i] : 0;
+            const int l = i < n ? (int)s.len[sl] : 0;
+            const int incl = wave_incl_scan(l);
+            const uint32_t at = carry + (uint32_t)(incl - l);
+            if (i < n) {
+                const uint8_t* src = arena + s.toff[sl];
+                for (int q = 0; q < l; q++) dst[at + q] = src[q];
+            }
+            wave_sync();
+            if (i < n) s.toff[sl] = at;
+            carry += (uint32_t)wave_last(incl);
+        }
+        __threadfence_block();
+        s.text_half = s.text_half ^ 1u;
+        s.text_top = carry;
+        arena = dst;
+        wave_sync();
+    }
+    MT_DEV bool arena_reserve(uint32_t need, int32_t seq) {
+        if (s.text_top + need <= textcap) return true;
+        compact_text();
+        if (s.text_top + need <= textcap) return true;
+        fail(MT_DERR_TEXT_ARENA, seq);
+        return false;
+    }
+
     // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245): split the segment visible to
     // (R, C) that strictly contains pos.  Keeps cum[] valid for the same view.
     MT_DEV bool boundary(int pos, int32_t R, int C, int32_t seq) {
@@ -450,16 +490,19 @@ struct Wave {
 
     // TextSegment.append (textSegment.ts:76-85): prev.text += seg.text
     MT_DEV void append_text(int prev, int sl) {
+        if (s.toff[prev] + s.len[prev] != s.toff[sl] && s.toff[prev] + s.len[prev] != s.text_top) {
+            if (!arena_reserve(s.len[prev] + s.len[sl], s.cur_seq)) return;
+        } else if (s.toff[prev] + s.len[prev] != s.toff[sl]) {
+            if (!arena_reserve(s.len[sl], s.cur_seq)) return;
+        }
         const uint32_t pt = s.toff[prev], pl = s.len[prev], qt = s.toff[sl], ql = s.len[sl];
         uint32_t top = s.text_top;
         if (pt + pl == qt) {
             // views are adjacent in the arena: nothing to copy
         } else if (pt + pl == top) {
-            if (top + ql > textcap) return (void)fail(MT_DERR_TEXT_ARENA, s.cur_seq);
             arena_copy(top, qt, ql);
             top += ql;
         } else {
-            if (top + pl + ql > textcap) return (void)fail(MT_DERR_TEXT_ARENA, s.cur_seq);
             arena_copy(top, pt, pl);
             arena_copy(top + pl, qt, ql);
             if (lane == 0) s.toff[prev] = top;
@@ -611,8 +654,8 @@ struct Wave {
             const int k = m ? st + first_lane(m) : st + c;
             const int t = alloc_slot(S);
             if (t < 0) return;
+            if (!arena_reserve((uint32_t)tlen, S)) return;
             const uint32_t top = s.text_top;
-            if (top + (uint32_t)tlen > textcap) return fail(MT_DERR_TEXT_ARENA, S);
             for (int base = 0; base < tlen; base += 64) {
                 const int i = base + lane;
                 if (i < tlen) arena[top + i] = pay[i];
@@ -753,6 +796,139 @@ struct Wave {
         if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
     }
 
+    // ---------------------------------------------------------------- generator
+    // Device form of mto_gen_op (mt_synth.h): synthesise op i of this document from the
+    // observer state, write its record + payload, and return it.  Must match the host form
+    // draw for draw (tests/test_gpu_parity.py compares the logs byte for byte).
+    MT_DEV mt_op_rec gen_op(const mt_synth_cfg& cfg, uint64_t key, uint32_t i, uint8_t* pay, uint32_t pay_off,
+                            uint32_t paycap) {
+        const int32_t seq = s.cur_seq;
+        const uint32_t C = cfg.n_clients;
+        const int c = (int)mt_ru(key, i, MT_R_CLIENT, 1, C);
+        const int32_t lag = (int32_t)mt_ru(key, i, MT_R_LAG, 0, cfg.max_lag);
+        int32_t want = seq - lag > 0 ? seq - lag : 0;
+        if (cfg.stall_ops && c == 1) {
+            if (seq < s.gstall) {
+                want = s.gcref[1];
+            } else if (mt_ru(key, i, MT_R_STALL, 1, cfg.stall_ops) == 1) {
+                wave_sync();
+                s.gstall = seq + (int32_t)cfg.stall_ops;
+            }
+        }
+        int32_t R = s.gcref[c] > want ? s.gcref[c] : want;
+        if (R > seq) R = seq;
+        wave_sync();
+        if (lane == 0) s.gcref[c] = R;
+        wave_sync();
+        const int32_t mine = (lane >= 1 && lane <= (int)C) ? s.gcref[lane] : 0x7fffffff;
+        const int32_t msn = min(R, wave_min(mine));
+        const int L = scan(R, c);
+        const uint32_t rt = (uint32_t)mto_rng(key, i, MT_R_TYPE);
+        const uint8_t type = (L == 0 || rt < cfg.p_insert) ? 0 : (rt - cfg.p_insert < cfg.p_remove ? 1 : 2);
+        mt_op_rec rec{};
+        rec.seq = seq + 1;
+        rec.ref_seq = R;
+        rec.msn = msn;
+        rec.client = (uint16_t)c;
+        rec.type = type;
+        uint32_t n = 0, np = 0;
+        uint8_t pr[4] = {0, 0, 0, 0};
+        if (type == 0) {
+            rec.pos1 = (int32_t)mt_ru(key, i, MT_R_POS1, 0, (uint32_t)L);
+            const uint32_t tl = mt_gen_text_len(key, i);
+            if (pay_off + tl + 2 <= paycap) {
+                for (uint32_t t = lane; t < tl; t += 64) pay[t] = mt_gen_char(key, i, t);
+            }
+            n = tl;
+            if (cfg.n_keys && mt_rp(key, i, MT_R_IPROPS, cfg.p_insert_props)) {
+                rec.flags |= MT_F_PROPS;
+                pr[0] = (uint8_t)mt_ru(key, i, MT_R_IKEY, 0, cfg.n_keys - 1);
+                pr[1] = (uint8_t)mt_ru(key, i, MT_R_IVAL, 1, cfg.n_values);
+                np = 1;
+            }
+        } else {
+            int32_t a = (int32_t)mt_ru(key, i, MT_R_POS1, 0, (uint32_t)L - 1), b = 0;
+            bool aimed = false;
+            if (type == 1 && cfg.p_overlap && mt_rp(key, i, MT_R_AIM, cfg.p_overlap)) {
+                // segments visible to (R, c) whose removal c has not seen: count, then pick one
+                const int nn = s.n;
+                uint32_t cnt = 0;
+                for (int base = 0; base < nn; base += 64) {
+                    const int k = base + lane;
+                    bool hit = false;
+                    if (k < nn) {
+                        const int sl = s.order[k];
+                        hit = s.cum[k] > cstart(k) && (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] > R;
+                    }
+                    cnt += (uint32_t)__popcll(wave_ballot(hit));
+                }
+                if (cnt) {
+                    const uint32_t pick = mt_ru(key, i, MT_R_AIMPICK, 0, cnt - 1);
+                    uint32_t seen = 0;
+                    int kk = -1;
+                    for (int base = 0; base < nn && kk < 0; base += 64) {
+                        const int k = base + lane;
+                        bool hit = false;
+                        if (k < nn) {
+                            const int sl = s.order[k];
+                            hit = s.cum[k] > cstart(k) && (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] > R;
+                        }
+                        const uint64_t m = wave_ballot(hit);
+                        const uint32_t pc = (uint32_t)__popcll(m);
+                        if (pick < seen + pc) {
+                            uint64_t mm = m;
+                            for (uint32_t q = seen; q < pick; q++) mm &= mm - 1;
+                            kk = base + first_lane(mm);
+                        }
+                        seen += pc;
+                    }
+                    const int32_t ppos = cstart(kk), plen = s.cum[kk] - cstart(kk);
+                    const int32_t pre = (int32_t)mt_ru(key, i, MT_R_AIMPRE, 0, 2);
+                    const int32_t post = (int32_t)mt_ru(key, i, MT_R_AIMPOST, 0, 2);
+                    a = ppos - pre > 0 ? ppos - pre : 0;
+                    b = ppos + plen + post < L ? ppos + plen + post : L;
+                    aimed = true;
+                }
+            }
+            if (!aimed) {
+                const int32_t big = (int32_t)((mto_rng(key, i, MT_R_BIGLEN) & 15) == 0);
+                const int32_t q = L / 4 > 1 ? L / 4 : 1;
+                const int32_t ln = big ? (int32_t)mt_ru(key, i, MT_R_LEN, 1, (uint32_t)q)
+                                       : (int32_t)mt_ru(key, i, MT_R_LEN, 1, 16);
+                b = a + ln < L ? a + ln : L;
+            }
+            rec.pos1 = a;
+            rec.pos2 = b;
+            if (type == 2) {
+                if (mt_rp(key, i, MT_R_REWRITE, cfg.p_rewrite)) rec.flags |= MT_F_REWRITE;
+                const uint32_t nk = mt_ru(key, i, MT_R_NKEYS, 1, 2);
+                const uint32_t k0 = mt_ru(key, i, MT_R_KEY0, 0, cfg.n_keys - 1);
+                const uint32_t k1 = (k0 + 3) % cfg.n_keys;
+                pr[0] = (uint8_t)k0;
+                pr[1] = mt_rp(key, i, MT_R_NULL0, cfg.p_null) ? 0 : (uint8_t)mt_ru(key, i, MT_R_VAL0, 1, cfg.n_values);
+                np = 1;
+                if (nk == 2 && k1 != k0) {
+                    pr[2] = (uint8_t)k1;
+                    pr[3] = mt_rp(key, i, MT_R_NULL1, cfg.p_null) ? 0 : (uint8_t)mt_ru(key, i, MT_R_VAL1, 1, cfg.n_values);
+                    np = 2;
+                }
+            }
+        }
+        if (pay_off + n + 2 * np > paycap) {
+            fail(MT_DERR_TEXT_ARENA, rec.seq);
+            n = 0;
+            np = 0;
+        } else if (lane == 0) {
+            for (uint32_t q = 0; q < 2 * np; q++) pay[n + q] = pr[q];
+        }
+        __threadfence_block();
+        rec.flags |= (uint8_t)(np << MT_F_NPAIRS_SHIFT);
+        rec.payload_len = n + 2 * np;
+        rec.payload_off = 0;  // caller rebases
+        wave_sync();
+        return rec;
+    }
+
     // ------------------------------------------------------------ load / store
     MT_DEV void load(const mt_gstate& g, uint32_t d) {
         const mt_doc_scalars& sc = g.sc[d];
@@ -796,8 +972,10 @@ struct Wave {
             s.nfree = 0;
             s.next_slot = n;
             s.text_top = sc.text_top;
+            s.text_half = sc.text_half;
         }
         wave_sync();
+        arena = abase + (size_t)s.text_half * textcap;
     }
 
     MT_DEV void store(const mt_gstate& g, uint32_t d) {
@@ -845,31 +1023,67 @@ struct Wave {
             sc.err = s.err;
             sc.err_seq = s.err_seq;
             sc.text_top = s.text_top;
+            sc.text_half = s.text_half;
         }
     }
 };
 
-template <int CAP>
-__global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
-                                                   const uint8_t* __restrict__ payload,
+struct GenArgs {
+    mt_synth_cfg cfg;
+    int32_t* cref;      // [doc][64]
+    int32_t* stall;     // [doc]
+    uint32_t* pay_used; // [doc]
+    uint32_t paycap;    // payload bytes per document region
+};
+
+template <int CAP, bool GEN>
+__global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
+                                                   uint8_t* __restrict__ payload,
                                                    const uint32_t* __restrict__ row_ptr,
                                                    const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
-                                                   uint32_t op_lo, uint32_t op_cnt) {
+                                                   uint32_t op_lo, uint32_t op_cnt, GenArgs gen) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     Lds<CAP>& lds = *reinterpret_cast<Lds<CAP>*>(smem);
-    Wave<CAP> wv(lds, g.text + (size_t)d * g.textcap, g.textcap);
+    Wave<CAP> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     wv.load(g, d);
-    for (uint32_t i = a; i < b; i++) {
-        if (lds.err) break;
-        const mt_op_rec op = ops[i];
-        wv.apply(op, payload);
+    if (GEN) {
+        lds.gcref[wv.lane] = gen.cref[(size_t)d * 64 + wv.lane];
+        if (wv.lane == 0) {
+            lds.gstall = gen.stall[d];
+            lds.gpay = gen.pay_used[d];
+        }
+        wave_sync();
+        const uint64_t key = mto_rng_key(gen.cfg.seed, d);
+        const size_t pbase = (size_t)d * gen.paycap;
+        for (uint32_t i = a; i < b; i++) {
+            if (lds.err) break;
+            const uint32_t off = lds.gpay;
+            mt_op_rec op = wv.gen_op(gen.cfg, key, i - r0, payload + pbase + off, off, gen.paycap);
+            if (lds.err) break;
+            op.payload_off = (uint32_t)(pbase + off);
+            if (wv.lane == 0) ops[i] = op;
+            lds.gpay = off + op.payload_len;
+            wave_sync();
+            wv.apply(op, payload);
+        }
+        gen.cref[(size_t)d * 64 + wv.lane] = lds.gcref[wv.lane];
+        if (wv.lane == 0) {
+            gen.stall[d] = lds.gstall;
+            gen.pay_used[d] = lds.gpay;
+        }
+    } else {
+        for (uint32_t i = a; i < b; i++) {
+            if (lds.err) break;
+            const mt_op_rec op = ops[i];
+            wv.apply(op, payload);
+        }
     }
     wv.store(g, d);
 }
@@ -878,16 +1092,20 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, const mt_op_rec*
 
 // ------------------------------------------------------------------------------------------
 // host-side launchers (called from mt_engine.cpp)
-extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
-                                      const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
-                                      uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+static hipError_t launch_any(int cap_class, bool gen, const mt_gstate* g, mt_op_rec* ops, uint8_t* payload,
+                             const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
+                             uint32_t op_cnt, const mt::GenArgs& ga, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     dim3 grid(n_docs), block(64);
 #define MT_LAUNCH(CAPV)                                                                                      \
     case CAPV: {                                                                                             \
         const size_t lds = sizeof(mt::Lds<CAPV>);                                                            \
-        hipLaunchKernelGGL(mt::apply_kernel<CAPV>, grid, block, lds, stream, *g, ops, payload, row_ptr,       \
-                           doc_ids, n_docs, op_lo, op_cnt);                                                  \
+        if (gen)                                                                                             \
+            hipLaunchKernelGGL((mt::apply_kernel<CAPV, true>), grid, block, lds, stream, *g, ops, payload,    \
+                               row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);                                 \
+        else                                                                                                 \
+            hipLaunchKernelGGL((mt::apply_kernel<CAPV, false>), grid, block, lds, stream, *g, ops, payload,   \
+                               row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);                                 \
         return hipGetLastError();                                                                            \
     }
     switch (cap_class) {
@@ -900,6 +1118,22 @@ extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const m
             return hipErrorInvalidValue;
     }
 #undef MT_LAUNCH
+}
+
+extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+                                      const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
+                                      uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+    mt::GenArgs ga{};
+    return launch_any(cap_class, false, g, const_cast<mt_op_rec*>(ops), const_cast<uint8_t*>(payload), row_ptr,
+                      doc_ids, n_docs, op_lo, op_cnt, ga, stream);
+}
+
+extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, int32_t* cref,
+                                    int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
+                                    uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                    uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+    mt::GenArgs ga{*cfg, cref, stall, pay_used, paycap};
+    return launch_any(cap_class, true, g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga, stream);
 }
 
 extern "C" size_t mt_lds_bytes(int cap_class) {

@@ -26,6 +26,10 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
                                     uint32_t* ids, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, int32_t* cref,
+                                    int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
+                                    uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                    uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 
 namespace {
 const int32_t kClasses[] = {128, 256, 512, 1024, 2048};
@@ -107,7 +111,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.lbcnt, D * g.lbcap)) || (st = dalloc(e, &g.lbscour, D * g.lbcap)) ||
         (st = dalloc(e, &g.ibcnt, D * (MT_MAXLEV - 1) * g.ibcap)) || (st = dalloc(e, &g.hseq, D * g.hcap)) ||
         (st = dalloc(e, &g.hslot, D * g.hcap)) || (st = dalloc(e, &g.sc, D)) ||
-        (st = dalloc(e, &g.text, D * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
+        (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
         (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
         mt_engine_destroy(e);
         return st;
@@ -225,6 +229,111 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     return MT_OK;
 }
 
+mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t payload_per_doc, mt_batch** out) {
+    if (!e || !cfg || !out || cfg->n_clients == 0 || cfg->n_clients >= MT_MAX_CLIENTS || cfg->n_keys > MT_MAX_KEYS ||
+        cfg->n_values > MT_MAX_VALUES)
+        return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    const uint32_t n = e->n_docs, per = cfg->ops_per_doc;
+    const uint64_t n_ops = (uint64_t)n * per;
+    if (n_ops >= (1ull << 32) || (uint64_t)n * payload_per_doc >= (1ull << 32)) return MT_ERR_ARG;
+    auto* b = new mt_batch();
+    b->n_docs = n;
+    b->n_ops = n_ops;
+    b->payload_bytes = (uint64_t)n * payload_per_doc;
+    b->max_ops_per_doc = per;
+    std::vector<uint32_t> rp(n + 1);
+    for (uint32_t d = 0; d <= n; d++) rp[d] = d * per;
+    int32_t *cref = nullptr, *stall = nullptr;
+    uint32_t* pay_used = nullptr;
+    if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
+        hipMalloc(&b->payload, std::max<uint64_t>(1, b->payload_bytes)) != hipSuccess ||
+        hipMalloc(&b->row_ptr, (n + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&cref, (size_t)n * 64 * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&stall, (size_t)n * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&pay_used, (size_t)n * sizeof(uint32_t)) != hipSuccess) {
+        if (cref) (void)hipFree(cref);
+        if (stall) (void)hipFree(stall);
+        if (pay_used) (void)hipFree(pay_used);
+        mt_batch_free(e, b);
+        return MT_ERR_NOMEM;
+    }
+    mt_status st = MT_OK;
+    hipError_t r = hipMemcpyAsync(b->row_ptr, rp.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = hipMemsetAsync(cref, 0, (size_t)n * 64 * sizeof(int32_t), e->stream);
+    if (r == hipSuccess) r = hipMemsetAsync(stall, 0, (size_t)n * sizeof(int32_t), e->stream);
+    if (r == hipSuccess) r = hipMemsetAsync(pay_used, 0, (size_t)n * sizeof(uint32_t), e->stream);
+    const uint32_t tick = 64;
+    for (uint32_t lo = 0; r == hipSuccess && lo < per; lo += tick) {
+        r = hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream);
+        if (r == hipSuccess)
+            r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
+                              e->stream);
+        if (r == hipSuccess)
+            r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               e->stream);
+        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+        for (int c = 0; r == hipSuccess && c < kNumClasses; c++) {
+            if (!e->h_counts[c]) continue;
+            r = mt_launch_gen(kClasses[c], &e->g, cfg, cref, stall, pay_used, payload_per_doc, b->ops, b->payload,
+                              b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);
+        }
+    }
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(cref);
+    (void)hipFree(stall);
+    (void)hipFree(pay_used);
+    if (r != hipSuccess) {
+        fprintf(stderr, "libmtgpu: mt_synth_generate: %s\n", hipGetErrorString(r));
+        mt_batch_free(e, b);
+        return MT_ERR_HIP;
+    }
+    *out = b;
+    return st;
+}
+
+mt_status mt_batch_info(const mt_batch* b, uint64_t* n_ops, uint64_t* payload_bytes, uint32_t* max_ops_per_doc) {
+    if (!b) return MT_ERR_ARG;
+    if (n_ops) *n_ops = b->n_ops;
+    if (payload_bytes) *payload_bytes = b->payload_bytes;
+    if (max_ops_per_doc) *max_ops_per_doc = b->max_ops_per_doc;
+    return MT_OK;
+}
+
+mt_status mt_batch_copy_docs(mt_engine* e, const mt_batch* b, uint32_t d0, uint32_t d1, mt_op_rec* ops,
+                             uint64_t* n_ops, uint8_t* payload, uint64_t* payload_bytes, uint32_t* row_ptr) {
+    if (!e || !b || d0 > d1 || d1 > b->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    std::vector<uint32_t> rp(d1 - d0 + 1);
+    HIP_OK(hipMemcpyAsync(rp.data(), b->row_ptr + d0, rp.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const uint64_t cnt = rp.back() - rp.front();
+    std::vector<mt_op_rec> tmp(cnt);
+    if (cnt)
+        HIP_OK(hipMemcpyAsync(tmp.data(), b->ops + rp.front(), cnt * sizeof(mt_op_rec), hipMemcpyDeviceToHost,
+                              e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    uint64_t lo = ~0ull, hi = 0;
+    for (const auto& o : tmp) {
+        lo = std::min<uint64_t>(lo, o.payload_off);
+        hi = std::max<uint64_t>(hi, (uint64_t)o.payload_off + o.payload_len);
+    }
+    if (!cnt) lo = hi = 0;
+    if (n_ops) *n_ops = cnt;
+    if (payload_bytes) *payload_bytes = hi - lo;
+    if (row_ptr)
+        for (size_t i = 0; i < rp.size(); i++) row_ptr[i] = rp[i] - rp.front();
+    if (ops) {
+        for (auto& o : tmp) o.payload_off -= (uint32_t)lo;
+        memcpy(ops, tmp.data(), cnt * sizeof(mt_op_rec));
+    }
+    if (payload && hi > lo) {
+        HIP_OK(hipMemcpyAsync(payload, b->payload + lo, hi - lo, hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+    }
+    return MT_OK;
+}
+
 mt_status mt_submit(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
                     uint64_t payload_bytes, const uint32_t* doc_row_ptr) {
     mt_batch* b = nullptr;
@@ -317,7 +426,7 @@ mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
     HIP_OK(fetch(h.client, g.client, so, n, e->stream));
     HIP_OK(fetch(h.rclient, g.rclient, so, n, e->stream));
     HIP_OK(fetch(h.flags, g.flags, so, n, e->stream));
-    HIP_OK(fetch(h.text, g.text, (size_t)d * g.textcap, h.sc.text_top, e->stream));
+    HIP_OK(fetch(h.text, g.text, ((size_t)d * 2 + h.sc.text_half) * g.textcap, h.sc.text_top, e->stream));
     h.levels.resize(h.sc.nlev);
     for (int L = 0; L < h.sc.nlev; L++) {
         if (L == 0) HIP_OK(fetch(h.levels[0], g.lbcnt, (size_t)d * g.lbcap, h.sc.nb[0], e->stream));

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
     const int lane = lane_id();
     const mt_doc_scalars sc = g.sc[d];
     const size_t so = (size_t)d * g.segcap;
-    const uint8_t* text = g.text + (size_t)d * g.textcap;
+    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
     uint64_t seg_sum = 0;
     for (int i = lane; i < sc.nseg; i += 64) {
         uint64_t h = MT_FNV_INIT;

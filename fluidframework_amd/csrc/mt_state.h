@@ -21,14 +21,16 @@
 #define MT_SC_TRUE 1
 #define MT_SC_FALSE 2
 
-struct mt_doc_scalars {      // 64 bytes
+struct mt_doc_scalars {      // 80 bytes
     int32_t nseg;            // linked segments
     int32_t nlev;            // block levels (1 = the root is the only, leaf, block)
     int32_t nb[MT_MAXLEV];   // blocks per level (level 0 = leaf blocks)
     int32_t heap_n;          // zamboni LRU heap size (entries 1..heap_n)
     int32_t cur_seq, min_seq;// collabWindow.currentSeq / minSeq
     int32_t err, err_seq;    // sticky per-document error (mt_doc_err) and the seq that raised it
-    uint32_t text_top;       // bytes used in the document's text arena
+    uint32_t text_top;       // bytes used in the current half of the document's text arena
+    uint32_t text_half;      // which half of the double-buffered arena is current (0/1)
+    uint32_t pad[3];
 };
 
 // Device pointers + capacities (one allocation per array, [n_docs][capacity]).
@@ -48,6 +50,6 @@ struct mt_gstate {
     int32_t* hseq;     // [doc][hcap]        heap maxSeq (1-based, entry 0 unused)
     uint16_t* hslot;   // [doc][hcap]        heap segment (position between launches)
     mt_doc_scalars* sc;// [doc]
-    uint8_t* text;     // [doc][textcap]     text arena
+    uint8_t* text;     // [doc][2][textcap]  text arena, double-buffered for in-kernel compaction
     uint32_t segcap, lbcap, ibcap, hcap, textcap;
 };

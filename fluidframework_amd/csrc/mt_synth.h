@@ -18,27 +18,7 @@
 #define MT_HD
 #endif
 
-#ifdef __cplusplus
-extern "C" {
-#endif
-typedef struct mt_synth_cfg {
-    uint32_t seed;
-    uint32_t n_clients;      /* remote clients 1..n_clients                                 */
-    uint32_t ops_per_doc;
-    uint32_t max_lag;        /* refSeq lag U[0, max_lag] behind the latest seq               */
-    uint32_t stall_ops;      /* >0: client 1 holds its refSeq for stretches of this many ops */
-    uint32_t n_keys;         /* property keys used by annotate / insert props (<= 8)         */
-    uint32_t n_values;       /* property value ids 1..n_values (<= 255)                      */
-    /* probabilities as 32-bit fixed point thresholds (p * 2^32) */
-    uint32_t p_insert, p_remove;  /* remainder = annotate                                    */
-    uint32_t p_overlap;      /* a remove aims at a segment removed concurrently (C can see it) */
-    uint32_t p_null;         /* annotate value null = delete the key                         */
-    uint32_t p_rewrite;      /* annotate with combiningOp "rewrite"                          */
-    uint32_t p_insert_props; /* insert carries a props object                                */
-} mt_synth_cfg;
-#ifdef __cplusplus
-}
-#endif
+/* mt_synth_cfg is declared in include/mtgpu.h (it is part of the bench-tooling C-ABI). */
 
 /* slot numbers of the per-op draws */
 enum {

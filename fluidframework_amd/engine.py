@@ -65,10 +65,14 @@ def lib():
         L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32),
                                           ctypes.POINTER(u64)]
         L.mt_seg_counts.argtypes = [vp, vp, u32]
+        L.mt_synth_generate.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
+        L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
+        L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mt_version.restype = ctypes.c_char_p
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
-                     'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts'):
+                     'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
+                     'mt_batch_copy_docs', 'mt_batch_info'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -84,15 +88,37 @@ def _ptr(a):
 
 
 class DeviceBatch:
-    """An op batch staged in HBM (mt_batch_upload); apply it with MergeEngine.apply_staged."""
+    """An op batch resident in HBM: staged from the host (mt_batch_upload) or synthesised on the
+    device (mt_synth_generate).  Apply it with MergeEngine.apply_staged."""
 
-    def __init__(self, engine, batch):
+    def __init__(self, engine, batch=None, handle=None):
         self.engine = engine
-        self.n_ops = batch.n_ops
-        self.h = ctypes.c_void_p()
-        _check(lib().mt_batch_upload(engine.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload),
-                                     len(batch.payload), _ptr(batch.row_ptr), ctypes.byref(self.h)),
-               'mt_batch_upload')
+        if handle is not None:
+            self.h = handle
+        else:
+            self.h = ctypes.c_void_p()
+            _check(lib().mt_batch_upload(engine.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload),
+                                         len(batch.payload), _ptr(batch.row_ptr), ctypes.byref(self.h)),
+                   'mt_batch_upload')
+        n_ops, nbytes, mx = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+        _check(lib().mt_batch_info(self.h, ctypes.byref(n_ops), ctypes.byref(nbytes), ctypes.byref(mx)),
+               'mt_batch_info')
+        self.n_ops, self.payload_region, self.max_ops_per_doc = n_ops.value, nbytes.value, mx.value
+
+    def to_host(self, d0=0, d1=None):
+        """Documents [d0, d1) as a host OpBatch (payload offsets rebased)."""
+        d1 = self.engine.n_docs if d1 is None else d1
+        n_ops, nbytes = ctypes.c_uint64(), ctypes.c_uint64()
+        L = lib()
+        _check(L.mt_batch_copy_docs(self.engine.h, self.h, d0, d1, None, ctypes.byref(n_ops), None,
+                                    ctypes.byref(nbytes), None), 'mt_batch_copy_docs')
+        from .oplog import OP_DTYPE
+        ops = np.zeros(n_ops.value, dtype=OP_DTYPE)
+        payload = np.zeros(nbytes.value, dtype=np.uint8)
+        row_ptr = np.zeros(d1 - d0 + 1, dtype=np.uint32)
+        _check(L.mt_batch_copy_docs(self.engine.h, self.h, d0, d1, _ptr(ops), ctypes.byref(n_ops), _ptr(payload),
+                                    ctypes.byref(nbytes), _ptr(row_ptr)), 'mt_batch_copy_docs')
+        return OpBatch(ops, payload, row_ptr)
 
     def free(self):
         if self.h:
@@ -137,6 +163,19 @@ class MergeEngine:
     def stage(self, batch: OpBatch):
         assert batch.n_docs == self.n_docs
         return DeviceBatch(self, batch)
+
+    def synthesize(self, payload_per_doc=32 * 1024, **cfg):
+        """Generate a synthetic op log for every document ON THE DEVICE (mt_synth.h model; the
+        documents end in the post-generation state -- call reset() before replaying it)."""
+        from .oplog import synth_cfg_array
+        raw = ctypes.create_string_buffer(synth_cfg_array(**cfg))
+        h = ctypes.c_void_p()
+        _check(lib().mt_synth_generate(self.h, raw, payload_per_doc, ctypes.byref(h)), 'mt_synth_generate')
+        return DeviceBatch(self, handle=h)
+
+    def reset(self):
+        """All documents back to empty (mt_docs_init)."""
+        _check(lib().mt_docs_init(self.h, self.n_docs), 'mt_docs_init')
 
     def apply_staged(self, dbatch: DeviceBatch):
         _check(lib().mt_batch_apply(self.h, dbatch.h), 'mt_batch_apply')

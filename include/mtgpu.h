@@ -128,6 +128,35 @@ mt_status mt_last_apply_stats(mt_engine* eng, float* ms, uint32_t* launches, uin
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 
+/* ---- bench tooling (not part of the applyMsg boundary) -------------------------------------
+ * Synthetic multi-client op streams (DESIGN.md "Synthetic workloads", after SURVEY.md §8d),
+ * generated ON THE DEVICE straight into HBM: every document's observer state drives the
+ * positions of its next op, so each op is valid for what its client had seen.  The engine's
+ * documents are left in the post-generation state (call mt_docs_init to replay from empty). */
+typedef struct mt_synth_cfg {
+    uint32_t seed;
+    uint32_t n_clients;      /* remote clients 1..n_clients (< MT_MAX_CLIENTS)              */
+    uint32_t ops_per_doc;
+    uint32_t max_lag;        /* refSeq lag U[0, max_lag] behind the latest seq               */
+    uint32_t stall_ops;      /* >0: client 1 holds its refSeq for stretches of this many ops */
+    uint32_t n_keys;         /* property keys used by annotate / insert props (<= 8)         */
+    uint32_t n_values;       /* property value ids 1..n_values (<= 255)                      */
+    uint32_t p_insert, p_remove;  /* probabilities as fixed point p * 2^32; rest = annotate   */
+    uint32_t p_overlap;      /* a remove aims at a segment removed concurrently, still visible */
+    uint32_t p_null;         /* annotate value null = delete the key                         */
+    uint32_t p_rewrite;      /* annotate with combiningOp "rewrite"                          */
+    uint32_t p_insert_props; /* insert carries a props object                                */
+} mt_synth_cfg;
+
+mt_status mt_synth_generate(mt_engine* eng, const mt_synth_cfg* cfg, uint32_t payload_per_doc, mt_batch** out);
+/* Copy documents [d0, d1) of a staged batch to the host: ops (payload_off rebased so the
+ * first copied document's payload region starts at 0), payload and row_ptr (d1-d0+1 entries).
+ * Sizes for a dry run: pass NULL buffers. */
+mt_status mt_batch_copy_docs(mt_engine* eng, const mt_batch* batch, uint32_t d0, uint32_t d1, mt_op_rec* ops,
+                             uint64_t* n_ops, uint8_t* payload, uint64_t* payload_bytes, uint32_t* row_ptr);
+/* algorithmic bytes of a batch's ops + payload (for the roofline accounting in bench.py) */
+mt_status mt_batch_info(const mt_batch* batch, uint64_t* n_ops, uint64_t* payload_bytes, uint32_t* max_ops_per_doc);
+
 const char* mt_version(void);
 
 #ifdef __cplusplus

@@ -55,3 +55,31 @@ def test_fuzz_against_oracle(oracle_lib, cfg_name):
         d = int(bad[0])
         pytest.fail(f'{len(bad)}/{n} docs differ; doc {d}: err={eng.error(d)} {_diff(eng.state(d), o.state(d))}')
     assert all(eng.error(d) == (0, 0) for d in range(0, n, 17))
+
+
+@pytest.mark.parametrize('cfg_name', ['C2', 'C3', 'C4'])
+def test_device_generator_matches_host_generator(oracle_lib, cfg_name):
+    """The bench's on-device op synthesis (mt_synth.h, GEN kernel) emits exactly the log the
+    oracle's host generator emits; replaying it from empty reproduces the generation state."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import CONFIGS
+    cfg = dict(CONFIGS[cfg_name])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 512
+    n = 96
+    eng = MergeEngine(n)
+    dev = eng.synthesize(seed=99, **cfg)
+    gen_cs = eng.checksums()
+    host = oracle_lib.generate(n, seed=99, **cfg)
+    got = dev.to_host()
+    for f in ('seq', 'ref_seq', 'msn', 'client', 'type', 'flags', 'pos1', 'pos2', 'payload_len'):
+        assert np.array_equal(got.ops[f], host.ops[f]), f
+    for d in range(n):
+        a = got.doc_slice(d, d + 1)
+        b = host.doc_slice(d, d + 1)
+        assert np.array_equal(a.payload, b.payload), d
+    eng.reset()
+    eng.apply_staged(dev)
+    assert np.array_equal(eng.checksums(), gen_cs)
+    o = oracle_lib.Oracle(n).apply(host, threads=8)
+    assert np.array_equal(o.checksums(), gen_cs)

@@ -24,9 +24,10 @@ extern "C" size_t mt_lds_bytes(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
-                                    uint32_t* ids, hipStream_t st);
+                                    uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
-extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, int32_t* cref,
+extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
+                                    int32_t* cref,
                                     int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
                                     uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                     uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
@@ -58,8 +59,10 @@ struct mt_engine {
     uint32_t* d_counts = nullptr;
     uint32_t* d_ids = nullptr;
     uint32_t* h_counts = nullptr;  // pinned
+    unsigned long long* d_acc = nullptr;
+    std::vector<hipEvent_t> kev;   // per apply launch: start/stop pairs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    float last_ms = 0.f;
+    float last_ms = 0.f, last_wall_ms = 0.f;
     uint32_t last_launches = 0;
     uint64_t last_bytes = 0;
 };
@@ -112,7 +115,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.ibcnt, D * (MT_MAXLEV - 1) * g.ibcap)) || (st = dalloc(e, &g.hseq, D * g.hcap)) ||
         (st = dalloc(e, &g.hslot, D * g.hcap)) || (st = dalloc(e, &g.sc, D)) ||
         (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
-        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
+        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_acc, 2)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
         mt_engine_destroy(e);
         return st;
     }
@@ -133,6 +136,7 @@ mt_status mt_engine_destroy(mt_engine* e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) hipFree(p);
     if (e->h_counts) hipHostFree(e->h_counts);
+    for (auto ev : e->kev) (void)hipEventDestroy(ev);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     if (e->stream) hipStreamDestroy(e->stream);
@@ -206,30 +210,51 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     e->last_launches = 0;
+    uint32_t nk = 0;
+    HIP_OK(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
     HIP_OK(hipEventRecord(e->ev0, e->stream));
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
         HIP_OK(hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream));
         HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
-                             e->stream));
+                             b->ops, e->d_acc, e->stream));
         HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
         for (int c = 0; c < kNumClasses; c++) {
             const uint32_t cnt = e->h_counts[c];
             if (!cnt) continue;
+            while (e->kev.size() < 2 * (nk + 1)) {
+                hipEvent_t ev;
+                HIP_OK(hipEventCreate(&ev));
+                e->kev.push_back(ev);
+            }
+            HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
             HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
                                    e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
-            e->last_launches++;
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
+            nk++;
         }
     }
     HIP_OK(hipEventRecord(e->ev1, e->stream));
     HIP_OK(hipEventSynchronize(e->ev1));
-    HIP_OK(hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
+    float kms = 0.f;
+    for (uint32_t k = 0; k < nk; k++) {
+        float m = 0.f;
+        HIP_OK(hipEventElapsedTime(&m, e->kev[2 * k], e->kev[2 * k + 1]));
+        kms += m;
+    }
+    HIP_OK(hipEventElapsedTime(&e->last_wall_ms, e->ev0, e->ev1));
+    unsigned long long acc[2];
+    HIP_OK(hipMemcpy(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost));
+    e->last_ms = kms;
+    e->last_launches = nk;
+    e->last_bytes = acc[0] + acc[1];
     return MT_OK;
 }
 
-mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t payload_per_doc, mt_batch** out) {
+mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_id_base, uint32_t payload_per_doc,
+                             mt_batch** out) {
     if (!e || !cfg || !out || cfg->n_clients == 0 || cfg->n_clients >= MT_MAX_CLIENTS || cfg->n_keys > MT_MAX_KEYS ||
         cfg->n_values > MT_MAX_VALUES)
         return MT_ERR_ARG;
@@ -268,15 +293,15 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t payl
         r = hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream);
         if (r == hipSuccess)
             r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
-                              e->stream);
+                              nullptr, nullptr, e->stream);
         if (r == hipSuccess)
             r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                e->stream);
         if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
         for (int c = 0; r == hipSuccess && c < kNumClasses; c++) {
             if (!e->h_counts[c]) continue;
-            r = mt_launch_gen(kClasses[c], &e->g, cfg, cref, stall, pay_used, payload_per_doc, b->ops, b->payload,
-                              b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);
+            r = mt_launch_gen(kClasses[c], &e->g, cfg, doc_id_base, cref, stall, pay_used, payload_per_doc, b->ops,
+                              b->payload, b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);
         }
     }
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
@@ -351,9 +376,10 @@ mt_status mt_sync(mt_engine* e) {
     return MT_OK;
 }
 
-mt_status mt_last_apply_stats(mt_engine* e, float* ms, uint32_t* launches, uint64_t* alg_bytes) {
+mt_status mt_last_apply_stats(mt_engine* e, float* ms, float* wall_ms, uint32_t* launches, uint64_t* alg_bytes) {
     if (!e) return MT_ERR_ARG;
     if (ms) *ms = e->last_ms;
+    if (wall_ms) *wall_ms = e->last_wall_ms;
     if (launches) *launches = e->last_launches;
     if (alg_bytes) *alg_bytes = e->last_bytes;
     return MT_OK;

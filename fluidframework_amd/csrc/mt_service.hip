@@ -27,7 +27,8 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
 // at most 2 leaf blocks, and a handful of heap entries.  classes[k] = {CAP, LB, IB, H}.
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes,
-                              uint32_t* __restrict__ counts, uint32_t* __restrict__ ids) {
+                              uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
+                              const mt_op_rec* __restrict__ ops, unsigned long long* __restrict__ acc) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n_docs) return;
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
@@ -35,14 +36,26 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     const mt_doc_scalars sc = g.sc[d];
     if (a >= b || sc.err) return;
-    const int ops = (int)(b - a);
+    if (acc) {
+        // algorithmic bytes of this document's launch (DESIGN.md "Roofline accounting"):
+        // state in + out, op records, payload
+        unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] + 6ull * sc.heap_n +
+                                sizeof(mt_doc_scalars);
+        for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
+        unsigned long long ob = 32ull * (b - a);
+        if (ops)
+            for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
+        atomicAdd(&acc[0], 2ull * st);
+        atomicAdd(&acc[1], ob);
+    }
+    const int nops = (int)(b - a);
     int ib_need = 0;
     for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
     int c = n_classes - 1;
     for (int k = 0; k < n_classes; k++) {
         const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2], h = classes[4 * k + 3];
-        if (sc.nseg + 2 * ops + 1 <= cap && sc.nb[0] + 2 * ops + 1 <= lb && ib_need + ops + 1 <= ib &&
-            sc.heap_n + 4 * ops + 16 <= h) {
+        if (sc.nseg + 2 * nops + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb && ib_need + nops + 1 <= ib &&
+            sc.heap_n + 4 * nops + 16 <= h) {
             c = k;
             break;
         }
@@ -91,9 +104,9 @@ extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStr
 }
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
-                                    uint32_t* ids, hipStream_t st) {
+                                    uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st) {
     hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
-                       classes, n_classes, counts, ids);
+                       classes, n_classes, counts, ids, ops, acc);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st) {

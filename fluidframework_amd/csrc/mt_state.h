@@ -8,7 +8,10 @@
 #pragma once
 #include <stdint.h>
 
-#define MT_MAXLEV 7          // block levels incl. leaf blocks: 8^7 leaves
+#define MT_MAXLEV 7
+// bytes of one segment's persistent state: seq, rseq, len, toff (4 each), overlap, props (8 each),
+// client, rclient, flags (1 each)
+#define MT_SEG_STATE_BYTES 35          // block levels incl. leaf blocks: 8^7 leaves
 #define MT_DEAD_SLOT 0xFFFFu // heap entry whose segment was unlinked (segment.parent === undefined)
 
 // segment flag bits

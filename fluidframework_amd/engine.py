@@ -62,10 +62,10 @@ def lib():
         L.mt_get_state.argtypes = [vp, u32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
         L.mt_checksums.argtypes = [vp, vp, u32]
         L.mt_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
-        L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32),
-                                          ctypes.POINTER(u64)]
+        L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_seg_counts.argtypes = [vp, vp, u32]
-        L.mt_synth_generate.argtypes = [vp, vp, u32, ctypes.POINTER(vp)]
+        L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mt_version.restype = ctypes.c_char_p
@@ -164,13 +164,14 @@ class MergeEngine:
         assert batch.n_docs == self.n_docs
         return DeviceBatch(self, batch)
 
-    def synthesize(self, payload_per_doc=32 * 1024, **cfg):
+    def synthesize(self, payload_per_doc=32 * 1024, doc_id_base=0, **cfg):
         """Generate a synthetic op log for every document ON THE DEVICE (mt_synth.h model; the
         documents end in the post-generation state -- call reset() before replaying it)."""
         from .oplog import synth_cfg_array
         raw = ctypes.create_string_buffer(synth_cfg_array(**cfg))
         h = ctypes.c_void_p()
-        _check(lib().mt_synth_generate(self.h, raw, payload_per_doc, ctypes.byref(h)), 'mt_synth_generate')
+        _check(lib().mt_synth_generate(self.h, raw, doc_id_base, payload_per_doc, ctypes.byref(h)),
+               'mt_synth_generate')
         return DeviceBatch(self, handle=h)
 
     def reset(self):
@@ -182,10 +183,11 @@ class MergeEngine:
         return self
 
     def last_stats(self):
-        ms, launches, nbytes = ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
-        _check(lib().mt_last_apply_stats(self.h, ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(nbytes)),
-               'mt_last_apply_stats')
-        return ms.value, launches.value, nbytes.value
+        """(kernel_ms, wall_ms, launches, alg_bytes) of the last apply (see mtgpu.h)."""
+        ms, wall, launches, nbytes = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
+        _check(lib().mt_last_apply_stats(self.h, ctypes.byref(ms), ctypes.byref(wall), ctypes.byref(launches),
+                                         ctypes.byref(nbytes)), 'mt_last_apply_stats')
+        return ms.value, wall.value, launches.value, nbytes.value
 
     # -- readout -------------------------------------------------------------------------
     def checksums(self):

@@ -122,9 +122,12 @@ mt_status mt_get_state(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, ui
 mt_status mt_checksums(mt_engine* eng, uint64_t* out, uint32_t n_docs);
 mt_status mt_doc_error(mt_engine* eng, uint32_t doc, int32_t* code, int32_t* seq);
 
-/* Measurement hooks for bench.py: device time of the last mt_batch_apply (ms, HIP events on
- * the engine stream), kernel launches it issued, and the algorithmic bytes it moved. */
-mt_status mt_last_apply_stats(mt_engine* eng, float* ms, uint32_t* launches, uint64_t* alg_bytes);
+/* Measurement hooks for bench.py, for the last mt_batch_apply: kernel_ms = sum of the apply
+ * kernels' durations (HIP events bracketing each launch on the engine stream), wall_ms = first
+ * to last event (incl. binning and the per-tick host sync), launches = apply kernels issued,
+ * alg_bytes = algorithmic bytes they move (DESIGN.md "Roofline accounting"). */
+mt_status mt_last_apply_stats(mt_engine* eng, float* kernel_ms, float* wall_ms, uint32_t* launches,
+                              uint64_t* alg_bytes);
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 
@@ -148,7 +151,9 @@ typedef struct mt_synth_cfg {
     uint32_t p_insert_props; /* insert carries a props object                                */
 } mt_synth_cfg;
 
-mt_status mt_synth_generate(mt_engine* eng, const mt_synth_cfg* cfg, uint32_t payload_per_doc, mt_batch** out);
+/* doc_id_base: global id of the engine's document 0 (a rank's shard of a multi-GPU job) */
+mt_status mt_synth_generate(mt_engine* eng, const mt_synth_cfg* cfg, uint32_t doc_id_base, uint32_t payload_per_doc,
+                            mt_batch** out);
 /* Copy documents [d0, d1) of a staged batch to the host: ops (payload_off rebased so the
  * first copied document's payload region starts at 0), payload and row_ptr (d1-d0+1 entries).
  * Sizes for a dry run: pass NULL buffers. */

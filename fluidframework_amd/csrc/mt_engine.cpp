@@ -63,6 +63,10 @@ struct mt_engine {
     std::vector<hipEvent_t> kev;   // per apply launch: start/stop pairs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f, last_wall_ms = 0.f;
+    float cls_ms[kNumClasses] = {0};
+    uint32_t cls_launches[kNumClasses] = {0};
+    uint64_t cls_bytes[kNumClasses] = {0};
+    std::vector<int> kev_cls;
     uint32_t last_launches = 0;
     uint64_t last_bytes = 0;
 };
@@ -115,7 +119,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.ibcnt, D * (MT_MAXLEV - 1) * g.ibcap)) || (st = dalloc(e, &g.hseq, D * g.hcap)) ||
         (st = dalloc(e, &g.hslot, D * g.hcap)) || (st = dalloc(e, &g.sc, D)) ||
         (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
-        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_acc, 2)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
+        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_acc, kNumClasses)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
         mt_engine_destroy(e);
         return st;
     }
@@ -211,7 +215,8 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     e->last_launches = 0;
     uint32_t nk = 0;
-    HIP_OK(hipMemsetAsync(e->d_acc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIP_OK(hipMemsetAsync(e->d_acc, 0, kNumClasses * sizeof(unsigned long long), e->stream));
+    e->kev_cls.clear();
     HIP_OK(hipEventRecord(e->ev0, e->stream));
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
@@ -233,23 +238,34 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
                                    e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
+            e->kev_cls.push_back(c);
             nk++;
         }
     }
     HIP_OK(hipEventRecord(e->ev1, e->stream));
     HIP_OK(hipEventSynchronize(e->ev1));
     float kms = 0.f;
+    for (int c = 0; c < kNumClasses; c++) {
+        e->cls_ms[c] = 0.f;
+        e->cls_launches[c] = 0;
+    }
     for (uint32_t k = 0; k < nk; k++) {
         float m = 0.f;
         HIP_OK(hipEventElapsedTime(&m, e->kev[2 * k], e->kev[2 * k + 1]));
         kms += m;
+        e->cls_ms[e->kev_cls[k]] += m;
+        e->cls_launches[e->kev_cls[k]]++;
     }
     HIP_OK(hipEventElapsedTime(&e->last_wall_ms, e->ev0, e->ev1));
-    unsigned long long acc[2];
+    unsigned long long acc[kNumClasses];
     HIP_OK(hipMemcpy(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost));
     e->last_ms = kms;
     e->last_launches = nk;
-    e->last_bytes = acc[0] + acc[1];
+    e->last_bytes = 0;
+    for (int c = 0; c < kNumClasses; c++) {
+        e->cls_bytes[c] = acc[c];
+        e->last_bytes += acc[c];
+    }
     return MT_OK;
 }
 
@@ -382,6 +398,16 @@ mt_status mt_last_apply_stats(mt_engine* e, float* ms, float* wall_ms, uint32_t*
     if (wall_ms) *wall_ms = e->last_wall_ms;
     if (launches) *launches = e->last_launches;
     if (alg_bytes) *alg_bytes = e->last_bytes;
+    return MT_OK;
+}
+
+mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capacity, float* kernel_ms,
+                                    uint32_t* launches, uint64_t* alg_bytes) {
+    if (!e || cls >= (uint32_t)kNumClasses) return MT_ERR_ARG;
+    if (capacity) *capacity = (uint32_t)kClasses[cls];
+    if (kernel_ms) *kernel_ms = e->cls_ms[cls];
+    if (launches) *launches = e->cls_launches[cls];
+    if (alg_bytes) *alg_bytes = e->cls_bytes[cls];
     return MT_OK;
 }
 

@@ -36,18 +36,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     const mt_doc_scalars sc = g.sc[d];
     if (a >= b || sc.err) return;
-    if (acc) {
-        // algorithmic bytes of this document's launch (DESIGN.md "Roofline accounting"):
-        // state in + out, op records, payload
-        unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] + 6ull * sc.heap_n +
-                                sizeof(mt_doc_scalars);
-        for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
-        unsigned long long ob = 32ull * (b - a);
-        if (ops)
-            for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
-        atomicAdd(&acc[0], 2ull * st);
-        atomicAdd(&acc[1], ob);
-    }
+
     const int nops = (int)(b - a);
     int ib_need = 0;
     for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
@@ -62,6 +51,17 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
     }
     const uint32_t at = atomicAdd(&counts[c], 1u);
     ids[(size_t)c * n_docs + at] = d;
+    if (acc) {
+        // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
+        // accounting"): persistent state in + out, op records, payload; per class
+        unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] + 6ull * sc.heap_n +
+                                sizeof(mt_doc_scalars);
+        for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
+        unsigned long long ob = 32ull * (b - a);
+        if (ops)
+            for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
+        atomicAdd(&acc[c], 2ull * st + ob);
+    }
 }
 
 // checksum of the canonical state (mt_checksum.h), one wave per document

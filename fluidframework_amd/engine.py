@@ -65,6 +65,8 @@ def lib():
         L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_seg_counts.argtypes = [vp, vp, u32]
+        L.mt_last_apply_class_stats.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float),
+                                                ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
@@ -72,7 +74,7 @@ def lib():
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
-                     'mt_batch_copy_docs', 'mt_batch_info'):
+                     'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -188,6 +190,16 @@ class MergeEngine:
         _check(lib().mt_last_apply_stats(self.h, ctypes.byref(ms), ctypes.byref(wall), ctypes.byref(launches),
                                          ctypes.byref(nbytes)), 'mt_last_apply_stats')
         return ms.value, wall.value, launches.value, nbytes.value
+
+    def last_class_stats(self):
+        """[(capacity, kernel_ms, launches, alg_bytes)] per LDS capacity class of the last apply."""
+        out = []
+        for c in range(5):
+            cap, ms, n, nb = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
+            _check(lib().mt_last_apply_class_stats(self.h, c, ctypes.byref(cap), ctypes.byref(ms), ctypes.byref(n),
+                                                   ctypes.byref(nb)), 'mt_last_apply_class_stats')
+            out.append((cap.value, ms.value, n.value, nb.value))
+        return out
 
     # -- readout -------------------------------------------------------------------------
     def checksums(self):

@@ -33,6 +33,26 @@ def build(force=False, verbose=False):
     return LIB
 
 
+JS = os.path.join(os.path.dirname(HERE), 'js')
+NAPI = os.path.join(JS, 'mtgpu.node')
+
+
+def build_napi(force=False):
+    """The Node N-API addon (js/mtgpu.node) over libmtgpu.so, if node's headers are present."""
+    inc = '/usr/include/node'
+    src = os.path.join(JS, 'mtgpu_napi.c')
+    if not os.path.exists(os.path.join(inc, 'node_api.h')):
+        return None
+    if not force and os.path.exists(NAPI) and os.path.getmtime(NAPI) >= max(os.path.getmtime(src),
+                                                                            os.path.getmtime(LIB)):
+        return NAPI
+    subprocess.check_call(['gcc', '-O2', '-fPIC', '-shared', '-Wall', '-Wno-unused-parameter',
+                           '-DNODE_GYP_MODULE_NAME=mtgpu', f'-I{inc}', '-o', NAPI, src, f'-L{HERE}',
+                           '-l:libmtgpu.so', "-Wl,-rpath,$ORIGIN/../fluidframework_amd"])
+    return NAPI
+
+
 if __name__ == '__main__':
     build(force='-f' in sys.argv, verbose=True)
+    build_napi(force=True)
     print(LIB)

@@ -1,0 +1,265 @@
+"use strict";
+// batchClient.js -- the reference's op-apply surface over the MI355X engine (CommonJS, node 12).
+//
+// BatchClient mirrors the observer `Client` of packages/dds/merge-tree/src/client.ts:
+//   applyMsg(msg)                       client.ts:797-819   (queued; applied in device batches)
+//   startOrUpdateCollaboration(longId)  client.ts:1051-1071
+//   getLength() / getCurrentSeq()       client.ts:1042-1049
+// plus the TestClient helpers of src/test/testClient.ts:102-234 (getText, makeOpMessage,
+// insertTextRemote, removeRangeRemote, enqueueMsg, applyMessages).  Many BatchClients share one
+// BatchEngine (one MI355X); any read flushes every client's queued ops as ONE batched submit.
+// Only remote ops exist for an observer: a message carrying the client's own long id (an ack of
+// a local op) throws, as do markers, register ops and combining ops other than "rewrite".
+const path = require("path");
+
+const native = require(path.join(__dirname, "mtgpu.node"));
+
+const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
+const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4;
+const MAX_CLIENTS = 64, MAX_KEYS = 8, MAX_VALUES = 255;
+const REC = 32;
+
+class BatchEngine {
+    constructor(opts = {}) {
+        this.maxDocs = opts.maxDocs || 1;
+        this.handle = native.createEngine({
+            device: opts.device || 0, maxDocs: this.maxDocs, opsPerLaunch: opts.opsPerLaunch || 0,
+            segCapacity: opts.segCapacity || 0, textCapacity: opts.textCapacity || 0,
+        });
+        this.clients = [];
+        this.pending = 0;
+    }
+
+    createClient() {
+        if (this.clients.length >= this.maxDocs) throw new Error("BatchEngine: maxDocs reached");
+        const c = new BatchClient(this, this.clients.length);
+        this.clients.push(c);
+        return c;
+    }
+
+    _encode() {
+        const n = this.maxDocs;
+        const rowPtr = new Uint32Array(n + 1);
+        let nops = 0, nbytes = 0;
+        for (let d = 0; d < n; d++) {
+            const c = this.clients[d];
+            if (c) for (const r of c.queue) { nops++; nbytes += r.payload.length; }
+            rowPtr[d + 1] = nops;
+        }
+        const ops = Buffer.alloc(nops * REC);
+        const payload = Buffer.alloc(Math.max(1, nbytes));
+        let i = 0, off = 0;
+        for (let d = 0; d < n; d++) {
+            const c = this.clients[d];
+            if (!c) continue;
+            for (const r of c.queue) {
+                const o = i * REC;
+                ops.writeInt32LE(r.seq, o); ops.writeInt32LE(r.ref, o + 4); ops.writeInt32LE(r.msn, o + 8);
+                ops.writeUInt16LE(r.client, o + 12); ops.writeUInt8(r.type, o + 14);
+                ops.writeUInt8(r.flags | (r.npairs << 3), o + 15);
+                ops.writeInt32LE(r.pos1, o + 16); ops.writeInt32LE(r.pos2, o + 20);
+                ops.writeUInt32LE(off, o + 24); ops.writeUInt32LE(r.payload.length, o + 28);
+                r.payload.copy(payload, off);
+                off += r.payload.length;
+                i++;
+            }
+            c.queue = [];
+        }
+        this.pending = 0;
+        return { ops, payload, rowPtr };
+    }
+
+    /** Apply every queued op of every client (one device batch). */
+    flush() {
+        if (!this.pending) return;
+        const { ops, payload, rowPtr } = this._encode();
+        native.submit(this.handle, ops, payload, rowPtr);
+    }
+
+    /** The same as a Promise (napi_async_work): the JS thread stays free while the GPU applies. */
+    flushAsync() {
+        if (!this.pending) return Promise.resolve();
+        const b = this._encode();
+        return native.submitAsync(this.handle, b.ops, b.payload, b.rowPtr);
+    }
+}
+
+class BatchClient {
+    constructor(engine, doc) {
+        this.engine = engine;
+        this.doc = doc;
+        this.queue = [];
+        this.longClientId = undefined;
+        this.shortIds = new Map();      // long client id -> short id (client.ts:636-660)
+        this.longIds = [];
+        this.keyIds = new Map();        // property key -> id
+        this.keys = [];
+        this.valueIds = new Map();      // JSON(value) -> id
+        this.values = [undefined];
+        this.currentSeq = 0;
+        this.minSeq = 0;
+        this.msgQueue = [];
+    }
+
+    startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
+        if (this.longClientId !== undefined) throw new Error("BatchClient: collaboration already started");
+        this.longClientId = longClientId;
+        this._shortId(longClientId);    // the observer is short id 0 (client.ts:1057-1062)
+        this.currentSeq = currentSeq;
+        this.minSeq = minSeq;
+        if (minSeq || currentSeq) throw new Error("BatchClient: documents start empty at seq 0");
+    }
+
+    _shortId(longId) {
+        let id = this.shortIds.get(longId);
+        if (id === undefined) {
+            id = this.longIds.length;
+            if (id >= MAX_CLIENTS) throw new Error(`BatchClient: more than ${MAX_CLIENTS} client ids in one document`);
+            this.shortIds.set(longId, id);
+            this.longIds.push(longId);
+        }
+        return id;
+    }
+
+    _pairs(props) {
+        const out = [];
+        for (const k of Object.keys(props || {})) {
+            let kid = this.keyIds.get(k);
+            if (kid === undefined) {
+                kid = this.keys.length;
+                if (kid >= MAX_KEYS) throw new Error(`BatchClient: more than ${MAX_KEYS} property keys`);
+                this.keyIds.set(k, kid);
+                this.keys.push(k);
+            }
+            const v = props[k];
+            let vid = 0;
+            if (v !== null) {
+                if (typeof v === "object" || typeof v === "undefined" || (typeof v === "number" && isNaN(v))) {
+                    throw new Error("BatchClient: property values must be JSON primitives");
+                }
+                const key = JSON.stringify(v);
+                vid = this.valueIds.get(key);
+                if (vid === undefined) {
+                    vid = this.values.length;
+                    if (vid > MAX_VALUES) throw new Error(`BatchClient: more than ${MAX_VALUES} property values`);
+                    this.valueIds.set(key, vid);
+                    this.values.push(v);
+                }
+            }
+            out.push(kid, vid);
+        }
+        return out;
+    }
+
+    _record(msg, op, client, more) {
+        const r = { seq: msg.sequenceNumber, ref: msg.referenceSequenceNumber, msn: msg.minimumSequenceNumber,
+            client, type: NOOP, flags: more ? F_GROUP_MORE : 0, npairs: 0, pos1: 0, pos2: 0, payload: Buffer.alloc(0) };
+        if (!op) return r;
+        if (op.type === INSERT) {
+            if (op.register || op.relativePos1) throw new Error("BatchClient: register/relative inserts unsupported");
+            let text, pairs = [];
+            if (typeof op.seg === "string") text = op.seg;
+            else if (op.seg && typeof op.seg === "object" && "text" in op.seg) {
+                text = op.seg.text;
+                if (op.seg.props) { r.flags |= F_PROPS; pairs = this._pairs(op.seg.props); }
+            } else throw new Error("BatchClient: only text segments are supported (markers: SURVEY §8f)");
+            r.type = INSERT; r.pos1 = op.pos1;
+            r.npairs = pairs.length / 2;
+            r.payload = Buffer.concat([Buffer.from(text, "latin1"), Buffer.from(pairs)]);
+        } else if (op.type === REMOVE || op.type === ANNOTATE) {
+            if (op.relativePos1 || op.relativePos2 || op.register) throw new Error("BatchClient: unsupported op form");
+            r.type = op.type; r.pos1 = op.pos1; r.pos2 = op.pos2;
+            if (op.type === ANNOTATE) {
+                if (op.combiningOp) {
+                    if (op.combiningOp.name !== "rewrite") throw new Error("BatchClient: combining ops unsupported");
+                    r.flags |= F_REWRITE;
+                }
+                const pairs = this._pairs(op.props);
+                r.npairs = pairs.length / 2;
+                r.payload = Buffer.from(pairs);
+            }
+        } else {
+            throw new Error(`BatchClient: op type ${op.type} unsupported`);
+        }
+        return r;
+    }
+
+    /** Client.applyMsg (client.ts:797-819): queued, applied in the next device batch. */
+    applyMsg(msg) {
+        const client = this._shortId(msg.clientId);
+        if (msg.type === "op" && msg.clientId === this.longClientId) {
+            throw new Error("BatchClient: acks of local ops are not supported by the observer engine");
+        }
+        const op = msg.type === "op" ? msg.contents : undefined;
+        if (op && op.type === GROUP) {
+            op.ops.forEach((m, i) => this.queue.push(this._record(msg, m, client, i + 1 < op.ops.length)));
+            this.engine.pending += op.ops.length;
+        } else {
+            this.queue.push(this._record(msg, op, client, false));
+            this.engine.pending++;
+        }
+        this.currentSeq = msg.sequenceNumber;
+        this.minSeq = Math.max(this.minSeq, msg.minimumSequenceNumber);
+    }
+
+    _checkError() {
+        const [code, seq] = native.docError(this.engine.handle, this.doc);
+        if (code) {
+            const msgs = { 1: "Incoming remote op sequence# <= local collabWindow's currentSequence#",
+                2: "Incoming remote op minSequence# < local collabWindow's minSequence#", 3: "MergeTree insert failed",
+                4: "device capacity exceeded", 5: "text arena exhausted", 6: "id limits exceeded", 7: "malformed op" };
+            throw new Error(`${msgs[code] || code} (seq ${seq})`);
+        }
+    }
+
+    getText() { this.engine.flush(); this._checkError(); return native.getText(this.engine.handle, this.doc); }
+    getLength() { this.engine.flush(); this._checkError(); return native.getLength(this.engine.handle, this.doc); }
+    getCurrentSeq() { return this.currentSeq; }
+    getClientId() { return 0; }
+    getLongClientId(id) { return this.longIds[id]; }
+
+    /** Canonical state with long client ids and original property keys/values. */
+    getState() {
+        this.engine.flush();
+        const st = JSON.parse(native.getState(this.engine.handle, this.doc));
+        for (const s of st.segs) {
+            s[2] = this.longIds[s[2]];
+            if (s[4] !== -1) s[4] = this.longIds[s[4]];
+            s[5] = s[5].map((x) => this.longIds[x]);
+            if (s[6]) {
+                const p = {};
+                for (const k of Object.keys(s[6])) p[this.keys[parseInt(k.slice(1), 10)]] = this.values[s[6][k]];
+                s[6] = p;
+            }
+        }
+        return st;
+    }
+
+    // ---- TestClient helpers (src/test/testClient.ts:112-234) --------------------------------
+    makeOpMessage(op, seq = -1, refSeq = this.currentSeq, longClientId, minSeqNumber = 0) {
+        return { clientId: longClientId === undefined ? this.longClientId : longClientId, clientSequenceNumber: 1,
+            contents: op, metadata: undefined, minimumSequenceNumber: minSeqNumber, origin: null,
+            referenceSequenceNumber: refSeq, sequenceNumber: seq, timestamp: Date.now(), term: 1, traces: [],
+            type: "op" };
+    }
+    insertTextRemote(pos, text, props, seq, refSeq, longClientId) {
+        const seg = props ? { text, props } : text;
+        this.applyMsg(this.makeOpMessage({ type: INSERT, pos1: pos, seg }, seq, refSeq, longClientId));
+    }
+    removeRangeRemote(start, end, seq, refSeq, longClientId) {
+        this.applyMsg(this.makeOpMessage({ type: REMOVE, pos1: start, pos2: end }, seq, refSeq, longClientId));
+    }
+    enqueueMsg(msg) { this.msgQueue.push(msg); }
+    dequeueMsg() { return this.msgQueue.shift(); }
+    getMessageCount() { return this.msgQueue.length; }
+    applyMessages(msgCount) {
+        for (let n = msgCount; n > 0; n--) {
+            const m = this.msgQueue.shift();
+            if (!m) break;
+            this.applyMsg(m);
+        }
+        return true;
+    }
+}
+
+module.exports = { BatchEngine, BatchClient, native };

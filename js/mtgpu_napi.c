@@ -1,0 +1,277 @@
+/* mtgpu_napi.c -- Node N-API addon over the C-ABI of libmtgpu.so (include/mtgpu.h).
+ * Plain C, N-API 8 (node 12+).  js/batchClient.js is the JavaScript surface above it. */
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mtgpu.h"
+
+#define NAPI_CALL(env, call)                                                   \
+    do {                                                                       \
+        if ((call) != napi_ok) {                                               \
+            napi_throw_error((env), NULL, "N-API call failed: " #call);        \
+            return NULL;                                                       \
+        }                                                                      \
+    } while (0)
+
+static napi_value throw_status(napi_env env, const char* what, mt_status st) {
+    char buf[160];
+    static const char* names[] = {"ok", "bad argument", "HIP error", "out of device memory", "bad state",
+                                  "document error"};
+    snprintf(buf, sizeof buf, "%s: %s", what, (unsigned)st < 6 ? names[st] : "unknown");
+    napi_throw_error(env, NULL, buf);
+    return NULL;
+}
+
+static mt_engine* get_engine(napi_env env, napi_value v) {
+    void* p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+    return (mt_engine*)p;
+}
+
+static void finalize_engine(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    if (data) mt_engine_destroy((mt_engine*)data);
+}
+
+static uint32_t get_u32(napi_env env, napi_value obj, const char* key, uint32_t dflt) {
+    napi_value v;
+    bool has = false;
+    uint32_t out = dflt;
+    if (napi_has_named_property(env, obj, key, &has) == napi_ok && has &&
+        napi_get_named_property(env, obj, key, &v) == napi_ok) {
+        napi_valuetype t;
+        napi_typeof(env, v, &t);
+        if (t == napi_number) napi_get_value_uint32(env, v, &out);
+    }
+    return out;
+}
+
+/* createEngine({device, maxDocs, segCapacity, textCapacity, heapCapacity, opsPerLaunch}) */
+static napi_value create_engine(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    mt_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.device = (int32_t)get_u32(env, argv[0], "device", 0);
+    cfg.max_docs = get_u32(env, argv[0], "maxDocs", 1);
+    cfg.seg_capacity = get_u32(env, argv[0], "segCapacity", 0);
+    cfg.text_capacity = get_u32(env, argv[0], "textCapacity", 0);
+    cfg.heap_capacity = get_u32(env, argv[0], "heapCapacity", 0);
+    cfg.ops_per_launch = get_u32(env, argv[0], "opsPerLaunch", 0);
+    mt_engine* e = NULL;
+    mt_status st = mt_engine_create(&cfg, &e);
+    if (st) return throw_status(env, "mt_engine_create", st);
+    st = mt_docs_init(e, cfg.max_docs);
+    if (st) {
+        mt_engine_destroy(e);
+        return throw_status(env, "mt_docs_init", st);
+    }
+    NAPI_CALL(env, napi_create_external(env, e, finalize_engine, NULL, &out));
+    return out;
+}
+
+static void* buffer_data(napi_env env, napi_value v, size_t* len) {
+    void* data = NULL;
+    bool is_buf = false, is_ta = false;
+    *len = 0;
+    if (napi_is_buffer(env, v, &is_buf) == napi_ok && is_buf) {
+        napi_get_buffer_info(env, v, &data, len);
+        return data;
+    }
+    if (napi_is_typedarray(env, v, &is_ta) == napi_ok && is_ta) {
+        napi_typedarray_type t;
+        size_t n, off;
+        napi_value ab;
+        napi_get_typedarray_info(env, v, &t, &n, &data, &ab, &off);
+        size_t el = (t == napi_uint32_array || t == napi_int32_array || t == napi_float32_array) ? 4
+                    : (t == napi_uint16_array || t == napi_int16_array) ? 2
+                    : (t == napi_float64_array || t == napi_bigint64_array || t == napi_biguint64_array) ? 8 : 1;
+        *len = n * el;
+        return data;
+    }
+    return NULL;
+}
+
+/* submit(engine, opsU8 (32-byte mt_op_rec rows), payloadU8, rowPtrU32): the batched applyMsg */
+static napi_value submit(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    mt_engine* e = get_engine(env, argv[0]);
+    size_t nops, npay, nrow;
+    const void* ops = buffer_data(env, argv[1], &nops);
+    const void* pay = buffer_data(env, argv[2], &npay);
+    const void* row = buffer_data(env, argv[3], &nrow);
+    if (!e || (!ops && nops) || !row) {
+        napi_throw_type_error(env, NULL, "submit(engine, ops, payload, rowPtr)");
+        return NULL;
+    }
+    mt_status st = mt_submit(e, (const mt_op_rec*)ops, nops / sizeof(mt_op_rec), (const uint8_t*)pay, npay,
+                             (const uint32_t*)row);
+    if (st) return throw_status(env, "mt_submit", st);
+    return NULL;
+}
+
+/* submitAsync: the same on a libuv worker thread (napi_async_work); returns a Promise.  The
+ * caller keeps the buffers alive until it settles. */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref refs[3];
+    mt_engine* e;
+    const void* ops;
+    const void* pay;
+    const void* row;
+    size_t nops, npay;
+    mt_status st;
+} submit_job;
+
+static void submit_execute(napi_env env, void* data) {
+    (void)env;
+    submit_job* j = (submit_job*)data;
+    j->st = mt_submit(j->e, (const mt_op_rec*)j->ops, j->nops / sizeof(mt_op_rec), (const uint8_t*)j->pay, j->npay,
+                      (const uint32_t*)j->row);
+}
+
+static void submit_complete(napi_env env, napi_status status, void* data) {
+    submit_job* j = (submit_job*)data;
+    napi_value v;
+    if (status == napi_ok && j->st == MT_OK) {
+        napi_get_undefined(env, &v);
+        napi_resolve_deferred(env, j->deferred, v);
+    } else {
+        napi_value msg;
+        napi_create_string_utf8(env, "mt_submit failed", NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &v);
+        napi_reject_deferred(env, j->deferred, v);
+    }
+    for (int i = 0; i < 3; i++) napi_delete_reference(env, j->refs[i]);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+static napi_value submit_async(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4], promise, name;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    submit_job* j = (submit_job*)calloc(1, sizeof *j);
+    j->e = get_engine(env, argv[0]);
+    j->ops = buffer_data(env, argv[1], &j->nops);
+    j->pay = buffer_data(env, argv[2], &j->npay);
+    size_t nrow;
+    j->row = buffer_data(env, argv[3], &nrow);
+    if (!j->e || !j->row) {
+        free(j);
+        napi_throw_type_error(env, NULL, "submitAsync(engine, ops, payload, rowPtr)");
+        return NULL;
+    }
+    for (int i = 0; i < 3; i++) napi_create_reference(env, argv[1 + i], 1, &j->refs[i]);
+    NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+    NAPI_CALL(env, napi_create_string_utf8(env, "mtgpu.submit", NAPI_AUTO_LENGTH, &name));
+    NAPI_CALL(env, napi_create_async_work(env, NULL, name, submit_execute, submit_complete, j, &j->work));
+    NAPI_CALL(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+typedef mt_status (*string_fn)(mt_engine*, uint32_t, char*, uint64_t, uint64_t*);
+
+static napi_value get_string(napi_env env, napi_callback_info info, string_fn fn, const char* what) {
+    size_t argc = 2;
+    napi_value argv[2], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    mt_engine* e = get_engine(env, argv[0]);
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    uint64_t n = 0;
+    mt_status st = fn(e, doc, NULL, 0, &n);
+    if (st) return throw_status(env, what, st);
+    char* buf = (char*)malloc(n + 1);
+    st = fn(e, doc, buf, n + 1, &n);
+    if (st) {
+        free(buf);
+        return throw_status(env, what, st);
+    }
+    napi_status ns = napi_create_string_latin1(env, buf, n, &out);
+    free(buf);
+    NAPI_CALL(env, ns);
+    return out;
+}
+
+static napi_value get_text(napi_env env, napi_callback_info info) {
+    return get_string(env, info, mt_get_text, "mt_get_text");
+}
+static napi_value get_state(napi_env env, napi_callback_info info) {
+    return get_string(env, info, mt_get_state, "mt_get_state");
+}
+
+static napi_value get_length(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t doc = 0, len = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    mt_status st = mt_get_length(get_engine(env, argv[0]), doc, &len);
+    if (st) return throw_status(env, "mt_get_length", st);
+    NAPI_CALL(env, napi_create_uint32(env, len, &out));
+    return out;
+}
+
+static napi_value doc_error(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out, a, b;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t doc = 0;
+    int32_t code = 0, seq = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    mt_status st = mt_doc_error(get_engine(env, argv[0]), doc, &code, &seq);
+    if (st) return throw_status(env, "mt_doc_error", st);
+    NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
+    NAPI_CALL(env, napi_create_int32(env, code, &a));
+    NAPI_CALL(env, napi_create_int32(env, seq, &b));
+    NAPI_CALL(env, napi_set_element(env, out, 0, a));
+    NAPI_CALL(env, napi_set_element(env, out, 1, b));
+    return out;
+}
+
+/* checksums(engine, nDocs) -> Buffer of nDocs little-endian u64 */
+static napi_value checksums(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t n = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &n));
+    void* data = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, (size_t)n * 8, &data, &out));
+    mt_status st = mt_checksums(get_engine(env, argv[0]), (uint64_t*)data, n);
+    if (st) return throw_status(env, "mt_checksums", st);
+    return out;
+}
+
+static napi_value version(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value out;
+    NAPI_CALL(env, napi_create_string_utf8(env, mt_version(), NAPI_AUTO_LENGTH, &out));
+    return out;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    napi_property_descriptor d[] = {
+        {"createEngine", NULL, create_engine, NULL, NULL, NULL, napi_default, NULL},
+        {"submit", NULL, submit, NULL, NULL, NULL, napi_default, NULL},
+        {"submitAsync", NULL, submit_async, NULL, NULL, NULL, napi_default, NULL},
+        {"getText", NULL, get_text, NULL, NULL, NULL, napi_default, NULL},
+        {"getState", NULL, get_state, NULL, NULL, NULL, napi_default, NULL},
+        {"getLength", NULL, get_length, NULL, NULL, NULL, napi_default, NULL},
+        {"docError", NULL, doc_error, NULL, NULL, NULL, napi_default, NULL},
+        {"checksums", NULL, checksums, NULL, NULL, NULL, napi_default, NULL},
+        {"version", NULL, version, NULL, NULL, NULL, napi_default, NULL},
+    };
+    napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

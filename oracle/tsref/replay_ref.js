@@ -16,83 +16,7 @@ const { Client } = require(path.join(ROOT, "client.js"));
 const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
 const { MergeTree } = require(path.join(ROOT, "mergeTree.js"));
 
-function loadLog(file) {
-    const buf = fs.readFileSync(file);
-    if (buf.toString("latin1", 0, 8) !== "MTLOG001") throw new Error("not an MTLOG file");
-    const nDocs = buf.readUInt32LE(8);
-    const nOps = Number(buf.readBigUInt64LE(16));
-    const nBytes = Number(buf.readBigUInt64LE(24));
-    let off = 32;
-    const rowPtr = new Uint32Array(nDocs + 1);
-    for (let i = 0; i <= nDocs; i++) rowPtr[i] = buf.readUInt32LE(off + 4 * i);
-    off += 4 * (nDocs + 1);
-    const opsOff = off;
-    const payOff = off + 32 * nOps;
-    return { buf, nDocs, nOps, nBytes, rowPtr, opsOff, payOff };
-}
-
-function readOp(log, i) {
-    const b = log.buf, o = log.opsOff + 32 * i;
-    return {
-        seq: b.readInt32LE(o), ref: b.readInt32LE(o + 4), msn: b.readInt32LE(o + 8),
-        client: b.readUInt16LE(o + 12), type: b.readUInt8(o + 14), flags: b.readUInt8(o + 15),
-        pos1: b.readInt32LE(o + 16), pos2: b.readInt32LE(o + 20),
-        poff: b.readUInt32LE(o + 24), plen: b.readUInt32LE(o + 28),
-    };
-}
-
-function propsOf(log, r) {
-    const np = r.flags >> 3;
-    const start = log.payOff + r.poff + r.plen - 2 * np;
-    const props = {};
-    for (let q = 0; q < np; q++) {
-        const k = log.buf.readUInt8(start + 2 * q), v = log.buf.readUInt8(start + 2 * q + 1);
-        props["k" + k] = v === 0 ? null : v;
-    }
-    return props;
-}
-
-// op record -> IMergeTreeOp JSON (ops.ts:63-110; opBuilder.ts:49-134)
-function toOp(log, r) {
-    const np = r.flags >> 3;
-    if (r.type === 0) {
-        const text = log.buf.toString("latin1", log.payOff + r.poff, log.payOff + r.poff + r.plen - 2 * np);
-        const seg = (r.flags & 2) ? { text, props: propsOf(log, r) } : text;
-        return { type: 0, pos1: r.pos1, seg };
-    }
-    if (r.type === 1) return { type: 1, pos1: r.pos1, pos2: r.pos2 };
-    if (r.type === 2) {
-        const op = { type: 2, pos1: r.pos1, pos2: r.pos2, props: propsOf(log, r) };
-        if (r.flags & 1) op.combiningOp = { name: "rewrite" };
-        return op;
-    }
-    return undefined;
-}
-
-function* messages(log, d) {
-    let group = null;
-    for (let i = log.rowPtr[d]; i < log.rowPtr[d + 1]; i++) {
-        const r = readOp(log, i);
-        const op = toOp(log, r);
-        if (group || (r.flags & 4)) {
-            if (!group) group = { r, ops: [] };
-            if (op) group.ops.push(op);
-            if (r.flags & 4) continue;
-            const g = group; group = null;
-            yield msgOf(g.r, { type: 3, ops: g.ops });
-            continue;
-        }
-        yield msgOf(r, op);
-    }
-}
-
-function msgOf(r, op) {
-    return {
-        clientId: "c" + r.client, clientSequenceNumber: 1, contents: op, metadata: undefined,
-        minimumSequenceNumber: r.msn, origin: undefined, referenceSequenceNumber: r.ref,
-        sequenceNumber: r.seq, timestamp: 0, term: 1, traces: [], type: op ? "op" : "noop",
-    };
-}
+const { loadLog, messages } = require(path.join(__dirname, "..", "..", "js", "mtlog.js"));
 
 function specToSegment(spec) { return TextSegment.fromJSONObject(spec); }
 

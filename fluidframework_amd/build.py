@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libmtgpu.so')
-SOURCES = ['mt_apply.hip', 'mt_service.hip', 'mt_synth.hip', 'mt_engine.cpp']
+SOURCES = ['mt_apply.hip', 'mt_apply_reg.hip', 'mt_service.hip', 'mt_engine.cpp']
 HEADERS = ['mt_state.h', 'mt_wave.h', 'mt_checksum.h', 'mt_synth.h', '../../include/mtgpu.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
@@ -20,17 +20,32 @@ def needs_build():
                if os.path.exists(os.path.join(CSRC, f)))
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
+def build(force=False, verbose=False, prof=False):
+    """Compile every source to an object in parallel (hipcc, gfx950), then link libmtgpu.so.
+    prof=True builds the diagnostic libmtgpu_prof.so (-DMT_PROF per-phase cycle stamps)."""
+    lib = LIB.replace('libmtgpu.so', 'libmtgpu_prof.so') if prof else LIB
+    if not prof and not force and not needs_build():
         return LIB
-    srcs = [os.path.join(CSRC, f) for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
-    cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall',
-           '-Wno-unused-function', '-o', LIB + '.tmp'] + srcs
-    if verbose:
-        print(' '.join(cmd))
-    subprocess.check_call(cmd)
-    os.replace(LIB + '.tmp', LIB)
-    return LIB
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(HERE, 'build')
+    os.makedirs(objdir, exist_ok=True)
+    srcs = [f for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
+    flags = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
+             '-Wno-unused-result']
+
+    def cc(f):
+        obj = os.path.join(objdir, f + ('.prof.o' if prof else '.o'))
+        cmd = [HIPCC] + flags + (['-DMT_PROF'] if prof else []) + ['-c', os.path.join(CSRC, f), '-o', obj]
+        if verbose:
+            print(' '.join(cmd))
+        subprocess.check_call(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
+        objs = list(ex.map(cc, srcs))
+    subprocess.check_call([HIPCC, f'--offload-arch={ARCH}', '-shared', '-o', lib + '.tmp'] + objs)
+    os.replace(lib + '.tmp', lib)
+    return lib
 
 
 JS = os.path.join(os.path.dirname(HERE), 'js')
@@ -53,6 +68,9 @@ def build_napi(force=False):
 
 
 if __name__ == '__main__':
+    if '--prof' in sys.argv:
+        print(build(prof=True, verbose=True))
+        sys.exit(0)
     build(force='-f' in sys.argv, verbose=True)
     build_napi(force=True)
     print(LIB)

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -20,6 +21,9 @@
 extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
                                       const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
                                       uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
+extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                          const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                          uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
@@ -69,7 +73,11 @@ struct mt_engine {
     std::vector<int> kev_cls;
     uint32_t last_launches = 0;
     uint64_t last_bytes = 0;
+    // register-resident engine (mt_apply_reg.hip) for classes up to kRegMaxCap segments; the
+    // LDS engine (mt_apply.hip) above that, or everywhere with MTGPU_ENGINE=lds
+    bool use_reg = true;
 };
+static constexpr int32_t kRegMaxCap = 1024;
 
 #define HIP_OK(x)                                                                                            \
     do {                                                                                                     \
@@ -130,6 +138,11 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         return MT_ERR_HIP;
     }
     HIP_OK(hipMemcpy(e->d_classes, kClassParams, sizeof(kClassParams), hipMemcpyHostToDevice));
+    {
+        const char* v = getenv("MTGPU_ENGINE");
+        // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
+        e->use_reg = !(v && strcmp(v, "lds") == 0) && e->cfg.text_capacity <= 65536;
+    }
     *out = e;
     return MT_OK;
 }
@@ -235,8 +248,12 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
-            HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
-                                   e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
+            if (e->use_reg && kClasses[c] <= kRegMaxCap)
+                HIP_OK(mt_launch_apply_reg(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                           e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
+            else
+                HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                       e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
             e->kev_cls.push_back(c);
             nk++;

@@ -13,7 +13,7 @@ import numpy as np
 from .oplog import OpBatch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libmtgpu.so')
+LIB_PATH = os.environ.get('MTGPU_LIB') or os.path.join(HERE, 'libmtgpu.so')
 
 MT_ERRORS = {0: 'ok', 1: 'bad argument', 2: 'HIP error', 3: 'out of device memory', 4: 'bad state',
              5: 'document error'}
@@ -194,12 +194,19 @@ class MergeEngine:
     def last_class_stats(self):
         """[(capacity, kernel_ms, launches, alg_bytes)] per LDS capacity class of the last apply."""
         out = []
-        for c in range(5):
+        for c in range(32):  # classes 0.. until the library reports MT_ERR_ARG
             cap, ms, n, nb = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
-            _check(lib().mt_last_apply_class_stats(self.h, c, ctypes.byref(cap), ctypes.byref(ms), ctypes.byref(n),
-                                                   ctypes.byref(nb)), 'mt_last_apply_class_stats')
+            if lib().mt_last_apply_class_stats(self.h, c, ctypes.byref(cap), ctypes.byref(ms), ctypes.byref(n),
+                                               ctypes.byref(nb)) != 0:
+                break
             out.append((cap.value, ms.value, n.value, nb.value))
         return out
+
+    def class_kernel(self, capacity):
+        """Kernel symbol (as rocprof names it) that applies documents of a capacity class."""
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().mt_class_kernel_name(self.h, capacity, buf, 128), 'mt_class_kernel_name')
+        return buf.value.decode()
 
     # -- readout -------------------------------------------------------------------------
     def checksums(self):

@@ -164,7 +164,7 @@ def main():
             'roofline': {
                 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                'kernel': f'mt::apply_kernel<{dom}, false>', 'launches': d_n,
+                'kernel': eng.class_kernel(dom), 'launches': d_n,
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
                 'all_apply_kernels': {'launches': launches, 'kernel_ms': round(kern_ms, 2),
                                       'achieved_GBps': round(all_achieved, 1),

@@ -998,10 +998,13 @@ struct Wave {
         }
         wave_sync();
         const size_t lo = (size_t)d * g.lbcap;
+        int nempty = 0;
         for (int i = lane; i < min(s.nb[0], (int)g.lbcap); i += 64) {
             g.lbcnt[lo + i] = s.lbcnt[i];
             g.lbscour[lo + i] = s.lbscour[i];
+            nempty += s.lbcnt[i] == 0 ? 1 : 0;
         }
+        nempty = wave_sum(nempty);
         for (int L = 1; L < s.nlev; L++) {
             const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
             for (int i = lane; i < min(s.nb[L], (int)g.ibcap); i += 64) g.ibcnt[io + i] = s.ibcnt[L - 1][i];
@@ -1024,6 +1027,7 @@ struct Wave {
             sc.err_seq = s.err_seq;
             sc.text_top = s.text_top;
             sc.text_half = s.text_half;
+            sc.n_empty = (uint32_t)nempty;
         }
     }
 };

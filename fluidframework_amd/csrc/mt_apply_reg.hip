@@ -1,23 +1,27 @@
 // mt_apply_reg.hip -- register-resident merge-tree apply engine for gfx950 (CDNA4).
 //
 // Same semantics as mt_apply.hip (the observer Client.applyMsg of the reference,
-// client.ts:797-828, bit-exact) with a different placement of the document state:
+// client.ts:797-828, bit-exact); a different home for the document state:
 //
-//   * the hot per-segment fields live in VGPRs, BLOCKED by lane: segment i of the document is
-//     register slot j = i % K of lane i / K (K = CAP / 64).  Visibility for an op's (refSeq,
-//     client) view (mergeTree.ts:1667-1697) is then K independent per-lane evaluations plus ONE
-//     wave-wide DPP scan -- the whole PartialSequenceLengths query (partialLengths.ts:433-487)
-//     costs ~K VALU ops per lane and no LDS traffic;
-//   * inserting a segment at document position p (a split, an insert) moves every later segment
-//     one slot: K predicated moves per field per lane, with the lane-crossing element carried
-//     by DPP wave_shr:1 (wave_shl:1 for an unlink);
-//   * cold per-segment fields (property set, text offset) stay in LDS indexed by a segment id
-//     that never changes while the segment is linked, so they never move; the B-tree shape
-//     (leaf/interior child counts, needsScour), the zamboni heap and small scratch are in LDS
-//     exactly as in mt_apply.hip.
-// Register budget sets the capacity classes: K = 2, 4, 8, 16 (128..1024 segments).  Documents
-// beyond 1024 segments run on mt_apply.hip's LDS engine (CAP 2048).  HBM layout (mt_state.h)
-// is shared by both engines, so documents move freely between classes from launch to launch.
+//   * every per-segment field the op path touches lives in VGPRs, BLOCKED by lane: slot i of
+//     the document is register j = i % K of lane i / K (K = CAP / 64).  The visibility of every
+//     segment for an op's (refSeq, client) view (mergeTree.ts:1667-1697) is K per-lane
+//     evaluations plus one wave-wide DPP scan: the PartialSequenceLengths query
+//     (partialLengths.ts:433-487) without any memory traffic;
+//   * the leaf level of the B-tree lives in the same registers: the slot that starts a leaf
+//     block carries a BS bit and that block's needsScour state, so "which leaf block holds slot
+//     k", "where does block b start" and "how many children has it" are ballot / popcount / DPP
+//     questions, not LDS walks.  Interior levels (touched only by leaf splits and packs) are
+//     child-count arrays in LDS, as in mt_apply.hip;
+//   * a zamboni unlink (mergeTree.ts:1289-1365) only marks its slot DEAD (zero length, no child
+//     of any block); dead slots are squeezed out when the document is written back, so nothing
+//     moves on an unlink.  An insert or a split moves the later slots one register to the right
+//     (K predicated moves per field per lane, DPP wave_shr:1 across lanes);
+//   * cold fields (property set, text offset) stay in LDS indexed by a segment id that never
+//     changes while the segment is linked; the zamboni heap holds those ids.
+// Capacity classes K = 2, 4, 8, 12, 16 (128..1024 slots).  Bigger documents, and documents that
+// ever see a client id above 32 (the register overlap set is 32 bits wide), run on mt_apply.hip's
+// LDS engine; both engines share the HBM layout of mt_state.h.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,14 +33,21 @@ namespace mtr {
 
 constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
+constexpr int kNarrowClients = 32;     // register overlap set: clients 1..32 at bit C-1
 constexpr uint32_t kLenBits = 17;      // li = len | id << 17  (len <= textcap <= 65536)
 constexpr uint32_t kLenMask = (1u << kLenBits) - 1;
-constexpr uint32_t kNoId = 0x7FFFu;    // id of an unused register slot
+constexpr uint32_t kNoId = 0x7FFFu;    // id of a padding slot
 constexpr uint32_t kEmptyLi = kNoId << kLenBits;
-constexpr uint32_t kEmptyCf = 0xFFu;   // client 255: never an op's client, len 0 -> invisible
+// cf = client (bits 0-7) | removedClientId (8-15) | segment flags (16-23) | leaf-block bits (24-31)
 constexpr uint32_t F_RM = (uint32_t)MT_SF_REMOVED << 16;
 constexpr uint32_t F_PDEF = (uint32_t)MT_SF_PDEF << 16;
 constexpr uint32_t F_NL = (uint32_t)MT_SF_NL << 16;
+constexpr uint32_t F_DEAD = 8u << 16;    // unlinked or padding: not a child of any block
+constexpr uint32_t F_BS = 1u << 24;      // first slot of a leaf block
+constexpr uint32_t SC_SHIFT = 25;        // that block's needsScour (MT_SC_*), kept on its first slot
+constexpr uint32_t SC_MASK = 3u << SC_SHIFT;
+constexpr uint32_t BLK_MASK = F_BS | SC_MASK;
+constexpr uint32_t kEmptyCf = 0xFFu | F_DEAD;  // client 255 never matches, length 0, dead
 constexpr uint16_t kDead = 0xFFFFu;
 
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -45,10 +56,13 @@ MT_DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstla
 MT_DEV int shr1(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false); }
 // lane l <- lane l+1 (lane 63 <- fill)
 MT_DEV int shl1(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false); }
+MT_DEV int wave_total(int v) { return wave_last(wave_incl_scan(v)); }
 
 // ---- optional per-phase cycle accounting (diagnostic build: -DMT_PROF; never in the product)
+enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, P_OPS, P_ZPOP, P_REPACK,
+       P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT, P_NSLOT };
 #ifdef MT_PROF
-__device__ unsigned long long mt_prof_acc[96];  // [class 0..3][24 slots]
+__device__ unsigned long long mt_prof_acc[120];  // [class 0..4][24 slots]
 MT_DEV uint64_t prof_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -58,15 +72,10 @@ MT_DEV uint64_t prof_now() {
 }
 #define PROF_BEGIN(v) const uint64_t v = prof_now()
 #define PROF_END(arr, slot, v) arr[slot] += prof_now() - (v)
+#define PROF_CNT(slot, v) prof[slot] += (v)
 #else
 #define PROF_BEGIN(v)
 #define PROF_END(arr, slot, v)
-#endif
-enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, P_OPS, P_ZPOP, P_REPACK,
-       P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT, P_NSLOT };
-#ifdef MT_PROF
-#define PROF_CNT(slot, v) prof[slot] += (v)
-#else
 #define PROF_CNT(slot, v)
 #endif
 
@@ -77,23 +86,20 @@ struct RLds {
     static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
     static constexpr int H = CAP / 2 + 64;  // heap entries (1-based)
     uint64_t props[CAP];    // by segment id: 8 keys x u8 value id
-    int32_t pcum[CAP];      // by position: spilled inclusive visible prefix (scratch)
-    int32_t bst[LB + 1];    // scratch: leaf-block start positions
+    int32_t scr[CAP + 1];   // scratch by slot / position / leaf block (load, store, compaction)
     int32_t hseq[H];
     uint16_t toff[CAP];     // by segment id: text view offset (at store: id -> position)
-    uint16_t pid[CAP];      // by position: spilled segment ids (scratch)
-    uint16_t hslot[H];      // heap entry -> segment id (kDead once unlinked)
-    uint8_t lbcnt[LB];
-    uint8_t lbscour[LB];
-    uint8_t ibcnt[MT_MAXLEV - 1][IB];
-    int32_t nb[MT_MAXLEV];
-    int32_t zseq[kMaxNodes + 1], zrseq[kMaxNodes + 1];   // scour scratch: one leaf block
-    uint32_t zli[kMaxNodes + 1], zcf[kMaxNodes + 1];
+    uint16_t hslot[H];      // heap entry -> segment id
+    uint8_t ibcnt[MT_MAXLEV - 1][IB];  // interior levels: level L's child counts in ibcnt[L - 1]
+    uint8_t lbsc[LB + 1];   // store staging: needsScour per leaf block
+    int32_t nb[MT_MAXLEV];  // blocks per interior level (leaf blocks are counted by BS bits)
+    int32_t zseq[kMaxNodes], zrseq[kMaxNodes], zslot[kMaxNodes];  // scour scratch: live children
+    uint32_t zli[kMaxNodes], zcf[kMaxNodes];
 };
 
 struct Elem {
     int32_t seq, rseq;
-    uint32_t li, cf, o0, o1;
+    uint32_t li, cf, ov;
     int32_t cum;
 };
 
@@ -101,27 +107,34 @@ template <int K>
 struct RWave {
     using L = RLds<K>;
     static constexpr int CAP = L::CAP;
+    static constexpr uint32_t kAll = (1u << K) - 1u;
+    // clang ext vectors: SSA values end to end, never a private-memory array
+    typedef int32_t VI __attribute__((ext_vector_type(K)));
+    typedef uint32_t VU __attribute__((ext_vector_type(K)));
+    typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t U2 __attribute__((ext_vector_type(2)));
     L& s;
     const int lane;
     uint8_t* const abase;
     uint8_t* arena;
     const uint32_t textcap;
 
-    // ---- document state in registers (blocked: element i = lane * K + j)
-    // (clang ext vectors: SSA values end to end, never a private-memory array)
-    typedef int32_t VI __attribute__((ext_vector_type(K)));
-    typedef uint32_t VU __attribute__((ext_vector_type(K)));
-    VI seq, rseq;
-    VU li, cf, o0, o1;
-    VI cum;   // per-op scratch: inclusive visible prefix for the op's view
+    // ---- document state in registers (blocked: slot i = lane * K + j).  Plain arrays that SROA
+    // splits into K independent SSA values each (every index is a constant after unrolling;
+    // element updates are selects, never a store on one branch, so no pointer phis).
+    int32_t seq[K], rseq[K];
+    uint32_t li[K], cf[K], ov[K];
+    int32_t cum[K];  // per-op scratch: inclusive visible prefix for the op's view
     // ---- uniform document scalars
-    int n, nlev, heap_n, cur_seq, min_seq, err, err_seq, next_id;
+    int ns, nlive, nb0, nlev, heap_n, cur_seq, min_seq, err, err_seq, next_id;
     uint32_t text_top, text_half;
+    bool dirty;  // arena stores issued and not yet waited for
 #ifdef MT_PROF
     uint64_t prof[P_NSLOT] = {};
 #endif
 
-    MT_DEV RWave(L& lds, uint8_t* a, uint32_t tc) : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc) {}
+    MT_DEV RWave(L& lds, uint8_t* a, uint32_t tc)
+        : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc), dirty(false) {}
 
     MT_DEV int idx(int j) const { return lane * K + j; }
 
@@ -131,122 +144,145 @@ struct RWave {
             err_seq = sq;
         }
     }
-
-    // ------------------------------------------------------------ element access
     MT_DEV static uint32_t len_of(uint32_t l) { return l & kLenMask; }
     MT_DEV static uint32_t id_of(uint32_t l) { return l >> kLenBits; }
 
-    // all fields of the element at uniform position k
-    MT_DEV Elem get(int k) const {
-        const int lk = k / K, jk = k % K;
-        int32_t a = seq[0], b = rseq[0], g = cum[0];
-        uint32_t c = li[0], d = cf[0], e = o0[0], f = o1[0];
+    // ------------------------------------------------------------ slot masks
+    MT_DEV uint32_t bs_bits() const {
+        uint32_t m = 0;
 #pragma unroll
-        for (int j = 1; j < K; j++) {
-            if (jk == j) {
-                a = seq[j];
-                b = rseq[j];
-                c = li[j];
-                d = cf[j];
-                e = o0[j];
-                f = o1[j];
-                g = cum[j];
-            }
+        for (int j = 0; j < K; j++) m |= (cf[j] & F_BS) ? (1u << j) : 0u;
+        return m;
+    }
+    MT_DEV uint32_t live_bits() const {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) m |= (cf[j] & F_DEAD) ? 0u : (1u << j);
+        return m;
+    }
+    // this lane's slots with index < k
+    MT_DEV uint32_t below(int k) const {
+        const int r = k - lane * K;
+        return r <= 0 ? 0u : (r >= K ? kAll : ((1u << r) - 1u));
+    }
+    // slot of the r-th (0-based) set bit of the lanes' masks m; -1 if there is none
+    MT_DEV int nth_slot(uint32_t m, int r) const {
+        const int c = __popc(m);
+        const int incl = wave_incl_scan(c);
+        const uint64_t hit = wave_ballot(r >= incl - c && r < incl);
+        if (!hit) return -1;
+        const int lk = first_lane(hit);
+        uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, lk);
+        for (int q = r - __builtin_amdgcn_readlane(incl - c, lk); q > 0; q--) mm &= mm - 1;
+        return lk * K + (int)__builtin_ctz(mm);
+    }
+    // first slot >= from whose bit is set in m; ns if none
+    MT_DEV int first_from(uint32_t m, int from) const {
+        const uint32_t x = m & ~below(from);
+        const uint64_t hit = wave_ballot(x != 0);
+        if (!hit) return ns;
+        const int lk = first_lane(hit);
+        return lk * K + (int)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)x, lk));
+    }
+    // ------------------------------------------------------------ leaf blocks
+    MT_DEV int leaf_of(int k) const { return wave_total(__popc(bs_bits() & below(k + 1))) - 1; }
+    MT_DEV int bs_slot(int b) const { return b >= nb0 ? ns : nth_slot(bs_bits(), b); }
+    MT_DEV int live_in(int a, int e) const { return wave_total(__popc(live_bits() & below(e) & ~below(a))); }
+
+    // ------------------------------------------------------------ element access
+    MT_DEV Elem get(int k) const {  // all fields of the slot at uniform position k
+        const int lk = k / K, jk = k % K;
+        // masked ORs, not selects: a select chain of loads folds into a load through a
+        // selected address, which would push the register arrays to scratch
+        uint32_t a = 0, b = 0, g = 0, c = 0, d = 0, e = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const uint32_t h = 0u - (uint32_t)(jk == j);
+            a |= (uint32_t)seq[j] & h;
+            b |= (uint32_t)rseq[j] & h;
+            c |= li[j] & h;
+            d |= cf[j] & h;
+            e |= ov[j] & h;
+            g |= (uint32_t)cum[j] & h;
         }
         Elem r;
-        r.seq = __builtin_amdgcn_readlane(a, lk);
-        r.rseq = __builtin_amdgcn_readlane(b, lk);
+        r.seq = __builtin_amdgcn_readlane((int)a, lk);
+        r.rseq = __builtin_amdgcn_readlane((int)b, lk);
         r.li = (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
         r.cf = (uint32_t)__builtin_amdgcn_readlane((int)d, lk);
-        r.o0 = (uint32_t)__builtin_amdgcn_readlane((int)e, lk);
-        r.o1 = (uint32_t)__builtin_amdgcn_readlane((int)f, lk);
-        r.cum = __builtin_amdgcn_readlane(g, lk);
+        r.ov = (uint32_t)__builtin_amdgcn_readlane((int)e, lk);
+        r.cum = __builtin_amdgcn_readlane((int)g, lk);
         return r;
+    }
+    MT_DEV uint32_t get_cf(int k) const {
+        const int lk = k / K, jk = k % K;
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) c |= cf[j] & (0u - (uint32_t)(jk == j));
+        return (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
     }
     MT_DEV uint32_t get_li(int k) const {
         const int lk = k / K, jk = k % K;
-        uint32_t c = li[0];
+        uint32_t c = 0;
 #pragma unroll
-        for (int j = 1; j < K; j++)
-            if (jk == j) c = li[j];
+        for (int j = 0; j < K; j++) c |= li[j] & (0u - (uint32_t)(jk == j));
         return (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
     }
-    // overwrite li / cf / cum of the element at uniform position k
     MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
         const int lk = k / K, jk = k % K;
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            if (jk == j && lane == lk) {
-                li[j] = lv;
-                cf[j] = cv;
-            }
+            const bool h = jk == j && lane == lk;
+            li[j] = h ? lv : li[j];
+            cf[j] = h ? cv : cf[j];
         }
+    }
+    MT_DEV void set_cf(int k, uint32_t cv) {
+        const int lk = k / K, jk = k % K;
+#pragma unroll
+        for (int j = 0; j < K; j++) cf[j] = (jk == j && lane == lk) ? cv : cf[j];
     }
     MT_DEV void set_cum(int k, int32_t v) {
         const int lk = k / K, jk = k % K;
 #pragma unroll
-        for (int j = 0; j < K; j++)
-            if (jk == j && lane == lk) cum[j] = v;
+        for (int j = 0; j < K; j++) cum[j] = (jk == j && lane == lk) ? v : cum[j];
     }
 
-    // insert element e at position p: positions >= p move one slot right
+    // insert e at slot p: slots >= p move one register right
     template <bool CUM>
     MT_DEV void shift_in(int p, const Elem& e) {
         const int32_t c_seq = shr1(seq[K - 1], 0), c_rseq = shr1(rseq[K - 1], 0);
         const uint32_t c_li = (uint32_t)shr1((int)li[K - 1], 0), c_cf = (uint32_t)shr1((int)cf[K - 1], 0);
-        const uint32_t c_o0 = (uint32_t)shr1((int)o0[K - 1], 0), c_o1 = (uint32_t)shr1((int)o1[K - 1], 0);
+        const uint32_t c_ov = (uint32_t)shr1((int)ov[K - 1], 0);
         const int32_t c_cum = CUM ? shr1(cum[K - 1], 0) : 0;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
             const int i = idx(j);
             const bool mv = i > p, at = i == p;
             const int32_t pseq = j ? seq[j - 1] : c_seq, prseq = j ? rseq[j - 1] : c_rseq;
-            const uint32_t pli = j ? li[j - 1] : c_li, pcf = j ? cf[j - 1] : c_cf;
-            const uint32_t po0 = j ? o0[j - 1] : c_o0, po1 = j ? o1[j - 1] : c_o1;
+            const uint32_t pli = j ? li[j - 1] : c_li, pcf = j ? cf[j - 1] : c_cf, pov = j ? ov[j - 1] : c_ov;
             seq[j] = mv ? pseq : (at ? e.seq : seq[j]);
             rseq[j] = mv ? prseq : (at ? e.rseq : rseq[j]);
             li[j] = mv ? pli : (at ? e.li : li[j]);
             cf[j] = mv ? pcf : (at ? e.cf : cf[j]);
-            o0[j] = mv ? po0 : (at ? e.o0 : o0[j]);
-            o1[j] = mv ? po1 : (at ? e.o1 : o1[j]);
+            ov[j] = mv ? pov : (at ? e.ov : ov[j]);
             if (CUM) {
                 const int32_t pcm = j ? cum[j - 1] : c_cum;
                 cum[j] = mv ? pcm : (at ? e.cum : cum[j]);
             }
         }
-        n = n + 1;
-    }
-
-    // remove the element at position p: positions > p move one slot left
-    MT_DEV void shift_out(int p) {
-        const int32_t c_seq = shl1(seq[0], 0x7fffffff), c_rseq = shl1(rseq[0], 0);
-        const uint32_t c_li = (uint32_t)shl1((int)li[0], (int)kEmptyLi), c_cf = (uint32_t)shl1((int)cf[0], (int)kEmptyCf);
-        const uint32_t c_o0 = (uint32_t)shl1((int)o0[0], 0), c_o1 = (uint32_t)shl1((int)o1[0], 0);
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const bool mv = idx(j) >= p;
-            const bool last = j == K - 1;
-            seq[j] = mv ? (last ? c_seq : seq[j + (last ? 0 : 1)]) : seq[j];
-            rseq[j] = mv ? (last ? c_rseq : rseq[j + (last ? 0 : 1)]) : rseq[j];
-            li[j] = mv ? (last ? c_li : li[j + (last ? 0 : 1)]) : li[j];
-            cf[j] = mv ? (last ? c_cf : cf[j + (last ? 0 : 1)]) : cf[j];
-            o0[j] = mv ? (last ? c_o0 : o0[j + (last ? 0 : 1)]) : o0[j];
-            o1[j] = mv ? (last ? c_o1 : o1[j + (last ? 0 : 1)]) : o1[j];
-        }
-        n = n - 1;
+        ns = ns + 1;
     }
 
     // ------------------------------------------------------------ visibility
-    // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697)
+    // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697); dead slots have length 0
     MT_DEV int vis(int j, int32_t R, int C) const {
         const uint32_t f = cf[j];
         const bool seen = ((int)(f & 0xFFu) == C) || (seq[j] <= R);
-        const uint32_t ob = C < 32 ? (o0[j] >> (C & 31)) : (o1[j] >> (C & 31));
-        const bool hid = (f & F_RM) && ((int)((f >> 8) & 0xFFu) == C || (ob & 1u) || rseq[j] <= R);
+        const bool hid = (f & F_RM) && ((int)((f >> 8) & 0xFFu) == C || ((ov[j] >> (C - 1)) & 1u) || rseq[j] <= R);
         return (seen && !hid) ? (int)len_of(li[j]) : 0;
     }
-
-    // cum[] = inclusive prefix of vis over document order; returns getLength(R, C)
+    // cum = inclusive prefix of vis over the slots; returns getLength(R, C)
     MT_DEV int scan(int32_t R, int C) {
         int acc = 0;
 #pragma unroll
@@ -260,24 +296,10 @@ struct RWave {
         for (int j = 0; j < K; j++) cum[j] += excl;
         return wave_last(incl);
     }
-    // visible start of this lane's first element
-    MT_DEV int cs0() const { return shr1(cum[K - 1], 0); }
+    MT_DEV int cs0() const { return shr1(cum[K - 1], 0); }  // visible start of this lane's first slot
 
-    // spill cum (and ids) to LDS by position for the block-level logic
-    MT_DEV void spill(bool ids) {
-#pragma unroll
-        for (int j = 0; j < K; j++) s.pcum[idx(j)] = cum[j];
-        if (ids) {
-#pragma unroll
-            for (int j = 0; j < K; j++) s.pid[idx(j)] = (uint16_t)id_of(li[j]);
-        }
-        wave_sync();
-    }
-    MT_DEV int pcstart(int k) const { return k > 0 ? s.pcum[k - 1] : 0; }
-
-    // ----------------------------------------------------------------- blocks
-    MT_DEV uint8_t* lvl(int Lv) { return Lv == 0 ? s.lbcnt : s.ibcnt[Lv - 1]; }
-    MT_DEV int lvlcap(int Lv) const { return Lv == 0 ? L::LB : L::IB; }
+    // ----------------------------------------------------------------- interior levels (LDS)
+    MT_DEV uint8_t* lvl(int Lv) { return s.ibcnt[Lv - 1]; }  // Lv >= 1
     MT_DEV int nbl(int Lv) const { return uni(s.nb[Lv]); }
 
     template <class T>
@@ -304,32 +326,7 @@ struct RWave {
             wave_sync();
         }
     }
-
-    // bst[b] = first position of leaf block b (bst[nb0] = n)
-    MT_DEV void block_starts() {
-        const int nb = nbl(0);
-        int carry = 0;
-        for (int base = 0; base < nb; base += 64) {
-            const int b = base + lane;
-            const int c = b < nb ? (int)s.lbcnt[b] : 0;
-            const int incl = wave_incl_scan(c) + carry;
-            if (b < nb) s.bst[b] = incl - c;
-            carry = wave_last(incl);
-        }
-        if (lane == 0) s.bst[nb] = carry;
-        wave_sync();
-    }
-    // leaf block holding position k (the first block whose end is past k); needs bst
-    MT_DEV int block_of_pos(int k) {
-        const int nb = nbl(0);
-        for (int base = 0; base < nb; base += 64) {
-            const int b = base + lane;
-            const bool hit = b < nb && s.bst[b] <= k && k < s.bst[b] + (int)s.lbcnt[b];
-            const uint64_t m = wave_ballot(hit);
-            if (m) return base + first_lane(m);
-        }
-        return -1;
-    }
+    // parent (at level Lv+1) of block b at level Lv, and that parent's first child
     MT_DEV int parent_of(int Lv, int b, int* first_child) {
         const uint8_t* pc = lvl(Lv + 1);
         const int np = nbl(Lv + 1);
@@ -348,29 +345,23 @@ struct RWave {
         }
         return -1;
     }
-    MT_DEV bool insert_block_after(int Lv, int b, int cnt) {
-        const int nb = nbl(Lv);
-        if (nb + 1 > lvlcap(Lv)) return false;
-        uint8_t* a = lvl(Lv);
-        lshift_right(a, b + 1, nb);
-        if (Lv == 0) lshift_right(s.lbscour, b + 1, nb);
-        if (lane == 0) {
-            a[b + 1] = (uint8_t)cnt;
-            if (Lv == 0) s.lbscour[b + 1] = MT_SC_UNDEF;
-            s.nb[Lv] = nb + 1;
-        }
-        wave_sync();
-        return true;
-    }
-    // split 4/4 upward + new root (mergeTree.ts:2446-2489, 1876-1887)
+    // an interior block b at level Lv >= 1 reached kMaxNodes children: split 4/4 upward and
+    // grow a new root (mergeTree.ts:2446-2489, 1876-1887)
     MT_DEV bool split_up(int Lv, int b, int32_t sq) {
         for (;;) {
             const int half = kMaxNodes / 2;
             int parent = -1;
             if (Lv < nlev - 1) parent = parent_of(Lv, b, nullptr);
-            if (lane == 0) lvl(Lv)[b] = (uint8_t)half;
+            const int nb = nbl(Lv);
+            if (nb + 1 > L::IB) return fail(MT_DERR_CAPACITY, sq), false;
+            uint8_t* a = lvl(Lv);
+            lshift_right(a, b + 1, nb);
+            if (lane == 0) {
+                a[b] = (uint8_t)half;
+                a[b + 1] = (uint8_t)half;
+                s.nb[Lv] = nb + 1;
+            }
             wave_sync();
-            if (!insert_block_after(Lv, b, half)) return fail(MT_DERR_CAPACITY, sq), false;
             if (Lv == nlev - 1) {
                 if (nlev + 1 > MT_MAXLEV) return fail(MT_DERR_CAPACITY, sq), false;
                 const int nl = nlev;
@@ -392,15 +383,42 @@ struct RWave {
         }
     }
 
-    // insert element e at position k of leaf block b (blockInsert/insertChildNode)
-    template <bool CUM>
-    MT_DEV bool insert_at(int k, int b, const Elem& e, int32_t sq) {
-        if (n + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
-        shift_in<CUM>(k, e);
-        const int c = uni(s.lbcnt[b]) + 1;
-        if (lane == 0) s.lbcnt[b] = (uint8_t)c;
+    // leaf block b = slots [a, e) reached kMaxNodes live children: its child of rank 4 starts
+    // block b+1 (split, mergeTree.ts:2476-2489)
+    MT_DEV bool split_leaf(int b, int a, int e, int32_t sq) {
+        if (nb0 + 1 > L::LB) return fail(MT_DERR_CAPACITY, sq), false;
+        const int s4 = nth_slot(live_bits() & below(e) & ~below(a), kMaxNodes / 2);
+        int parent = -1;
+        if (nlev > 1) parent = parent_of(0, b, nullptr);
+        set_cf(s4, (get_cf(s4) & ~BLK_MASK) | F_BS);  // new block, needsScour undefined
+        nb0 += 1;
+        if (nlev == 1) {  // the root was the only leaf block: new root with 2 children
+            if (lane == 0) {
+                s.ibcnt[0][0] = 2;
+                s.nb[1] = 1;
+            }
+            nlev = 2;
+            wave_sync();
+            return true;
+        }
+        const int c = uni(s.ibcnt[0][parent]) + 1;
+        if (lane == 0) s.ibcnt[0][parent] = (uint8_t)c;
         wave_sync();
-        if (c >= kMaxNodes) return split_up(0, b, sq);
+        if (c < kMaxNodes) return true;
+        return split_up(1, parent, sq);
+    }
+
+    // insert e at slot k of leaf block b (insertingWalk's child insert, mergeTree.ts:2446-2470)
+    MT_DEV bool insert_at(int k, int b, Elem e, int32_t sq) {
+        if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
+        const int a = bs_slot(b);
+        const bool front = k == a;  // new first child: it takes over the block's marks
+        if (front) e.cf = (e.cf & ~BLK_MASK) | (get_cf(a) & BLK_MASK);
+        shift_in<true>(k, e);
+        if (front) set_cf(k + 1, get_cf(k + 1) & ~BLK_MASK);
+        nlive += 1;
+        const int en = bs_slot(b + 1);
+        if (live_in(a, en) >= kMaxNodes) return split_leaf(b, a, en, sq);
         return true;
     }
     MT_DEV int alloc_id(int32_t sq) {
@@ -412,42 +430,44 @@ struct RWave {
     }
 
     // ------------------------------------------------------------------- text
+    // The arena is global memory; arena stores stay in flight until the next arena read.
+    MT_DEV void arena_sync() {
+        if (dirty) {
+            __threadfence_block();
+            dirty = false;
+        }
+    }
     MT_DEV void arena_copy(uint32_t dst, uint32_t src, uint32_t cnt) {
+        arena_sync();
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t i = base + lane;
-            uint8_t v = 0;
-            if (i < cnt) v = arena[src + i];
-            __threadfence_block();
-            if (i < cnt) arena[dst + i] = v;
+            if (i < cnt) arena[dst + i] = arena[src + i];
         }
-        __threadfence_block();
+        dirty = true;
     }
-    // relocate every linked segment's text, in document order, into the other arena half.
-    // (len, id) go through the pcum/pid scratch so the copy loop is not unrolled K times;
-    // callers never need pcum/pid after a reserve.
+    // relocate every linked segment's text, in slot order, into the other arena half
     MT_DEV void compact_text() {
+        arena_sync();
 #pragma unroll
-        for (int j = 0; j < K; j++) {
-            s.pcum[idx(j)] = (int32_t)len_of(li[j]);
-            s.pid[idx(j)] = (uint16_t)id_of(li[j]);
-        }
+        for (int j = 0; j < K; j++) s.scr[idx(j)] = (int32_t)li[j];
         wave_sync();
         uint8_t* dst = abase + (size_t)(text_half ^ 1u) * textcap;
         uint32_t carry = 0;
-        for (int base = 0; base < n; base += 64) {
+        for (int base = 0; base < ns; base += 64) {
             const int i = base + lane;
-            const uint32_t l = i < n ? (uint32_t)s.pcum[i] : 0u;
+            const uint32_t v = i < ns ? (uint32_t)s.scr[i] : 0u;
+            const uint32_t l = len_of(v);
             const uint32_t incl = (uint32_t)wave_incl_scan((int)l);
             const uint32_t at = carry + incl - l;
             if (l) {
-                const uint32_t id = s.pid[i];
+                const uint32_t id = id_of(v);
                 const uint8_t* src = arena + s.toff[id];
                 for (uint32_t q = 0; q < l; q++) dst[at + q] = src[q];
                 s.toff[id] = (uint16_t)at;
             }
             carry += (uint32_t)wave_last((int)incl);
         }
-        __threadfence_block();
+        dirty = true;
         wave_sync();
         text_half ^= 1u;
         text_top = carry;
@@ -461,9 +481,10 @@ struct RWave {
         return false;
     }
 
-    // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245): split the segment visible to the
-    // op's view that strictly contains pos; keeps cum valid for that view.
-    MT_DEV bool boundary(int pos, int32_t sq) {
+    // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245), first half: find the segment
+    // visible to the op's view that strictly contains pos, cut it (left part in place, cum kept
+    // valid for the view) and return its right part r, to be inserted at slot k1 of leaf block b.
+    MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& b) {
         int cs = cs0();
         int hitj = -1;
 #pragma unroll
@@ -472,7 +493,7 @@ struct RWave {
             cs = cum[j];
         }
         const uint64_t m = wave_ballot(hitj >= 0);
-        if (!m) return true;
+        if (!m) return false;
         PROF_CNT(P_N_SPLIT, 1);
         PROF_BEGIN(tb0);
         const int lk = first_lane(m);
@@ -484,28 +505,27 @@ struct RWave {
         const int t = alloc_id(sq);
         if (t < 0) return false;
         PROF_BEGIN(tb1);
-        block_starts();
-        const int b = block_of_pos(k);
+        b = leaf_of(k);
         PROF_END(prof, P_B_BLK, tb1);
         PROF_BEGIN(tb2);
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
         const uint32_t id = id_of(e.li);
         const uint32_t to = uniu(s.toff[id]);
+        arena_sync();
         const uint8_t last = arena[to + (uint32_t)off - 1];
         if (lane == 0) {
             s.props[t] = s.props[id];
             s.toff[t] = (uint16_t)(to + (uint32_t)off);
         }
-        Elem r = e;
+        r = e;
         r.li = (len - (uint32_t)off) | ((uint32_t)t << kLenBits);
+        r.cf = e.cf & ~BLK_MASK;
         set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & ~F_NL) | (last == '\n' ? F_NL : 0u));
         set_cum(k, pos);
         wave_sync();
         PROF_END(prof, P_B_TXT, tb2);
-        PROF_BEGIN(tb3);
-        const bool ok = insert_at<true>(k + 1, b, r, sq);
-        PROF_END(prof, P_B_INS, tb3);
-        return ok;
+        k1 = k + 1;
+        return true;
     }
 
     // ------------------------------------------------------------------- heap
@@ -558,132 +578,168 @@ struct RWave {
     }
     // addToLRUSet (mergeTree.ts:1273-1283) for segment `id` in leaf block b
     MT_DEV bool add_lru(int b, int id, int32_t sq) {
-        if (uni(s.lbscour[b]) != MT_SC_TRUE && sq > cur_seq) {
-            if (lane == 0) s.lbscour[b] = MT_SC_TRUE;
-            wave_sync();
+        const int a = bs_slot(b);
+        const uint32_t c = get_cf(a);
+        if (((c >> SC_SHIFT) & 3u) != MT_SC_TRUE && sq > cur_seq) {
+            set_cf(a, (c & ~SC_MASK) | ((uint32_t)MT_SC_TRUE << SC_SHIFT));
             return heap_push(sq, id, sq);
         }
         return true;
     }
 
     // ---------------------------------------------------------------- zamboni
-    MT_DEV int pos_of_id(int id) const {
+    MT_DEV int slot_of_id(int id) const {  // -1 once unlinked (segment.parent === undefined)
         int hit = -1;
 #pragma unroll
         for (int j = 0; j < K; j++)
-            if ((int)id_of(li[j]) == id) hit = idx(j);
+            if ((int)id_of(li[j]) == id && !(cf[j] & F_DEAD)) hit = idx(j);
         const uint64_t m = wave_ballot(hit >= 0);
         if (!m) return -1;
         return __builtin_amdgcn_readlane(hit, first_lane(m));
     }
 
-    // TextSegment.append (textSegment.ts:76-85): prev.text += seg.text.  prev/q index the
-    // scour scratch (block positions st + prev / st + q).
-    MT_DEV void append_text(int st, int prev, int q) {
-        const uint32_t pid_ = id_of(uniu(s.zli[prev])), qid = id_of(uniu(s.zli[q]));
-        const uint32_t pl = len_of(uniu(s.zli[prev])), ql = len_of(uniu(s.zli[q]));
-        {
-            const uint32_t pt = uniu(s.toff[pid_]), qt = uniu(s.toff[qid]);
-            uint32_t need = 0;
-            if (pt + pl != qt && pt + pl != text_top) need = pl + ql;
-            else if (pt + pl != qt) need = ql;
-            if (need && !arena_reserve(need, cur_seq)) return;
-        }
-        const uint32_t pt = uniu(s.toff[pid_]), qt = uniu(s.toff[qid]);
-        uint32_t top = text_top;
-        if (pt + pl == qt) {
-            // adjacent views: nothing to copy
-        } else if (pt + pl == top) {
-            arena_copy(top, qt, ql);
-            top += ql;
-        } else {
-            arena_copy(top, pt, pl);
-            arena_copy(top + pl, qt, ql);
+    // TextSegment.append (textSegment.ts:76-85) of a whole run: the live child of rank p absorbs
+    // the following children whose bits are set in runm.  Only the text content is state, so
+    // the run is made contiguous once (or found contiguous) instead of pair by pair.  Lane q of
+    // (vli, vcf, vslot) holds the block's live child of rank q.
+    MT_DEV void append_run(int p, uint32_t runm, uint32_t vli, uint32_t vcf, int vslot) {
+        const uint32_t pli = (uint32_t)__builtin_amdgcn_readlane((int)vli, p);
+        const uint32_t pid_ = id_of(pli);
+        const uint32_t lastq = 31u - (uint32_t)__builtin_clz(runm);
+        // per-lane piece: lane q of the run holds (offset, length); exclusive prefix = its place
+        const bool in_run = lane == p || (lane < 32 && ((runm >> lane) & 1u));
+        const uint32_t myl = in_run ? len_of(vli) : 0u;
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)myl);
+        const uint32_t total = (uint32_t)wave_last((int)incl);
+        for (int pass = 0; pass < 2; pass++) {
+            // adjacent views: every piece starts where the run's text so far would end
+            const uint32_t myt = in_run ? (uint32_t)s.toff[id_of(vli)] : 0u;
+            const uint32_t pt = uniu((uint32_t)__builtin_amdgcn_readlane((int)myt, p));
+            const bool adj = __ballot(in_run && myt != pt + (incl - myl)) == 0;
+            if (adj) break;  // nothing to copy
+            if (pass == 0) {
+                if (!arena_reserve(total, cur_seq)) return;
+                continue;    // a compaction lays the run out contiguously
+            }
+            const uint32_t top = text_top;
+            uint64_t pieces = __ballot(in_run);
+            while (pieces) {
+                const int q = first_lane(pieces);
+                pieces &= pieces - 1;
+                const uint32_t ql = (uint32_t)__builtin_amdgcn_readlane((int)myl, q);
+                const uint32_t qt = (uint32_t)__builtin_amdgcn_readlane((int)myt, q);
+                const uint32_t at = top + (uint32_t)__builtin_amdgcn_readlane((int)(incl - myl), q);
+                arena_copy(at, qt, ql);
+            }
             if (lane == 0) s.toff[pid_] = (uint16_t)top;
-            top += pl + ql;
+            text_top = top + total;
+            wave_sync();
         }
-        const uint32_t nli = (pl + ql) | (pid_ << kLenBits);
-        const uint32_t ncf = (uniu(s.zcf[prev]) & ~F_NL) | (uniu(s.zcf[q]) & F_NL);
-        wave_sync();
-        if (lane == 0) {
-            s.zli[prev] = nli;
-            s.zcf[prev] = ncf;
-        }
-        set_li_cf(st + prev, nli, ncf);  // registers stay current (a compaction may follow)
-        text_top = top;
-        wave_sync();
+        const uint32_t pcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, p);
+        const uint32_t lcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, (int)lastq);
+        set_li_cf(__builtin_amdgcn_readlane(vslot, p), total | (pid_ << kLenBits), (pcf & ~F_NL) | (lcf & F_NL));
     }
 
-    // scourNode on leaf block b (mergeTree.ts:1289-1365); returns the new child count
-    MT_DEV int scour(int b) {
-        const int st = uni(s.bst[b]);
-        const int cnt = uni(s.lbcnt[b]);
+    // scourNode on the leaf block whose slots are [a, e) (mergeTree.ts:1289-1365); returns the
+    // block's new child count.  Unlinked children become DEAD slots in place.
+    MT_DEV int scour(int a, int e) {
+        const uint32_t lb = live_bits() & below(e) & ~below(a);
+        const int c = __popc(lb);
+        const int incl = wave_incl_scan(c);
+        const int rbase = incl - c;
+        const int cnt = wave_last(incl);
+        if (cnt > kMaxNodes) return fail(MT_DERR_CAPACITY, cur_seq), cnt;
+        // the live children, rank by rank, through LDS scratch: lane q gets the child of rank q
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            const int i = idx(j);
-            if (i >= st && i < st + cnt) {
-                const int q = i - st;
+            if ((lb >> j) & 1u) {
+                const int q = rbase + __popc(lb & ((1u << j) - 1u));
                 s.zseq[q] = seq[j];
                 s.zrseq[q] = rseq[j];
                 s.zli[q] = li[j];
                 s.zcf[q] = cf[j];
+                s.zslot[q] = idx(j);
             }
         }
         wave_sync();
+        const bool mine = lane < cnt;
+        const int32_t vseq = mine ? s.zseq[lane] : 0, vrseq = mine ? s.zrseq[lane] : 0;
+        const uint32_t vli = mine ? s.zli[lane] : 0u, vcf = mine ? s.zcf[lane] : 0u;
+        const int vslot = mine ? s.zslot[lane] : 0;
+        const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
+        // the sequential decisions (scalar), reading child q from lane q
         const int32_t minSeq = min_seq;
         int kept = 0, prev = -1;
-        uint32_t unlink = 0;
+        uint32_t plen = 0, pflags = 0, unlink = 0;
+        uint64_t pprops = 0;
+        int vtgt = -1;  // lane q: rank of the child it appends into, or -1
         for (int q = 0; q < cnt; q++) {
-            const uint32_t f = uniu(s.zcf[q]);
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)vcf, q);
             if (f & F_RM) {
-                if (uni(s.zrseq[q]) > minSeq) kept++;
+                if (__builtin_amdgcn_readlane(vrseq, q) > minSeq) kept++;
                 else unlink |= 1u << q;  // UNLINK
                 prev = -1;
-            } else if (uni(s.zseq[q]) <= minSeq) {
-                bool app = false;
-                const uint32_t ql = len_of(uniu(s.zli[q]));
-                if (prev >= 0) {
-                    const uint32_t pf = uniu(s.zcf[prev]);
-                    const uint32_t pl = len_of(uniu(s.zli[prev]));
-                    const bool pm = ((pf ^ f) & F_PDEF) == 0 &&
-                                    s.props[id_of(uniu(s.zli[prev]))] == s.props[id_of(uniu(s.zli[q]))];
-                    // canAppend + matchProperties (textSegment.ts:63-68, properties.ts:62-93)
-                    app = !(pf & F_NL) && (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
-                          pm && ql > 0;
-                }
-                if (uni(app ? 1 : 0)) {
-                    append_text(st, prev, q);
-                    PROF_CNT(P_N_APPEND, 1);
-                    if (err) return cnt;
-                    unlink |= 1u << q;  // APPEND: segment.parent = undefined
+            } else if (__builtin_amdgcn_readlane(vseq, q) <= minSeq) {
+                const uint32_t ql = len_of((uint32_t)__builtin_amdgcn_readlane((int)vli, q));
+                const uint64_t qp = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vpr, q) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vpr >> 32), q)
+                                     << 32);
+                // canAppend + matchProperties (textSegment.ts:63-68, properties.ts:62-93)
+                const bool app = prev >= 0 && !(pflags & F_NL) &&
+                                 (plen <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
+                                 ((pflags ^ f) & F_PDEF) == 0 && pprops == qp && ql > 0;
+                if (app) {  // APPEND: segment.parent = undefined
+                    unlink |= 1u << q;
+                    if (lane == q) vtgt = prev;
+                    plen += ql;
+                    pflags = (pflags & ~F_NL) | (f & F_NL);
                 } else {
                     kept++;
-                    prev = ql > 0 ? q : -1;
+                    if (ql > 0) {
+                        prev = q;
+                        plen = ql;
+                        pflags = f;
+                        pprops = qp;
+                    } else {
+                        prev = -1;
+                    }
                 }
             } else {
                 kept++;
                 prev = -1;
             }
         }
-        if (kept < cnt) {
-            for (int q = cnt - 1; q >= 0; q--)
-                if (unlink & (1u << q)) shift_out(st + q);
-            PROF_CNT(P_N_UNLINK, __popc(unlink));
-            const int d = cnt - kept;
-            if (lane == 0) s.lbcnt[b] = (uint8_t)kept;
-            const int nb = nbl(0);
-            for (int base = b + 1; base <= nb; base += 64) {
-                const int jb = base + lane;
-                if (jb <= nb) s.bst[jb] -= d;
-            }
-            wave_sync();
+        PROF_CNT(P_N_UNLINK, __popc(unlink));
+        uint64_t appm = __ballot(vtgt >= 0);
+        while (appm) {
+            const int p = __builtin_amdgcn_readlane(vtgt, first_lane(appm));
+            const uint64_t runm = __ballot(vtgt == p);
+            appm &= ~runm;
+            PROF_CNT(P_N_APPEND, __popcll(runm));
+            append_run(p, (uint32_t)runm, vli, vcf, vslot);
+            if (err) return cnt;
         }
+        // unlink: the slots become dead in place (their block marks stay)
+        const bool gone = mine && ((unlink >> lane) & 1u);
+        uint64_t gm = __ballot(gone);
+        uint32_t kill = 0;
+        while (gm) {
+            const int sl = __builtin_amdgcn_readlane(vslot, first_lane(gm));
+            gm &= gm - 1;
+            if (sl / K == lane) kill |= 1u << (sl % K);
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const bool k_ = (kill >> j) & 1u;
+            li[j] = k_ ? (li[j] & ~kLenMask) : li[j];
+            cf[j] = k_ ? (cf[j] | F_DEAD) : cf[j];
+        }
+        nlive -= __popc(unlink);
         return kept;
     }
 
-    // The block-count half of pack (mergeTree.ts:1368-1420): the m children of block P at
-    // level Lv+1 (first child first_child, `total` grandchildren after scouring) are repacked
-    // evenly, recursing upward on underflow.
+    // The block-count half of pack (mergeTree.ts:1368-1420) for interior levels Lv >= 1: the m
+    // children of block P at level Lv+1 (`total` grandchildren) are repacked evenly, recursing up.
     MT_DEV void repack(int Lv, int P, int first_child, int m, int total) {
         for (;;) {
             const int half = kMaxNodes / 2;
@@ -695,24 +751,16 @@ struct RWave {
             wave_sync();
             if (cc < m) {
                 lshift_left(a, first_child + m, nb, m - cc);
-                if (Lv == 0) lshift_left(s.lbscour, first_child + m, nb, m - cc);
             } else if (cc > m) {
-                for (int q = 0; q < cc - m; q++) {
-                    lshift_right(a, first_child + m, nb + q);
-                    if (Lv == 0) lshift_right(s.lbscour, first_child + m, nb + q);
-                }
+                for (int q = 0; q < cc - m; q++) lshift_right(a, first_child + m, nb + q);
             }
-            if (lane < cc) {
-                a[first_child + lane] = (uint8_t)(base + (lane < extra ? 1 : 0));
-                if (Lv == 0) s.lbscour[first_child + lane] = MT_SC_UNDEF;
-            }
+            if (lane < cc) a[first_child + lane] = (uint8_t)(base + (lane < extra ? 1 : 0));
             wave_sync();
             if (lane == 0) {
                 s.nb[Lv] = nb + cc - m;
                 lvl(Lv + 1)[P] = (uint8_t)cc;
             }
             wave_sync();
-            if (Lv == 0) block_starts();
             if (!(cc < kMaxNodes / 2 && (Lv + 1) < nlev - 1)) return;  // underflow(parent) && parent.parent
             int fc = 0;
             const int PP = parent_of(Lv + 1, P, &fc);
@@ -725,6 +773,43 @@ struct RWave {
             for (int j = first_child; j < first_child + m; j++) total += uni(c[j]);
         }
     }
+    // pack at the leaf level: the m leaf blocks under level-1 block P (first fc; `total` live
+    // children after scouring) become cc evenly filled blocks -- only block marks change
+    MT_DEV void repack_leaf(int P, int fc, int m, int total) {
+        const int half = kMaxNodes / 2;
+        int cc = min(kMaxNodes - 1, total / half);
+        if (cc < 1) cc = 1;
+        const int base = total / cc, extra = total % cc;
+        const int A = bs_slot(fc), E = bs_slot(fc + m);
+        const uint32_t lb = live_bits() & below(E) & ~below(A);
+        const int c = __popc(lb);
+        const int rbase = wave_incl_scan(c) - c;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int i = idx(j);
+            if (i >= A && i < E) {
+                uint32_t v = cf[j] & ~BLK_MASK;  // every new block: needsScour undefined
+                if (i == A) v |= F_BS;
+                if ((lb >> j) & 1u) {
+                    const int r = rbase + __popc(lb & ((1u << j) - 1u));
+                    for (int t = 1; t < cc; t++)
+                        if (r == t * base + min(t, extra)) v |= F_BS;
+                }
+                cf[j] = v;
+            }
+        }
+        nb0 += cc - m;
+        if (lane == 0) s.ibcnt[0][P] = (uint8_t)cc;
+        wave_sync();
+        if (cc < kMaxNodes / 2 && 1 < nlev - 1) {  // underflow(parent) && parent.parent
+            int fc2 = 0;
+            const int PP = parent_of(1, P, &fc2);
+            const int m2 = uni(lvl(2)[PP]);
+            int total2 = 0;
+            for (int j = fc2; j < fc2 + m2; j++) total2 += uni(lvl(1)[j]);
+            repack(1, PP, fc2, m2, total2);
+        }
+    }
 
     // zamboniSegments (mergeTree.ts:1422-1478), zamboniSegmentsMaxCount = 2.  One scour call
     // site: step 0 scours the popped segment's block; on underflow steps 1..m scour every
@@ -735,24 +820,27 @@ struct RWave {
             PROF_BEGIN(tz);
             const int id = heap_pop();
             if (id == (int)kDead) continue;
-            const int k = pos_of_id(id);
-            if (k < 0) continue;  // segment.parent === undefined
-            block_starts();
-            const int b = block_of_pos(k);
+            const int k = slot_of_id(id);
+            if (k < 0) continue;
+            const int b = leaf_of(k);
+            const int a = bs_slot(b), e = bs_slot(b + 1);
             PROF_END(prof, P_ZPOP, tz);
-            if (uni(s.lbscour[b]) == MT_SC_FALSE) continue;
-            const int cnt = uni(s.lbcnt[b]);
+            if (((get_cf(a) >> SC_SHIFT) & 3u) == MT_SC_FALSE) continue;
+            const int cnt = live_in(a, e);
             int P = -1, fc = 0, m = 0, total = 0;
             for (int step = 0;; step++) {
-                const int blk = step == 0 ? b : fc + step - 1;
+                int aa = a, ee = e;
+                if (step > 0) {
+                    aa = bs_slot(fc + step - 1);
+                    ee = bs_slot(fc + step);
+                }
                 PROF_BEGIN(ts);
                 PROF_CNT(P_N_SCOUR, 1);
-                const int kept = scour(blk);
+                const int kept = scour(aa, ee);
                 PROF_END(prof, P_SCOUR, ts);
                 if (err) return;
                 if (step == 0) {
-                    if (lane == 0) s.lbscour[b] = MT_SC_FALSE;
-                    wave_sync();
+                    set_cf(a, (get_cf(a) & ~SC_MASK) | ((uint32_t)MT_SC_FALSE << SC_SHIFT));
                     if (!(kept < cnt && kept < kMaxNodes / 2 && nlev > 1)) break;
                     P = parent_of(0, b, &fc);
                     m = uni(s.ibcnt[0][P]);
@@ -762,7 +850,7 @@ struct RWave {
                 if (step == m) break;
             }
             PROF_BEGIN(tr);
-            if (P >= 0) repack(0, P, fc, m, total);
+            if (P >= 0) repack_leaf(P, fc, m, total);
             PROF_END(prof, P_REPACK, tr);
             if (err) return;
         }
@@ -778,33 +866,31 @@ struct RWave {
         return p;
     }
 
-    // blockInsert (mergeTree.ts:2141-2224) of a text segment at pos, after the boundary split
-    MT_DEV void place_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np) {
+    // blockInsert (mergeTree.ts:2141-2224) of a text segment at pos, after the boundary split:
+    // choose its slot k in leaf block b, write its text and cold fields, build its element.
+    // Returns its id (< 0 on error) and its child index inside block b before a possible split.
+    MT_DEV int place_prep(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np, Elem& en,
+                          int& k, int& b, int& idx_in) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, pos = op.pos1;
-        spill(false);
-        block_starts();
-        const int nb = nbl(0);
-        // first leaf block whose cumulative visible end >= pos (insertingWalk descent)
-        int b = -1;
-        for (int base = 0; base < nb; base += 64) {
-            const int jb = base + lane;
-            bool hit = false;
-            if (jb < nb) {
-                const int st = s.bst[jb], c = s.lbcnt[jb];
-                const int bend = c > 0 ? s.pcum[st + c - 1] : pcstart(st);
-                hit = bend >= pos;
-            }
-            const uint64_t m = wave_ballot(hit);
-            if (m) {
-                b = base + first_lane(m);
-                break;
-            }
+        // insertingWalk descends into the first block whose cumulative visible end >= pos
+        // (breakTie is true for blocks, :2248-2277): that leaf block's last slot is the first
+        // block-ending slot with cum >= pos
+        const uint32_t bsm = bs_bits();
+        const int nxt = shl1((int)(bsm & 1u), 0);
+        int last = 0x7fffffff;
+#pragma unroll
+        for (int j = K - 1; j >= 0; j--) {
+            const int i = idx(j);
+            const bool ends = (j + 1 < K ? ((bsm >> (j + 1)) & 1u) != 0 : nxt != 0) || i == ns - 1;
+            last = (i < ns && ends && cum[j] >= pos) ? i : last;
         }
-        if (b < 0) return fail(MT_DERR_INSERT_FAILED, S);
-        const int st = uni(s.bst[b]), c = uni(s.lbcnt[b]);
-        // leaf placement: first child with pos < len, or pos == len == 0 and breakTie
-        // (mergeTree.ts:2248-2277); else the end of block b (:2431-2444)
+        last = wave_min(last);
+        if (last == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
+        b = leaf_of(last);
+        const int a = bs_slot(b), e = last + 1;
+        // leaf placement: first child with pos < len, or pos == len == 0 and breakTie; else the
+        // end of the block (:2431-2444)
         int best = 0x7fffffff;
         {
             const int cs = cs0();
@@ -814,21 +900,23 @@ struct RWave {
                 const int ce = cum[j];
                 const int csj = j ? cum[j - 1] : cs;
                 const bool rm_before = (cf[j] & F_RM) && rseq[j] <= R;
-                const bool h = i >= st && i < st + c && (ce > pos || (ce == pos && csj == pos && !rm_before));
-                if (h) best = i;
+                const bool h = !(cf[j] & F_DEAD) && i >= a && i < e &&
+                               (ce > pos || (ce == pos && csj == pos && !rm_before));
+                best = h ? i : best;
             }
         }
         best = wave_min(best);
-        const int k = best != 0x7fffffff ? best : st + c;
+        k = best != 0x7fffffff ? best : e;
+        idx_in = live_in(a, k);
         const int t = alloc_id(S);
-        if (t < 0) return;
-        if (!arena_reserve((uint32_t)tlen, S)) return;
+        if (t < 0) return -1;
+        if (!arena_reserve((uint32_t)tlen, S)) return -1;
         const uint32_t top = text_top;
         for (int base = 0; base < tlen; base += 64) {
             const int i = base + lane;
             if (i < tlen) arena[top + i] = pay[i];
         }
-        __threadfence_block();
+        dirty = true;
         uint32_t fl = pay[tlen - 1] == '\n' ? F_NL : 0u;
         uint64_t p = 0;
         if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
@@ -841,19 +929,13 @@ struct RWave {
         }
         text_top = top + (uint32_t)tlen;
         wave_sync();
-        Elem e;
-        e.seq = S;
-        e.rseq = 0;
-        e.li = (uint32_t)tlen | ((uint32_t)t << kLenBits);
-        e.cf = (uint32_t)C | fl;
-        e.o0 = 0;
-        e.o1 = 0;
-        e.cum = 0;
-        const int idx_in = k - st;  // index inside block b before a possible split
-        const int before_nb = nbl(0);
-        if (!insert_at<false>(k, b, e, S)) return;
-        const int bb = (nbl(0) > before_nb && idx_in >= kMaxNodes / 2) ? b + 1 : b;
-        if (S > min_seq) add_lru(bb, t, S);  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
+        en.seq = S;
+        en.rseq = 0;
+        en.li = (uint32_t)tlen | ((uint32_t)t << kLenBits);
+        en.cf = (uint32_t)C | fl;
+        en.ov = 0;
+        en.cum = pos + tlen;
+        return t;
     }
 
     // markRangeRemoved / annotateRange leaf actions over mapRange (mergeTree.ts:2607-2719,
@@ -863,64 +945,49 @@ struct RWave {
         const int C = op.client, start = op.pos1, end = op.pos2;
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = op.flags & MT_F_REWRITE;
-        const uint32_t cb0 = C < 32 ? (1u << C) : 0u, cb1 = C < 32 ? 0u : (1u << (C - 32));
+        const uint32_t cbit = 1u << (C - 1);
+        uint32_t tm = 0;  // touched slots of this lane
         {
             int cs = cs0();
 #pragma unroll
             for (int j = 0; j < K; j++) {
                 const int ce = cum[j];
-                if (ce > cs && cs < end && ce > start) {
-                    if (is_remove) {
-                        if (cf[j] & F_RM) {  // addOverlappingClient (first remover wins)
-                            o0[j] |= cb0;
-                            o1[j] |= cb1;
-                        } else {
-                            cf[j] = (cf[j] & ~0xFF00u) | F_RM | ((uint32_t)C << 8);
-                            rseq[j] = S;
-                        }
-                    } else {  // SegmentPropertiesManager.addProperties (remote, no combining op)
-                        const uint32_t id = id_of(li[j]);
-                        uint64_t p = (cf[j] & F_PDEF) ? s.props[id] : 0;
-                        if (rewrite) p = 0;
-                        s.props[id] = apply_pairs(p, pairs, np);
-                        cf[j] |= F_PDEF;
-                    }
+                const bool touched = ce > cs && cs < end && ce > start;
+                tm |= touched ? (1u << j) : 0u;
+                // branch-free register updates (a store per branch would merge into a
+                // pointer phi and push the state arrays to scratch)
+                const uint32_t f = cf[j];
+                const bool was_rm = (f & F_RM) != 0;
+                const bool mark = touched && is_remove && !was_rm;  // first remover wins
+                const bool overlap = touched && is_remove && was_rm;  // addOverlappingClient
+                const bool annot = touched && !is_remove;
+                ov[j] = overlap ? (ov[j] | cbit) : ov[j];
+                rseq[j] = mark ? S : rseq[j];
+                cf[j] = mark ? ((f & ~0xFF00u) | F_RM | ((uint32_t)C << 8)) : (annot ? (f | F_PDEF) : f);
+                if (annot) {  // SegmentPropertiesManager.addProperties (remote, no combining op)
+                    const uint32_t id = id_of(li[j]);
+                    uint64_t p = (f & F_PDEF) ? s.props[id] : 0;
+                    if (rewrite) p = 0;
+                    s.props[id] = apply_pairs(p, pairs, np);
                 }
                 cs = ce;
             }
         }
-        spill(true);
-        // addToLRUSet for touched segments in document order: one heap push per leaf block
-        // whose needsScour is not already true, for its first touched segment
-        block_starts();
-        const int nb = nbl(0);
-        for (int base = 0; base < nb; base += 64) {
-            const int jb = base + lane;
-            int first = -1;
-            if (jb < nb) {
-                const int st = s.bst[jb], c = s.lbcnt[jb];
-                for (int q = 0; q < c; q++) {
-                    const int k = st + q;
-                    const int ce = s.pcum[k], cs = pcstart(k);
-                    if (ce > cs && cs < end && ce > start) {
-                        first = k;
-                        break;
-                    }
-                }
-            }
-            uint64_t m = wave_ballot(first >= 0);
-            while (m) {
-                const int fl = first_lane(m);
-                m &= m - 1;
-                const int k = __builtin_amdgcn_readlane(first, fl);
-                if (!add_lru(base + fl, uni(s.pid[k]), S)) return;
-            }
+        // addToLRUSet for the touched segments in document order: one push per leaf block
+        // (its first touched child) whose needsScour is not already true
+        int from = 0;
+        for (;;) {
+            const int k = first_from(tm, from);
+            if (k >= ns) break;
+            const int b = leaf_of(k);
+            if (!add_lru(b, (int)id_of(get_li(k)), S)) return;
+            from = first_from(bs_bits(), k + 1);
         }
     }
 
     // Client.applyMsg for the observer (client.ts:797-828): the op, then updateSeqNumbers
-    // (client.ts:821-828, MergeTree.setMinSeq mergeTree.ts:1718-1736).  Written so every
-    // register-heavy routine has exactly one call site.
+    // (client.ts:821-828, MergeTree.setMinSeq mergeTree.ts:1718-1736).  Every register-heavy
+    // routine has exactly one call site.
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
         const int np = op.flags >> MT_F_NPAIRS_SHIFT;
         const int32_t S = op.seq;
@@ -929,7 +996,7 @@ struct RWave {
         const int tlen = (int)op.payload_len - 2 * np;
         const uint8_t* pairs = pay + tlen;
         if (op.type != MT_OP_NOOP) {
-            if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
+            if (op.client == 0 || op.client > kNarrowClients) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
             if (!(cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);      // client.ts:461-462
             if (!(min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // client.ts:463-464
@@ -940,16 +1007,38 @@ struct RWave {
             PROF_BEGIN(t0);
             scan(op.ref_seq, op.client);
             PROF_END(prof, P_SCAN, t0);
-            PROF_BEGIN(t1);
-            const int nbd = ins ? 1 : 2;
-            for (int bi = 0; bi < nbd; bi++)
-                if (!boundary(bi == 0 ? op.pos1 : op.pos2, S)) return;
-            PROF_END(prof, P_BOUND, t1);
-            PROF_BEGIN(t2);
-            if (ins) {
-                if (tlen > 0) place_insert(op, pay, tlen, pairs, np);
-                PROF_END(prof, P_INSERT, t2);
-            } else {
+            // insertion steps: the boundary splits (ensureIntervalBoundary), then for an insert
+            // the new segment; every step ends in the one insert_at call site
+            const int nsteps = ins ? (tlen > 0 ? 2 : 1) : 2;
+            for (int step = 0; step < nsteps; step++) {
+                PROF_BEGIN(t1);
+                const bool placing = ins && step == 1;
+                Elem e;
+                int k = 0, b = 0, idx_in = 0, t = -1;
+                if (!placing) {
+                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, e, k, b)) {
+                        if (err) return;
+                        continue;
+                    }
+                } else {
+                    t = place_prep(op, pay, tlen, pairs, np, e, k, b, idx_in);
+                    if (t < 0) return;
+                }
+                const int before_nb = nb0;
+                const bool ok = insert_at(k, b, e, S);
+                if (placing) {
+                    PROF_END(prof, P_INSERT, t1);
+                } else {
+                    PROF_END(prof, P_BOUND, t1);
+                }
+                if (!ok) return;
+                if (placing && S > min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
+                    const int bb = (nb0 > before_nb && idx_in >= kMaxNodes / 2) ? b + 1 : b;
+                    if (!add_lru(bb, t, S)) return;
+                }
+            }
+            if (!ins) {
+                PROF_BEGIN(t2);
                 range_action(op, pairs, np);
                 PROF_END(prof, P_RANGE, t2);
             }
@@ -975,9 +1064,51 @@ struct RWave {
     }
 
     // ------------------------------------------------------------ load / store
+    // K consecutive u32 of one lane (16-byte aligned when K % 4 == 0, 8-byte when K == 2)
+    MT_DEV VU ld_u32(const uint32_t* p) const {
+        VU v;
+        if constexpr (K % 4 == 0) {
+#pragma unroll
+            for (int c = 0; c < K / 4; c++) {
+                const U4 x = reinterpret_cast<const U4*>(p)[c];
+                v[4 * c] = x[0];
+                v[4 * c + 1] = x[1];
+                v[4 * c + 2] = x[2];
+                v[4 * c + 3] = x[3];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < K / 2; c++) {
+                const U2 x = reinterpret_cast<const U2*>(p)[c];
+                v[2 * c] = x[0];
+                v[2 * c + 1] = x[1];
+            }
+        }
+        return v;
+    }
+    MT_DEV VU ld_u8(const uint8_t* p) const {  // K consecutive bytes of one lane
+        VU v;
+        if constexpr (K % 4 == 0) {
+#pragma unroll
+            for (int c = 0; c < K / 4; c++) {
+                const uint32_t w = reinterpret_cast<const uint32_t*>(p)[c];
+#pragma unroll
+                for (int q = 0; q < 4; q++) v[4 * c + q] = (w >> (8 * q)) & 0xFFu;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < K / 2; c++) {
+                const uint32_t w = reinterpret_cast<const uint16_t*>(p)[c];
+                v[2 * c] = w & 0xFFu;
+                v[2 * c + 1] = w >> 8;
+            }
+        }
+        return v;
+    }
+
     MT_DEV void load(const mt_gstate& g, uint32_t d) {
         const mt_doc_scalars& sc = g.sc[d];
-        n = uni(sc.nseg);
+        const int n = uni(sc.nseg);
         nlev = uni(sc.nlev);
         heap_n = uni(sc.heap_n);
         cur_seq = uni(sc.cur_seq);
@@ -986,19 +1117,16 @@ struct RWave {
         err_seq = uni(sc.err_seq);
         text_top = uniu(sc.text_top);
         text_half = uniu(sc.text_half);
+        nb0 = uni(sc.nb[0]);
         next_id = n;
+        nlive = n;
+        ns = n;
         const size_t so = (size_t)d * g.segcap;
 #pragma clang loop unroll(disable) vectorize(disable)
         for (int i = lane; i < n; i += 64) {
             s.props[i] = g.props[so + i];
             s.toff[i] = (uint16_t)g.toff[so + i];
-        }
-        const size_t lo = (size_t)d * g.lbcap;
-        const int nb0 = uni(sc.nb[0]);
-#pragma clang loop unroll(disable) vectorize(disable)
-        for (int i = lane; i < nb0; i += 64) {
-            s.lbcnt[i] = g.lbcnt[lo + i];
-            s.lbscour[i] = g.lbscour[lo + i];
+            s.scr[i] = 0;
         }
         for (int Lv = 1; Lv < nlev; Lv++) {
             const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv - 1)) * g.ibcap;
@@ -1013,135 +1141,185 @@ struct RWave {
             s.hslot[i] = g.hslot[ho + i];  // position at store == id at load
         }
         if (lane < MT_MAXLEV) s.nb[lane] = sc.nb[lane];
-        // whole-lane vector loads (segcap >= CAP, so reading past n stays inside the document's
-        // rows); lanes past the last segment skip HBM entirely
-        typedef uint32_t V2U __attribute__((ext_vector_type(2 * K)));
-        typedef uint8_t VB __attribute__((ext_vector_type(K)));
+        wave_sync();
+        // leaf blocks -> a mark (1 | needsScour << 1) at the first position of every non-empty block
+        const size_t lo = (size_t)d * g.lbcap;
+        int nempty = 0;
+        {
+            int carry = 0;
+            for (int base = 0; base < nb0; base += 64) {
+                const int b = base + lane;
+                const int c = b < nb0 ? (int)g.lbcnt[lo + b] : 0;
+                const int scv = b < nb0 ? (int)g.lbscour[lo + b] : 0;
+                const int incl = wave_incl_scan(c) + carry;
+                if (b < nb0 && c > 0) s.scr[incl - c] = 1 | (scv << 1);
+                nempty += __popcll(wave_ballot(b < nb0 && c == 0));
+                carry = wave_last(incl);
+            }
+        }
+        wave_sync();
+        // the register state, one field at a time
         const int i0 = lane * K;
-        // field by field, with scheduling barriers: the loaded rows never coexist with the state
-        seq = 0x7fffffff;
-        rseq = 0;
-        li = kEmptyLi;
-        cf = kEmptyCf;
-        o0 = 0;
-        o1 = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            seq[j] = 0x7fffffff;
+            rseq[j] = 0;
+            li[j] = kEmptyLi;
+            cf[j] = kEmptyCf;
+            ov[j] = 0;
+            cum[j] = 0;
+        }
         if (i0 < n) {
-            VI live;
-#pragma unroll
-            for (int j = 0; j < K; j++) live[j] = i0 + j < n ? -1 : 0;
+            // rows are read whole (segcap >= CAP keeps them inside the document); only li and
+            // cf need the padding values past n: padding is dead and has length 0
             {
-                const VI v = *reinterpret_cast<const VI*>(g.seq + so + i0);
-                seq = (v & live) | (0x7fffffff & ~live);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            rseq = *reinterpret_cast<const VI*>(g.rseq + so + i0) & live;
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                const VU v = *reinterpret_cast<const VU*>(g.len + so + i0);
+                const VU v = ld_u32(reinterpret_cast<const uint32_t*>(g.seq + so + i0));
 #pragma unroll
-                for (int j = 0; j < K; j++) li[j] = live[j] ? (v[j] | ((uint32_t)(i0 + j) << kLenBits)) : kEmptyLi;
+                for (int j = 0; j < K; j++) seq[j] = (int32_t)v[j];
             }
             __builtin_amdgcn_sched_barrier(0);
             {
-                const V2U ov = *reinterpret_cast<const V2U*>(g.ovl + so + i0);
+                const VU v = ld_u32(reinterpret_cast<const uint32_t*>(g.rseq + so + i0));
 #pragma unroll
-                for (int j = 0; j < K; j++) {
-                    o0[j] = live[j] ? ov[2 * j] : 0u;
-                    o1[j] = live[j] ? ov[2 * j + 1] : 0u;
+                for (int j = 0; j < K; j++) rseq[j] = (int32_t)v[j];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const VU v = ld_u32(g.len + so + i0);
+#pragma unroll
+                for (int j = 0; j < K; j++) li[j] = i0 + j < n ? (v[j] | ((uint32_t)(i0 + j) << kLenBits)) : kEmptyLi;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const uint32_t* op = reinterpret_cast<const uint32_t*>(g.ovl + so + i0);
+#pragma unroll
+                for (int c = 0; c < K / 2; c++) {
+                    const U4 x = reinterpret_cast<const U4*>(op)[c];  // two u64: (lo, hi), (lo, hi)
+                    ov[2 * c] = (x[0] >> 1) | (x[1] << 31);
+                    ov[2 * c + 1] = (x[2] >> 1) | (x[3] << 31);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
             {
-                const VB bc = *reinterpret_cast<const VB*>(g.client + so + i0);
-                const VB br = *reinterpret_cast<const VB*>(g.rclient + so + i0);
-                const VB bf = *reinterpret_cast<const VB*>(g.flags + so + i0);
+                const VU bc = ld_u8(g.client + so + i0);
+                const VU br = ld_u8(g.rclient + so + i0);
+                const VU bf = ld_u8(g.flags + so + i0);
 #pragma unroll
-                for (int j = 0; j < K; j++)
-                    cf[j] = live[j] ? ((uint32_t)bc[j] | ((uint32_t)br[j] << 8) | ((uint32_t)bf[j] << 16)) : kEmptyCf;
+                for (int j = 0; j < K; j++) {
+                    const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
+                    const uint32_t v = bc[j] | (br[j] << 8) | ((bf[j] & 7u) << 16) |
+                                       ((mk & 1) ? (F_BS | ((uint32_t)(mk >> 1) << SC_SHIFT)) : 0u);
+                    cf[j] = i0 + j < n ? v : kEmptyCf;
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        cum = 0;
-        wave_sync();
+        // empty leaf blocks (rare): a dead slot holds each one's place and marks
+        if (nempty) {
+            if (ns + nempty > CAP) {
+                fail(MT_DERR_CAPACITY, cur_seq);
+            } else {
+                int carry = 0, placed = 0;
+                for (int base = 0; base < nb0; base += 64) {
+                    const int b = base + lane;
+                    const int c = b < nb0 ? (int)g.lbcnt[lo + b] : 0;
+                    const int scv = b < nb0 ? (int)g.lbscour[lo + b] : 0;
+                    const int incl = wave_incl_scan(c) + carry;
+                    uint64_t em = wave_ballot(b < nb0 && c == 0);
+                    while (em) {
+                        const int fl = first_lane(em);
+                        em &= em - 1;
+                        Elem ph;
+                        ph.seq = 0x7fffffff;
+                        ph.rseq = 0;
+                        ph.li = kEmptyLi;
+                        ph.cf = kEmptyCf | F_BS | ((uint32_t)__builtin_amdgcn_readlane(scv, fl) << SC_SHIFT);
+                        ph.ov = 0;
+                        ph.cum = 0;
+                        shift_in<false>(__builtin_amdgcn_readlane(incl - c, fl) + placed, ph);
+                        placed++;
+                    }
+                    carry = wave_last(incl);
+                }
+            }
+        }
         arena = abase + (size_t)text_half * textcap;
+    }
+
+    // one register field -> HBM in position order, staged through LDS (scattered LDS writes,
+    // coalesced HBM stores; no per-slot 64-bit addresses kept live)
+    template <class T, class F>
+    MT_DEV void store_field(const T (&v)[K], uint32_t lb, int pbase, int nn, F&& put) {
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if ((lb >> j) & 1u) s.scr[pbase + __popc(lb & ((1u << j) - 1u))] = (int32_t)v[j];
+        wave_sync();
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int i = lane; i < nn; i += 64) put(i, (uint32_t)s.scr[i]);
+        wave_sync();
     }
 
     MT_DEV void store(const mt_gstate& g, uint32_t d) {
         const size_t so = (size_t)d * g.segcap;
-        if ((uint32_t)n > g.segcap || nbl(0) > (int)g.lbcap || heap_n >= (int)g.hcap) fail(MT_DERR_CAPACITY, cur_seq);
-        const int nn = min(n, (int)g.segcap);
-        typedef uint32_t V2U __attribute__((ext_vector_type(2 * K)));
-        typedef uint8_t VB __attribute__((ext_vector_type(K)));
-        typedef uint64_t V64 __attribute__((ext_vector_type(K)));
-        const int i0 = lane * K;
-        if (i0 < nn) {  // whole-lane vector stores, field by field; slots past nn carry filler
-            *reinterpret_cast<VI*>(g.seq + so + i0) = seq;
-            *reinterpret_cast<VI*>(g.rseq + so + i0) = rseq;
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                V2U ov;
+        // live slots -> positions (dead slots are squeezed out here)
+        const uint32_t lb = live_bits();
+        const int c = __popc(lb);
+        const int incl = wave_incl_scan(c);
+        const int pbase = incl - c;
+        const int nn = wave_last(incl);
+        store_field(seq, lb, pbase, nn, [&](int i, uint32_t v) { g.seq[so + i] = (int32_t)v; });
+        store_field(rseq, lb, pbase, nn, [&](int i, uint32_t v) { g.rseq[so + i] = (int32_t)v; });
+        store_field(ov, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] = (uint64_t)v << 1; });
+        store_field(cf, lb, pbase, nn, [&](int i, uint32_t v) {
+            g.client[so + i] = (uint8_t)(v & 0xFFu);
+            g.rclient[so + i] = (uint8_t)((v >> 8) & 0xFFu);
+            g.flags[so + i] = (uint8_t)((v >> 16) & 7u);
+        });
+        store_field(li, lb, pbase, nn, [&](int i, uint32_t v) {
+            const uint32_t id = id_of(v);
+            g.len[so + i] = len_of(v);
+            g.toff[so + i] = s.toff[id];
+            g.props[so + i] = s.props[id];
+        });
+        // leaf blocks: live children and needsScour, in block order
+        const uint32_t bm = bs_bits();
+        const int bc = __popc(bm);
+        const int bbase = wave_incl_scan(bc) - bc;
 #pragma unroll
-                for (int j = 0; j < K; j++) {
-                    ov[2 * j] = o0[j];
-                    ov[2 * j + 1] = o1[j];
-                }
-                *reinterpret_cast<V2U*>(g.ovl + so + i0) = ov;
+        for (int j = 0; j < K; j++) {
+            if ((bm >> j) & 1u) {
+                const int b = bbase + __popc(bm & ((1u << j) - 1u));
+                s.scr[b] = pbase + __popc(lb & ((1u << j) - 1u));
+                s.lbsc[b] = (uint8_t)((cf[j] >> SC_SHIFT) & 3u);
             }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                VB bc, br, bf;
-#pragma unroll
-                for (int j = 0; j < K; j++) {
-                    bc[j] = (uint8_t)(cf[j] & 0xFFu);
-                    br[j] = (uint8_t)((cf[j] >> 8) & 0xFFu);
-                    bf[j] = (uint8_t)((cf[j] >> 16) & 0xFFu);
-                }
-                *reinterpret_cast<VB*>(g.client + so + i0) = bc;
-                *reinterpret_cast<VB*>(g.rclient + so + i0) = br;
-                *reinterpret_cast<VB*>(g.flags + so + i0) = bf;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                VU ln;
-#pragma unroll
-                for (int j = 0; j < K; j++) ln[j] = len_of(li[j]);
-                *reinterpret_cast<VU*>(g.len + so + i0) = ln;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                VU to;
-#pragma unroll
-                for (int j = 0; j < K; j++) to[j] = s.toff[min(id_of(li[j]), (uint32_t)(CAP - 1))];
-                *reinterpret_cast<VU*>(g.toff + so + i0) = to;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < K; j++) g.props[so + i0 + j] = s.props[min(id_of(li[j]), (uint32_t)(CAP - 1))];
         }
+        if (lane == 0) s.scr[nb0] = nn;
         wave_sync();
+        const size_t lo = (size_t)d * g.lbcap;
+        int nempty = 0;
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int b = lane; b < nb0; b += 64) {
+            const int cnt = s.scr[b + 1] - s.scr[b];
+            g.lbcnt[lo + b] = (uint8_t)cnt;
+            g.lbscour[lo + b] = s.lbsc[b];
+            nempty += cnt == 0 ? 1 : 0;
+        }
+        nempty = wave_total(nempty);
         // id -> position for the heap remap (toff is dead now)
 #pragma clang loop unroll(disable) vectorize(disable)
         for (int i = lane; i < next_id; i += 64) s.toff[i] = kDead;
         wave_sync();
 #pragma unroll
-        for (int j = 0; j < K; j++) {
-            const int i = idx(j);
-            if (i < nn) s.toff[id_of(li[j])] = (uint16_t)i;
-        }
+        for (int j = 0; j < K; j++)
+            if ((lb >> j) & 1u) s.toff[id_of(li[j])] = (uint16_t)(pbase + __popc(lb & ((1u << j) - 1u)));
         wave_sync();
-        const size_t lo = (size_t)d * g.lbcap;
-        const int nb0 = min(nbl(0), (int)g.lbcap);
-#pragma clang loop unroll(disable) vectorize(disable)
-        for (int i = lane; i < nb0; i += 64) {
-            g.lbcnt[lo + i] = s.lbcnt[i];
-            g.lbscour[lo + i] = s.lbscour[i];
-        }
         for (int Lv = 1; Lv < nlev; Lv++) {
             const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv - 1)) * g.ibcap;
             const int nbl_ = min(nbl(Lv), (int)g.ibcap);
 #pragma clang loop unroll(disable) vectorize(disable)
             for (int i = lane; i < nbl_; i += 64) g.ibcnt[io + i] = s.ibcnt[Lv - 1][i];
         }
+        if (heap_n >= (int)g.hcap) fail(MT_DERR_CAPACITY, cur_seq);
         const size_t ho = (size_t)d * g.hcap;
         const int hn = min(heap_n, (int)g.hcap - 1);
 #pragma clang loop unroll(disable) vectorize(disable)
@@ -1161,13 +1339,18 @@ struct RWave {
             sc.err_seq = err_seq;
             sc.text_top = text_top;
             sc.text_half = text_half;
+            sc.n_empty = (uint32_t)nempty;
+            sc.nb[0] = nb0;
         }
-        if (lane < MT_MAXLEV) g.sc[d].nb[lane] = s.nb[lane];
+        if (lane >= 1 && lane < MT_MAXLEV) g.sc[d].nb[lane] = s.nb[lane];
     }
 };
 
+// Two waves per SIMD for the big classes: the state is register-resident, so occupancy is what
+// hides the latency of each op's dependent steps (a few spills at K = 16 are cheaper than one
+// wave per SIMD).
 template <int K>
-__global__ __launch_bounds__(64) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 8 ? 2 : 3))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
@@ -1198,7 +1381,9 @@ __global__ __launch_bounds__(64) void reg_apply_kernel(mt_gstate g, const mt_op_
     PROF_END(wv.prof, P_STORE, tt);
 #ifdef MT_PROF
     if (wv.lane == 0)
-        for (int q = 0; q < P_NSLOT; q++) atomicAdd(&mt_prof_acc[(K == 2 ? 0 : K == 4 ? 24 : K == 8 ? 48 : 72) + q], (unsigned long long)wv.prof[q]);
+        for (int q = 0; q < P_NSLOT; q++)
+            atomicAdd(&mt_prof_acc[(K == 2 ? 0 : K == 4 ? 24 : K == 8 ? 48 : K == 12 ? 72 : 96) + q],
+                      (unsigned long long)wv.prof[q]);
 #endif
 }
 
@@ -1220,6 +1405,7 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
         MTR_LAUNCH(128)
         MTR_LAUNCH(256)
         MTR_LAUNCH(512)
+        MTR_LAUNCH(768)
         MTR_LAUNCH(1024)
         default:
             return hipErrorInvalidValue;
@@ -1230,9 +1416,10 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
 // diagnostic: read (and clear) the per-phase cycle totals of a -DMT_PROF build (zeros otherwise)
 extern "C" int mt_prof_read(unsigned long long* out, int n) {
 #ifdef MT_PROF
-    if (n > 96) n = 96;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mtr::mt_prof_acc), n * sizeof(unsigned long long)) != hipSuccess) return -1;
-    unsigned long long z[96] = {0};
+    if (n > 120) n = 120;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mtr::mt_prof_acc), n * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long z[120] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(mtr::mt_prof_acc), z, sizeof z) != hipSuccess) return -1;
     return n;
 #else

@@ -37,11 +37,13 @@ extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_
                                     uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 
 namespace {
-const int32_t kClasses[] = {128, 256, 512, 1024, 2048};
-constexpr int kNumClasses = 5;
-// {CAP, LB, IB, H} per class: must match mt::Lds<CAP> in mt_apply.hip
-const int32_t kClassParams[kNumClasses * 4] = {
-    128, 64, 24, 128, 256, 128, 40, 192, 512, 256, 72, 320, 1024, 512, 136, 576, 2048, 1024, 264, 1088};
+const int32_t kClasses[] = {128, 256, 512, 768, 1024, 2048};
+constexpr int kNumClasses = 6;
+// {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
+const int32_t kClassParams[kNumClasses * 4] = {128,  64,  24,  128, 256,  128, 40,  192, 512,  256,  72,  320,
+                                               768,  384, 104, 448, 1024, 512, 136, 576, 2048, 1024, 264, 1088};
+// the LDS engine has no 768 instantiation: its 1024 kernel serves that class
+int lds_cap(int cap) { return cap == 768 ? 1024 : cap; }
 }  // namespace
 
 struct mt_batch {
@@ -252,7 +254,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 HIP_OK(mt_launch_apply_reg(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
                                            e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
             else
-                HIP_OK(mt_launch_apply(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
                                        e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
             e->kev_cls.push_back(c);
@@ -333,7 +335,7 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
         if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
         for (int c = 0; r == hipSuccess && c < kNumClasses; c++) {
             if (!e->h_counts[c]) continue;
-            r = mt_launch_gen(kClasses[c], &e->g, cfg, doc_id_base, cref, stall, pay_used, payload_per_doc, b->ops,
+            r = mt_launch_gen(lds_cap(kClasses[c]), &e->g, cfg, doc_id_base, cref, stall, pay_used, payload_per_doc, b->ops,
                               b->payload, b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);
         }
     }
@@ -425,6 +427,19 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
     if (kernel_ms) *kernel_ms = e->cls_ms[cls];
     if (launches) *launches = e->cls_launches[cls];
     if (alg_bytes) *alg_bytes = e->cls_bytes[cls];
+    return MT_OK;
+}
+
+mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint64_t cap) {
+    if (!e || !buf || !cap) return MT_ERR_ARG;
+    char tmp[96];
+    if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)
+        snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel<%u>", capacity / 64);
+    else
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)capacity));
+    const size_t n = std::min<size_t>(cap - 1, strlen(tmp));
+    memcpy(buf, tmp, n);
+    buf[n] = 0;
     return MT_OK;
 }
 

@@ -17,50 +17,76 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     sc.nseg = 0;
     sc.nlev = 1;
     sc.nb[0] = 1;
+    sc.n_empty = 1;  // the root leaf block starts empty
     g.sc[d] = sc;
     g.lbcnt[(size_t)d * g.lbcap] = 0;
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
 }
 
-// Bin the documents that have ops in this launch by the LDS capacity class they need.
-// Each op adds at most 2 segments (a boundary split + an insert, or two boundary splits),
-// at most 2 leaf blocks, and a handful of heap entries.  classes[k] = {CAP, LB, IB, H}.
+// Bin the documents that have ops in this launch by the capacity class they need.  Each op
+// adds at most 2 segments (a boundary split + an insert, or two boundary splits), at most 2 leaf
+// blocks, and a handful of heap entries; the register engine also pads one slot per empty leaf
+// block.  classes[k] = {CAP, LB, IB, H}.  Documents that ever see a client id above 32 go to the
+// last class (the LDS engine, 64-client overlap sets).  Binning is wave-aggregated: one atomic
+// per (wave, class).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes,
                               uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
                               const mt_op_rec* __restrict__ ops, unsigned long long* __restrict__ acc) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= n_docs) return;
-    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
-    const uint32_t a = min(r1, r0 + op_lo);
-    const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
-    const mt_doc_scalars sc = g.sc[d];
-    if (a >= b || sc.err) return;
-
-    const int nops = (int)(b - a);
-    int ib_need = 0;
-    for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
-    int c = n_classes - 1;
-    for (int k = 0; k < n_classes; k++) {
-        const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2], h = classes[4 * k + 3];
-        if (sc.nseg + 2 * nops + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb && ib_need + nops + 1 <= ib &&
-            sc.heap_n + 4 * nops + 16 <= h) {
-            c = k;
-            break;
+    int c = -1;
+    unsigned long long bytes = 0;
+    if (d < n_docs) {
+        const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+        const uint32_t a = min(r1, r0 + op_lo);
+        const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
+        const mt_doc_scalars sc = g.sc[d];
+        if (a < b && !sc.err) {
+            const int nops = (int)(b - a);
+            bool wide = sc.wide != 0;
+            if (!wide && ops) {
+                for (uint32_t i = a; i < b; i++) wide = wide || ops[i].client > 32;
+                if (wide) g.sc[d].wide = 1u;
+            }
+            int ib_need = 0;
+            for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
+            c = n_classes - 1;
+            for (int k = 0; k < n_classes && !wide; k++) {
+                const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
+                          h = classes[4 * k + 3];
+                if (sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb &&
+                    ib_need + nops + 1 <= ib && sc.heap_n + 4 * nops + 16 <= h) {
+                    c = k;
+                    break;
+                }
+            }
+            if (acc) {
+                // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
+                // accounting"): persistent state in + out, op records, payload
+                unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] +
+                                        6ull * sc.heap_n + sizeof(mt_doc_scalars);
+                for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
+                unsigned long long ob = 32ull * (b - a);
+                if (ops)
+                    for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
+                bytes = 2ull * st + ob;
+            }
         }
     }
-    const uint32_t at = atomicAdd(&counts[c], 1u);
-    ids[(size_t)c * n_docs + at] = d;
-    if (acc) {
-        // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
-        // accounting"): persistent state in + out, op records, payload; per class
-        unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] + 6ull * sc.heap_n +
-                                sizeof(mt_doc_scalars);
-        for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
-        unsigned long long ob = 32ull * (b - a);
-        if (ops)
-            for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
-        atomicAdd(&acc[c], 2ull * st + ob);
+    const int lane = (int)(threadIdx.x & 63u);
+    for (int k = 0; k < n_classes; k++) {
+        const uint64_t m = wave_ballot(c == k);
+        if (!m) continue;
+        const int leader = first_lane(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&counts[k], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (c == k) ids[(size_t)k * n_docs + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = d;
+        if (acc) {
+            unsigned long long v = c == k ? bytes : 0ull;
+            for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == leader) atomicAdd(&acc[k], v);
+        }
     }
 }
 

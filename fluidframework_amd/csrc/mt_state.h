@@ -33,7 +33,9 @@ struct mt_doc_scalars {      // 80 bytes
     int32_t err, err_seq;    // sticky per-document error (mt_doc_err) and the seq that raised it
     uint32_t text_top;       // bytes used in the current half of the document's text arena
     uint32_t text_half;      // which half of the double-buffered arena is current (0/1)
-    uint32_t pad[3];
+    uint32_t n_empty;        // leaf blocks without children (the register engine pads one slot each)
+    uint32_t wide;           // a client id above 32 was seen: the document stays on the LDS engine
+    uint32_t pad;
 };
 
 // Device pointers + capacities (one allocation per array, [n_docs][capacity]).

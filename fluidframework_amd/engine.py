@@ -70,11 +70,12 @@ def lib():
         L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
+        L.mt_class_kernel_name.argtypes = [vp, u32, ctypes.c_char_p, u64]
         L.mt_version.restype = ctypes.c_char_p
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
-                     'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats'):
+                     'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib

@@ -128,10 +128,13 @@ mt_status mt_doc_error(mt_engine* eng, uint32_t doc, int32_t* code, int32_t* seq
  * alg_bytes = algorithmic bytes they move (DESIGN.md "Roofline accounting"). */
 mt_status mt_last_apply_stats(mt_engine* eng, float* kernel_ms, float* wall_ms, uint32_t* launches,
                               uint64_t* alg_bytes);
-/* The same, per LDS capacity class (cls = 0..4 for 128/256/512/1024/2048 segments): each class
- * is one kernel instantiation, mt::apply_kernel<capacity, false> in a rocprof trace. */
+/* The same, per capacity class (cls = 0..5 for 128/256/512/768/1024/2048 segments; MT_ERR_ARG
+ * past the last): each class is one kernel instantiation (see mt_class_kernel_name). */
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);
+/* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class
+ * `capacity` on this engine: the register engine for <= 1024 segments, else the LDS engine. */
+mt_status mt_class_kernel_name(mt_engine* eng, uint32_t capacity, char* buf, uint64_t cap);
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 

@@ -30,12 +30,12 @@ eng = MergeEngine(a.docs, ops_per_launch=32)
 dev = eng.synthesize(seed=5, **cfg)
 L = lib()
 L.mt_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 96)()
-L.mt_prof_read(buf, 96)  # clear
+buf = (ctypes.c_ulonglong * 120)()
+L.mt_prof_read(buf, 120)  # clear
 eng.reset()
 eng.apply_staged(dev)
-L.mt_prof_read(buf, 96)
-for c, k in enumerate((2, 4, 8, 16)):
+L.mt_prof_read(buf, 120)
+for c, k in enumerate((2, 4, 8, 12, 16)):
     v = list(buf[24 * c:24 * c + len(SLOTS)])
     ops = v[SLOTS.index('ops')]
     if not ops:

@@ -1,0 +1,72 @@
+"""Both device engines against the CPU oracle on workloads that push them into their corners:
+documents that shrink to nothing (empty leaf blocks, packs, the register engine's padding slots),
+documents with more than 32 clients (routed to the LDS engine), every capacity class, several
+launch sizes; and the two engines against each other.  Run on the GPU box:
+python -m pytest tests -m gpu"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+WORKLOADS = {
+    # removes outpace inserts: documents repeatedly shrink towards empty
+    'shrink': dict(n_clients=8, ops_per_doc=1536, max_lag=16, p_insert=0.3, p_remove=0.7),
+    # 48 clients: overlap sets need 64 bits, so these documents run on the LDS engine
+    'wide': dict(n_clients=48, ops_per_doc=768, max_lag=24, n_keys=4, n_values=8, p_insert=0.5, p_remove=0.3,
+                 p_overlap=0.4, p_insert_props=0.2),
+    # annotate-heavy with a wide window: property runs block zamboni appends
+    'annotate': dict(n_clients=16, ops_per_doc=1024, max_lag=64, n_keys=8, n_values=4, p_insert=0.4,
+                     p_remove=0.15, p_overlap=0.3, p_null=0.2, p_rewrite=0.1, p_insert_props=0.3),
+    # insert-heavy: documents grow through every capacity class
+    'grow': dict(n_clients=4, ops_per_doc=2048, max_lag=4, n_keys=2, n_values=3, p_insert=0.85, p_remove=0.1,
+                 p_insert_props=0.5),
+}
+
+
+def _engine(n, b, engine=None):
+    from fluidframework_amd.engine import MergeEngine
+    old = os.environ.get('MTGPU_ENGINE')
+    try:
+        if engine:
+            os.environ['MTGPU_ENGINE'] = engine
+        else:
+            os.environ.pop('MTGPU_ENGINE', None)
+        return MergeEngine(n, ops_per_launch=b)
+    finally:
+        if old is None:
+            os.environ.pop('MTGPU_ENGINE', None)
+        else:
+            os.environ['MTGPU_ENGINE'] = old
+
+
+@pytest.mark.parametrize('b', [32, 7])
+@pytest.mark.parametrize('name', sorted(WORKLOADS))
+def test_workload_against_oracle(oracle_lib, name, b):
+    n = 128
+    batch = oracle_lib.generate(n, seed=4242, **WORKLOADS[name])
+    want = oracle_lib.Oracle(n).apply(batch, threads=8).checksums()
+    eng = _engine(n, b)
+    eng.apply(batch)
+    got = eng.checksums()
+    bad = np.nonzero(want != got)[0]
+    assert not len(bad), f'{len(bad)}/{n} docs differ, first {int(bad[0])}: err={eng.error(int(bad[0]))}'
+    assert all(eng.error(d) == (0, 0) for d in range(n))
+
+
+def test_engines_agree():
+    """The register engine and the LDS engine end in the same state on the same log."""
+    from fluidframework_amd.oplog import CONFIGS
+    from oracle import oracle
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 512
+    n = 192
+    batch = oracle.generate(n, seed=77, **cfg)
+    sums = []
+    for engine in (None, 'lds'):
+        eng = _engine(n, 32, engine)
+        eng.apply(batch)
+        sums.append(eng.checksums())
+    assert np.array_equal(sums[0], sums[1])

@@ -511,7 +511,7 @@ struct Wave {
         wave_sync();
         if (lane == 0) {
             s.len[prev] = pl + ql;
-            s.flags[prev] = (uint8_t)((s.flags[prev] & ~MT_SF_NL) | (s.flags[sl] & MT_SF_NL));
+            s.flags[prev] = (uint8_t)((s.flags[prev] & ~MT_SF_NL) | (s.flags[sl] & (MT_SF_NL | MT_SF_HASNL)));
         }
         s.text_top = top;
         wave_sync();
@@ -656,9 +656,15 @@ struct Wave {
             if (t < 0) return;
             if (!arena_reserve((uint32_t)tlen, S)) return;
             const uint32_t top = s.text_top;
+            bool hasnl = false;
             for (int base = 0; base < tlen; base += 64) {
                 const int i = base + lane;
-                if (i < tlen) arena[top + i] = pay[i];
+                uint8_t c = 0;
+                if (i < tlen) {
+                    c = pay[i];
+                    arena[top + i] = c;
+                }
+                hasnl = hasnl || wave_ballot(i < tlen && c == '\n') != 0;
             }
             __threadfence_block();
             if (lane == 0) {
@@ -669,7 +675,7 @@ struct Wave {
                 s.ovl[t] = 0;
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
-                uint8_t f = pay[tlen - 1] == '\n' ? MT_SF_NL : 0;
+                uint8_t f = (pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0);
                 uint64_t p = 0;
                 if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
                     f |= MT_SF_PDEF;

@@ -42,7 +42,8 @@ constexpr uint32_t kEmptyLi = kNoId << kLenBits;
 constexpr uint32_t F_RM = (uint32_t)MT_SF_REMOVED << 16;
 constexpr uint32_t F_PDEF = (uint32_t)MT_SF_PDEF << 16;
 constexpr uint32_t F_NL = (uint32_t)MT_SF_NL << 16;
-constexpr uint32_t F_DEAD = 8u << 16;    // unlinked or padding: not a child of any block
+constexpr uint32_t F_HASNL = (uint32_t)MT_SF_HASNL << 16;
+constexpr uint32_t F_DEAD = 0x80u << 16;  // unlinked or padding: not a child of any block
 constexpr uint32_t F_BS = 1u << 24;      // first slot of a leaf block
 constexpr uint32_t SC_SHIFT = 25;        // that block's needsScour (MT_SC_*), kept on its first slot
 constexpr uint32_t SC_MASK = 3u << SC_SHIFT;
@@ -119,16 +120,19 @@ struct RWave {
     uint8_t* arena;
     const uint32_t textcap;
 
-    // ---- document state in registers (blocked: slot i = lane * K + j).  Plain arrays that SROA
-    // splits into K independent SSA values each (every index is a constant after unrolling;
-    // element updates are selects, never a store on one branch, so no pointer phis).
-    int32_t seq[K], rseq[K];
-    uint32_t li[K], cf[K], ov[K];
-    int32_t cum[K];  // per-op scratch: inclusive visible prefix for the op's view
+    // ---- document state in registers (blocked: slot i = lane * K + j).  ext vectors: SSA values
+    // end to end, and a wave-uniform dynamic index becomes s_set_gpr_idx register indexing.
+    VI seq, rseq;
+    VU li, cf, ov;
+    VI cum;  // per-op scratch: inclusive visible prefix for the op's view
     // ---- uniform document scalars
     int ns, nlive, nb0, nlev, heap_n, cur_seq, min_seq, err, err_seq, next_id;
     uint32_t text_top, text_half;
     bool dirty;  // arena stores issued and not yet waited for
+    uint32_t pb; // the current op's payload, prefetched: lane i holds byte i (i < 64)
+    // per-lane K-bit masks of this lane's slots that start a leaf block / are live, kept in step
+    // with cf by every writer of the BS or DEAD bits
+    uint32_t bsm, lvm;
 #ifdef MT_PROF
     uint64_t prof[P_NSLOT] = {};
 #endif
@@ -148,17 +152,38 @@ struct RWave {
     MT_DEV static uint32_t id_of(uint32_t l) { return l >> kLenBits; }
 
     // ------------------------------------------------------------ slot masks
-    MT_DEV uint32_t bs_bits() const {
-        uint32_t m = 0;
+    MT_DEV uint32_t bs_bits() const { return bsm; }
+    MT_DEV uint32_t live_bits() const { return lvm; }
+    MT_DEV void remask() {  // recompute both masks from cf
+        uint32_t b = 0, l = 0;
 #pragma unroll
-        for (int j = 0; j < K; j++) m |= (cf[j] & F_BS) ? (1u << j) : 0u;
-        return m;
+        for (int j = 0; j < K; j++) {
+            b |= (cf[j] & F_BS) ? (1u << j) : 0u;
+            l |= (cf[j] & F_DEAD) ? 0u : (1u << j);
+        }
+        bsm = b;
+        lvm = l;
     }
-    MT_DEV uint32_t live_bits() const {
-        uint32_t m = 0;
-#pragma unroll
-        for (int j = 0; j < K; j++) m |= (cf[j] & F_DEAD) ? 0u : (1u << j);
-        return m;
+    // the masks after slot k's cf became v (uniform k)
+    MT_DEV void mask_slot(int k, uint32_t v) {
+        const int r = k - lane * K;
+        if (r >= 0 && r < K) {
+            const uint32_t bit = 1u << r;
+            bsm = (v & F_BS) ? (bsm | bit) : (bsm & ~bit);
+            lvm = (v & F_DEAD) ? (lvm & ~bit) : (lvm | bit);
+        }
+    }
+    // the masks after shift_in(p, e): slots >= p move up one, slot p takes e's bits
+    MT_DEV void mask_shift(int p, uint32_t ecf) {
+        const uint32_t lo = below(p);
+        const int r = p - lane * K;
+        const uint32_t cb = (uint32_t)shr1((int)((bsm >> (K - 1)) & 1u), 0);
+        const uint32_t cl = (uint32_t)shr1((int)((lvm >> (K - 1)) & 1u), 0);
+        const bool at = r >= 0 && r < K, above = r < 0;
+        const uint32_t eb = at ? (((ecf & F_BS) ? 1u : 0u) << r) : 0u;
+        const uint32_t el = at ? (((ecf & F_DEAD) ? 0u : 1u) << r) : 0u;
+        bsm = (bsm & lo) | (((bsm & ~lo) << 1) & kAll) | eb | (above ? cb : 0u);
+        lvm = (lvm & lo) | (((lvm & ~lo) << 1) & kAll) | el | (above ? cl : 0u);
     }
     // this lane's slots with index < k
     MT_DEV uint32_t below(int k) const {
@@ -191,66 +216,45 @@ struct RWave {
 
     // ------------------------------------------------------------ element access
     MT_DEV Elem get(int k) const {  // all fields of the slot at uniform position k
-        const int lk = k / K, jk = k % K;
-        // masked ORs, not selects: a select chain of loads folds into a load through a
-        // selected address, which would push the register arrays to scratch
-        uint32_t a = 0, b = 0, g = 0, c = 0, d = 0, e = 0;
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const uint32_t h = 0u - (uint32_t)(jk == j);
-            a |= (uint32_t)seq[j] & h;
-            b |= (uint32_t)rseq[j] & h;
-            c |= li[j] & h;
-            d |= cf[j] & h;
-            e |= ov[j] & h;
-            g |= (uint32_t)cum[j] & h;
-        }
+        const int lk = k / K, jk = uni(k % K);
         Elem r;
-        r.seq = __builtin_amdgcn_readlane((int)a, lk);
-        r.rseq = __builtin_amdgcn_readlane((int)b, lk);
-        r.li = (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
-        r.cf = (uint32_t)__builtin_amdgcn_readlane((int)d, lk);
-        r.ov = (uint32_t)__builtin_amdgcn_readlane((int)e, lk);
-        r.cum = __builtin_amdgcn_readlane((int)g, lk);
+        r.seq = __builtin_amdgcn_readlane(seq[jk], lk);
+        r.rseq = __builtin_amdgcn_readlane(rseq[jk], lk);
+        r.li = (uint32_t)__builtin_amdgcn_readlane((int)li[jk], lk);
+        r.cf = (uint32_t)__builtin_amdgcn_readlane((int)cf[jk], lk);
+        r.ov = (uint32_t)__builtin_amdgcn_readlane((int)ov[jk], lk);
+        r.cum = __builtin_amdgcn_readlane(cum[jk], lk);
         return r;
     }
     MT_DEV uint32_t get_cf(int k) const {
-        const int lk = k / K, jk = k % K;
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < K; j++) c |= cf[j] & (0u - (uint32_t)(jk == j));
-        return (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
+        const int jk = uni(k % K);
+        return (uint32_t)__builtin_amdgcn_readlane((int)cf[jk], k / K);
     }
     MT_DEV uint32_t get_li(int k) const {
-        const int lk = k / K, jk = k % K;
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < K; j++) c |= li[j] & (0u - (uint32_t)(jk == j));
-        return (uint32_t)__builtin_amdgcn_readlane((int)c, lk);
+        const int jk = uni(k % K);
+        return (uint32_t)__builtin_amdgcn_readlane((int)li[jk], k / K);
     }
     MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
-        const int lk = k / K, jk = k % K;
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const bool h = jk == j && lane == lk;
-            li[j] = h ? lv : li[j];
-            cf[j] = h ? cv : cf[j];
-        }
+        mask_slot(k, cv);
+        const int lk = k / K, jk = uni(k % K);
+        const bool me = lane == lk;
+        li[jk] = me ? lv : li[jk];
+        cf[jk] = me ? cv : cf[jk];
     }
     MT_DEV void set_cf(int k, uint32_t cv) {
-        const int lk = k / K, jk = k % K;
-#pragma unroll
-        for (int j = 0; j < K; j++) cf[j] = (jk == j && lane == lk) ? cv : cf[j];
+        mask_slot(k, cv);
+        const int lk = k / K, jk = uni(k % K);
+        cf[jk] = lane == lk ? cv : cf[jk];
     }
     MT_DEV void set_cum(int k, int32_t v) {
-        const int lk = k / K, jk = k % K;
-#pragma unroll
-        for (int j = 0; j < K; j++) cum[j] = (jk == j && lane == lk) ? v : cum[j];
+        const int lk = k / K, jk = uni(k % K);
+        cum[jk] = lane == lk ? v : cum[jk];
     }
 
     // insert e at slot p: slots >= p move one register right
     template <bool CUM>
     MT_DEV void shift_in(int p, const Elem& e) {
+        mask_shift(p, e.cf);
         const int32_t c_seq = shr1(seq[K - 1], 0), c_rseq = shr1(rseq[K - 1], 0);
         const uint32_t c_li = (uint32_t)shr1((int)li[K - 1], 0), c_cf = (uint32_t)shr1((int)cf[K - 1], 0);
         const uint32_t c_ov = (uint32_t)shr1((int)ov[K - 1], 0);
@@ -277,10 +281,12 @@ struct RWave {
     // ------------------------------------------------------------ visibility
     // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697); dead slots have length 0
     MT_DEV int vis(int j, int32_t R, int C) const {
+        // bitwise, not short-circuit: no branch per slot
         const uint32_t f = cf[j];
-        const bool seen = ((int)(f & 0xFFu) == C) || (seq[j] <= R);
-        const bool hid = (f & F_RM) && ((int)((f >> 8) & 0xFFu) == C || ((ov[j] >> (C - 1)) & 1u) || rseq[j] <= R);
-        return (seen && !hid) ? (int)len_of(li[j]) : 0;
+        const bool seen = ((f & 0xFFu) == (uint32_t)C) | (seq[j] <= R);
+        const bool hid = ((f & F_RM) != 0) & ((((f >> 8) & 0xFFu) == (uint32_t)C) | (((ov[j] >> (C - 1)) & 1u) != 0) |
+                                              (rseq[j] <= R));
+        return (seen & !hid) ? (int)len_of(li[j]) : 0;
     }
     // cum = inclusive prefix of vis over the slots; returns getLength(R, C)
     MT_DEV int scan(int32_t R, int C) {
@@ -511,8 +517,11 @@ struct RWave {
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
         const uint32_t id = id_of(e.li);
         const uint32_t to = uniu(s.toff[id]);
-        arena_sync();
-        const uint8_t last = arena[to + (uint32_t)off - 1];
+        uint8_t last = 0;  // a segment without any "\n" needs no text read
+        if (e.cf & F_HASNL) {
+            arena_sync();
+            last = arena[to + (uint32_t)off - 1];
+        }
         if (lane == 0) {
             s.props[t] = s.props[id];
             s.toff[t] = (uint16_t)(to + (uint32_t)off);
@@ -637,7 +646,8 @@ struct RWave {
         }
         const uint32_t pcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, p);
         const uint32_t lcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, (int)lastq);
-        set_li_cf(__builtin_amdgcn_readlane(vslot, p), total | (pid_ << kLenBits), (pcf & ~F_NL) | (lcf & F_NL));
+        const uint32_t anynl = __ballot(in_run && (vcf & F_HASNL)) ? F_HASNL : 0u;
+        set_li_cf(__builtin_amdgcn_readlane(vslot, p), total | (pid_ << kLenBits), (pcf & ~F_NL) | (lcf & F_NL) | anynl);
     }
 
     // scourNode on the leaf block whose slots are [a, e) (mergeTree.ts:1289-1365); returns the
@@ -734,6 +744,7 @@ struct RWave {
             li[j] = k_ ? (li[j] & ~kLenMask) : li[j];
             cf[j] = k_ ? (cf[j] | F_DEAD) : cf[j];
         }
+        lvm &= ~kill;
         nlive -= __popc(unlink);
         return kept;
     }
@@ -798,6 +809,7 @@ struct RWave {
                 cf[j] = v;
             }
         }
+        remask();
         nb0 += cc - m;
         if (lane == 0) s.ibcnt[0][P] = (uint8_t)cc;
         wave_sync();
@@ -857,10 +869,16 @@ struct RWave {
     }
 
     // -------------------------------------------------------------------- ops
-    static MT_DEV uint64_t apply_pairs(uint64_t p, const uint8_t* pairs, int np) {
+    // byte i of the current op's payload (uniform i): from the prefetch register when it can
+    MT_DEV uint32_t pbyte(const uint8_t* pay, int i) const {
+        return i < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)pb, i) : (uint32_t)pay[i];
+    }
+    // props: apply the op's (key, value) pairs at payload offset off; value 0 = null = delete
+    // (properties.ts:95-116)
+    MT_DEV uint64_t apply_pairs(uint64_t p, const uint8_t* pay, int off, int np) const {
         for (int q = 0; q < np; q++) {
-            const int k = pairs[2 * q];
-            const uint64_t v = pairs[2 * q + 1];
+            const int k = (int)pbyte(pay, off + 2 * q);
+            const uint64_t v = pbyte(pay, off + 2 * q + 1);
             p = (p & ~(0xFFull << (8 * k))) | (v << (8 * k));
         }
         return p;
@@ -869,20 +887,20 @@ struct RWave {
     // blockInsert (mergeTree.ts:2141-2224) of a text segment at pos, after the boundary split:
     // choose its slot k in leaf block b, write its text and cold fields, build its element.
     // Returns its id (< 0 on error) and its child index inside block b before a possible split.
-    MT_DEV int place_prep(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np, Elem& en,
+    MT_DEV int place_prep(const mt_op_rec op, const uint8_t* pay, int tlen, int np, Elem& en,
                           int& k, int& b, int& idx_in) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, pos = op.pos1;
         // insertingWalk descends into the first block whose cumulative visible end >= pos
         // (breakTie is true for blocks, :2248-2277): that leaf block's last slot is the first
         // block-ending slot with cum >= pos
-        const uint32_t bsm = bs_bits();
-        const int nxt = shl1((int)(bsm & 1u), 0);
+        const uint32_t bm = bs_bits();
+        const int nxt = shl1((int)(bm & 1u), 0);
         int last = 0x7fffffff;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
             const int i = idx(j);
-            const bool ends = (j + 1 < K ? ((bsm >> (j + 1)) & 1u) != 0 : nxt != 0) || i == ns - 1;
+            const bool ends = (j + 1 < K ? ((bm >> (j + 1)) & 1u) != 0 : nxt != 0) || i == ns - 1;
             last = (i < ns && ends && cum[j] >= pos) ? i : last;
         }
         last = wave_min(last);
@@ -912,16 +930,19 @@ struct RWave {
         if (t < 0) return -1;
         if (!arena_reserve((uint32_t)tlen, S)) return -1;
         const uint32_t top = text_top;
+        bool hasnl = false;
         for (int base = 0; base < tlen; base += 64) {
             const int i = base + lane;
-            if (i < tlen) arena[top + i] = pay[i];
+            const uint8_t c = i < tlen ? (uint8_t)(base == 0 ? pb : pay[i]) : 0;
+            if (i < tlen) arena[top + i] = c;
+            hasnl = hasnl || __ballot(i < tlen && c == '\n') != 0;
         }
         dirty = true;
-        uint32_t fl = pay[tlen - 1] == '\n' ? F_NL : 0u;
+        uint32_t fl = (pbyte(pay, tlen - 1) == '\n' ? F_NL : 0u) | (hasnl ? F_HASNL : 0u);
         uint64_t p = 0;
         if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
             fl |= F_PDEF;
-            p = apply_pairs(0, pairs, np);
+            p = apply_pairs(0, pay, tlen, np);
         }
         if (lane == 0) {
             s.props[t] = p;
@@ -940,7 +961,7 @@ struct RWave {
 
     // markRangeRemoved / annotateRange leaf actions over mapRange (mergeTree.ts:2607-2719,
     // 2565-2605, 2903-2965) after the two boundary splits
-    MT_DEV void range_action(const mt_op_rec& op, const uint8_t* pairs, int np) {
+    MT_DEV void range_action(const mt_op_rec op, const uint8_t* pay, int tlen, int np) {
         const int32_t S = op.seq;
         const int C = op.client, start = op.pos1, end = op.pos2;
         const bool is_remove = op.type == MT_OP_REMOVE;
@@ -968,7 +989,7 @@ struct RWave {
                     const uint32_t id = id_of(li[j]);
                     uint64_t p = (f & F_PDEF) ? s.props[id] : 0;
                     if (rewrite) p = 0;
-                    s.props[id] = apply_pairs(p, pairs, np);
+                    s.props[id] = apply_pairs(p, pay, tlen, np);
                 }
                 cs = ce;
             }
@@ -988,20 +1009,19 @@ struct RWave {
     // Client.applyMsg for the observer (client.ts:797-828): the op, then updateSeqNumbers
     // (client.ts:821-828, MergeTree.setMinSeq mergeTree.ts:1718-1736).  Every register-heavy
     // routine has exactly one call site.
-    MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
+    MT_DEV void apply(const mt_op_rec op, const uint8_t* payload) {
         const int np = op.flags >> MT_F_NPAIRS_SHIFT;
         const int32_t S = op.seq;
         if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
-        const uint8_t* pairs = pay + tlen;
         if (op.type != MT_OP_NOOP) {
             if (op.client == 0 || op.client > kNarrowClients) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
             if (!(cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);      // client.ts:461-462
             if (!(min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // client.ts:463-464
             for (int q = 0; q < np; q++)
-                if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
+                if (pbyte(pay, tlen + 2 * q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
             const bool ins = op.type == MT_OP_INSERT;
             if (op.pos1 < 0 || (!ins && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
             PROF_BEGIN(t0);
@@ -1021,7 +1041,7 @@ struct RWave {
                         continue;
                     }
                 } else {
-                    t = place_prep(op, pay, tlen, pairs, np, e, k, b, idx_in);
+                    t = place_prep(op, pay, tlen, np, e, k, b, idx_in);
                     if (t < 0) return;
                 }
                 const int before_nb = nb0;
@@ -1039,7 +1059,7 @@ struct RWave {
             }
             if (!ins) {
                 PROF_BEGIN(t2);
-                range_action(op, pairs, np);
+                range_action(op, pay, tlen, np);
                 PROF_END(prof, P_RANGE, t2);
             }
             if (err) return;
@@ -1207,13 +1227,14 @@ struct RWave {
 #pragma unroll
                 for (int j = 0; j < K; j++) {
                     const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
-                    const uint32_t v = bc[j] | (br[j] << 8) | ((bf[j] & 7u) << 16) |
+                    const uint32_t v = bc[j] | (br[j] << 8) | ((bf[j] & 0xFu) << 16) |
                                        ((mk & 1) ? (F_BS | ((uint32_t)(mk >> 1) << SC_SHIFT)) : 0u);
                     cf[j] = i0 + j < n ? v : kEmptyCf;
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        remask();
         // empty leaf blocks (rare): a dead slot holds each one's place and marks
         if (nempty) {
             if (ns + nempty > CAP) {
@@ -1249,7 +1270,7 @@ struct RWave {
     // one register field -> HBM in position order, staged through LDS (scattered LDS writes,
     // coalesced HBM stores; no per-slot 64-bit addresses kept live)
     template <class T, class F>
-    MT_DEV void store_field(const T (&v)[K], uint32_t lb, int pbase, int nn, F&& put) {
+    MT_DEV void store_field(const T& v, uint32_t lb, int pbase, int nn, F&& put) {
 #pragma unroll
         for (int j = 0; j < K; j++)
             if ((lb >> j) & 1u) s.scr[pbase + __popc(lb & ((1u << j) - 1u))] = (int32_t)v[j];
@@ -1273,7 +1294,7 @@ struct RWave {
         store_field(cf, lb, pbase, nn, [&](int i, uint32_t v) {
             g.client[so + i] = (uint8_t)(v & 0xFFu);
             g.rclient[so + i] = (uint8_t)((v >> 8) & 0xFFu);
-            g.flags[so + i] = (uint8_t)((v >> 16) & 7u);
+            g.flags[so + i] = (uint8_t)((v >> 16) & 0xFu);
         });
         store_field(li, lb, pbase, nn, [&](int i, uint32_t v) {
             const uint32_t id = id_of(v);
@@ -1349,6 +1370,22 @@ struct RWave {
 // Two waves per SIMD for the big classes: the state is register-resident, so occupancy is what
 // hides the latency of each op's dependent steps (a few spills at K = 16 are cheaper than one
 // wave per SIMD).
+// an op record as field loads (a struct copy would go through a private-memory temporary)
+MT_DEV mt_op_rec load_op(const mt_op_rec* p) {
+    mt_op_rec r;
+    r.seq = p->seq;
+    r.ref_seq = p->ref_seq;
+    r.msn = p->msn;
+    r.client = p->client;
+    r.type = p->type;
+    r.flags = p->flags;
+    r.pos1 = p->pos1;
+    r.pos2 = p->pos2;
+    r.payload_off = p->payload_off;
+    r.payload_len = p->payload_len;
+    return r;
+}
+
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 8 ? 2 : 3))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
@@ -1368,9 +1405,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 8 ? 2 :
     PROF_BEGIN(tl);
     wv.load(g, d);
     PROF_END(wv.prof, P_LOAD, tl);
+    // software pipeline: the record of op i+2 and the payload of op i+1 are in flight while op i
+    // is applied
+    mt_op_rec q0 = load_op(ops + a);
+    mt_op_rec q1 = a + 1 < b ? load_op(ops + a + 1) : q0;
+    uint32_t pb0 = wv.lane < (int)q0.payload_len ? payload[q0.payload_off + wv.lane] : 0u;
     for (uint32_t i = a; i < b; i++) {
         if (wv.err) break;
-        const mt_op_rec op = ops[i];
+        const mt_op_rec op = q0;
+        wv.pb = pb0;
+        q0 = q1;
+        if (i + 2 < b) q1 = load_op(ops + i + 2);
+        pb0 = (i + 1 < b && wv.lane < (int)q0.payload_len) ? payload[q0.payload_off + wv.lane] : 0u;
         wv.apply(op, payload);
 #ifdef MT_PROF
         wv.prof[P_OPS]++;

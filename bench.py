@@ -33,6 +33,19 @@ sys.path.insert(0, HERE)
 
 METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofline'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof_r01.sh -> tools/pmc_traffic.py)
+PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r01_pmc_traffic.json')
+
+
+def pmc_traffic(kernel):
+    """Measured HBM bytes per launch of `kernel` (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected),
+    from the committed PMC summary of the same bench command; None if it was not profiled."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            k = json.load(f)['kernels'].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return int(k['hbm_bytes_per_launch']) if k else None
 
 
 def parse():
@@ -163,7 +176,8 @@ def main():
             },
             'roofline': {
                 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(eng.class_kernel(dom)),
+                'traffic_source': os.path.relpath(PMC_TRAFFIC, HERE) + ' (bytes per launch)',
                 'kernel': eng.class_kernel(dom), 'launches': d_n,
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
                 'all_apply_kernels': {'launches': launches, 'kernel_ms': round(kern_ms, 2),

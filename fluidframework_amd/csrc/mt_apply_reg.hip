@@ -1387,7 +1387,7 @@ MT_DEV mt_op_rec load_op(const mt_op_rec* p) {
 }
 
 template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 8 ? 2 : 3))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? 2 : (K == 8 ? 3 : 4)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,

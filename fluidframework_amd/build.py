@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libmtgpu.so')
-SOURCES = ['mt_apply.hip', 'mt_apply_reg.hip', 'mt_service.hip', 'mt_engine.cpp']
+SOURCES = ['mt_apply.hip', 'mt_apply_reg.hip', 'mt_service.hip', 'mt_deli.hip', 'mt_engine.cpp']
 HEADERS = ['mt_state.h', 'mt_wave.h', 'mt_checksum.h', 'mt_synth.h', '../../include/mtgpu.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')

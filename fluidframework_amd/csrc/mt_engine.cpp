@@ -360,6 +360,14 @@ mt_status mt_batch_info(const mt_batch* b, uint64_t* n_ops, uint64_t* payload_by
     return MT_OK;
 }
 
+mt_status mt_batch_device_ptrs(const mt_batch* b, mt_op_rec** ops, uint8_t** payload, uint32_t** row_ptr) {
+    if (!b) return MT_ERR_ARG;
+    if (ops) *ops = b->ops;
+    if (payload) *payload = b->payload;
+    if (row_ptr) *row_ptr = b->row_ptr;
+    return MT_OK;
+}
+
 mt_status mt_batch_copy_docs(mt_engine* e, const mt_batch* b, uint32_t d0, uint32_t d1, mt_op_rec* ops,
                              uint64_t* n_ops, uint8_t* payload, uint64_t* payload_bytes, uint32_t* row_ptr) {
     if (!e || !b || d0 > d1 || d1 > b->n_docs) return MT_ERR_ARG;

@@ -168,8 +168,116 @@ mt_status mt_batch_copy_docs(mt_engine* eng, const mt_batch* batch, uint32_t d0,
                              uint64_t* n_ops, uint8_t* payload, uint64_t* payload_bytes, uint32_t* row_ptr);
 /* algorithmic bytes of a batch's ops + payload (for the roofline accounting in bench.py) */
 mt_status mt_batch_info(const mt_batch* batch, uint64_t* n_ops, uint64_t* payload_bytes, uint32_t* max_ops_per_doc);
+/* device pointers of a staged batch (to chain device-side stages, e.g. deli -> apply) */
+mt_status mt_batch_device_ptrs(const mt_batch* batch, mt_op_rec** ops, uint8_t** payload, uint32_t** row_ptr);
 
 const char* mt_version(void);
+
+/* ---- deli: per-document sequence-number / MSN ticketing ----------------
+ * Replaces, for many documents at once, the ordering service's per-document sequencer:
+ *   DeliLambda.ticket(rawMessage)        server/routerlicious/packages/lambdas/src/deli/lambda.ts:255-544
+ *   DeliLambda.handler's lastSentMSN     lambda.ts:173-246 (lastSentMSN = msn of every sent or nacked ticket)
+ *   ClientSequenceNumberManager          deli/clientSeqManager.ts:70-143 (upsert/remove/min refSeq)
+ *   new DeliLambda(.., lastCheckpoint)   lambda.ts:112-171 (clients + sequenceNumber from IDeliState)
+ * Raw messages arrive grouped by document (CSR row_ptr, each document's messages in log order);
+ * client ids are per-document short ids 0..63 interned by the host (the reference keys clients by
+ * their long id string).  One output ticket per raw message.  Out of scope: branch Integrate
+ * messages, idle-client eviction and NoClient/idle timers (they only enqueue new raw messages back
+ * to the ordering service, which a host feeds in as MT_RAW_LEAVE / MT_RAW_SERVER_NOOP), summarize
+ * scopes (every client may summarize), traces, DSN bookkeeping of Control messages. */
+typedef enum mt_raw_kind {
+    MT_RAW_OP = 0,          /* client op (Operation, Summarize, ...): revs seq        lambda.ts:414-435 */
+    MT_RAW_NOOP = 1,        /* client NoOp, contents null: consolidated later       lambda.ts:463-465 */
+    MT_RAW_NOOP_DATA = 2,   /* client NoOp with contents: revs only if the msn moved lambda.ts:466-471 */
+    MT_RAW_JOIN = 3,        /* ClientJoin of `client` (system message)              lambda.ts:286-299 */
+    MT_RAW_LEAVE = 4,       /* ClientLeave of `client`                              lambda.ts:281-285 */
+    MT_RAW_SERVER_NOOP = 5, /* server NoOp: revs if the msn moved, else never sent  lambda.ts:473-479 */
+    MT_RAW_NOCLIENT = 6,    /* NoClient: revs (ref = msn = seq) when nobody joined  lambda.ts:481-489 */
+    MT_RAW_CONTROL = 7      /* Control: never sent, never revs                      lambda.ts:490-517 */
+} mt_raw_kind;
+
+typedef struct mt_raw_msg {  /* 16 bytes */
+    int32_t csn;             /* operation.clientSequenceNumber                                     */
+    int32_t ref_seq;         /* operation.referenceSequenceNumber; -1 = REST op (revved to its seq) */
+    uint16_t client;         /* short id of the sending client, or of the joiner / leaver (< 64)   */
+    uint8_t kind;            /* mt_raw_kind                                                        */
+    uint8_t pad;
+    uint32_t reserved;
+} mt_raw_msg;
+
+typedef enum mt_ticket_status {
+    MT_TK_DROPPED = 0,      /* ticket() returns nothing: duplicate csn (lambda.ts:267-268), join of a
+                               joined client (:295-298), leave of an absent one (:283-285)          */
+    MT_TK_SENT = 1,         /* sequenced and sent (SendType.Immediate)                              */
+    MT_TK_LATER = 2,        /* SendType.Later: a consolidated client no-op                          */
+    MT_TK_NEVER = 3,        /* SendType.Never                                                       */
+    MT_TK_NACK_GAP = 4,     /* "Gap detected in incoming op"              lambda.ts:269-275, 613-620 */
+    MT_TK_NACK_CLIENT = 5,  /* "Nonexistent client" (never joined, left, or nacked) lambda.ts:309-316 */
+    MT_TK_NACK_REFSEQ = 6,  /* "Refseq r < msn"; the client stays nacked          lambda.ts:319-335 */
+    MT_TK_HALTED = 7        /* the document stopped at an earlier error (mt_deli_doc_error)         */
+} mt_ticket_status;
+
+typedef struct mt_ticket {  /* 16 bytes */
+    int32_t seq;            /* sequenceNumber of the output message (a nack: the msn it carries)   */
+    int32_t msn;            /* minimumSequenceNumber of the output message                         */
+    int32_t ref_seq;        /* referenceSequenceNumber as sequenced (REST -1 and NoClient: = seq)  */
+    uint8_t status;         /* mt_ticket_status                                                    */
+    uint8_t pad[3];
+} mt_ticket;
+
+/* per-document sticky deli errors (the reference lambda throws / has no representation) */
+typedef enum mt_deli_err {
+    MT_DELI_OK = 0,
+    MT_DELI_ERR_CLIENT = 1, /* short client id >= MT_MAX_CLIENTS                                    */
+    MT_DELI_ERR_KIND = 2,   /* unknown mt_raw_kind                                                  */
+    MT_DELI_ERR_ASSERT = 3  /* assert(refSeq >= msn) lambda.ts:426-428 (a client no-op with ref -1) */
+} mt_deli_err;
+
+typedef struct mt_deli_client {
+    int32_t csn;            /* clientSequenceNumber (IClientSequenceNumber)                         */
+    int32_t ref_seq;        /* referenceSequenceNumber                                              */
+    uint8_t joined;         /* tracked by the ClientSequenceNumberManager                           */
+    uint8_t nack;           /* nacked: every later message of this client is nacked                 */
+    uint8_t pad[2];
+} mt_deli_client;
+
+typedef struct mt_deli_checkpoint {  /* IDeliState (lambda.ts:754-764), device-representable part */
+    int32_t seq;            /* sequenceNumber                                                       */
+    int32_t msn;            /* minimumSequenceNumber (read back; derived on restore, lambda.ts:166-167) */
+    int32_t last_sent_msn;  /* lastSentMSN (0 for a freshly constructed lambda, lambda.ts:103)      */
+    int32_t err;            /* mt_deli_err (read back; ignored on restore)                          */
+    mt_deli_client clients[MT_MAX_CLIENTS];
+} mt_deli_checkpoint;
+
+typedef struct mt_deli mt_deli;
+mt_status mt_deli_create(int32_t device, uint32_t max_docs, mt_deli** out);
+mt_status mt_deli_destroy(mt_deli* dl);
+/* Construct documents [doc0, doc0+n) from checkpoints (NULL: new documents, sequenceNumber 0, no
+ * clients; lambda.ts:124-167).  The msn is derived from the clients as the constructor does. */
+mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_checkpoint* ckpts);
+/* Ticket a CSR batch of raw messages (host buffers, synchronous): n_docs+1 row pointers, document
+ * d's messages are msgs[row_ptr[d] .. row_ptr[d+1]).  out: one ticket per message. */
+mt_status mt_deli_ticket(mt_deli* dl, const mt_raw_msg* msgs, uint64_t n_msgs, const uint32_t* doc_row_ptr,
+                         uint32_t n_docs, mt_ticket* out);
+/* The same on device-resident buffers (HBM), asynchronous on the deli's stream.  d_ops (optional)
+ * fuses the hand-off to the apply engine: message i carries op record i (a stream of op messages
+ * only, 1:1), and each record gets the seq / msn / ref_seq of its ticket (seq = -1 when the
+ * message was not sent, which the apply engine rejects as MT_DERR_SEQ_ORDER). */
+mt_status mt_deli_ticket_device(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row_ptr, uint32_t n_docs,
+                                mt_ticket* d_out, mt_op_rec* d_ops);
+/* Bench tooling: construct documents [0, n_docs) all from the same checkpoint (device fill). */
+mt_status mt_deli_restore_all(mt_deli* dl, uint32_t n_docs, const mt_deli_checkpoint* ckpt);
+/* Bench tooling: the raw op messages behind a device op log (one MT_RAW_OP per record, client
+ * sequence numbers counted per client, ref_seq copied).  With every client joined at seq 0
+ * (mt_deli_restore_all), deli re-derives exactly the seq / msn the synthetic log carries. */
+mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
+                               mt_raw_msg* d_msgs);
+mt_status mt_deli_sync(mt_deli* dl);
+/* Kernel time of the last mt_deli_ticket / mt_deli_ticket_device (HIP events around the launch). */
+mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms);
+mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);
+/* err = mt_deli_err, index = position of the failing message inside the document's stream */
+mt_status mt_deli_doc_error(mt_deli* dl, uint32_t doc, int32_t* err, int32_t* index);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,122 @@
+"""GPU deli ticketing (fluidframework_amd/csrc/mt_deli.hip) through the C-ABI against the CPU
+oracle (oracle/deli.py): the lambda.spec.ts known answers, seeded random streams that take every
+branch of DeliLambda.ticket, checkpoints (restore / read back), sticky errors, and the fused
+deli -> apply hand-off on a synthetic op log.  Bit-exact: every ticket field and every
+checkpoint field must match.  Run on the GPU box: python -m pytest tests -m gpu"""
+import numpy as np
+import pytest
+
+from deli_streams import FIELDS, SPEC, oracle_tickets, random_streams, to_batch
+from oracle import deli as od
+
+pytestmark = pytest.mark.gpu
+
+
+def _tickets(t):
+    return np.stack([t['seq'], t['msn'], t['ref_seq'], t['status']], axis=1).astype(np.int64)
+
+
+def _seq(n):
+    from fluidframework_amd.deli import DeliSequencer
+    return DeliSequencer(n)
+
+
+def test_lambda_spec_known_answers():
+    streams = [s for _, s, _ in SPEC]
+    dl = _seq(len(streams))
+    got = _tickets(dl.ticket(*to_batch(streams)))
+    _, row_ptr = to_batch(streams)
+    want, _ = oracle_tickets(streams)
+    assert np.array_equal(got, want)
+    for d, (name, _, checks) in enumerate(SPEC):
+        for i, field, v in checks:
+            assert got[row_ptr[d] + i, FIELDS[field]] == v, (name, i, field)
+
+
+@pytest.mark.parametrize('seed,n_msgs,kw', [(1, 300, {}), (2, 1500, {'n_clients': 40}),
+                                            (3, 200, {'n_clients': 64, 'p_assert': 0.02, 'wide': True}),
+                                            (4, 64, {}), (5, 65, {'n_clients': 3})])
+def test_random_streams_against_oracle(seed, n_msgs, kw):
+    streams = random_streams(96, n_msgs, seed=seed, **kw)
+    streams[0] = []                                   # an empty document
+    want, docs = oracle_tickets(streams)
+    dl = _seq(len(streams))
+    got = _tickets(dl.ticket(*to_batch(streams)))
+    bad = np.nonzero(np.any(got != want, axis=1))[0]
+    assert not len(bad), f'{len(bad)} tickets differ, first {int(bad[0])}: got {got[bad[0]]} want {want[bad[0]]}'
+    for d in range(len(streams)):
+        ck = dl.checkpoint(d)
+        o = docs[d].checkpoint()
+        assert (ck['seq'], ck['msn'], ck['last_sent_msn'], ck['err']) == (o['seq'], o['msn'], o['last_sent_msn'],
+                                                                         o['err']), d
+        assert ck['clients'] == o['clients'], d
+        if o['err']:
+            assert dl.error(d) == (o['err'], docs[d].err_at)
+
+
+def test_batches_continue_the_state():
+    """Two launches over the halves of every stream == one launch over the whole streams."""
+    streams = random_streams(64, 700, seed=9, n_clients=20)
+    want, _ = oracle_tickets(streams)
+    _, rp = to_batch(streams)
+    dl = _seq(len(streams))
+    a = [s[:len(s) // 2] for s in streams]
+    b = [s[len(s) // 2:] for s in streams]
+    ta, tb = _tickets(dl.ticket(*to_batch(a))), _tickets(dl.ticket(*to_batch(b)))
+    _, rp_a = to_batch(a)
+    _, rp_b = to_batch(b)
+    for d in range(len(streams)):
+        got = np.concatenate([ta[rp_a[d]:rp_a[d + 1]], tb[rp_b[d]:rp_b[d + 1]]])
+        assert np.array_equal(got, want[rp[d]:rp[d + 1]]), d
+
+
+def test_restore_from_checkpoints():
+    streams = random_streams(32, 400, seed=21, n_clients=30)
+    cks = []
+    for d, s in enumerate(streams):
+        doc = od.DeliDoc()
+        for m in s[:len(s) // 2]:
+            doc.ticket(*m)
+        ck = doc.checkpoint()
+        cks.append({'seq': ck['seq'], 'clients': ck['clients'], 'last_sent_msn': ck['last_sent_msn']})
+    rest = [s[len(s) // 2:] for s in streams]
+    want, _ = oracle_tickets(rest, checkpoints=cks)
+    dl = _seq(len(streams))
+    dl.restore(cks)
+    assert np.array_equal(_tickets(dl.ticket(*to_batch(rest))), want)
+
+
+def test_deli_feeds_apply():
+    """C5's hand-off: raw op messages from a synthetic op log (every client joined at seq 0),
+    deli re-derives each op's seq / msn from (client, csn, refSeq) alone and stamps them into the
+    staged op records, and the apply engine replays the stamped log into the generator's state
+    (the synthetic msn is deli's: min over the clients' latest refSeq)."""
+    from fluidframework_amd.deli import RAW_DTYPE, TICKET_DTYPE, batch_device_ptrs
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.hipmem import DeviceBuffer
+    from fluidframework_amd.oplog import CONFIGS
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 256
+    n = 512
+    eng = MergeEngine(n, ops_per_launch=32)
+    dev = eng.synthesize(seed=3, **cfg)
+    want_cs = eng.checksums()
+    host = dev.to_host()
+    d_ops, _, d_row = batch_device_ptrs(dev)
+    msgs = DeviceBuffer(dev.n_ops * RAW_DTYPE.itemsize)
+    tick = DeviceBuffer(dev.n_ops * TICKET_DTYPE.itemsize)
+    dl = _seq(n)
+    dl.restore_all(seq=0, clients={c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)})
+    dl.raw_from_ops(d_ops, d_row, n, msgs.ptr)
+    dl.ticket_device(msgs.ptr, d_row, n, tick.ptr, d_ops)
+    dl.sync()
+    raw = msgs.download(RAW_DTYPE)
+    assert np.array_equal(raw['ref_seq'], host.ops['ref_seq']) and np.all(raw['kind'] == od.OP)
+    t = tick.download(TICKET_DTYPE)
+    assert np.all(t['status'] == od.SENT)
+    assert np.array_equal(t['seq'], host.ops['seq']) and np.array_equal(t['msn'], host.ops['msn'])
+    assert np.array_equal(dev.to_host().ops, host.ops)
+    eng.reset()
+    eng.apply_staged(dev)
+    assert np.array_equal(eng.checksums(), want_cs)

@@ -76,6 +76,7 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import CONFIGS
+    from fluidframework_amd.shard import doc_id_base, gather_checksums, max_over_ranks
 
     cfg = dict(CONFIGS[args.config])
     n_docs = args.docs or cfg.pop('n_docs')
@@ -91,7 +92,7 @@ def main():
 
     eng = MergeEngine(n_docs, device=local_rank, ops_per_launch=args.ops_per_launch)
     t0 = time.time()
-    dev = eng.synthesize(doc_id_base=rank * n_docs, seed=args.seed, **cfg)
+    dev = eng.synthesize(doc_id_base=doc_id_base(rank, n_docs), seed=args.seed, **cfg)
     gen_s = time.time() - t0
     gen_cs = eng.checksums()
     n_ops = dev.n_ops
@@ -119,25 +120,14 @@ def main():
             a[1] += n
             a[2] += b
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, device='cuda')
 
     cs = eng.checksums()
     errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 64)) if eng.error(d)[0])
     assert np.array_equal(cs, gen_cs), 'replay does not reproduce the generation state'
 
     # final per-document checksum gather to rank 0 over RCCL (the only collective)
-    digest = int(np.bitwise_xor.reduce(cs.view(np.int64))) if len(cs) else 0
-    if dist is not None:
-        t = torch.from_numpy(cs.view(np.int64).copy()).cuda()
-        gathered = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-        dist.gather(t, gathered, dst=0)
-        if rank == 0:
-            allcs = torch.cat(gathered).cpu().numpy()
-            digest = int(np.bitwise_xor.reduce(allcs))
+    _, digest = gather_checksums(cs, dist, device='cuda')
 
     total_ops = n_ops * world * args.steps
     value = total_ops / elapsed
@@ -187,7 +177,7 @@ def main():
             'cpu_baseline': cpu,
             'parity': parity,
             'doc_errors_sampled': errs,
-            'checksum_digest': '%016x' % (digest & 0xFFFFFFFFFFFFFFFF),
+            'checksum_digest': '%016x' % digest,
             'gen_seconds': round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)

@@ -8,13 +8,11 @@
 // sequenceNumber / minimumSequenceNumber.  Messages of one document are strictly sequential,
 // documents are independent.
 //
-// Device mapping: one wave64 per document, lane c owns client c's record (clientSequenceNumber,
-// referenceSequenceNumber, joined / nacked) in VGPRs, so the heap becomes a wave-wide min (six
-// DPP steps, no data-dependent memory traffic) and a client lookup is one v_readlane.  The
-// document's scalars (sequenceNumber, msn, lastSentMSN) live in SGPRs; the per-message decision
-// tree is wave-uniform scalar code.  Messages are read 64 at a time with one coalesced 16-byte
-// load per lane, and tickets are written back the same way.  HBM traffic is the algorithmic
-// minimum: 16 B in + 16 B out per message, plus 9 B per client slot in and out per document.
+// Device mapping: eight documents per wave64, eight lanes per document, each lane owning eight
+// client records in VGPRs, so the heap becomes a group-wide min (no data-dependent memory
+// traffic) and the per-message decision tree runs as VALU selects on all four SIMDs of a CU
+// (see deli_kernel).  HBM traffic is the algorithmic minimum: 16 B in + 16 B out per message,
+// plus 9 B per client slot and 20 B of scalars in and out per document.
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -40,147 +38,201 @@ struct DeliState {
     uint8_t* fl;      // CL_JOINED | CL_NACK
 };
 
-// wave-wide minimum: row_shr 1/2/4/8 leave each 16-lane row's minimum in its lane 15,
-// row_bcast:15 / row_bcast:31 carry it across rows, lane 63 ends with the wave's minimum
-MT_DEV int wave_min_dpp(int v) {
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
-    return __builtin_amdgcn_readlane(v, 63);
+constexpr int kGroup = 8;                             // lanes per document
+constexpr int kPerLane = MT_MAX_CLIENTS / kGroup;     // client slots per lane
+typedef int32_t V8 __attribute__((ext_vector_type(kPerLane)));
+
+// min over the 8 lanes of a document's group, in every lane of the group: quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i inside each half-row)
+MT_DEV int group_min(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0xB1, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x4E, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x141, 0xf, 0xf, false));
+    return v;
+}
+// slot k of a lane's 8 client slots (k differs between groups: a select chain, not an index)
+MT_DEV int pick(const V8& a, int k) {
+    int r = a[0];
+#pragma unroll
+    for (int i = 1; i < kPerLane; i++) r = k == i ? a[i] : r;
+    return r;
 }
 
-// One wave per document: ticket every raw message of the document in order.
+// Eight documents per wave, eight lanes per document; lane q of a document's group owns its
+// clients 8q..8q+7 (csn, refSeq in VGPRs; joined / nacked as 2-bit fields of one VGPR).  Every
+// branch of ticket() is evaluated as per-lane selects, so the CU's four SIMDs do the work in
+// parallel (a wave-per-document form runs the decision tree on the CU's single scalar unit).
+// A client lookup is one ds_bpermute from its owner lane; the heap minimum is 8 local mins and
+// three DPP steps.  Messages are staged through LDS eight per document at a time (one coalesced
+// 16-byte load per lane, prefetched a chunk ahead); tickets go back the same way.
 __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __restrict__ msgs,
                                                   const uint32_t* __restrict__ row_ptr, uint32_t n_docs,
                                                   int4* __restrict__ out, mt_op_rec* __restrict__ ops) {
-    const uint32_t d = blockIdx.x;
-    if (d >= n_docs) return;
+    __shared__ int4 stage[64];
     const int lane = lane_id();
-    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
-    if (r0 >= r1) return;
-    const int4 s0 = g.sc[d];
+    const int li = lane & (kGroup - 1), gbase = lane & ~(kGroup - 1);
+    const uint32_t d = blockIdx.x * (64 / kGroup) + (uint32_t)(lane / kGroup);
+    const bool live = d < n_docs;
+    uint32_t r0 = 0;
+    int len = 0;
+    if (live) {
+        r0 = row_ptr[d];
+        len = (int)(row_ptr[d + 1] - r0);
+    }
+    const int maxlen = -wave_min(-len);  // wave-uniform trip count
+    if (maxlen == 0) return;
+    int4 s0 = make_int4(0, 0, 0, 0);
+    int err_at = -1;
+    V8 csn = 0, ref = 0;
+    uint32_t fl = 0;
+    const size_t cb = (size_t)d * MT_MAX_CLIENTS + (size_t)li * kPerLane;
+    if (live) {
+        s0 = g.sc[d];
+        err_at = g.err_at[d];
+        const int4 c0 = *reinterpret_cast<const int4*>(g.csn + cb), c1 = *reinterpret_cast<const int4*>(g.csn + cb + 4);
+        const int4 f0 = *reinterpret_cast<const int4*>(g.ref + cb), f1 = *reinterpret_cast<const int4*>(g.ref + cb + 4);
+        csn = V8{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        ref = V8{f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+        const uint2 fb = *reinterpret_cast<const uint2*>(g.fl + cb);
+#pragma unroll
+        for (int i = 0; i < kPerLane; i++) fl |= (((i < 4 ? fb.x >> (8 * i) : fb.y >> (8 * (i - 4)))) & 3u) << (2 * i);
+    }
     int seq = s0.x, msn = s0.y, last = s0.z, err = s0.w;
-    int err_at = g.err_at[d];
-    const size_t cb = (size_t)d * MT_MAX_CLIENTS + lane;
-    int csn = g.csn[cb], ref = g.ref[cb], fl = g.fl[cb];
 
-    int4 m = make_int4(0, 0, 0, 0);
-    if (r0 + lane < r1) m = msgs[r0 + lane];
-    for (uint32_t base = r0; base < r1; base += 64) {
-        const int n = (int)min(64u, r1 - base);
-        const int4 cur = m;
-        // the next 64 messages are in flight while these are ticketed
-        if (base + 64 + lane < r1) m = msgs[base + 64 + lane];
+    int4 nxt = make_int4(0, 0, 0, 0);
+    if (li < len) nxt = msgs[r0 + li];
+    for (int jb = 0; jb < maxlen; jb += kGroup) {
+        const int4 cur = nxt;
+        if (jb + kGroup + li < len) nxt = msgs[r0 + jb + kGroup + li];  // next chunk in flight
+        wave_sync();
+        stage[lane] = cur;
+        wave_sync();
         int4 t = make_int4(0, 0, 0, 0);
-        for (int j = 0; j < n; j++) {
-            const int mc = __builtin_amdgcn_readlane(cur.x, j);
-            const int mr = __builtin_amdgcn_readlane(cur.y, j);
-            const int w = __builtin_amdgcn_readlane(cur.z, j);
-            const int c = w & 0xFFFF, kind = (w >> 16) & 0xFF;
-            int ts = seq, tr = mr, st = MT_TK_SENT;
-            if (err) {
-                st = MT_TK_HALTED;
-            } else if (c >= MT_MAX_CLIENTS || kind > MT_RAW_CONTROL) {
-                err = c >= MT_MAX_CLIENTS ? MT_DELI_ERR_CLIENT : MT_DELI_ERR_KIND;
-                err_at = (int)(base + j - r0);
-                st = MT_TK_HALTED;
-            } else {
-                const int cfl = __builtin_amdgcn_readlane(fl, c);
-                const int ccsn = __builtin_amdgcn_readlane(csn, c);
-                const bool joined = (cfl & CL_JOINED) != 0;
-                int upd = 0, ucsn = 0, uref = 0, unack = 0;  // upd: 1 upsert, 2 remove
-                if (kind <= MT_RAW_NOOP_DATA) {  // a client message (message.clientId set)
-                    if (joined && mc > ccsn + 1) {
-                        st = MT_TK_NACK_GAP;           // checkOrder Gap (:613-620, 269-275)
-                    } else if (joined && mc < ccsn + 1) {
-                        st = MT_TK_DROPPED;            // checkOrder Duplicate (:621-625, 267-268)
-                    } else if (!joined || (cfl & CL_NACK)) {
-                        st = MT_TK_NACK_CLIENT;        // (:308-316)
-                    } else if (mr != -1 && mr < msn) {  // (:317-335): the client stays nacked
-                        st = MT_TK_NACK_REFSEQ;
-                        upd = 1, ucsn = mc, uref = msn, unack = CL_NACK;
-                    } else {
-                        if (kind == MT_RAW_OP) {       // client no-ops do not rev (:414-425)
-                            ts = ++seq;
-                            if (mr == -1) tr = ts;
-                        }
-                        if (tr < msn) {                // assert(refSeq >= msn) (:426-428) throws
-                            err = MT_DELI_ERR_ASSERT;
-                            err_at = (int)(base + j - r0);
-                            st = MT_TK_HALTED;
-                        } else {
-                            upd = 1, ucsn = mc, uref = tr;  // upsertClient (:430-435)
-                        }
-                    }
-                } else if (kind == MT_RAW_LEAVE) {     // removeClient (:281-285)
-                    if (!joined) st = MT_TK_DROPPED;
-                    else upd = 2, ts = ++seq;
-                } else if (kind == MT_RAW_JOIN) {      // upsertClient(c, 0, msn) (:286-299)
-                    upd = 1, ucsn = 0, uref = msn;
-                    if (joined) st = MT_TK_DROPPED;    // the state is reset all the same
-                    else ts = ++seq;
+        const int steps = min(kGroup, maxlen - jb);
+        for (int jj = 0; jj < steps; jj++) {
+            const int4 mm = stage[gbase + jj];
+            const bool act = live && jb + jj < len;
+            const int mc = mm.x, mr = mm.y;
+            const int c = mm.z & 0xFFFF, kind = (mm.z >> 16) & 0xFF;
+            const bool bad = c >= MT_MAX_CLIENTS || kind > MT_RAW_CONTROL;
+            const int cq = c & (kPerLane - 1), owner = gbase + ((c / kPerLane) & (kGroup - 1));
+            // client c's record, from its owner lane
+            const int ccsn = __builtin_amdgcn_ds_bpermute(owner << 2, pick(csn, cq));
+            const int cfl = __builtin_amdgcn_ds_bpermute(owner << 2, (int)((fl >> (2 * cq)) & 3u));
+            const bool joined = (cfl & CL_JOINED) != 0, nacked = (cfl & CL_NACK) != 0;
+            const bool go = act && !err && !bad;
+            // checkOrder + the client / system branches of ticket() (lambda.ts:265-347)
+            const bool isc = kind <= MT_RAW_NOOP_DATA;
+            const bool gap = isc && joined && mc > ccsn + 1;
+            const bool dup = isc && joined && mc < ccsn + 1;
+            const bool nackc = isc && !gap && !dup && (!joined || nacked);
+            const bool nackr = isc && !gap && !dup && !nackc && mr != -1 && mr < msn;
+            const bool clok = isc && !gap && !dup && !nackc && !nackr;
+            const bool rev_op = clok && kind == MT_RAW_OP;          // client no-ops do not rev (:414-425)
+            const int s1 = seq + (rev_op ? 1 : 0);
+            const int tr0 = (rev_op && mr == -1) ? s1 : mr;          // REST op (:422-424)
+            const bool afail = clok && tr0 < msn;                   // assert (:426-428)
+            const bool leave_ok = kind == MT_RAW_LEAVE && joined;
+            const bool join_new = kind == MT_RAW_JOIN && !joined;
+            const bool drop = dup || (kind == MT_RAW_LEAVE && !joined) || (kind == MT_RAW_JOIN && joined);
+            const bool nack = gap || nackc || nackr;
+            // ClientSequenceNumberManager updates, by the owner lane
+            const bool ups = go && ((clok && !afail) || nackr || kind == MT_RAW_JOIN);
+            const bool rem = go && leave_ok;
+            if ((ups || rem) && lane == owner) {
+                const int ucsn = kind == MT_RAW_JOIN ? 0 : mc;
+                const int uref = (nackr || kind == MT_RAW_JOIN) ? msn : tr0;
+#pragma unroll
+                for (int i = 0; i < kPerLane; i++) {
+                    csn[i] = (ups && cq == i) ? ucsn : csn[i];
+                    ref[i] = (ups && cq == i) ? uref : ref[i];
                 }
-                if (upd && lane == c) {
-                    if (upd == 2) {
-                        fl = 0;
-                    } else {
-                        csn = ucsn;
-                        ref = uref;
-                        fl = CL_JOINED | unack;
-                    }
-                }
-                if (st == MT_TK_SENT) {
-                    // getMinimumSequenceNumber over the tracked clients (:446-455)
-                    const int mn = wave_min_dpp((fl & CL_JOINED) ? ref : INT_MAX);
-                    const bool none = mn == INT_MAX;
-                    msn = none ? ts : mn;
-                    if (kind == MT_RAW_NOOP) {                 // contents null: Later (:463-465)
-                        st = MT_TK_LATER;
-                    } else if (kind == MT_RAW_NOOP_DATA) {     // (:466-471)
-                        if (msn <= last) st = MT_TK_LATER;
-                        else ts = ++seq;
-                    } else if (kind == MT_RAW_SERVER_NOOP) {   // (:473-479)
-                        if (msn <= last) st = MT_TK_NEVER;
-                        else ts = ++seq;
-                    } else if (kind == MT_RAW_NOCLIENT) {      // (:481-489)
-                        if (none) {
-                            ts = ++seq;
-                            tr = ts;
-                            msn = ts;
-                        } else {
-                            st = MT_TK_NEVER;
-                        }
-                    } else if (kind == MT_RAW_CONTROL) {       // (:490-517)
-                        st = MT_TK_NEVER;
-                    }
-                    if (st == MT_TK_SENT) last = msn;          // handler (:217-218)
-                } else if (st >= MT_TK_NACK_GAP && st <= MT_TK_NACK_REFSEQ) {
-                    ts = msn;                                  // createNackMessage (:683-712)
-                    last = msn;
-                }
+                const uint32_t ufl = ups ? (uint32_t)(CL_JOINED | (nackr ? CL_NACK : 0)) : 0u;
+                fl = (fl & ~(3u << (2 * cq))) | (ufl << (2 * cq));
             }
-            if (lane == j) t = make_int4(ts, msn, tr, st);
+            const int s2 = s1 + ((leave_ok || join_new) ? 1 : 0);  // join / leave rev (:437-442)
+            // getMinimumSequenceNumber (:446-455)
+            int mv = INT_MAX;
+#pragma unroll
+            for (int i = 0; i < kPerLane; i++) mv = min(mv, ((fl >> (2 * i)) & 1u) ? ref[i] : INT_MAX);
+            mv = group_min(mv);
+            const bool none = mv == INT_MAX;
+            int msn2 = none ? s2 : mv;
+            // send type (:457-517)
+            int st = MT_TK_SENT, s3 = s2, tr = tr0;
+            if (kind == MT_RAW_NOOP) {
+                st = MT_TK_LATER;
+            } else if (kind == MT_RAW_NOOP_DATA || kind == MT_RAW_SERVER_NOOP) {
+                if (msn2 <= last) st = kind == MT_RAW_NOOP_DATA ? MT_TK_LATER : MT_TK_NEVER;
+                else s3 = s2 + 1;
+            } else if (kind == MT_RAW_NOCLIENT) {
+                if (none) {
+                    s3 = s2 + 1;
+                    tr = s3;
+                    msn2 = s3;
+                } else {
+                    st = MT_TK_NEVER;
+                }
+            } else if (kind == MT_RAW_CONTROL) {
+                st = MT_TK_NEVER;
+            }
+            // outcome
+            int ts = seq, tm = msn, to = mr, tst = MT_TK_HALTED;
+            if (go) {
+                if (drop) {
+                    tst = MT_TK_DROPPED;
+                } else if (nack) {                                 // createNackMessage (:683-712)
+                    tst = gap ? MT_TK_NACK_GAP : (nackc ? MT_TK_NACK_CLIENT : MT_TK_NACK_REFSEQ);
+                    ts = msn;
+                    last = msn;
+                } else if (afail) {
+                    err = MT_DELI_ERR_ASSERT;
+                    err_at = jb + jj;
+                    seq = s1;
+                    ts = s1;
+                    to = tr0;
+                } else {
+                    seq = s3;
+                    msn = msn2;
+                    if (st == MT_TK_SENT) last = msn2;             // handler (:217-218)
+                    ts = s3;
+                    tm = msn2;
+                    to = tr;
+                    tst = st;
+                }
+            } else if (act && !err) {
+                err = c >= MT_MAX_CLIENTS ? MT_DELI_ERR_CLIENT : MT_DELI_ERR_KIND;
+                err_at = jb + jj;
+            }
+            if (li == jj) t = make_int4(ts, tm, to, tst);
         }
-        if (lane < n) {
-            out[base + lane] = t;
+        if (jb + li < len) {
+            out[r0 + jb + li] = t;
             if (ops) {
-                mt_op_rec* o = ops + base + lane;
+                mt_op_rec* o = ops + r0 + jb + li;
                 o->seq = t.w == MT_TK_SENT ? t.x : -1;
                 o->msn = t.y;
                 o->ref_seq = t.z;
             }
         }
     }
-    if (lane == 0) {
+    if (!live) return;
+    if (li == 0) {
         g.sc[d] = make_int4(seq, msn, last, err);
         g.err_at[d] = err_at;
     }
-    g.csn[cb] = csn;
-    g.ref[cb] = ref;
-    g.fl[cb] = (uint8_t)fl;
+    *reinterpret_cast<int4*>(g.csn + cb) = make_int4(csn[0], csn[1], csn[2], csn[3]);
+    *reinterpret_cast<int4*>(g.csn + cb + 4) = make_int4(csn[4], csn[5], csn[6], csn[7]);
+    *reinterpret_cast<int4*>(g.ref + cb) = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    *reinterpret_cast<int4*>(g.ref + cb + 4) = make_int4(ref[4], ref[5], ref[6], ref[7]);
+    uint2 fb = make_uint2(0u, 0u);
+#pragma unroll
+    for (int i = 0; i < kPerLane; i++) {
+        const uint32_t v = (fl >> (2 * i)) & 3u;
+        if (i < 4) fb.x |= v << (8 * i);
+        else fb.y |= v << (8 * (i - 4));
+    }
+    *reinterpret_cast<uint2*>(g.fl + cb) = fb;
 }
 
 // every document from one checkpoint (bench tooling)
@@ -255,7 +307,7 @@ int32_t ckpt_msn(const mt_deli_checkpoint& ck) {
 mt_status launch_ticket(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row, uint32_t n_docs,
                         mt_ticket* d_out, mt_op_rec* d_ops) {
     DL_HIP(hipEventRecord(dl->e0, dl->stream));
-    hipLaunchKernelGGL(mtd::deli_kernel, dim3(n_docs), dim3(64), 0, dl->stream, dl->g,
+    hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, dl->stream, dl->g,
                        reinterpret_cast<const int4*>(d_msgs), d_row, n_docs, reinterpret_cast<int4*>(d_out), d_ops);
     DL_HIP(hipGetLastError());
     DL_HIP(hipEventRecord(dl->e1, dl->stream));

@@ -8,14 +8,15 @@
 //     segment for an op's (refSeq, client) view (mergeTree.ts:1667-1697) is K per-lane
 //     evaluations plus one wave-wide DPP scan: the PartialSequenceLengths query
 //     (partialLengths.ts:433-487) without any memory traffic;
-//   * the leaf level of the B-tree lives in the same registers: the slot that starts a leaf
-//     block carries a BS bit and that block's needsScour state, so "which leaf block holds slot
-//     k", "where does block b start" and "how many children has it" are ballot / popcount / DPP
-//     questions, not LDS walks.  Interior levels (touched only by leaf splits and packs) are
-//     child-count arrays in LDS, as in mt_apply.hip;
-//   * a zamboni unlink (mergeTree.ts:1289-1365) only marks its slot DEAD (zero length, no child
-//     of any block); dead slots are squeezed out when the document is written back, so nothing
-//     moves on an unlink.  An insert or a split moves the later slots one register to the right
+//   * the leaf level of the B-tree is a set of per-lane K-bit masks over the same slots: block
+//     starts (bsm), the starting slot's needsScour state (sc0 / sc1), live slots (lvm); so
+//     "which leaf block holds slot k", "where does block b start" and "how many children has it"
+//     are ballot / popcount / DPP questions, not LDS walks, and block edits touch one register.
+//     Interior levels (touched only by leaf splits and packs) are child-count arrays in LDS, as
+//     in mt_apply.hip;
+//   * a zamboni unlink (mergeTree.ts:1289-1365) only clears its slot's live bit (a dead slot has
+//     no length in any view and is no child of any block); dead slots are squeezed out when the
+//     document is written back, so nothing moves on an unlink.  An insert or a split moves the later slots one register to the right
 //     (K predicated moves per field per lane, DPP wave_shr:1 across lanes);
 //   * cold fields (property set, text offset) stay in LDS indexed by a segment id that never
 //     changes while the segment is linked; the zamboni heap holds those ids.
@@ -38,17 +39,12 @@ constexpr uint32_t kLenBits = 17;      // li = len | id << 17  (len <= textcap <
 constexpr uint32_t kLenMask = (1u << kLenBits) - 1;
 constexpr uint32_t kNoId = 0x7FFFu;    // id of a padding slot
 constexpr uint32_t kEmptyLi = kNoId << kLenBits;
-// cf = client (bits 0-7) | removedClientId (8-15) | segment flags (16-23) | leaf-block bits (24-31)
+// cf = client (bits 0-7) | removedClientId (8-15) | segment flags (16-23)
 constexpr uint32_t F_RM = (uint32_t)MT_SF_REMOVED << 16;
 constexpr uint32_t F_PDEF = (uint32_t)MT_SF_PDEF << 16;
 constexpr uint32_t F_NL = (uint32_t)MT_SF_NL << 16;
 constexpr uint32_t F_HASNL = (uint32_t)MT_SF_HASNL << 16;
-constexpr uint32_t F_DEAD = 0x80u << 16;  // unlinked or padding: not a child of any block
-constexpr uint32_t F_BS = 1u << 24;      // first slot of a leaf block
-constexpr uint32_t SC_SHIFT = 25;        // that block's needsScour (MT_SC_*), kept on its first slot
-constexpr uint32_t SC_MASK = 3u << SC_SHIFT;
-constexpr uint32_t BLK_MASK = F_BS | SC_MASK;
-constexpr uint32_t kEmptyCf = 0xFFu | F_DEAD;  // client 255 never matches, length 0, dead
+constexpr uint32_t kEmptyCf = 0xFFu;     // padding: client 255 never matches (and the slot is dead)
 constexpr uint16_t kDead = 0xFFFFu;
 
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -130,9 +126,9 @@ struct RWave {
     uint32_t text_top, text_half;
     bool dirty;  // arena stores issued and not yet waited for
     uint32_t pb; // the current op's payload, prefetched: lane i holds byte i (i < 64)
-    // per-lane K-bit masks of this lane's slots that start a leaf block / are live, kept in step
-    // with cf by every writer of the BS or DEAD bits
-    uint32_t bsm, lvm;
+    // per-lane K-bit masks over this lane's slots: starts a leaf block (bsm), live (lvm), and the
+    // needsScour state (MT_SC_*) of the block a start slot begins: bit 0 in sc0, bit 1 in sc1
+    uint32_t bsm, lvm, sc0, sc1;
 #ifdef MT_PROF
     uint64_t prof[P_NSLOT] = {};
 #endif
@@ -154,36 +150,38 @@ struct RWave {
     // ------------------------------------------------------------ slot masks
     MT_DEV uint32_t bs_bits() const { return bsm; }
     MT_DEV uint32_t live_bits() const { return lvm; }
-    MT_DEV void remask() {  // recompute both masks from cf
-        uint32_t b = 0, l = 0;
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            b |= (cf[j] & F_BS) ? (1u << j) : 0u;
-            l |= (cf[j] & F_DEAD) ? 0u : (1u << j);
-        }
-        bsm = b;
-        lvm = l;
-    }
-    // the masks after slot k's cf became v (uniform k)
-    MT_DEV void mask_slot(int k, uint32_t v) {
+    // this lane's bit of uniform slot k (0 if another lane holds it)
+    MT_DEV uint32_t kbit(int k) const {
         const int r = k - lane * K;
-        if (r >= 0 && r < K) {
-            const uint32_t bit = 1u << r;
-            bsm = (v & F_BS) ? (bsm | bit) : (bsm & ~bit);
-            lvm = (v & F_DEAD) ? (lvm & ~bit) : (lvm | bit);
-        }
+        return (r >= 0 && r < K) ? (1u << r) : 0u;
     }
-    // the masks after shift_in(p, e): slots >= p move up one, slot p takes e's bits
-    MT_DEV void mask_shift(int p, uint32_t ecf) {
+    // needsScour state of the block starting at uniform slot a; set it / the block-start bit
+    MT_DEV int sc_of(int a) const {
+        const int r = uni(a % K);
+        return __builtin_amdgcn_readlane((int)(((sc0 >> r) & 1u) | (((sc1 >> r) & 1u) << 1)), a / K);
+    }
+    MT_DEV void set_sc(int a, int v) {
+        const uint32_t b = kbit(a);
+        sc0 = (v & 1) ? (sc0 | b) : (sc0 & ~b);
+        sc1 = (v & 2) ? (sc1 | b) : (sc1 & ~b);
+    }
+    MT_DEV void set_bs(int a, bool on) {
+        const uint32_t b = kbit(a);
+        bsm = on ? (bsm | b) : (bsm & ~b);
+    }
+    // the masks after shift_in(p, ..): slots >= p move up one, slot p gets (bs, scv, live)
+    MT_DEV static uint32_t shift_mask(uint32_t m, uint32_t lo, bool at, bool above, int r, bool bit) {
+        const uint32_t c = (uint32_t)shr1((int)((m >> (K - 1)) & 1u), 0);
+        return (m & lo) | (((m & ~lo) << 1) & kAll) | ((at && bit) ? (1u << r) : 0u) | (above ? c : 0u);
+    }
+    MT_DEV void mask_shift(int p, bool bs, int scv, bool live) {
         const uint32_t lo = below(p);
         const int r = p - lane * K;
-        const uint32_t cb = (uint32_t)shr1((int)((bsm >> (K - 1)) & 1u), 0);
-        const uint32_t cl = (uint32_t)shr1((int)((lvm >> (K - 1)) & 1u), 0);
         const bool at = r >= 0 && r < K, above = r < 0;
-        const uint32_t eb = at ? (((ecf & F_BS) ? 1u : 0u) << r) : 0u;
-        const uint32_t el = at ? (((ecf & F_DEAD) ? 0u : 1u) << r) : 0u;
-        bsm = (bsm & lo) | (((bsm & ~lo) << 1) & kAll) | eb | (above ? cb : 0u);
-        lvm = (lvm & lo) | (((lvm & ~lo) << 1) & kAll) | el | (above ? cl : 0u);
+        bsm = shift_mask(bsm, lo, at, above, r, bs);
+        lvm = shift_mask(lvm, lo, at, above, r, live);
+        sc0 = shift_mask(sc0, lo, at, above, r, (scv & 1) != 0);
+        sc1 = shift_mask(sc1, lo, at, above, r, (scv & 2) != 0);
     }
     // this lane's slots with index < k
     MT_DEV uint32_t below(int k) const {
@@ -226,25 +224,15 @@ struct RWave {
         r.cum = __builtin_amdgcn_readlane(cum[jk], lk);
         return r;
     }
-    MT_DEV uint32_t get_cf(int k) const {
-        const int jk = uni(k % K);
-        return (uint32_t)__builtin_amdgcn_readlane((int)cf[jk], k / K);
-    }
     MT_DEV uint32_t get_li(int k) const {
         const int jk = uni(k % K);
         return (uint32_t)__builtin_amdgcn_readlane((int)li[jk], k / K);
     }
     MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
-        mask_slot(k, cv);
         const int lk = k / K, jk = uni(k % K);
         const bool me = lane == lk;
         li[jk] = me ? lv : li[jk];
         cf[jk] = me ? cv : cf[jk];
-    }
-    MT_DEV void set_cf(int k, uint32_t cv) {
-        mask_slot(k, cv);
-        const int lk = k / K, jk = uni(k % K);
-        cf[jk] = lane == lk ? cv : cf[jk];
     }
     MT_DEV void set_cum(int k, int32_t v) {
         const int lk = k / K, jk = uni(k % K);
@@ -253,8 +241,8 @@ struct RWave {
 
     // insert e at slot p: slots >= p move one register right
     template <bool CUM>
-    MT_DEV void shift_in(int p, const Elem& e) {
-        mask_shift(p, e.cf);
+    MT_DEV void shift_in(int p, const Elem& e, bool bs, int scv, bool live) {
+        mask_shift(p, bs, scv, live);
         const int32_t c_seq = shr1(seq[K - 1], 0), c_rseq = shr1(rseq[K - 1], 0);
         const uint32_t c_li = (uint32_t)shr1((int)li[K - 1], 0), c_cf = (uint32_t)shr1((int)cf[K - 1], 0);
         const uint32_t c_ov = (uint32_t)shr1((int)ov[K - 1], 0);
@@ -286,7 +274,7 @@ struct RWave {
         const bool seen = ((f & 0xFFu) == (uint32_t)C) | (seq[j] <= R);
         const bool hid = ((f & F_RM) != 0) & ((((f >> 8) & 0xFFu) == (uint32_t)C) | (((ov[j] >> (C - 1)) & 1u) != 0) |
                                               (rseq[j] <= R));
-        return (seen & !hid) ? (int)len_of(li[j]) : 0;
+        return (seen & !hid & (((lvm >> j) & 1u) != 0)) ? (int)len_of(li[j]) : 0;
     }
     // cum = inclusive prefix of vis over the slots; returns getLength(R, C)
     MT_DEV int scan(int32_t R, int C) {
@@ -396,7 +384,8 @@ struct RWave {
         const int s4 = nth_slot(live_bits() & below(e) & ~below(a), kMaxNodes / 2);
         int parent = -1;
         if (nlev > 1) parent = parent_of(0, b, nullptr);
-        set_cf(s4, (get_cf(s4) & ~BLK_MASK) | F_BS);  // new block, needsScour undefined
+        set_bs(s4, true);  // new block, needsScour undefined
+        set_sc(s4, MT_SC_UNDEF);
         nb0 += 1;
         if (nlev == 1) {  // the root was the only leaf block: new root with 2 children
             if (lane == 0) {
@@ -419,9 +408,11 @@ struct RWave {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
         const int a = bs_slot(b);
         const bool front = k == a;  // new first child: it takes over the block's marks
-        if (front) e.cf = (e.cf & ~BLK_MASK) | (get_cf(a) & BLK_MASK);
-        shift_in<true>(k, e);
-        if (front) set_cf(k + 1, get_cf(k + 1) & ~BLK_MASK);
+        shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
+        if (front) {
+            set_bs(k + 1, false);
+            set_sc(k + 1, MT_SC_UNDEF);
+        }
         nlive += 1;
         const int en = bs_slot(b + 1);
         if (live_in(a, en) >= kMaxNodes) return split_leaf(b, a, en, sq);
@@ -455,7 +446,7 @@ struct RWave {
     MT_DEV void compact_text() {
         arena_sync();
 #pragma unroll
-        for (int j = 0; j < K; j++) s.scr[idx(j)] = (int32_t)li[j];
+        for (int j = 0; j < K; j++) s.scr[idx(j)] = (int32_t)(((lvm >> j) & 1u) ? li[j] : kEmptyLi);
         wave_sync();
         uint8_t* dst = abase + (size_t)(text_half ^ 1u) * textcap;
         uint32_t carry = 0;
@@ -528,7 +519,7 @@ struct RWave {
         }
         r = e;
         r.li = (len - (uint32_t)off) | ((uint32_t)t << kLenBits);
-        r.cf = e.cf & ~BLK_MASK;
+        r.cf = e.cf;
         set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & ~F_NL) | (last == '\n' ? F_NL : 0u));
         set_cum(k, pos);
         wave_sync();
@@ -588,9 +579,8 @@ struct RWave {
     // addToLRUSet (mergeTree.ts:1273-1283) for segment `id` in leaf block b
     MT_DEV bool add_lru(int b, int id, int32_t sq) {
         const int a = bs_slot(b);
-        const uint32_t c = get_cf(a);
-        if (((c >> SC_SHIFT) & 3u) != MT_SC_TRUE && sq > cur_seq) {
-            set_cf(a, (c & ~SC_MASK) | ((uint32_t)MT_SC_TRUE << SC_SHIFT));
+        if (sc_of(a) != MT_SC_TRUE && sq > cur_seq) {
+            set_sc(a, MT_SC_TRUE);
             return heap_push(sq, id, sq);
         }
         return true;
@@ -601,7 +591,7 @@ struct RWave {
         int hit = -1;
 #pragma unroll
         for (int j = 0; j < K; j++)
-            if ((int)id_of(li[j]) == id && !(cf[j] & F_DEAD)) hit = idx(j);
+            if ((int)id_of(li[j]) == id && ((lvm >> j) & 1u)) hit = idx(j);
         const uint64_t m = wave_ballot(hit >= 0);
         if (!m) return -1;
         return __builtin_amdgcn_readlane(hit, first_lane(m));
@@ -738,12 +728,6 @@ struct RWave {
             gm &= gm - 1;
             if (sl / K == lane) kill |= 1u << (sl % K);
         }
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const bool k_ = (kill >> j) & 1u;
-            li[j] = k_ ? (li[j] & ~kLenMask) : li[j];
-            cf[j] = k_ ? (cf[j] | F_DEAD) : cf[j];
-        }
         lvm &= ~kill;
         nlive -= __popc(unlink);
         return kept;
@@ -795,21 +779,20 @@ struct RWave {
         const uint32_t lb = live_bits() & below(E) & ~below(A);
         const int c = __popc(lb);
         const int rbase = wave_incl_scan(c) - c;
+        uint32_t nbs = 0;  // the new block starts; every new block: needsScour undefined
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            const int i = idx(j);
-            if (i >= A && i < E) {
-                uint32_t v = cf[j] & ~BLK_MASK;  // every new block: needsScour undefined
-                if (i == A) v |= F_BS;
-                if ((lb >> j) & 1u) {
-                    const int r = rbase + __popc(lb & ((1u << j) - 1u));
-                    for (int t = 1; t < cc; t++)
-                        if (r == t * base + min(t, extra)) v |= F_BS;
-                }
-                cf[j] = v;
+            bool v = idx(j) == A;
+            if ((lb >> j) & 1u) {
+                const int r = rbase + __popc(lb & ((1u << j) - 1u));
+                for (int t = 1; t < cc; t++) v = v || r == t * base + min(t, extra);
             }
+            nbs |= v ? (1u << j) : 0u;
         }
-        remask();
+        const uint32_t rng = below(E) & ~below(A);
+        bsm = (bsm & ~rng) | (nbs & rng);
+        sc0 &= ~rng;
+        sc1 &= ~rng;
         nb0 += cc - m;
         if (lane == 0) s.ibcnt[0][P] = (uint8_t)cc;
         wave_sync();
@@ -837,7 +820,7 @@ struct RWave {
             const int b = leaf_of(k);
             const int a = bs_slot(b), e = bs_slot(b + 1);
             PROF_END(prof, P_ZPOP, tz);
-            if (((get_cf(a) >> SC_SHIFT) & 3u) == MT_SC_FALSE) continue;
+            if (sc_of(a) == MT_SC_FALSE) continue;
             const int cnt = live_in(a, e);
             int P = -1, fc = 0, m = 0, total = 0;
             for (int step = 0;; step++) {
@@ -852,7 +835,7 @@ struct RWave {
                 PROF_END(prof, P_SCOUR, ts);
                 if (err) return;
                 if (step == 0) {
-                    set_cf(a, (get_cf(a) & ~SC_MASK) | ((uint32_t)MT_SC_FALSE << SC_SHIFT));
+                    set_sc(a, MT_SC_FALSE);
                     if (!(kept < cnt && kept < kMaxNodes / 2 && nlev > 1)) break;
                     P = parent_of(0, b, &fc);
                     m = uni(s.ibcnt[0][P]);
@@ -918,7 +901,7 @@ struct RWave {
                 const int ce = cum[j];
                 const int csj = j ? cum[j - 1] : cs;
                 const bool rm_before = (cf[j] & F_RM) && rseq[j] <= R;
-                const bool h = !(cf[j] & F_DEAD) && i >= a && i < e &&
+                const bool h = ((lvm >> j) & 1u) && i >= a && i < e &&
                                (ce > pos || (ce == pos && csj == pos && !rm_before));
                 best = h ? i : best;
             }
@@ -1180,6 +1163,7 @@ struct RWave {
         wave_sync();
         // the register state, one field at a time
         const int i0 = lane * K;
+        bsm = lvm = sc0 = sc1 = 0u;
 #pragma unroll
         for (int j = 0; j < K; j++) {
             seq[j] = 0x7fffffff;
@@ -1227,14 +1211,17 @@ struct RWave {
 #pragma unroll
                 for (int j = 0; j < K; j++) {
                     const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
-                    const uint32_t v = bc[j] | (br[j] << 8) | ((bf[j] & 0xFu) << 16) |
-                                       ((mk & 1) ? (F_BS | ((uint32_t)(mk >> 1) << SC_SHIFT)) : 0u);
-                    cf[j] = i0 + j < n ? v : kEmptyCf;
+                    const bool in = i0 + j < n;
+                    cf[j] = in ? (bc[j] | (br[j] << 8) | ((bf[j] & 0xFu) << 16)) : kEmptyCf;
+                    const uint32_t bit = in ? (1u << j) : 0u;
+                    lvm |= bit;
+                    bsm |= (mk & 1) ? bit : 0u;
+                    sc0 |= (mk & 2) ? bit : 0u;
+                    sc1 |= (mk & 4) ? bit : 0u;
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        remask();
         // empty leaf blocks (rare): a dead slot holds each one's place and marks
         if (nempty) {
             if (ns + nempty > CAP) {
@@ -1254,10 +1241,11 @@ struct RWave {
                         ph.seq = 0x7fffffff;
                         ph.rseq = 0;
                         ph.li = kEmptyLi;
-                        ph.cf = kEmptyCf | F_BS | ((uint32_t)__builtin_amdgcn_readlane(scv, fl) << SC_SHIFT);
+                        ph.cf = kEmptyCf;
                         ph.ov = 0;
                         ph.cum = 0;
-                        shift_in<false>(__builtin_amdgcn_readlane(incl - c, fl) + placed, ph);
+                        shift_in<false>(__builtin_amdgcn_readlane(incl - c, fl) + placed, ph, true,
+                                        __builtin_amdgcn_readlane(scv, fl), false);
                         placed++;
                     }
                     carry = wave_last(incl);
@@ -1311,7 +1299,7 @@ struct RWave {
             if ((bm >> j) & 1u) {
                 const int b = bbase + __popc(bm & ((1u << j) - 1u));
                 s.scr[b] = pbase + __popc(lb & ((1u << j) - 1u));
-                s.lbsc[b] = (uint8_t)((cf[j] >> SC_SHIFT) & 3u);
+                s.lbsc[b] = (uint8_t)(((sc0 >> j) & 1u) | (((sc1 >> j) & 1u) << 1));
             }
         }
         if (lane == 0) s.scr[nb0] = nn;

@@ -258,6 +258,71 @@ static napi_value version(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* ---- deli (include/mtgpu.h "deli" section) ---------------------------------------------- */
+static void finalize_deli(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    if (data) mt_deli_destroy((mt_deli*)data);
+}
+static mt_deli* get_deli(napi_env env, napi_value v) {
+    void* p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+    return (mt_deli*)p;
+}
+
+/* createDeli({device, maxDocs}): new DeliLambda state for maxDocs documents (lambda.ts:112-171) */
+static napi_value create_deli(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    mt_deli* dl = NULL;
+    mt_status st = mt_deli_create((int32_t)get_u32(env, argv[0], "device", 0), get_u32(env, argv[0], "maxDocs", 1), &dl);
+    if (st) return throw_status(env, "mt_deli_create", st);
+    NAPI_CALL(env, napi_create_external(env, dl, finalize_deli, NULL, &out));
+    return out;
+}
+
+/* deliTicket(deli, msgsU8 (16-byte mt_raw_msg rows), rowPtrU32) -> Buffer of 16-byte mt_ticket
+ * rows: DeliLambda.ticket over every raw message of every document (lambda.ts:255-544) */
+static napi_value deli_ticket(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    mt_deli* dl = get_deli(env, argv[0]);
+    size_t nmsg, nrow;
+    const void* msgs = buffer_data(env, argv[1], &nmsg);
+    const void* row = buffer_data(env, argv[2], &nrow);
+    if (!dl || (!msgs && nmsg) || !row || nrow < 4) {
+        napi_throw_type_error(env, NULL, "deliTicket(deli, msgs, rowPtr)");
+        return NULL;
+    }
+    const uint64_t n = nmsg / sizeof(mt_raw_msg);
+    void* data = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(mt_ticket) : 1, &data, &out));
+    mt_status st = mt_deli_ticket(dl, (const mt_raw_msg*)msgs, n, (const uint32_t*)row,
+                                  (uint32_t)(nrow / 4 - 1), (mt_ticket*)data);
+    if (st) return throw_status(env, "mt_deli_ticket", st);
+    return out;
+}
+
+/* deliError(deli, doc) -> [mt_deli_err, message index] */
+static napi_value deli_error(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out, a, b;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t doc = 0;
+    int32_t err = 0, idx = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    mt_status st = mt_deli_doc_error(get_deli(env, argv[0]), doc, &err, &idx);
+    if (st) return throw_status(env, "mt_deli_doc_error", st);
+    NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
+    NAPI_CALL(env, napi_create_int32(env, err, &a));
+    NAPI_CALL(env, napi_create_int32(env, idx, &b));
+    NAPI_CALL(env, napi_set_element(env, out, 0, a));
+    NAPI_CALL(env, napi_set_element(env, out, 1, b));
+    return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor d[] = {
         {"createEngine", NULL, create_engine, NULL, NULL, NULL, napi_default, NULL},
@@ -269,6 +334,9 @@ static napi_value init(napi_env env, napi_value exports) {
         {"docError", NULL, doc_error, NULL, NULL, NULL, napi_default, NULL},
         {"checksums", NULL, checksums, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, version, NULL, NULL, NULL, napi_default, NULL},
+        {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
+        {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},
+        {"deliError", NULL, deli_error, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -52,3 +52,29 @@ def test_batchclient_replays_golden(name):
         assert r['text'] == e['text']
         assert r['length'] == len(e['text'])
         assert _to_log_ids(r['state']) == e['state'], (name, r['doc'])
+
+
+def test_addon_exports_deli():
+    if not _addon():
+        pytest.skip('node headers absent')
+    out = subprocess.run([NODE, '-e', "const n=require('./js/mtgpu.node');"
+                          "for (const f of ['createDeli','deliTicket','deliError']) if (typeof n[f] !== 'function') throw f;"
+                          "require('./js/deliSequencer.js');"], cwd=REPO, capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+
+
+@pytest.mark.gpu
+def test_deli_sequencer_replays_lambda_spec():
+    """lambda.spec.ts's scenarios as IRawOperationMessages through js/deliSequencer.js: the
+    asserted MSN values (0, 1, 4, 7, 7 and 20, 22) and nacks."""
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'deli_spec.js')], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    docs = [json.loads(x) for x in out.stdout.strip().split('\n')]
+    disconnect, above, nacked = docs
+    assert [disconnect[i][2] for i in (0, 3, 5, 6, 8)] == [0, 1, 4, 7, 7]
+    assert all(r[0] == 'sent' for r in disconnect)
+    assert above[2][2] == 20 and above[5][2] == 22
+    assert nacked[3][0] == 'nack' and nacked[3][3].startswith('Refseq')
+    assert nacked[4][0] == 'nack' and nacked[4][3] == 'Nonexistent client'

@@ -1374,6 +1374,16 @@ MT_DEV mt_op_rec load_op(const mt_op_rec* p) {
     return r;
 }
 
+// The document arrays of mt_gstate are only needed by load() and store().  Both read them
+// through a pointer to the kernel's own argument block that the compiler cannot see through, so
+// the ~40 SGPRs of pointers are not held live across the op loop (where they were spilled into
+// VGPR lanes and reloaded in the hot phases).  g is the kernel's first argument: offset 0.
+MT_DEV const mt_gstate& kernarg_gstate() {
+    const mt_gstate* p = (const mt_gstate*)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? 2 : (K == 8 ? 3 : 4)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
@@ -1391,7 +1401,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? 2 
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     PROF_BEGIN(tl);
-    wv.load(g, d);
+    wv.load(kernarg_gstate(), d);
     PROF_END(wv.prof, P_LOAD, tl);
     // software pipeline: the record of op i+2 and the payload of op i+1 are in flight while op i
     // is applied
@@ -1411,7 +1421,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? 2 
 #endif
     }
     PROF_BEGIN(tt);
-    wv.store(g, d);
+    wv.store(kernarg_gstate(), d);
     PROF_END(wv.prof, P_STORE, tt);
 #ifdef MT_PROF
     if (wv.lane == 0)

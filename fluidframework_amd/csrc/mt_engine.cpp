@@ -30,6 +30,8 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
                                     uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
+                                         uint32_t* specs, uint32_t* counts, hipStream_t st);
 extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
                                     int32_t* cref,
                                     int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
@@ -594,6 +596,131 @@ std::string state_json(const HostDoc& h) {
     return o;
 }
 
+
+// JSON.stringify's string escaping (ECMA-262 QuoteJSONString): \b \t \n \f \r short forms,
+// other control characters as \u00xx
+void js_str(std::string& o, const uint8_t* p, size_t n) {
+    o += '"';
+    for (size_t i = 0; i < n; i++) {
+        const unsigned char c = p[i];
+        switch (c) {
+            case '"': o += "\\\""; break;
+            case '\\': o += "\\\\"; break;
+            case '\b': o += "\\b"; break;
+            case '\t': o += "\\t"; break;
+            case '\n': o += "\\n"; break;
+            case '\f': o += "\\f"; break;
+            case '\r': o += "\\r"; break;
+            default:
+                if (c < 0x20) {
+                    char buf[8];
+                    snprintf(buf, sizeof buf, "\\u%04x", c);
+                    o += buf;
+                } else {
+                    o += (char)c;
+                }
+        }
+    }
+    o += '"';
+}
+
+// props as the reference's map: keys "k<id>" (interned key ids), values = interned value ids
+void props_json(std::string& o, uint64_t props) {
+    o += '{';
+    bool first = true;
+    for (int k = 0; k < MT_MAX_KEYS; k++) {
+        const unsigned v = (unsigned)((props >> (8 * k)) & 0xFF);
+        if (!v) continue;
+        if (!first) o += ',';
+        first = false;
+        o += "\"k" + std::to_string(k) + "\":" + std::to_string(v);
+    }
+    o += '}';
+}
+
+// TextSegment.toJSONObject (textSegment.ts:47-53) of `text` with the props of segment i
+void seg_json(std::string& o, const HostDoc& h, int i, const std::string& text) {
+    if (h.flags[i] & MT_SF_PDEF) {
+        o += "{\"text\":";
+        js_str(o, (const uint8_t*)text.data(), text.size());
+        o += ",\"props\":";
+        props_json(o, h.props[i]);
+        o += '}';
+    } else {
+        js_str(o, (const uint8_t*)text.data(), text.size());
+    }
+}
+
+std::string client_name(const char* const* names, uint32_t n_names, uint32_t c) {
+    if (names && c < n_names && names[c]) return names[c];
+    return std::to_string(c);
+}
+
+// SnapshotV1.emit (snapshotV1.ts:85-149) from the device's extraction specs: the tree entries as
+// one JSON object {"header": chunk, "body_0": chunk, ...}
+std::string snapshot_json(const HostDoc& h, const std::vector<uint32_t>& sp, uint32_t nspec, uint32_t chunk,
+                          const char* const* names, uint32_t n_names) {
+    std::vector<std::string> specs(nspec);
+    std::vector<uint32_t> lens(nspec);
+    for (uint32_t k = 0; k < nspec; k++) {
+        const int pos = (int)sp[3 * k];
+        const int cnt = (int)(sp[3 * k + 1] >> 1);
+        const bool meta = sp[3 * k + 1] & 1u;
+        std::string text;
+        for (int i = pos; i < pos + cnt; i++) {
+            if ((h.flags[i] & MT_SF_REMOVED) && h.rseq[i] <= h.sc.min_seq) continue;  // elided inside the run
+            text.append((const char*)h.text.data() + h.toff[i], h.len[i]);
+        }
+        lens[k] = sp[3 * k + 2];
+        std::string& o = specs[k];
+        if (!meta) {
+            seg_json(o, h, pos, text);
+            continue;
+        }
+        o += "{\"json\":";
+        seg_json(o, h, pos, text);
+        if (h.seq[pos] > h.sc.min_seq)
+            o += ",\"seq\":" + std::to_string(h.seq[pos]) + ",\"client\":\"" + client_name(names, n_names, h.client[pos]) +
+                 "\"";
+        if (h.flags[pos] & MT_SF_REMOVED)
+            o += ",\"removedSeq\":" + std::to_string(h.rseq[pos]) + ",\"removedClient\":\"" +
+                 client_name(names, n_names, h.rclient[pos]) + "\"";
+        o += '}';
+    }
+    // getSeqLengthSegs (:57-79): chunks of >= `chunk` characters
+    struct Chunk { uint32_t start, count; uint64_t length; };
+    std::vector<Chunk> chunks;
+    uint32_t total_count = 0;
+    uint64_t total_len = 0;
+    do {
+        Chunk c{total_count, 0, 0};
+        while (c.length < chunk && c.start + c.count < nspec) c.length += lens[c.start + c.count++];
+        chunks.push_back(c);
+        total_count += c.count;
+        total_len += c.length;
+    } while (total_count < nspec);
+    auto chunk_json = [&](const Chunk& c, bool header) {
+        std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) + ",\"length\":" +
+                        std::to_string(c.length) + ",\"segments\":[";
+        for (uint32_t k = 0; k < c.count; k++) {
+            if (k) o += ',';
+            o += specs[c.start + k];
+        }
+        o += "],\"startIndex\":" + std::to_string(c.start);
+        if (header) {
+            o += ",\"headerMetadata\":{\"minSequenceNumber\":" + std::to_string(h.sc.min_seq) +
+                 ",\"sequenceNumber\":" + std::to_string(h.sc.cur_seq) + ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+            for (size_t b = 1; b < chunks.size(); b++) o += ",{\"id\":\"body_" + std::to_string(b - 1) + "\"}";
+            o += "],\"totalLength\":" + std::to_string(total_len) + ",\"totalSegmentCount\":" +
+                 std::to_string(total_count) + '}';
+        }
+        return o + '}';
+    };
+    std::string o = "{\"header\":" + chunk_json(chunks[0], true);
+    for (size_t b = 1; b < chunks.size(); b++) o += ",\"body_" + std::to_string(b - 1) + "\":" + chunk_json(chunks[b], false);
+    return o + '}';
+}
+
 mt_status copy_out(const std::string& s, char* buf, uint64_t cap, uint64_t* len) {
     if (len) *len = s.size();
     if (buf && cap) {
@@ -614,6 +741,58 @@ mt_status mt_get_state(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint
     mt_status st = read_doc(e, doc, h);
     if (st) return st;
     return copy_out(state_json(h), buf, cap, len);
+}
+
+mt_status mt_get_snapshot(mt_engine* e, uint32_t doc, uint32_t chunk_size, const char* const* client_names,
+                          uint32_t n_names, char* buf, uint64_t cap, uint64_t* len) {
+    if (!e || doc >= e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HostDoc h;
+    mt_status st = read_doc(e, doc, h);
+    if (st) return st;
+    const uint32_t scap = std::max<uint32_t>(1, (uint32_t)h.sc.nseg);
+    uint32_t* d = nullptr;
+    HIP_OK(hipMalloc(&d, (3 * (size_t)scap + 1) * sizeof(uint32_t)));
+    std::vector<uint32_t> sp(3 * (size_t)scap);
+    uint32_t nspec = 0;
+    hipError_t r = mt_launch_snapshot(&e->g, doc, 1, scap, d + 1, d, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(&nspec, d, sizeof nspec, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(sp.data(), d + 1, sp.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (r != hipSuccess) return MT_ERR_HIP;
+    if (nspec > scap) return MT_ERR_STATE;
+    return copy_out(snapshot_json(h, sp, nspec, chunk_size ? chunk_size : 10000u, client_names, n_names), buf, cap,
+                    len);
+}
+
+mt_status mt_snapshot_extract(mt_engine* e, uint32_t d0, uint32_t n, float* kernel_ms, uint64_t* n_specs) {
+    if (!e || d0 > e->n_docs || n > e->n_docs - d0) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    if (n == 0) return MT_OK;
+    const uint32_t cap = e->g.segcap;
+    uint32_t *specs = nullptr, *counts = nullptr;
+    if (hipMalloc(&specs, (size_t)n * cap * 3 * sizeof(uint32_t)) != hipSuccess) return MT_ERR_NOMEM;
+    if (hipMalloc(&counts, (size_t)n * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(specs);
+        return MT_ERR_NOMEM;
+    }
+    hipError_t r = hipEventRecord(e->ev0, e->stream);
+    if (r == hipSuccess) r = mt_launch_snapshot(&e->g, d0, n, cap, specs, counts, e->stream);
+    if (r == hipSuccess) r = hipEventRecord(e->ev1, e->stream);
+    if (r == hipSuccess) r = hipEventSynchronize(e->ev1);
+    float ms = 0.f;
+    if (r == hipSuccess) r = hipEventElapsedTime(&ms, e->ev0, e->ev1);
+    std::vector<uint32_t> hc(n);
+    if (r == hipSuccess) r = hipMemcpy(hc.data(), counts, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(specs);
+    (void)hipFree(counts);
+    if (r != hipSuccess) return MT_ERR_HIP;
+    uint64_t tot = 0;
+    for (uint32_t c : hc) tot += c;
+    if (kernel_ms) *kernel_ms = ms;
+    if (n_specs) *n_specs = tot;
+    return MT_OK;
 }
 
 mt_status mt_get_text(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint64_t* len) {

@@ -139,3 +139,91 @@ extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, ui
     hipLaunchKernelGGL(mt_checksum_kernel, dim3(n_docs), dim3(64), 0, st, *g, n_docs, out);
     return hipGetLastError();
 }
+
+// SnapshotV1.extractSync (packages/dds/merge-tree/src/snapshotV1.ts:151-247) for every document
+// of [d0, d0 + n_docs), one wave per document: each segment is classified lane-parallel (elided:
+// removed at or below the MSN; coalescable: acked below the MSN and live; else it keeps its merge
+// info), then the coalescing decisions (canAppend textSegment.ts:63-68 on the run so far,
+// matchProperties properties.ts:62-93) run in order over the lanes with readlane.  Output per
+// document: specs of 3 u32 {first segment position, span << 1 | has_merge_info, text length},
+// at most nseg of them, and their count.  A coalesced run spans the positions from its first to its
+// last segment; the elided segments inside it (removed at or below the MSN) are not part of it.
+__global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d0, uint32_t n_docs, uint32_t cap,
+                                                         uint32_t* __restrict__ specs, uint32_t* __restrict__ counts) {
+    const uint32_t w = blockIdx.x;
+    if (w >= n_docs) return;
+    const uint32_t d = d0 + w;
+    const int lane = lane_id();
+    const mt_doc_scalars sc = g.sc[d];
+    const int n = sc.nseg;
+    const int32_t msn = sc.min_seq;
+    const size_t so = (size_t)d * g.segcap;
+    uint32_t* out = specs + (size_t)w * cap * 3;
+    int k = 0;
+    bool have = false;
+    int ps = 0, pc = 0;
+    uint32_t plen = 0, pfl = 0;
+    uint64_t pprops = 0;
+    auto emit = [&](int pos, int cnt, bool meta, uint32_t len) {
+        if (lane == 0 && k < (int)cap) {
+            out[3 * k] = (uint32_t)pos;
+            out[3 * k + 1] = ((uint32_t)cnt << 1) | (meta ? 1u : 0u);
+            out[3 * k + 2] = len;
+        }
+        k++;
+    };
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        int cls = 0;  // 0 elided, 1 coalescable, 2 merge info
+        uint32_t len = 0, fl = 0;
+        uint64_t pr = 0;
+        if (i < n) {
+            fl = g.flags[so + i];
+            len = g.len[so + i];
+            pr = g.props[so + i];
+            const bool rm = fl & MT_SF_REMOVED;
+            const int32_t s = g.seq[so + i];
+            if (rm && g.rseq[so + i] <= msn) cls = 0;
+            else if (s <= msn && !rm) cls = 1;
+            else cls = 2;
+        }
+        const int m = min(64, n - base);
+        for (int j = 0; j < m; j++) {
+            const int c = __builtin_amdgcn_readlane(cls, j);
+            if (c == 0) continue;
+            const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+            if (c == 2) {
+                if (have) emit(ps, pc, false, plen);
+                have = false;
+                emit(base + j, 1, true, lj);
+                continue;
+            }
+            const uint32_t fj = (uint32_t)__builtin_amdgcn_readlane((int)fl, j);
+            const uint64_t pj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pr, j) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), j) << 32);
+            if (have && !(pfl & MT_SF_NL) && (plen <= 256u || lj <= 256u) && ((pfl ^ fj) & MT_SF_PDEF) == 0 &&
+                pprops == pj) {
+                pc = base + j - ps + 1;  // span from the run's first segment (elided ones inside it skipped by the reader)
+                plen += lj;
+                pfl = (pfl & ~MT_SF_NL) | (fj & MT_SF_NL);
+            } else {
+                if (have) emit(ps, pc, false, plen);
+                have = true;
+                ps = base + j;
+                pc = 1;
+                plen = lj;
+                pfl = fj;
+                pprops = pj;
+            }
+        }
+    }
+    if (have) emit(ps, pc, false, plen);
+    if (lane == 0) counts[w] = (uint32_t)k;
+}
+
+extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
+                                         uint32_t* specs, uint32_t* counts, hipStream_t st) {
+    if (n_docs == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_snapshot_kernel, dim3(n_docs), dim3(64), 0, st, *g, d0, n_docs, cap, specs, counts);
+    return hipGetLastError();
+}

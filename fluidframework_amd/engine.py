@@ -71,11 +71,15 @@ def lib():
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mt_class_kernel_name.argtypes = [vp, u32, ctypes.c_char_p, u64]
+        L.mt_get_snapshot.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
+                                      ctypes.POINTER(u64)]
+        L.mt_snapshot_extract.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
-                     'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name'):
+                     'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
+                     'mt_get_snapshot', 'mt_snapshot_extract'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -234,6 +238,29 @@ class MergeEngine:
 
     def state(self, doc):
         return json.loads(self._string(lib().mt_get_state, doc))
+
+    def snapshot(self, doc, chunk_size=0, client_names=None):
+        """SnapshotV1 extractSync + emit of one document (snapshotV1.ts:85-247): the emitted
+        tree's blobs as {path: parsed JSON}.  client_names[short id] -> long client id."""
+        names = None
+        n = 0
+        if client_names is not None:
+            n = len(client_names)
+            names = (ctypes.c_char_p * n)(*[x.encode() for x in client_names])
+        L = lib()
+        ln = ctypes.c_uint64()
+        _check(L.mt_get_snapshot(self.h, doc, chunk_size, names, n, None, 0, ctypes.byref(ln)), 'mt_get_snapshot')
+        buf = ctypes.create_string_buffer(ln.value + 1)
+        _check(L.mt_get_snapshot(self.h, doc, chunk_size, names, n, buf, ln.value + 1, ctypes.byref(ln)),
+               'mt_get_snapshot')
+        return json.loads(buf.raw[:ln.value].decode('latin-1'))
+
+    def snapshot_extract(self, d0=0, n=None):
+        """Device extraction for documents [d0, d0+n): (kernel_ms, segment specs)."""
+        n = self.n_docs - d0 if n is None else n
+        ms, cnt = ctypes.c_float(), ctypes.c_uint64()
+        _check(lib().mt_snapshot_extract(self.h, d0, n, ctypes.byref(ms), ctypes.byref(cnt)), 'mt_snapshot_extract')
+        return ms.value, cnt.value
 
     def text(self, doc):
         return self._string(lib().mt_get_text, doc)

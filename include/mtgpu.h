@@ -135,6 +135,19 @@ mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capa
 /* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class
  * `capacity` on this engine: the register engine for <= 1024 segments, else the LDS engine. */
 mt_status mt_class_kernel_name(mt_engine* eng, uint32_t capacity, char* buf, uint64_t cap);
+/* Snapshot of one document: what `new SnapshotV1(mergeTree).extractSync()`
+ * + `emit()` write (packages/dds/merge-tree/src/snapshotV1.ts:85-247) -- the segments below the
+ * MSN coalesced (canAppend + matchProperties), the others with their merge info -- as one JSON
+ * object {"header": chunk, "body_0": chunk, ...} of the emitted tree's blobs.  The extraction
+ * decisions run on the device (mt_service.hip); the JSON is written on the host.  chunk_size =
+ * mergeTreeSnapshotChunkSize (0: 10000).  client_names[short id] = long client id (NULL or a
+ * short table: the short id in decimal).  Props are written as {"k<key id>": value id} (ids as
+ * interned by the host; JSON key order is key-id order, the reference's is insertion order). */
+mt_status mt_get_snapshot(mt_engine* eng, uint32_t doc, uint32_t chunk_size, const char* const* client_names,
+                          uint32_t n_names, char* buf, uint64_t cap, uint64_t* len);
+/* Run the device extraction for documents [d0, d0+n) (all docs of a summary in one launch);
+ * reports the kernel time and the number of segment specs produced (bench tooling). */
+mt_status mt_snapshot_extract(mt_engine* eng, uint32_t d0, uint32_t n, float* kernel_ms, uint64_t* n_specs);
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 

@@ -7,6 +7,8 @@
 //
 //   node replay_ref.js state <log.mtlog> [d0 d1]     -> JSON lines {doc, err, state}
 //   node replay_ref.js bench <log.mtlog> <threads>   -> ops/sec over all docs (worker_threads)
+//   node replay_ref.js snapshot <log.mtlog> [d0 d1 [chunk]]  -> JSON lines {doc, err, snapshot}: the
+//        entries SnapshotV1.extractSync() + emit() write (snapshotV1.ts:85-246), path -> contents
 const fs = require("fs");
 const path = require("path");
 const { Worker, isMainThread, parentPort, workerData } = require("worker_threads");
@@ -15,6 +17,7 @@ const ROOT = path.join(__dirname, "..", "_tsref", "merge-tree", "src");
 const { Client } = require(path.join(ROOT, "client.js"));
 const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
 const { MergeTree } = require(path.join(ROOT, "mergeTree.js"));
+const { SnapshotV1 } = require(path.join(ROOT, "snapshotV1.js"));
 
 const { loadLog, messages } = require(path.join(__dirname, "..", "..", "js", "mtlog.js"));
 
@@ -90,6 +93,27 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "snapshot") {
+        const d0 = process.argv[4] ? parseInt(process.argv[4], 10) : 0;
+        const d1 = Math.min(log.nDocs, process.argv[5] ? parseInt(process.argv[5], 10) : log.nDocs);
+        const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+        const out = [];
+        for (let d = d0; d < d1; d++) {
+            const { c, err } = replayDoc(log, d);
+            if (process.argv[6]) {  // mergeTreeSnapshotChunkSize option (snapshotV1.ts:54)
+                c.mergeTree.options = Object.assign({}, c.mergeTree.options,
+                    { mergeTreeSnapshotChunkSize: parseInt(process.argv[6], 10) });
+            }
+            const snap = new SnapshotV1(c.mergeTree, logger);
+            snap.extractSync();
+            const tree = snap.emit();
+            const entries = {};
+            for (const e of tree.entries) entries[e.path] = JSON.parse(e.value.contents);
+            out.push(JSON.stringify({ doc: d, err, snapshot: entries }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "bench") {
         const threads = parseInt(process.argv[4] || "1", 10);
         const file = process.argv[3];
@@ -110,7 +134,7 @@ function main() {
         }
         return;
     }
-    throw new Error("mode: state | bench");
+    throw new Error("mode: state | snapshot | bench");
 }
 
 if (isMainThread) {

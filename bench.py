@@ -37,6 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r01_pmc_traffic.json')
 
 
+CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
+                'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs'}
+
+
 def pmc_traffic(kernel):
     """Measured HBM bytes per launch of `kernel` (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected),
     from the committed PMC summary of the same bench command; None if it was not profiled."""
@@ -75,7 +79,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     from fluidframework_amd.engine import MergeEngine
-    from fluidframework_amd.oplog import CONFIGS
+    from fluidframework_amd.oplog import CONFIGS, DELI_CONFIGS
     from fluidframework_amd.shard import doc_id_base, gather_checksums, max_over_ranks
 
     cfg = dict(CONFIGS[args.config])
@@ -97,9 +101,34 @@ def main():
     gen_cs = eng.checksums()
     n_ops = dev.n_ops
 
-    for _ in range(args.warmup):
+    deli = None
+    if args.config in DELI_CONFIGS:
+        # C5: the op records' seq / msn are re-derived by deli from the raw client messages inside
+        # every step (deli_kernel stamps them into the staged records; the apply then reads them)
+        from fluidframework_amd.deli import RAW_DTYPE, TICKET_DTYPE, DeliSequencer, batch_device_ptrs
+        from fluidframework_amd.hipmem import DeviceBuffer
+        d_ops, _, d_row = batch_device_ptrs(dev)
+        deli = DeliSequencer(n_docs, device=local_rank)
+        d_msgs = DeviceBuffer(n_ops * RAW_DTYPE.itemsize)
+        d_tick = DeviceBuffer(n_ops * TICKET_DTYPE.itemsize)
+        joined = {c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)}
+        deli.raw_from_ops(d_ops, d_row, n_docs, d_msgs.ptr)
+        deli.sync()
+    deli_ms = 0.0
+
+    def step():
+        nonlocal deli_ms
+        if deli is not None:
+            deli.restore_all(seq=0, clients=joined)
+            deli.ticket_device(d_msgs.ptr, d_row, n_docs, d_tick.ptr, d_ops)
+            deli.sync()
+            deli_ms += deli.last_ms()
         eng.reset()
         eng.apply_staged(dev)
+
+    for _ in range(args.warmup):
+        step()
+    deli_ms = 0.0
 
     kern_ms = 0.0
     launches = 0
@@ -108,8 +137,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.reset()
-        eng.apply_staged(dev)
+        step()
         k, _, nl, nb = eng.last_stats()
         kern_ms += k
         launches += nl
@@ -125,6 +153,9 @@ def main():
     cs = eng.checksums()
     errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 64)) if eng.error(d)[0])
     assert np.array_equal(cs, gen_cs), 'replay does not reproduce the generation state'
+    if deli is not None:
+        t = d_tick.download(TICKET_DTYPE)
+        assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
 
     # final per-document checksum gather to rank 0 over RCCL (the only collective)
     _, digest = gather_checksums(cs, dist, device='cuda')
@@ -160,7 +191,9 @@ def main():
             'data': 'synthetic (device-generated observer-driven op logs, mt_synth.h)',
             'config': {
                 'workload': f'{args.config}: {n_docs} docs/GPU x {cfg["n_clients"]} clients x {ops_per_doc} '
-                            f'sequenced ops/doc (BASELINE.json configs[2]), full merge-tree apply incl. zamboni',
+                            f'sequenced ops/doc ({CONFIG_NAMES.get(args.config, args.config)}), '
+                            + ('deli seq/msn ticketing + ' if deli is not None else '')
+                            + 'full merge-tree apply incl. zamboni',
                 'docs_per_gpu': n_docs, 'ops_per_doc': ops_per_doc, 'ops_per_launch': args.ops_per_launch,
                 'ops_per_step': n_ops * world, 'parallelism': f'doc-sharded x{world} (no collective in apply)',
             },
@@ -174,6 +207,10 @@ def main():
                                       'achieved_GBps': round(all_achieved, 1),
                                       'kernel_share_of_step': round(kern_ms / (elapsed * 1e3), 3)},
             },
+            'deli': None if deli is None else {
+                'kernel_ms_per_step': round(deli_ms / args.steps, 3),
+                'tickets_per_s_kernel': round(n_ops / (deli_ms / args.steps * 1e-3), 1) if deli_ms else None,
+                'share_of_step': round(deli_ms / (elapsed * 1e3), 4)},
             'cpu_baseline': cpu,
             'parity': parity,
             'doc_errors_sampled': errs,

@@ -80,6 +80,12 @@ struct mt_engine {
     // register-resident engine (mt_apply_reg.hip) for classes up to kRegMaxCap segments; the
     // LDS engine (mt_apply.hip) above that, or everywhere with MTGPU_ENGINE=lds
     bool use_reg = true;
+    // the capacity classes of one tick touch disjoint documents: each runs on its own stream
+    // (fork/join around the tick) so the small classes and every class's tail overlap;
+    // MTGPU_SERIAL=1 keeps them on the engine stream, one after another
+    bool concurrent = true;
+    hipStream_t side[kNumClasses] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
 };
 static constexpr int32_t kRegMaxCap = 1024;
 
@@ -146,6 +152,19 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         const char* v = getenv("MTGPU_ENGINE");
         // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
         e->use_reg = !(v && strcmp(v, "lds") == 0) && e->cfg.text_capacity <= 65536;
+        const char* sv = getenv("MTGPU_SERIAL");
+        e->concurrent = !(sv && strcmp(sv, "1") == 0);
+    }
+    if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess) {
+        mt_engine_destroy(e);
+        return MT_ERR_HIP;
+    }
+    for (int c = 0; c < kNumClasses; c++) {
+        if (hipStreamCreateWithFlags(&e->side[c], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->join_ev[c], hipEventDisableTiming) != hipSuccess) {
+            mt_engine_destroy(e);
+            return MT_ERR_HIP;
+        }
     }
     *out = e;
     return MT_OK;
@@ -161,6 +180,14 @@ mt_status mt_engine_destroy(mt_engine* e) {
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     if (e->stream) hipStreamDestroy(e->stream);
+    for (int c = 0; c < kNumClasses; c++) {
+        if (e->side[c]) {
+            (void)hipStreamSynchronize(e->side[c]);
+            (void)hipStreamDestroy(e->side[c]);
+        }
+        if (e->join_ev[c]) (void)hipEventDestroy(e->join_ev[c]);
+    }
+    if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
     delete e;
     return MT_OK;
 }
@@ -243,24 +270,37 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
+        if (e->concurrent) HIP_OK(hipEventRecord(e->fork_ev, e->stream));
+        bool joined[kNumClasses] = {};
         for (int c = 0; c < kNumClasses; c++) {
             const uint32_t cnt = e->h_counts[c];
             if (!cnt) continue;
+            hipStream_t st = e->stream;
+            if (e->concurrent) {
+                st = e->side[c];
+                HIP_OK(hipStreamWaitEvent(st, e->fork_ev, 0));
+                joined[c] = true;
+            }
             while (e->kev.size() < 2 * (nk + 1)) {
                 hipEvent_t ev;
                 HIP_OK(hipEventCreate(&ev));
                 e->kev.push_back(ev);
             }
-            HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
+            HIP_OK(hipEventRecord(e->kev[2 * nk], st));
             if (e->use_reg && kClasses[c] <= kRegMaxCap)
                 HIP_OK(mt_launch_apply_reg(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
-                                           e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
+                                           e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
             else
                 HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
-                                       e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->stream));
-            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
+                                       e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], st));
             e->kev_cls.push_back(c);
             nk++;
+        }
+        for (int c = 0; c < kNumClasses; c++) {  // join: the next tick's binning sees every class done
+            if (!joined[c]) continue;
+            HIP_OK(hipEventRecord(e->join_ev[c], e->side[c]));
+            HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
     }
     HIP_OK(hipEventRecord(e->ev1, e->stream));
@@ -418,6 +458,12 @@ mt_status mt_sync(mt_engine* e) {
     if (!e) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+mt_status mt_set_concurrent_classes(mt_engine* e, int on) {
+    if (!e) return MT_ERR_ARG;
+    e->concurrent = on != 0;
     return MT_OK;
 }
 

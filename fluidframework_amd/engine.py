@@ -65,6 +65,7 @@ def lib():
         L.mt_last_apply_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_seg_counts.argtypes = [vp, vp, u32]
+        L.mt_set_concurrent_classes.argtypes = [vp, i32]
         L.mt_last_apply_class_stats.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float),
                                                 ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
@@ -79,7 +80,7 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_snapshot_extract'):
+                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -195,6 +196,10 @@ class MergeEngine:
         _check(lib().mt_last_apply_stats(self.h, ctypes.byref(ms), ctypes.byref(wall), ctypes.byref(launches),
                                          ctypes.byref(nbytes)), 'mt_last_apply_stats')
         return ms.value, wall.value, launches.value, nbytes.value
+
+    def set_concurrent_classes(self, on):
+        """Capacity classes of a tick on concurrent streams (True, default) or serialized (False)."""
+        _check(lib().mt_set_concurrent_classes(self.h, 1 if on else 0), 'mt_set_concurrent_classes')
 
     def last_class_stats(self):
         """[(capacity, kernel_ms, launches, alg_bytes)] per LDS capacity class of the last apply."""

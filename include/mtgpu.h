@@ -128,6 +128,10 @@ mt_status mt_doc_error(mt_engine* eng, uint32_t doc, int32_t* code, int32_t* seq
  * alg_bytes = algorithmic bytes they move (DESIGN.md "Roofline accounting"). */
 mt_status mt_last_apply_stats(mt_engine* eng, float* kernel_ms, float* wall_ms, uint32_t* launches,
                               uint64_t* alg_bytes);
+/* Capacity classes of one tick run concurrently on their own streams (on = 1, the default; the
+ * environment variable MTGPU_SERIAL=1 starts an engine with 0) or one after another on the
+ * engine stream (on = 0: each class kernel has the GPU to itself, for per-kernel rooflines). */
+mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
 /* The same, per capacity class (cls = 0..5 for 128/256/512/768/1024/2048 segments; MT_ERR_ARG
  * past the last): each class is one kernel instantiation (see mt_class_kernel_name). */
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,

@@ -1358,19 +1358,28 @@ struct RWave {
 // Two waves per SIMD for the big classes: the state is register-resident, so occupancy is what
 // hides the latency of each op's dependent steps (a few spills at K = 16 are cheaper than one
 // wave per SIMD).
-// an op record as field loads (a struct copy would go through a private-memory temporary)
-MT_DEV mt_op_rec load_op(const mt_op_rec* p) {
+// Op records in blocks of 8 (256 B: lane l holds dword l % 8 of record base + l / 8), double-
+// buffered: a record's fields are readlanes of a register loaded 7..15 ops earlier, so the op loop
+// never waits on the memory latency of the record it is about to apply (scalar loads would: the
+// LDS waits of the apply share their lgkm counter).
+MT_DEV uint32_t load_op_block(const mt_op_rec* ops, uint32_t base, uint32_t end, int lane) {
+    const uint32_t r = base + (uint32_t)(lane >> 3);
+    return r < end ? reinterpret_cast<const uint32_t*>(ops + r)[lane & 7] : 0u;
+}
+MT_DEV mt_op_rec op_from_block(uint32_t blk, uint32_t j) {
+    const int l = (int)(j * 8);
     mt_op_rec r;
-    r.seq = p->seq;
-    r.ref_seq = p->ref_seq;
-    r.msn = p->msn;
-    r.client = p->client;
-    r.type = p->type;
-    r.flags = p->flags;
-    r.pos1 = p->pos1;
-    r.pos2 = p->pos2;
-    r.payload_off = p->payload_off;
-    r.payload_len = p->payload_len;
+    r.seq = __builtin_amdgcn_readlane((int)blk, l + 0);
+    r.ref_seq = __builtin_amdgcn_readlane((int)blk, l + 1);
+    r.msn = __builtin_amdgcn_readlane((int)blk, l + 2);
+    const uint32_t w3 = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 3);
+    r.client = (uint16_t)(w3 & 0xFFFFu);
+    r.type = (uint8_t)((w3 >> 16) & 0xFFu);
+    r.flags = (uint8_t)(w3 >> 24);
+    r.pos1 = __builtin_amdgcn_readlane((int)blk, l + 4);
+    r.pos2 = __builtin_amdgcn_readlane((int)blk, l + 5);
+    r.payload_off = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 6);
+    r.payload_len = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 7);
     return r;
 }
 
@@ -1411,18 +1420,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? MT
     PROF_BEGIN(tl);
     wv.load(kernarg_gstate(), d);
     PROF_END(wv.prof, P_LOAD, tl);
-    // software pipeline: the record of op i+2 and the payload of op i+1 are in flight while op i
-    // is applied
-    mt_op_rec q0 = load_op(ops + a);
-    mt_op_rec q1 = a + 1 < b ? load_op(ops + a + 1) : q0;
-    uint32_t pb0 = wv.lane < (int)q0.payload_len ? payload[q0.payload_off + wv.lane] : 0u;
+    // software pipeline: the records of the next 7..15 ops and the payload of op i+1 are in flight
+    // while op i is applied
+    uint32_t blk0 = load_op_block(ops, a, b, wv.lane);
+    uint32_t blk1 = load_op_block(ops, a + 8, b, wv.lane);
+    mt_op_rec nx = op_from_block(blk0, 0);
+    uint32_t pb0 = wv.lane < (int)nx.payload_len ? payload[nx.payload_off + wv.lane] : 0u;
     for (uint32_t i = a; i < b; i++) {
         if (wv.err) break;
-        const mt_op_rec op = q0;
+        const mt_op_rec op = nx;
         wv.pb = pb0;
-        q0 = q1;
-        if (i + 2 < b) q1 = load_op(ops + i + 2);
-        pb0 = (i + 1 < b && wv.lane < (int)q0.payload_len) ? payload[q0.payload_off + wv.lane] : 0u;
+        const uint32_t j = (i + 1 - a) & 7u;  // op i+1's record in its block
+        if (j == 0) {
+            blk0 = blk1;
+            blk1 = load_op_block(ops, i + 9, b, wv.lane);
+        }
+        if (i + 1 < b) {
+            nx = op_from_block(blk0, j);
+            pb0 = wv.lane < (int)nx.payload_len ? payload[nx.payload_off + wv.lane] : 0u;
+        }
         wv.apply(op, payload);
 #ifdef MT_PROF
         wv.prof[P_OPS]++;

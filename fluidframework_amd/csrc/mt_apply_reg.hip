@@ -1393,16 +1393,20 @@ MT_DEV const mt_gstate& kernarg_gstate() {
     return *p;
 }
 
-// (tools/variants.sh A/Bs other choices: 3 or 4 waves at K = 12 spill 150-400 VGPRs and run at
-// 0.63x / 0.39x on C3)
+// (tools/variants.sh A/Bs other choices on MI355X: K = 12 at 3 / 4 waves spills 150-400 VGPRs and
+// runs C3 at 0.63x / 0.39x; K = 8 at 2 / 4 waves runs C4 at 0.87x / 0.72x; K = 4 at 3 waves runs
+// C5 at 0.92x)
 #ifndef MT_WPE12
 #define MT_WPE12 2
 #endif
 #ifndef MT_WPE8
 #define MT_WPE8 3
 #endif
+#ifndef MT_WPE4
+#define MT_WPE4 4
+#endif
 template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? MT_WPE12 : (K == 8 ? MT_WPE8 : 4)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? MT_WPE12 : (K == 8 ? MT_WPE8 : MT_WPE4)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,

@@ -34,18 +34,22 @@ sys.path.insert(0, HERE)
 METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofline'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof_r01.sh -> tools/pmc_traffic.py)
-PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r01_pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r01_pmc_traffic.json')  # C3; other configs: _<config>.json
+
+
+def pmc_path(config):
+    return PMC_TRAFFIC if config == 'C3' else PMC_TRAFFIC.replace('.json', f'_{config}.json')
 
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
                 'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs'}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, config):
     """Measured HBM bytes per launch of `kernel` (2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected),
-    from the committed PMC summary of the same bench command; None if it was not profiled."""
+    from the committed PMC summary of the same bench command and config; None if not profiled."""
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(pmc_path(config)) as f:
             k = json.load(f)['kernels'].get(kernel)
     except (OSError, ValueError, KeyError):
         return None
@@ -213,8 +217,8 @@ def main():
             },
             'roofline': {
                 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(eng.class_kernel(dom)),
-                'traffic_source': os.path.relpath(PMC_TRAFFIC, HERE) + ' (bytes per launch)',
+                'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(eng.class_kernel(dom), args.config),
+                'traffic_source': os.path.relpath(pmc_path(args.config), HERE) + ' (bytes per launch)',
                 'kernel': eng.class_kernel(dom), 'launches': d_n,
                 'measured_in': 'an extra untimed step with the capacity classes serialized'
                                if rcls is not cls else 'the timed steps (classes serialized)',

@@ -57,7 +57,8 @@ MT_DEV int wave_total(int v) { return wave_last(wave_incl_scan(v)); }
 
 // ---- optional per-phase cycle accounting (diagnostic build: -DMT_PROF; never in the product)
 enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, P_OPS, P_ZPOP, P_REPACK,
-       P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT, P_NSLOT };
+       P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT,
+       P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_NSLOT };
 #ifdef MT_PROF
 __device__ unsigned long long mt_prof_acc[120];  // [class 0..4][24 slots]
 MT_DEV uint64_t prof_now() {
@@ -444,6 +445,8 @@ struct RWave {
     }
     // relocate every linked segment's text, in slot order, into the other arena half
     MT_DEV void compact_text() {
+        PROF_BEGIN(tc);
+        PROF_CNT(P_N_COMPACT, 1);
         arena_sync();
 #pragma unroll
         for (int j = 0; j < K; j++) s.scr[idx(j)] = (int32_t)(((lvm >> j) & 1u) ? li[j] : kEmptyLi);
@@ -469,6 +472,7 @@ struct RWave {
         text_half ^= 1u;
         text_top = carry;
         arena = dst;
+        PROF_END(prof, P_COMPACT, tc);
     }
     MT_DEV bool arena_reserve(uint32_t need, int32_t sq) {
         if (text_top + need <= textcap) return true;
@@ -621,6 +625,7 @@ struct RWave {
                 continue;    // a compaction lays the run out contiguously
             }
             const uint32_t top = text_top;
+            PROF_CNT(P_N_APPBYTES, total);
             uint64_t pieces = __ballot(in_run);
             while (pieces) {
                 const int q = first_lane(pieces);

@@ -70,3 +70,23 @@ def test_engines_agree():
         eng.apply(batch)
         sums.append(eng.checksums())
     assert np.array_equal(sums[0], sums[1])
+
+
+def test_concurrent_classes_match_serialized(oracle_lib):
+    """The capacity classes of a tick run on their own streams by default; serializing them
+    (mt_set_concurrent_classes(eng, 0)) must give the same state, and both the oracle's.  A mix
+    of growing documents and > 32-client documents puts several classes (and both engines) into
+    the same ticks."""
+    n = 96
+    grow = oracle_lib.generate(n, seed=31, **WORKLOADS['grow'])
+    want = oracle_lib.Oracle(n).apply(grow, threads=8).checksums()
+    sums = []
+    for concurrent in (True, False):
+        eng = _engine(n, 16)
+        eng.set_concurrent_classes(concurrent)
+        eng.apply(grow)
+        sums.append(eng.checksums())
+        classes = [cap for cap, _, launches, _ in eng.last_class_stats() if launches]
+        assert len(classes) >= 3, classes
+    assert np.array_equal(sums[0], sums[1])
+    assert np.array_equal(sums[0], want)

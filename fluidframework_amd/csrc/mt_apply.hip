@@ -617,8 +617,7 @@ struct Wave {
     MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, pos = op.pos1;
-        scan(R, C);
-        if (!boundary(pos, R, C, S)) return;
+        if (!boundary(pos, R, C, S)) return;  // cum: apply() scanned for (R, C)
         if (tlen > 0) {  // blockInsert (mergeTree.ts:2141-2224)
             block_starts();
             const int nb = s.nb[0];
@@ -701,8 +700,7 @@ struct Wave {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, start = op.pos1, end = op.pos2;
         const bool is_remove = op.type == MT_OP_REMOVE;
-        scan(R, C);
-        if (!boundary(start, R, C, S)) return;
+        if (!boundary(start, R, C, S)) return;  // cum: apply() scanned for (R, C)
         if (!boundary(end, R, C, S)) return;
         // markRangeRemoved / annotateRange leaf actions over mapRange (mergeTree.ts:2903-2965)
         const int n = s.n;
@@ -783,20 +781,28 @@ struct Wave {
         if (op.type != MT_OP_NOOP) {
             if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
-            if (!(s.cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);   // client.ts:461-462
-            if (!(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // client.ts:463-464
+        } else {  // every assert of the message before any edit: the document halts before it
+            if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);  // client.ts:824
+            if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
         }
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
         const uint8_t* pairs = pay + tlen;
         for (int q = 0; q < np; q++)
             if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
-        if (op.type == MT_OP_INSERT) {
-            if (op.pos1 < 0) return fail(MT_DERR_BAD_OP, S);
-            op_insert(op, pay, tlen, pairs, np);
-        } else if (op.type != MT_OP_NOOP) {
-            if (op.pos1 < 0 || op.pos2 < 0) return fail(MT_DERR_BAD_OP, S);
-            op_range(op, pairs, np);
+        if (op.type != MT_OP_NOOP) {
+            if (op.pos1 < 0 || (op.type != MT_OP_INSERT && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
+            const int L = scan(op.ref_seq, op.client);  // cum for the op's view (no edit yet)
+            // the window asserts run after the op in the reference (completeAndLogOp, client.ts:461-464;
+            // updateSeqNumbers :826), so a failing insert (mergeTree.ts:2210) is reported first; all of
+            // them are decided here, before any edit: the document halts before the failing message
+            int wc = 0;
+            if (!(s.cur_seq < S)) wc = MT_DERR_SEQ_ORDER;
+            else if (!(s.min_seq <= op.msn) || !(op.msn <= S)) wc = MT_DERR_MSN_ORDER;
+            if (op.type == MT_OP_INSERT && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
+            if (wc) return fail(wc, S);
+            if (op.type == MT_OP_INSERT) op_insert(op, pay, tlen, pairs, np);
+            else op_range(op, pairs, np);
         }
         if (s.err) return;
         if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);

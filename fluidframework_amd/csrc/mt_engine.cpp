@@ -114,6 +114,8 @@ const char* mt_version(void) { return "libmtgpu 0.1 (gfx950)"; }
 
 mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     if (!cfg || !out || cfg->max_docs == 0) return MT_ERR_ARG;
+    // the register / LDS classes reach 2048 slots and read whole rows of that size
+    if (cfg->seg_capacity != 0 && cfg->seg_capacity < 2048) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(cfg->device));
     auto* e = new mt_engine();
     e->cfg = *cfg;
@@ -189,6 +191,13 @@ mt_status mt_engine_destroy(mt_engine* e) {
     }
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
     delete e;
+    return MT_OK;
+}
+
+mt_status mt_engine_info(const mt_engine* e, uint32_t* n_docs, uint32_t* max_docs) {
+    if (!e) return MT_ERR_ARG;
+    if (n_docs) *n_docs = e->n_docs;
+    if (max_docs) *max_docs = e->cfg.max_docs;
     return MT_OK;
 }
 

@@ -91,8 +91,12 @@ typedef struct mt_cfg {
 typedef struct mt_engine mt_engine;
 typedef struct mt_batch mt_batch;
 
+/* seg_capacity: 0 = 2048; values below 2048 are rejected (MT_ERR_ARG) -- the capacity classes
+ * go up to 2048 segments and every document's slot rows must hold the largest one. */
 mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out);
 mt_status mt_engine_destroy(mt_engine* eng);
+/* documents started by the last mt_docs_init, and the engine's max_docs (either may be NULL) */
+mt_status mt_engine_info(const mt_engine* eng, uint32_t* n_docs, uint32_t* max_docs);
 
 /* Start `n_docs` empty documents: Client + startOrUpdateCollaboration(observer, 0, 0)
  * (client.ts:1051-1071, mergeTree.ts:1254-1271). */

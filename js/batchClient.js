@@ -163,6 +163,13 @@ class BatchClient {
                 text = op.seg.text;
                 if (op.seg.props) { r.flags |= F_PROPS; pairs = this._pairs(op.seg.props); }
             } else throw new Error("BatchClient: only text segments are supported (markers: SURVEY §8f)");
+            if (typeof text !== "string") throw new Error("BatchClient: segment text must be a string");
+            // the device arena holds one byte per UTF-16 code unit, so lengths and positions equal the
+            // reference's cachedLength = text.length (textSegment.ts:45) only up to U+00FF: anything
+            // wider is refused here rather than stored truncated
+            if (/[^\u0000-\u00ff]/.test(text)) {
+                throw new Error("BatchClient: text with UTF-16 code units above U+00FF is not supported by the device engine");
+            }
             r.type = INSERT; r.pos1 = op.pos1;
             r.npairs = pairs.length / 2;
             r.payload = Buffer.concat([Buffer.from(text, "latin1"), Buffer.from(pairs)]);

@@ -25,6 +25,10 @@ class DeliSequencer {
         this.maxDocs = opts.maxDocs || 1;
         this.handle = native.createDeli({ device: opts.device || 0, maxDocs: this.maxDocs });
         this.ids = Array.from({ length: this.maxDocs }, () => new Map());  // long client id -> short
+        // short ids given back by processed leaves, reused before new ones (Fluid gives every
+        // connection a new client id, so a long-lived document sees far more than 64 of them)
+        this.free = Array.from({ length: this.maxDocs }, () => []);
+        this.next = new Uint32Array(this.maxDocs);
         this.queues = Array.from({ length: this.maxDocs }, () => []);
         this.pending = 0;
     }
@@ -33,10 +37,22 @@ class DeliSequencer {
         const m = this.ids[doc];
         let s = m.get(longId);
         if (s === undefined) {
-            s = m.size;
-            if (s >= MAX_CLIENTS) throw new Error(`deli: more than ${MAX_CLIENTS} clients in document ${doc}`);
+            s = this._freeSlot(doc, true);
             m.set(longId, s);
         }
+        return s;
+    }
+
+    // a short id no long id holds: its device record is not joined (never used, or cleared by the
+    // leave that gave it back).  take = reserve it for a new long id.
+    _freeSlot(doc, take) {
+        const f = this.free[doc];
+        if (f.length) return take ? f.shift() : f[0];
+        const s = this.next[doc];
+        if (s >= MAX_CLIENTS) {
+            throw new Error(`deli: more than ${MAX_CLIENTS} concurrently known clients in document ${doc}`);
+        }
+        if (take) this.next[doc] = s + 1;
         return s;
     }
 
@@ -51,7 +67,13 @@ class DeliSequencer {
         }
         switch (op.type) {
             case "join": return [JOIN, this._short(doc, JSON.parse(op.data).clientId), csn, ref];
-            case "leave": return [LEAVE, this._short(doc, JSON.parse(op.data)), csn, ref];
+            case "leave": {
+                // a leave of a client this document never saw is dropped by ticket() (lambda.ts:281-285):
+                // it takes any unjoined slot and interns nothing
+                const leaver = JSON.parse(op.data);
+                const s = this.ids[doc].get(leaver);
+                return [LEAVE, s === undefined ? this._freeSlot(doc, false) : s, csn, ref, leaver];
+            }
             case "noop": return [SERVER_NOOP, 0, csn, ref];
             case "noClient": return [NOCLIENT, 0, csn, ref];
             case "control": return [CONTROL, 0, csn, ref];
@@ -88,9 +110,16 @@ class DeliSequencer {
         k = 0;
         for (let d = 0; d < this.maxDocs; d++) {
             const res = [];
-            for (const [raw] of this.queues[d]) {
+            for (const [raw, enc] of this.queues[d]) {
                 const o = k * REC;
                 const status = t.readUInt8(o + 12);
+                if (enc[0] === LEAVE && enc[4] !== undefined && this.ids[d].get(enc[4]) === enc[1] &&
+                    status !== 7) {
+                    // after its leave the client is out of the ClientSequenceNumberManager
+                    // (removeClient, lambda.ts:281-285): its short id is free again
+                    this.ids[d].delete(enc[4]);
+                    this.free[d].push(enc[1]);
+                }
                 const r = { status: STATUS[status], message: raw };
                 if (status === 1 || status === 2 || status === 3) {
                     r.sequenceNumber = t.readInt32LE(o);

@@ -1,6 +1,7 @@
 /* mtgpu_napi.c -- Node N-API addon over the C-ABI of libmtgpu.so (include/mtgpu.h).
  * Plain C, N-API 8 (node 12+).  js/batchClient.js is the JavaScript surface above it. */
 #include <node_api.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -24,16 +25,62 @@ static napi_value throw_status(napi_env env, const char* what, mt_status st) {
     return NULL;
 }
 
-static mt_engine* get_engine(napi_env env, napi_value v) {
+/* One engine + a FIFO turnstile.  libmtgpu's engine is not thread-safe (mtgpu.h), and
+ * submitAsync runs mt_submit on a libuv pool thread while the JS thread stays free: every entry
+ * point takes a ticket in call order on the JS thread and runs only when every earlier ticket
+ * has finished, so batches apply in the order they were flushed and a readout sees every batch
+ * flushed before it (a sync call blocks the JS thread until the async work ahead of it is done). */
+typedef struct {
+    mt_engine* e;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    uint64_t next, serving;
+} engine_box;
+
+static uint64_t take_ticket(engine_box* b) {
+    pthread_mutex_lock(&b->mu);
+    const uint64_t t = b->next++;
+    pthread_mutex_unlock(&b->mu);
+    return t;
+}
+static void wait_turn(engine_box* b, uint64_t t) {
+    pthread_mutex_lock(&b->mu);
+    while (b->serving != t) pthread_cond_wait(&b->cv, &b->mu);
+    pthread_mutex_unlock(&b->mu);
+}
+static void end_turn(engine_box* b) {
+    pthread_mutex_lock(&b->mu);
+    b->serving++;
+    pthread_cond_broadcast(&b->cv);
+    pthread_mutex_unlock(&b->mu);
+}
+/* a synchronous entry point: its turn comes after every ticket handed out before it */
+static engine_box* enter(engine_box* b) {
+    if (b) wait_turn(b, take_ticket(b));
+    return b;
+}
+static void leave(engine_box* b) {
+    if (b) end_turn(b);
+}
+
+static engine_box* get_box(napi_env env, napi_value v) {
     void* p = NULL;
     if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
-    return (mt_engine*)p;
+    return (engine_box*)p;
 }
 
 static void finalize_engine(napi_env env, void* data, void* hint) {
     (void)env;
     (void)hint;
-    if (data) mt_engine_destroy((mt_engine*)data);
+    engine_box* b = (engine_box*)data;
+    if (!b) return;
+    /* an external is finalized only when unreachable, i.e. after every pending job released it */
+    enter(b);
+    mt_engine_destroy(b->e);
+    leave(b);
+    pthread_cond_destroy(&b->cv);
+    pthread_mutex_destroy(&b->mu);
+    free(b);
 }
 
 static uint32_t get_u32(napi_env env, napi_value obj, const char* key, uint32_t dflt) {
@@ -70,8 +117,20 @@ static napi_value create_engine(napi_env env, napi_callback_info info) {
         mt_engine_destroy(e);
         return throw_status(env, "mt_docs_init", st);
     }
-    NAPI_CALL(env, napi_create_external(env, e, finalize_engine, NULL, &out));
+    engine_box* b = (engine_box*)calloc(1, sizeof *b);
+    b->e = e;
+    pthread_mutex_init(&b->mu, NULL);
+    pthread_cond_init(&b->cv, NULL);
+    NAPI_CALL(env, napi_create_external(env, b, finalize_engine, NULL, &out));
     return out;
+}
+
+/* rows of a CSR batch the engine will read: rowPtr must cover n_docs + 1 entries and ops whole
+ * 32-byte records (mtgpu.h mt_batch_upload) */
+static int batch_shape_ok(mt_engine* e, size_t nops, size_t nrow) {
+    uint32_t n_docs = 0;
+    if (mt_engine_info(e, &n_docs, NULL) != MT_OK) return 0;
+    return nops % sizeof(mt_op_rec) == 0 && nrow >= 4 * ((size_t)n_docs + 1);
 }
 
 static void* buffer_data(napi_env env, napi_value v, size_t* len) {
@@ -101,17 +160,21 @@ static napi_value submit(napi_env env, napi_callback_info info) {
     size_t argc = 4;
     napi_value argv[4];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    mt_engine* e = get_engine(env, argv[0]);
+    engine_box* b = get_box(env, argv[0]);
     size_t nops, npay, nrow;
     const void* ops = buffer_data(env, argv[1], &nops);
     const void* pay = buffer_data(env, argv[2], &npay);
     const void* row = buffer_data(env, argv[3], &nrow);
-    if (!e || (!ops && nops) || !row) {
+    if (!b || (!ops && nops) || !row) {
         napi_throw_type_error(env, NULL, "submit(engine, ops, payload, rowPtr)");
         return NULL;
     }
-    mt_status st = mt_submit(e, (const mt_op_rec*)ops, nops / sizeof(mt_op_rec), (const uint8_t*)pay, npay,
-                             (const uint32_t*)row);
+    enter(b);
+    mt_status st = batch_shape_ok(b->e, nops, nrow)
+                       ? mt_submit(b->e, (const mt_op_rec*)ops, nops / sizeof(mt_op_rec), (const uint8_t*)pay, npay,
+                                   (const uint32_t*)row)
+                       : MT_ERR_ARG;
+    leave(b);
     if (st) return throw_status(env, "mt_submit", st);
     return NULL;
 }
@@ -121,8 +184,9 @@ static napi_value submit(napi_env env, napi_callback_info info) {
 typedef struct {
     napi_async_work work;
     napi_deferred deferred;
-    napi_ref refs[3];
-    mt_engine* e;
+    napi_ref refs[4];
+    engine_box* b;
+    uint64_t ticket;
     const void* ops;
     const void* pay;
     const void* row;
@@ -133,8 +197,10 @@ typedef struct {
 static void submit_execute(napi_env env, void* data) {
     (void)env;
     submit_job* j = (submit_job*)data;
-    j->st = mt_submit(j->e, (const mt_op_rec*)j->ops, j->nops / sizeof(mt_op_rec), (const uint8_t*)j->pay, j->npay,
+    wait_turn(j->b, j->ticket);
+    j->st = mt_submit(j->b->e, (const mt_op_rec*)j->ops, j->nops / sizeof(mt_op_rec), (const uint8_t*)j->pay, j->npay,
                       (const uint32_t*)j->row);
+    end_turn(j->b);
 }
 
 static void submit_complete(napi_env env, napi_status status, void* data) {
@@ -145,11 +211,13 @@ static void submit_complete(napi_env env, napi_status status, void* data) {
         napi_resolve_deferred(env, j->deferred, v);
     } else {
         napi_value msg;
-        napi_create_string_utf8(env, "mt_submit failed", NAPI_AUTO_LENGTH, &msg);
+        char buf[64];
+        snprintf(buf, sizeof buf, "mt_submit failed (status %d)", (int)j->st);
+        napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &msg);
         napi_create_error(env, NULL, msg, &v);
         napi_reject_deferred(env, j->deferred, v);
     }
-    for (int i = 0; i < 3; i++) napi_delete_reference(env, j->refs[i]);
+    for (int i = 0; i < 4; i++) napi_delete_reference(env, j->refs[i]);
     napi_delete_async_work(env, j->work);
     free(j);
 }
@@ -159,17 +227,24 @@ static napi_value submit_async(napi_env env, napi_callback_info info) {
     napi_value argv[4], promise, name;
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     submit_job* j = (submit_job*)calloc(1, sizeof *j);
-    j->e = get_engine(env, argv[0]);
+    j->b = get_box(env, argv[0]);
     j->ops = buffer_data(env, argv[1], &j->nops);
     j->pay = buffer_data(env, argv[2], &j->npay);
     size_t nrow;
     j->row = buffer_data(env, argv[3], &nrow);
-    if (!j->e || !j->row) {
+    if (!j->b || !j->row || (!j->ops && j->nops)) {
         free(j);
         napi_throw_type_error(env, NULL, "submitAsync(engine, ops, payload, rowPtr)");
         return NULL;
     }
-    for (int i = 0; i < 3; i++) napi_create_reference(env, argv[1 + i], 1, &j->refs[i]);
+    /* the shape check reads only engine constants (n_docs), safe outside the turnstile */
+    if (!batch_shape_ok(j->b->e, j->nops, nrow)) {
+        free(j);
+        return throw_status(env, "submitAsync", MT_ERR_ARG);
+    }
+    /* the engine external is referenced too: it cannot be finalized while the job is pending */
+    for (int i = 0; i < 4; i++) napi_create_reference(env, argv[i], 1, &j->refs[i]);
+    j->ticket = take_ticket(j->b);  /* call order = apply order */
     NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
     NAPI_CALL(env, napi_create_string_utf8(env, "mtgpu.submit", NAPI_AUTO_LENGTH, &name));
     NAPI_CALL(env, napi_create_async_work(env, NULL, name, submit_execute, submit_complete, j, &j->work));
@@ -183,14 +258,19 @@ static napi_value get_string(napi_env env, napi_callback_info info, string_fn fn
     size_t argc = 2;
     napi_value argv[2], out;
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    mt_engine* e = get_engine(env, argv[0]);
+    engine_box* b = get_box(env, argv[0]);
     uint32_t doc = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    if (!b) return throw_status(env, what, MT_ERR_ARG);
     uint64_t n = 0;
-    mt_status st = fn(e, doc, NULL, 0, &n);
-    if (st) return throw_status(env, what, st);
-    char* buf = (char*)malloc(n + 1);
-    st = fn(e, doc, buf, n + 1, &n);
+    char* buf = NULL;
+    enter(b);
+    mt_status st = fn(b->e, doc, NULL, 0, &n);
+    if (!st) {
+        buf = (char*)malloc(n + 1);
+        st = fn(b->e, doc, buf, n + 1, &n);
+    }
+    leave(b);
     if (st) {
         free(buf);
         return throw_status(env, what, st);
@@ -214,7 +294,11 @@ static napi_value get_length(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     uint32_t doc = 0, len = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
-    mt_status st = mt_get_length(get_engine(env, argv[0]), doc, &len);
+    engine_box* b = get_box(env, argv[0]);
+    if (!b) return throw_status(env, "mt_get_length", MT_ERR_ARG);
+    enter(b);
+    mt_status st = mt_get_length(b->e, doc, &len);
+    leave(b);
     if (st) return throw_status(env, "mt_get_length", st);
     NAPI_CALL(env, napi_create_uint32(env, len, &out));
     return out;
@@ -222,18 +306,22 @@ static napi_value get_length(napi_env env, napi_callback_info info) {
 
 static napi_value doc_error(napi_env env, napi_callback_info info) {
     size_t argc = 2;
-    napi_value argv[2], out, a, b;
+    napi_value argv[2], out, a, bv;
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     uint32_t doc = 0;
     int32_t code = 0, seq = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
-    mt_status st = mt_doc_error(get_engine(env, argv[0]), doc, &code, &seq);
+    engine_box* b = get_box(env, argv[0]);
+    if (!b) return throw_status(env, "mt_doc_error", MT_ERR_ARG);
+    enter(b);
+    mt_status st = mt_doc_error(b->e, doc, &code, &seq);
+    leave(b);
     if (st) return throw_status(env, "mt_doc_error", st);
     NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
     NAPI_CALL(env, napi_create_int32(env, code, &a));
-    NAPI_CALL(env, napi_create_int32(env, seq, &b));
+    NAPI_CALL(env, napi_create_int32(env, seq, &bv));
     NAPI_CALL(env, napi_set_element(env, out, 0, a));
-    NAPI_CALL(env, napi_set_element(env, out, 1, b));
+    NAPI_CALL(env, napi_set_element(env, out, 1, bv));
     return out;
 }
 
@@ -246,7 +334,11 @@ static napi_value checksums(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &n));
     void* data = NULL;
     NAPI_CALL(env, napi_create_buffer(env, (size_t)n * 8, &data, &out));
-    mt_status st = mt_checksums(get_engine(env, argv[0]), (uint64_t*)data, n);
+    engine_box* b = get_box(env, argv[0]);
+    if (!b) return throw_status(env, "mt_checksums", MT_ERR_ARG);
+    enter(b);
+    mt_status st = mt_checksums(b->e, (uint64_t*)data, n);
+    leave(b);
     if (st) return throw_status(env, "mt_checksums", st);
     return out;
 }
@@ -292,7 +384,7 @@ static napi_value deli_ticket(napi_env env, napi_callback_info info) {
     size_t nmsg, nrow;
     const void* msgs = buffer_data(env, argv[1], &nmsg);
     const void* row = buffer_data(env, argv[2], &nrow);
-    if (!dl || (!msgs && nmsg) || !row || nrow < 4) {
+    if (!dl || (!msgs && nmsg) || !row || nrow < 4 || nmsg % sizeof(mt_raw_msg) != 0 || nrow % 4 != 0) {
         napi_throw_type_error(env, NULL, "deliTicket(deli, msgs, rowPtr)");
         return NULL;
     }

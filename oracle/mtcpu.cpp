@@ -402,11 +402,28 @@ struct Doc {
         if (err) return;
         const int32_t S = op.seq, R = op.ref_seq, C = op.client;
         const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        // Every assert the reference raises for this message is checked BEFORE anything is
+        // applied, in the reference's order: the document halts in the state of the messages
+        // before it (the reference throws after the op's tree edits, leaving them half-done).
+        if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
         if (op.type != MT_OP_NOOP) {
             if (op.client >= MT_MAX_CLIENTS || op.client == 0) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
-            if (!(currentSeq < S)) return fail(MT_DERR_SEQ_ORDER, S);   // client.ts:461-462
-            if (!(minSeq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S); // client.ts:463-464
+            int wc = 0;
+            if (!(currentSeq < S)) wc = MT_DERR_SEQ_ORDER;              // completeAndLogOp, client.ts:461-462
+            else if (!(minSeq <= op.msn)) wc = MT_DERR_MSN_ORDER;       // client.ts:463-464
+            else if (!(op.msn <= S)) wc = MT_DERR_MSN_ORDER;            // updateSeqNumbers, client.ts:826
+            if (wc) {
+                // those asserts run after the op: a failing insert throws first (mergeTree.ts:2210)
+                const int tl = (int)op.payload_len - 2 * np;
+                if (op.type == MT_OP_INSERT && tl > 0 && op.pos1 > nodeLen(root, op.ref_seq, op.client))
+                    wc = MT_DERR_INSERT_FAILED;
+                return fail(wc, S);
+            }
+        } else {
+            if (!(currentSeq <= S)) return fail(MT_DERR_SEQ_ORDER, S);  // updateSeqNumbers, client.ts:824
+            if (!(op.msn <= S)) return fail(MT_DERR_MSN_ORDER, S);      // client.ts:826
+            if (!(minSeq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S); // setMinSeq, mergeTree.ts:1722
         }
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;

@@ -6,6 +6,10 @@
 // TEST INFRASTRUCTURE ONLY (this container; the reference never travels to the GPU box).
 //
 //   node replay_ref.js state <log.mtlog> [d0 d1]     -> JSON lines {doc, err, state}
+//   node replay_ref.js errstate <log.mtlog>           -> JSON lines {doc, err, err_msg_index, err_seq,
+//        state}: where applyMsg throws, the thrown message, the index and sequenceNumber of the
+//        message that threw, and the state after the messages BEFORE it (the reference leaves a
+//        half-applied op behind a throw; the engine halts the document before the failing op)
 //   node replay_ref.js bench <log.mtlog> <threads>   -> ops/sec over all docs (worker_threads)
 //   node replay_ref.js snapshot <log.mtlog> [d0 d1 [chunk]]  -> JSON lines {doc, err, snapshot}: the
 //        entries SnapshotV1.extractSync() + emit() write (snapshotV1.ts:85-246), path -> contents
@@ -93,6 +97,29 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "errstate") {
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const msgs = Array.from(messages(log, d));
+            let c = newObserver(), err = null, at = -1;
+            for (let i = 0; i < msgs.length && err === null; i++) {
+                try {
+                    c.applyMsg(msgs[i]);
+                } catch (e) {
+                    err = String(e.message || e);
+                    at = i;
+                }
+            }
+            if (err !== null) {
+                c = newObserver();
+                for (let i = 0; i < at; i++) c.applyMsg(msgs[i]);
+            }
+            out.push(JSON.stringify({ doc: d, err, err_msg_index: at, err_seq: at >= 0 ? msgs[at].sequenceNumber : null,
+                state: canonical(c) }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "snapshot") {
         const d0 = process.argv[4] ? parseInt(process.argv[4], 10) : 0;
         const d1 = Math.min(log.nDocs, process.argv[5] ? parseInt(process.argv[5], 10) : log.nDocs);
@@ -134,7 +161,7 @@ function main() {
         }
         return;
     }
-    throw new Error("mode: state | snapshot | bench");
+    throw new Error("mode: state | errstate | snapshot | bench");
 }
 
 if (isMainThread) {

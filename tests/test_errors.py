@@ -1,0 +1,186 @@
+"""Error semantics of applyMsg, pinned by the reference itself.
+
+tests/golden/errors.{mtlog,expected.jsonl} (tests/golden/make_golden.py `errors()`): logs on which
+the reference's observer Client THROWS -- seq order (client.ts:461-462, 824), msn order
+(client.ts:463-464, 826; mergeTree.ts:1722 setMinSeq), "MergeTree insert failed"
+(mergeTree.ts:2210-2216) -- next to out-of-range removes / annotates and a same-seq non-op message
+that the reference accepts.  For each document the fixture holds the thrown message, the
+sequenceNumber of the message that threw, and the reference's state after the messages BEFORE it.
+The engine (and the oracle) must report the matching sticky code with that seq and halt in
+exactly that state.
+
+Device-only limits (capacity, malformed records, id ranges) have no reference counterpart: the
+engine must flag exactly the offending document and leave every other document of the batch
+bit-exact with the oracle.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+# the reference's Error messages -> mt_doc_err (include/mtgpu.h)
+REF_ERRORS = [
+    ("Incoming remote op sequence# <= local collabWindow's currentSequence#", 1),  # client.ts:461-462
+    ("Incoming op sequence# < local collabWindow's currentSequence#", 1),          # client.ts:824
+    ("Incoming remote op minSequence# < local collabWindow's minSequence#", 2),    # client.ts:463-464
+    ("Incoming op sequence# < minSequence#", 2),                                   # client.ts:826
+    ("MergeTree insert failed", 3),                                                # mergeTree.ts:2210-2216
+    ("Error", 2),  # setMinSeq's message-less assert(minSeq <= msn) (mergeTree.ts:1722), via common-utils assert
+]
+
+
+def ref_code(msg):
+    if msg is None:
+        return 0
+    for prefix, code in REF_ERRORS:
+        if msg == prefix or (prefix != 'Error' and msg.startswith(prefix)):
+            return code
+    raise AssertionError(f'unmapped reference error {msg!r}')
+
+
+def test_fixture_covers_every_reference_error():
+    _, exp = load_golden('errors')
+    codes = {ref_code(r['err']) for r in exp}
+    assert codes == {0, 1, 2, 3}
+    assert sum(1 for r in exp if r['err']) >= 10
+
+
+def test_oracle_matches_reference_errors(oracle_lib):
+    batch, exp = load_golden('errors')
+    o = oracle_lib.Oracle(batch.n_docs).apply(batch)
+    cs = o.checksums()
+    for r in exp:
+        d = r['doc']
+        code = ref_code(r['err'])
+        assert o.error(d) == ((code, r['err_seq']) if code else (0, 0)), (d, r['err'])
+        assert o.state(d) == r['state'], d
+        assert '%016x' % cs[d] == r['checksum'], d
+
+
+def _engine(n, b, engine=None):
+    import os
+
+    from fluidframework_amd.engine import MergeEngine
+    old = os.environ.get('MTGPU_ENGINE')
+    try:
+        if engine:
+            os.environ['MTGPU_ENGINE'] = engine
+        else:
+            os.environ.pop('MTGPU_ENGINE', None)
+        return MergeEngine(n, ops_per_launch=b)
+    finally:
+        if old is None:
+            os.environ.pop('MTGPU_ENGINE', None)
+        else:
+            os.environ['MTGPU_ENGINE'] = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('engine', [None, 'lds'])
+@pytest.mark.parametrize('b', [0, 2])
+def test_engine_matches_reference_errors(engine, b):
+    batch, exp = load_golden('errors')
+    eng = _engine(batch.n_docs, b, engine)
+    eng.apply(batch)
+    cs = eng.checksums()
+    for r in exp:
+        d = r['doc']
+        code = ref_code(r['err'])
+        assert eng.error(d) == ((code, r['err_seq']) if code else (0, 0)), (d, r['err'], engine, b)
+        assert eng.state(d) == r['state'], (d, engine, b)
+        assert '%016x' % cs[d] == r['checksum'], (d, engine, b)
+
+
+@pytest.mark.gpu
+def test_errors_stay_sticky_across_batches():
+    """A halted document ignores every later batch; its neighbours keep going."""
+    from fluidframework_amd.oplog import OpBatch
+    batch, exp = load_golden('errors')
+    eng = _engine(batch.n_docs, 4)
+    eng.apply(batch)
+    before = eng.checksums()
+    # a second batch: one valid NOOP per document, seq far ahead, msn unchanged per document
+    ops = np.zeros(batch.n_docs, dtype=batch.ops.dtype)
+    for d in range(batch.n_docs):
+        last = batch.ops[int(batch.row_ptr[d + 1]) - 1]
+        ops[d]['seq'] = 1000
+        ops[d]['ref_seq'] = 999
+        ops[d]['msn'] = exp[d]['state']['msn']
+        ops[d]['client'] = last['client']
+        ops[d]['type'] = 3
+    eng.apply(OpBatch(ops, np.zeros(1, np.uint8), np.arange(batch.n_docs + 1, dtype=np.uint32)))
+    after = eng.checksums()
+    for r in exp:
+        d = r['doc']
+        if r['err']:
+            assert after[d] == before[d], d
+            assert eng.error(d)[0] == ref_code(r['err'])
+        else:
+            assert eng.state(d)['seq'] == 1000, d
+
+
+def _device_limit_batch(oracle_lib, faulty=True):
+    """8 healthy synthetic documents, 4 of which end in an op that breaks a device limit, and one
+    document that grows past 2048 segments.  faulty=False: the same without the breaking ops.
+    Returns (batch, {doc: expected device code})."""
+    from fluidframework_amd.oplog import INSERT, NOOP, OP_DTYPE, REMOVE, OpBatch
+    healthy = oracle_lib.generate(8, seed=61, n_clients=6, ops_per_doc=200, max_lag=8, n_keys=2, n_values=4,
+                                  p_insert=0.6, p_remove=0.3, p_insert_props=0.2)
+    docs, payload = [], bytearray()
+
+    def rec(seq, ref, msn, client, typ, p1=0, p2=0, data=b'', flags=0):
+        docs[-1].append((seq, ref, msn, client, typ, flags, p1, p2, len(payload), len(data)))
+        payload.extend(data)
+    for d in range(8):
+        docs.append([])
+        m = int(healthy.ops[healthy.row_ptr[d + 1] - 1]['msn'])
+        for o in healthy.ops[healthy.row_ptr[d]:healthy.row_ptr[d + 1]]:
+            data = bytes(healthy.payload[o['payload_off']:o['payload_off'] + o['payload_len']])
+            rec(int(o['seq']), int(o['ref_seq']), int(o['msn']), int(o['client']), int(o['type']), int(o['pos1']),
+                int(o['pos2']), data, int(o['flags']))
+        if not faulty:
+            continue
+        if d == 1:   # client id 65 (short ids < 64: MT_DERR_LIMITS)
+            rec(201, 200, m, 65, INSERT, 0, 0, b'x')
+        if d == 3:   # unknown op type (MT_DERR_BAD_OP)
+            rec(201, 200, m, 1, 9)
+        if d == 5:   # property key 8 (8 keys per document on the device: MT_DERR_LIMITS)
+            rec(201, 200, m, 2, INSERT, 0, 0, b'ab' + bytes([8, 1]), 2 | (1 << 3))
+        if d == 7:   # negative position (MT_DERR_BAD_OP)
+            rec(201, 200, m, 2, REMOVE, -3, 2)
+    # one more document: > 2048 single-char segments (device capacity: MT_DERR_CAPACITY)
+    docs.append([])
+    for k in range(2300):
+        rec(k + 1, k, 0, 1 + k % 3, INSERT, 0, 0, b'abcdefghij'[k % 10:k % 10 + 1])
+    rec(2301, 2300, 0, 1, NOOP)
+    rows = np.cumsum([0] + [len(x) for x in docs]).astype(np.uint32)
+    ops = np.array([r for x in docs for r in x], dtype=OP_DTYPE)
+    return OpBatch(ops, np.frombuffer(bytes(payload), np.uint8), rows), {1: 6, 3: 7, 5: 6, 7: 7, 8: 4}
+
+
+def test_oracle_flags_malformed_records(oracle_lib):
+    """The oracle shares the record-level checks (client ids, op type, positions); its tree and
+    key table are unbounded (32 keys), so the key-8 and > 2048-segment documents replay fine."""
+    batch, _ = _device_limit_batch(oracle_lib)
+    o = oracle_lib.Oracle(batch.n_docs).apply(batch)
+    want = {1: (6, 201), 3: (7, 201), 7: (7, 201)}
+    for d in range(batch.n_docs):
+        assert o.error(d) == want.get(d, (0, 0)), d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('engine', [None, 'lds'])
+def test_engine_flags_device_limits(oracle_lib, engine):
+    """Malformed records and device limits: the expected code at the breaking op's seq, the
+    document halted in the state before that op (the oracle's replay without it); the
+    > 2048-segment document: MT_DERR_CAPACITY; every other document bit-exact."""
+    batch, bad = _device_limit_batch(oracle_lib)
+    clean, _ = _device_limit_batch(oracle_lib, faulty=False)
+    want = oracle_lib.Oracle(clean.n_docs).apply(clean).checksums()
+    eng = _engine(batch.n_docs, 32, engine)
+    eng.apply(batch)
+    got = eng.checksums()
+    for d in range(8):
+        assert eng.error(d) == ((bad[d], 201) if d in bad else (0, 0)), d
+        assert got[d] == want[d], d
+    assert eng.error(8)[0] == bad[8]

@@ -78,3 +78,57 @@ def test_deli_sequencer_replays_lambda_spec():
     assert above[2][2] == 20 and above[5][2] == 22
     assert nacked[3][0] == 'nack' and nacked[3][3].startswith('Refseq')
     assert nacked[4][0] == 'nack' and nacked[4][3] == 'Nonexistent client'
+
+
+def test_batchclient_refuses_text_beyond_latin1():
+    """The device arena stores one byte per UTF-16 code unit: text above U+00FF (CJK, a surrogate
+    pair) must throw at applyMsg, never be stored truncated (textSegment.ts:45 cachedLength =
+    text.length); Latin-1 text is accepted.  No device work: the record is refused on the host."""
+    if not _addon():
+        pytest.skip('node headers absent')
+    js = ("const {BatchClient}=require('./js/batchClient.js');"
+          "const c=new BatchClient({pending:0},0);c.startOrUpdateCollaboration('observer');"
+          "const bad=[];for (const t of ['\\u4e2d\\u6587','a\\ud83d\\ude00b']) {"
+          " try {c.insertTextRemote(0,t,undefined,1,0,'w');bad.push(t);} catch(e) {"
+          "  if (!/U\\+00FF/.test(e.message)) throw e;}}"
+          "c.insertTextRemote(0,'caf\\u00e9',undefined,1,0,'w');"
+          "if (bad.length) throw new Error('accepted '+JSON.stringify(bad));"
+          "if (c.queue.length!==1||c.queue[0].payload.length!==4) throw new Error('latin-1 record');"
+          "console.log('ok')")
+    out = subprocess.run([NODE, '-e', js], cwd=REPO, capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == 'ok'
+
+
+@pytest.mark.gpu
+def test_flush_async_in_order_then_sync_read():
+    """submitAsync runs on a libuv pool thread; two unawaited flushAsync() and a sync
+    getText() must not overlap on the engine: batches apply once each, in flush order."""
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'async_order.js')], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout)
+    # every insert at position 0 with refSeq = seq - 1 lands in front: the text is the inserts
+    # of the document in reverse seq order
+    seq, want = 0, [[] for _ in range(4)]
+    for _ in range(6):
+        for d in range(4):
+            for _ in range(5):
+                seq += 1
+                want[d].append(chr(97 + seq % 26))
+    assert r['text'] == [''.join(reversed(w)) for w in want]
+    assert r['length'] == [30] * 4
+
+
+@pytest.mark.gpu
+def test_deli_reuses_short_ids_after_leave():
+    """200 sessions (join, 2 ops, leave) of one document through DeliSequencer: ids of
+    processed leaves are reused, every op is sent, the leave of a never-seen client is dropped."""
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'deli_reuse.js')], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout)
+    assert r['statuses'] == {'dropped': 1, 'sent': 800}
+    assert r['seq'] == 800 and r['interned'] == 0

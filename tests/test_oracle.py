@@ -80,3 +80,29 @@ def test_differential_fuzz_against_reference(oracle_lib, tmp_path):
         r = json.loads(line)
         assert r['err'] is None
         assert o.state(r['doc']) == r['state']
+
+
+# The reference's own merge-tree spec files, run on the type-stripped reference (oracle/_tsref)
+# through oracle/tsref/run_specs.js: this pins the transpile that produced every golden fixture
+# ("record the oracle pin in-repo").  The farms (conflict / reconnect) are the slow
+# ones (~55 s together).
+REFERENCE_SPECS = [
+    'client.applyMsg.spec', 'mergeTree.markRangeRemoved.spec', 'mergeTree.insertingWalk.spec',
+    'mergeTree.annotate.spec', 'mergeTree.insert.deltaCallback.spec', 'mergeTree.markRangeRemoved.deltaCallback.spec',
+    'mergeTree.annotate.deltaCallback.spec', 'properties.spec', 'snapshot.spec', 'snapshotlegacy.spec', 'client.spec',
+    'tracking.spec', 'client.localReference.spec', 'resetPendingSegmentsToOp.spec', 'segmentGroupCollection.spec',
+    'collections.list.spec', 'client.walkSegments.spec', 'client.conflictFarm.spec', 'client.reconnectFarm.spec',
+]
+
+
+@pytest.mark.reference
+@pytest.mark.skipif(not os.path.isdir('/root/reference/packages/dds/merge-tree/src') or not shutil.which('node'),
+                    reason='needs /root/reference and node (build container)')
+def test_reference_specs_pass_on_the_transpile():
+    subprocess.check_call([os.sys.executable, os.path.join(REPO, 'oracle', 'tsref', 'build_ref.py')],
+                          stdout=subprocess.DEVNULL)
+    out = subprocess.run(['node', os.path.join(REPO, 'oracle', 'tsref', 'run_specs.js')] + REFERENCE_SPECS,
+                         capture_output=True, text=True, timeout=600)
+    res = json.loads(out.stdout.strip().split('\n')[-1])
+    assert out.returncode == 0 and res['fail'] == 0, out.stdout[-3000:]
+    assert res['pass'] >= 130, res

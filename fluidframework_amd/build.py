@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libmtgpu.so')
-SOURCES = ['mt_apply.hip', 'mt_apply_reg.hip', 'mt_service.hip', 'mt_deli.hip', 'mt_engine.cpp']
+SOURCES = ['mt_apply.hip', 'mt_apply_reg.hip', 'mt_service.hip', 'mt_deli.hip', 'mt_engine.cpp', 'mt_comm.cpp']
 HEADERS = ['mt_state.h', 'mt_wave.h', 'mt_checksum.h', 'mt_synth.h', '../../include/mtgpu.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
@@ -43,7 +43,9 @@ def build(force=False, verbose=False, prof=False):
 
     with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
         objs = list(ex.map(cc, srcs))
-    subprocess.check_call([HIPCC, f'--offload-arch={ARCH}', '-shared', '-o', lib + '.tmp'] + objs)
+    # RCCL (the end-of-run checksum gather, mt_comm.cpp) from /opt/rocm
+    subprocess.check_call([HIPCC, f'--offload-arch={ARCH}', '-shared', '-o', lib + '.tmp'] + objs +
+                          ['-L/opt/rocm/lib', '-lrccl', '-Wl,-rpath,/opt/rocm/lib'])
     os.replace(lib + '.tmp', lib)
     return lib
 

@@ -1051,6 +1051,7 @@ struct GenArgs {
     uint32_t* pay_used; // [doc]
     uint32_t paycap;    // payload bytes per document region
     uint32_t doc_id_base; // global id of local document 0 (the RNG stream is per global doc id)
+    const uint32_t* gids; // or the global id of every local document (a hash-routed shard)
 };
 
 template <int CAP, bool GEN>
@@ -1077,7 +1078,7 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
             lds.gpay = gen.pay_used[d];
         }
         wave_sync();
-        const uint64_t key = mto_rng_key(gen.cfg.seed, gen.doc_id_base + d);
+        const uint64_t key = mto_rng_key(gen.cfg.seed, gen.gids ? gen.gids[d] : gen.doc_id_base + d);
         const size_t pbase = (size_t)d * gen.paycap;
         for (uint32_t i = a; i < b; i++) {
             if (lds.err) break;
@@ -1146,10 +1147,10 @@ extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const m
 }
 
 extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
-                                    int32_t* cref, int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
+                                    const uint32_t* gids, int32_t* cref, int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
                                     uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                     uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
-    mt::GenArgs ga{*cfg, cref, stall, pay_used, paycap, doc_id_base};
+    mt::GenArgs ga{*cfg, cref, stall, pay_used, paycap, doc_id_base, gids};
     return launch_any(cap_class, true, g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga, stream);
 }
 

@@ -67,7 +67,8 @@ MT_DEV int pick(const V8& a, int k) {
 // 16-byte load per lane, prefetched a chunk ahead); tickets go back the same way.
 __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __restrict__ msgs,
                                                   const uint32_t* __restrict__ row_ptr, uint32_t n_docs,
-                                                  int4* __restrict__ out, mt_op_rec* __restrict__ ops) {
+                                                  int4* __restrict__ out, mt_op_rec* __restrict__ ops,
+                                                  uint64_t n_ops) {
     __shared__ int4 stage[64];
     const int lane = lane_id();
     const int li = lane & (kGroup - 1), gbase = lane & ~(kGroup - 1);
@@ -208,8 +209,10 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
         }
         if (jb + li < len) {
             out[r0 + jb + li] = t;
-            if (ops) {
-                mt_op_rec* o = ops + r0 + jb + li;
+            // my message of this chunk is still staged: its op_index links the op record
+            const uint32_t opi = (uint32_t)stage[lane].w;
+            if (ops && opi && opi <= n_ops) {
+                mt_op_rec* o = ops + (opi - 1u);
                 o->seq = t.w == MT_TK_SENT ? t.x : -1;
                 o->msn = t.y;
                 o->ref_seq = t.z;
@@ -273,7 +276,44 @@ __global__ __launch_bounds__(64) void raw_from_ops_kernel(const mt_op_rec* __res
             const int v = __builtin_amdgcn_readlane(cnt, c);
             if (lane == j) mine = v;
         }
-        if (lane < n) msgs[base + lane] = make_int4(mine, rf, (cl & 0xFFFF) | (MT_RAW_OP << 16), 0);
+        if (lane < n) msgs[base + lane] = make_int4(mine, rf, (cl & 0xFFFF) | (MT_RAW_OP << 16), (int)(base + lane + 1));
+    }
+}
+
+// a new document's raw stream: n_join joins, then the op messages (refSeq + n_join)
+__global__ __launch_bounds__(64) void raw_stream_kernel(const mt_op_rec* __restrict__ ops,
+                                                        const uint32_t* __restrict__ row_ptr, uint32_t n_docs,
+                                                        uint32_t n_join, int4* __restrict__ msgs,
+                                                        uint32_t* __restrict__ msg_row) {
+    const uint32_t d = blockIdx.x;
+    if (d >= n_docs) return;
+    const int lane = lane_id();
+    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+    const uint32_t m0 = r0 + d * n_join;
+    if (lane == 0) {
+        msg_row[d] = m0;
+        if (d + 1 == n_docs) msg_row[n_docs] = r1 + n_docs * n_join;
+    }
+    for (uint32_t j = (uint32_t)lane; j < n_join; j += 64)
+        msgs[m0 + j] = make_int4(-1, -1, (int)((j + 1) & 0xFFFF) | (MT_RAW_JOIN << 16), 0);
+    int cnt = 0;
+    for (uint32_t base = r0; base < r1; base += 64) {
+        const int n = (int)min(64u, r1 - base);
+        int cl = 0, rf = 0;
+        if (lane < n) {
+            cl = ops[base + lane].client;
+            rf = ops[base + lane].ref_seq;
+        }
+        int mine = 0;
+        for (int j = 0; j < n; j++) {
+            const int c = __builtin_amdgcn_readlane(cl, j) & (MT_MAX_CLIENTS - 1);
+            if (lane == c) cnt++;
+            const int v = __builtin_amdgcn_readlane(cnt, c);
+            if (lane == j) mine = v;
+        }
+        if (lane < n)
+            msgs[m0 + n_join + (base - r0) + lane] =
+                make_int4(mine, rf + (int)n_join, (cl & 0xFFFF) | (MT_RAW_OP << 16), (int)(base + lane + 1));
     }
 }
 
@@ -305,10 +345,11 @@ int32_t ckpt_msn(const mt_deli_checkpoint& ck) {
     return m == INT_MAX ? ck.seq : m;
 }
 mt_status launch_ticket(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row, uint32_t n_docs,
-                        mt_ticket* d_out, mt_op_rec* d_ops) {
+                        mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops) {
     DL_HIP(hipEventRecord(dl->e0, dl->stream));
     hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, dl->stream, dl->g,
-                       reinterpret_cast<const int4*>(d_msgs), d_row, n_docs, reinterpret_cast<int4*>(d_out), d_ops);
+                       reinterpret_cast<const int4*>(d_msgs), d_row, n_docs, reinterpret_cast<int4*>(d_out), d_ops,
+                       n_ops);
     DL_HIP(hipGetLastError());
     DL_HIP(hipEventRecord(dl->e1, dl->stream));
     return MT_OK;
@@ -428,7 +469,7 @@ mt_status mt_deli_ticket(mt_deli* dl, const mt_raw_msg* msgs, uint64_t n_msgs, c
          hipMemcpyAsync(d_row, doc_row_ptr, (n_docs + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, dl->stream) !=
              hipSuccess))
         st = MT_ERR_HIP;
-    if (st == MT_OK) st = launch_ticket(dl, d_msgs, d_row, n_docs, d_out, nullptr);
+    if (st == MT_OK) st = launch_ticket(dl, d_msgs, d_row, n_docs, d_out, nullptr, 0);
     if (st == MT_OK &&
         (hipMemcpyAsync(out, d_out, n_msgs * sizeof(mt_ticket), hipMemcpyDeviceToHost, dl->stream) != hipSuccess ||
          hipStreamSynchronize(dl->stream) != hipSuccess))
@@ -441,11 +482,11 @@ mt_status mt_deli_ticket(mt_deli* dl, const mt_raw_msg* msgs, uint64_t n_msgs, c
 }
 
 mt_status mt_deli_ticket_device(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row_ptr, uint32_t n_docs,
-                                mt_ticket* d_out, mt_op_rec* d_ops) {
+                                mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops) {
     if (!dl || !d_msgs || !d_row_ptr || !d_out || n_docs > dl->max_docs) return MT_ERR_ARG;
     if (n_docs == 0) return MT_OK;
     DL_HIP(hipSetDevice(dl->device));
-    return launch_ticket(dl, d_msgs, d_row_ptr, n_docs, d_out, d_ops);
+    return launch_ticket(dl, d_msgs, d_row_ptr, n_docs, d_out, d_ops, n_ops);
 }
 
 mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
@@ -455,6 +496,17 @@ mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32
     DL_HIP(hipSetDevice(dl->device));
     hipLaunchKernelGGL(mtd::raw_from_ops_kernel, dim3(n_docs), dim3(64), 0, dl->stream, d_ops, d_row_ptr, n_docs,
                        reinterpret_cast<int4*>(d_msgs));
+    DL_HIP(hipGetLastError());
+    return MT_OK;
+}
+
+mt_status mt_deli_raw_stream(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
+                             uint32_t n_join, mt_raw_msg* d_msgs, uint32_t* d_msg_row_ptr) {
+    if (!dl || !d_ops || !d_row_ptr || !d_msgs || !d_msg_row_ptr || n_join >= MT_MAX_CLIENTS) return MT_ERR_ARG;
+    if (n_docs == 0) return MT_OK;
+    DL_HIP(hipSetDevice(dl->device));
+    hipLaunchKernelGGL(mtd::raw_stream_kernel, dim3(n_docs), dim3(64), 0, dl->stream, d_ops, d_row_ptr, n_docs, n_join,
+                       reinterpret_cast<int4*>(d_msgs), d_msg_row_ptr);
     DL_HIP(hipGetLastError());
     return MT_OK;
 }

@@ -33,7 +33,7 @@ extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, ui
 extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
                                          uint32_t* specs, uint32_t* counts, hipStream_t st);
 extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
-                                    int32_t* cref,
+                                    const uint32_t* gids, int32_t* cref,
                                     int32_t* stall, uint32_t* pay_used, uint32_t paycap, mt_op_rec* ops,
                                     uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                     uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
@@ -339,8 +339,8 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     return MT_OK;
 }
 
-mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_id_base, uint32_t payload_per_doc,
-                             mt_batch** out) {
+static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_id_base, const uint32_t* ids,
+                                uint32_t payload_per_doc, mt_batch** out) {
     if (!e || !cfg || !out || cfg->n_clients == 0 || cfg->n_clients >= MT_MAX_CLIENTS || cfg->n_keys > MT_MAX_KEYS ||
         cfg->n_values > MT_MAX_VALUES)
         return MT_ERR_ARG;
@@ -356,8 +356,9 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
     std::vector<uint32_t> rp(n + 1);
     for (uint32_t d = 0; d <= n; d++) rp[d] = d * per;
     int32_t *cref = nullptr, *stall = nullptr;
-    uint32_t* pay_used = nullptr;
-    if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
+    uint32_t *pay_used = nullptr, *gids = nullptr;
+    if ((ids && hipMalloc(&gids, std::max<uint32_t>(1, n) * sizeof(uint32_t)) != hipSuccess) ||
+        hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
         hipMalloc(&b->payload, std::max<uint64_t>(1, b->payload_bytes)) != hipSuccess ||
         hipMalloc(&b->row_ptr, (n + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&cref, (size_t)n * 64 * sizeof(int32_t)) != hipSuccess ||
@@ -366,11 +367,14 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
         if (cref) (void)hipFree(cref);
         if (stall) (void)hipFree(stall);
         if (pay_used) (void)hipFree(pay_used);
+        if (gids) (void)hipFree(gids);
         mt_batch_free(e, b);
         return MT_ERR_NOMEM;
     }
     mt_status st = MT_OK;
     hipError_t r = hipMemcpyAsync(b->row_ptr, rp.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess && gids)
+        r = hipMemcpyAsync(gids, ids, n * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream);
     if (r == hipSuccess) r = hipMemsetAsync(cref, 0, (size_t)n * 64 * sizeof(int32_t), e->stream);
     if (r == hipSuccess) r = hipMemsetAsync(stall, 0, (size_t)n * sizeof(int32_t), e->stream);
     if (r == hipSuccess) r = hipMemsetAsync(pay_used, 0, (size_t)n * sizeof(uint32_t), e->stream);
@@ -386,7 +390,7 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
         if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
         for (int c = 0; r == hipSuccess && c < kNumClasses; c++) {
             if (!e->h_counts[c]) continue;
-            r = mt_launch_gen(lds_cap(kClasses[c]), &e->g, cfg, doc_id_base, cref, stall, pay_used, payload_per_doc, b->ops,
+            r = mt_launch_gen(lds_cap(kClasses[c]), &e->g, cfg, doc_id_base, gids, cref, stall, pay_used, payload_per_doc, b->ops,
                               b->payload, b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);
         }
     }
@@ -394,6 +398,7 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
     (void)hipFree(cref);
     (void)hipFree(stall);
     (void)hipFree(pay_used);
+    if (gids) (void)hipFree(gids);
     if (r != hipSuccess) {
         fprintf(stderr, "libmtgpu: mt_synth_generate: %s\n", hipGetErrorString(r));
         mt_batch_free(e, b);
@@ -401,6 +406,17 @@ mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_
     }
     *out = b;
     return st;
+}
+
+mt_status mt_synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_id_base, uint32_t payload_per_doc,
+                            mt_batch** out) {
+    return synth_generate(e, cfg, doc_id_base, nullptr, payload_per_doc, out);
+}
+
+mt_status mt_synth_generate_ids(mt_engine* e, const mt_synth_cfg* cfg, const uint32_t* doc_ids,
+                                uint32_t payload_per_doc, mt_batch** out) {
+    if (!doc_ids) return MT_ERR_ARG;
+    return synth_generate(e, cfg, 0, doc_ids, payload_per_doc, out);
 }
 
 mt_status mt_batch_info(const mt_batch* b, uint64_t* n_ops, uint64_t* payload_bytes, uint32_t* max_ops_per_doc) {
@@ -505,6 +521,15 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
     const size_t n = std::min<size_t>(cap - 1, strlen(tmp));
     memcpy(buf, tmp, n);
     buf[n] = 0;
+    return MT_OK;
+}
+
+mt_status mt_checksums_device(mt_engine* e, uint64_t* d_out, uint32_t n_docs) {
+    if (!e || !d_out || n_docs > e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    if (!n_docs) return MT_OK;
+    HIP_OK(mt_launch_checksum(&e->g, n_docs, d_out, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
     return MT_OK;
 }
 

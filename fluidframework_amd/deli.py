@@ -23,7 +23,7 @@ DELI_ERRORS = {0: None, 1: 'client id out of range', 2: 'unknown message kind',
 MAX_CLIENTS = 64
 
 RAW_DTYPE = np.dtype([('csn', '<i4'), ('ref_seq', '<i4'), ('client', '<u2'), ('kind', 'u1'), ('pad', 'u1'),
-                      ('reserved', '<u4')])
+                      ('op_index', '<u4')])  # 1 + linked op record (fused hand-off), 0 = none
 TICKET_DTYPE = np.dtype([('seq', '<i4'), ('msn', '<i4'), ('ref_seq', '<i4'), ('status', 'u1'), ('pad', 'u1', (3,))])
 assert RAW_DTYPE.itemsize == 16 and TICKET_DTYPE.itemsize == 16
 
@@ -51,15 +51,16 @@ def _lib():
         L.mt_deli_restore.argtypes = [vp, u32, u32, vp]
         L.mt_deli_restore_all.argtypes = [vp, u32, vp]
         L.mt_deli_ticket.argtypes = [vp, vp, u64, vp, u32, vp]
-        L.mt_deli_ticket_device.argtypes = [vp, vp, vp, u32, vp, vp]
+        L.mt_deli_ticket_device.argtypes = [vp, vp, vp, u32, vp, vp, u64]
         L.mt_deli_raw_from_ops.argtypes = [vp, vp, vp, u32, vp]
+        L.mt_deli_raw_stream.argtypes = [vp, vp, vp, u32, u32, vp, vp]
         L.mt_deli_sync.argtypes = [vp]
         L.mt_deli_last_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.mt_deli_get_checkpoint.argtypes = [vp, u32, vp]
         L.mt_deli_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.mt_batch_device_ptrs.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]
         for name in ('mt_deli_create', 'mt_deli_destroy', 'mt_deli_restore', 'mt_deli_restore_all', 'mt_deli_ticket',
-                     'mt_deli_ticket_device', 'mt_deli_raw_from_ops', 'mt_deli_sync', 'mt_deli_last_ms',
+                     'mt_deli_ticket_device', 'mt_deli_raw_from_ops', 'mt_deli_raw_stream', 'mt_deli_sync', 'mt_deli_last_ms',
                      'mt_deli_get_checkpoint', 'mt_deli_doc_error', 'mt_batch_device_ptrs'):
             getattr(L, name).restype = ctypes.c_int
         _bound = True
@@ -119,12 +120,19 @@ class DeliSequencer:
                'mt_deli_ticket')
         return out
 
-    def ticket_device(self, d_msgs, d_row_ptr, n_docs, d_out, d_ops=None):
-        """Asynchronous ticketing of device-resident buffers (raw device pointers as ints)."""
-        _check(_lib().mt_deli_ticket_device(self.h, d_msgs, d_row_ptr, n_docs, d_out, d_ops), 'mt_deli_ticket_device')
+    def ticket_device(self, d_msgs, d_row_ptr, n_docs, d_out, d_ops=None, n_ops=0):
+        """Asynchronous ticketing of device-resident buffers (raw device pointers as ints); with
+        d_ops, messages whose op_index = k + 1 stamp op record k (k < n_ops)."""
+        _check(_lib().mt_deli_ticket_device(self.h, d_msgs, d_row_ptr, n_docs, d_out, d_ops, n_ops),
+               'mt_deli_ticket_device')
 
     def raw_from_ops(self, d_ops, d_row_ptr, n_docs, d_msgs):
         _check(_lib().mt_deli_raw_from_ops(self.h, d_ops, d_row_ptr, n_docs, d_msgs), 'mt_deli_raw_from_ops')
+
+    def raw_stream(self, d_ops, d_row_ptr, n_docs, n_join, d_msgs, d_msg_row_ptr):
+        """C5's raw streams: n_join joins then the log's op messages, per document (mtgpu.h)."""
+        _check(_lib().mt_deli_raw_stream(self.h, d_ops, d_row_ptr, n_docs, n_join, d_msgs, d_msg_row_ptr),
+               'mt_deli_raw_stream')
 
     def sync(self):
         _check(_lib().mt_deli_sync(self.h), 'mt_deli_sync')

@@ -69,6 +69,9 @@ def lib():
         L.mt_last_apply_class_stats.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float),
                                                 ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
+        L.mt_synth_generate_ids.argtypes = [vp, vp, vp, u32, ctypes.POINTER(vp)]
+        L.mt_engine_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+        L.mt_checksums_device.argtypes = [vp, vp, u32]
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mt_class_kernel_name.argtypes = [vp, u32, ctypes.c_char_p, u64]
@@ -80,7 +83,8 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes'):
+                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_synth_generate_ids',
+                     'mt_engine_info', 'mt_checksums_device'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -172,14 +176,22 @@ class MergeEngine:
         assert batch.n_docs == self.n_docs
         return DeviceBatch(self, batch)
 
-    def synthesize(self, payload_per_doc=32 * 1024, doc_id_base=0, **cfg):
+    def synthesize(self, payload_per_doc=32 * 1024, doc_id_base=0, doc_ids=None, **cfg):
         """Generate a synthetic op log for every document ON THE DEVICE (mt_synth.h model; the
-        documents end in the post-generation state -- call reset() before replaying it)."""
+        documents end in the post-generation state -- call reset() before replaying it).  The
+        RNG stream of engine document i is global document doc_ids[i] (a hash-routed shard), or
+        doc_id_base + i."""
         from .oplog import synth_cfg_array
         raw = ctypes.create_string_buffer(synth_cfg_array(**cfg))
         h = ctypes.c_void_p()
-        _check(lib().mt_synth_generate(self.h, raw, doc_id_base, payload_per_doc, ctypes.byref(h)),
-               'mt_synth_generate')
+        if doc_ids is not None:
+            ids = np.ascontiguousarray(doc_ids, dtype=np.uint32)
+            assert len(ids) == self.n_docs
+            _check(lib().mt_synth_generate_ids(self.h, raw, _ptr(ids), payload_per_doc, ctypes.byref(h)),
+                   'mt_synth_generate_ids')
+        else:
+            _check(lib().mt_synth_generate(self.h, raw, doc_id_base, payload_per_doc, ctypes.byref(h)),
+                   'mt_synth_generate')
         return DeviceBatch(self, handle=h)
 
     def reset(self):

@@ -62,3 +62,9 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def device_synchronize():
+    """hipDeviceSynchronize on libmtgpu's runtime (bench.py's timed-region brackets)."""
+    if hip().hipDeviceSynchronize() != 0:
+        raise MtError('hipDeviceSynchronize failed')

@@ -50,6 +50,27 @@ class OpBatch:
         ops['payload_off'] -= lo
         return OpBatch(ops, self.payload[lo:hi].copy(), self.row_ptr[d0:d1 + 1] - a)
 
+    def select(self, docs):
+        """The given documents (in the given order) as a self-contained batch."""
+        parts = [self.doc_slice(int(d), int(d) + 1) for d in docs]
+        return OpBatch.concat(parts)
+
+    @staticmethod
+    def concat(parts):
+        """Documents of several batches, in order, as one batch."""
+        ops, pays, rows, off, nops = [], [], [np.zeros(1, np.uint32)], 0, 0
+        for b in parts:
+            o = b.ops.copy()
+            o['payload_off'] += off
+            ops.append(o)
+            pays.append(b.payload)
+            rows.append(b.row_ptr[1:].astype(np.int64) + nops)
+            off += len(b.payload)
+            nops += b.n_ops
+        return OpBatch(np.concatenate(ops) if ops else np.zeros(0, OP_DTYPE),
+                       np.concatenate(pays) if pays else np.zeros(0, np.uint8),
+                       np.concatenate(rows).astype(np.uint32))
+
     def save(self, path):
         with open(path, 'wb') as f:
             f.write(MAGIC)

@@ -64,7 +64,8 @@ typedef enum mt_status {
     MT_ERR_HIP = 2,
     MT_ERR_NOMEM = 3,
     MT_ERR_STATE = 4,
-    MT_ERR_DOC = 5          /* at least one document has a sticky error (see mt_doc_error) */
+    MT_ERR_DOC = 5,         /* at least one document has a sticky error (see mt_doc_error) */
+    MT_ERR_COMM = 6         /* an RCCL call failed (mt_comm_*) */
 } mt_status;
 
 /* per-document sticky error codes (mirror the reference's assert/throw sites) */
@@ -124,6 +125,8 @@ mt_status mt_get_text(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uin
 mt_status mt_get_state(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uint64_t* len);
 /* Per-document 64-bit checksum of the canonical state (DESIGN.md "Checksum"). */
 mt_status mt_checksums(mt_engine* eng, uint64_t* out, uint32_t n_docs);
+/* The same into device memory (HBM, n_docs u64), complete on return. */
+mt_status mt_checksums_device(mt_engine* eng, uint64_t* d_out, uint32_t n_docs);
 mt_status mt_doc_error(mt_engine* eng, uint32_t doc, int32_t* code, int32_t* seq);
 
 /* Measurement hooks for bench.py, for the last mt_batch_apply: kernel_ms = sum of the apply
@@ -182,6 +185,10 @@ typedef struct mt_synth_cfg {
 /* doc_id_base: global id of the engine's document 0 (a rank's shard of a multi-GPU job) */
 mt_status mt_synth_generate(mt_engine* eng, const mt_synth_cfg* cfg, uint32_t doc_id_base, uint32_t payload_per_doc,
                             mt_batch** out);
+/* The same with an explicit global id per engine document (host array of n_docs ids): a rank's
+ * hash-routed shard of a multi-GPU job (mt_route_docs). */
+mt_status mt_synth_generate_ids(mt_engine* eng, const mt_synth_cfg* cfg, const uint32_t* doc_ids,
+                                uint32_t payload_per_doc, mt_batch** out);
 /* Copy documents [d0, d1) of a staged batch to the host: ops (payload_off rebased so the
  * first copied document's payload region starts at 0), payload and row_ptr (d1-d0+1 entries).
  * Sizes for a dry run: pass NULL buffers. */
@@ -193,6 +200,30 @@ mt_status mt_batch_info(const mt_batch* batch, uint64_t* n_ops, uint64_t* payloa
 mt_status mt_batch_device_ptrs(const mt_batch* batch, mt_op_rec** ops, uint8_t** payload, uint32_t** row_ptr);
 
 const char* mt_version(void);
+
+/* ---- multi-GPU: document routing and the end-of-run gather -----------------
+ * Documents are independent; the reference partitions by documentId (Kafka key,
+ * server/routerlicious/packages/services/src/kafkaNodeProducer.ts:131,156; lambda routing
+ * lambdas-driver/src/document-router/documentLambda.ts:52-58).  Here document docId lives on GPU
+ * splitmix64(docId) mod n_gpus (mt_route_doc), with no collective in the apply loop; one process
+ * per GPU.  RCCL (over xGMI) is used only for the final per-document checksum gather. */
+uint32_t mt_route_doc(uint64_t doc_id, uint32_t n_shards);
+mt_status mt_route_docs(const uint64_t* doc_ids, uint64_t n, uint32_t n_shards, uint32_t* shard_out);
+
+#define MT_COMM_ID_BYTES 128
+typedef struct mt_comm mt_comm;
+/* rank 0 makes the id, every rank passes the same bytes to mt_comm_create (ncclUniqueId) */
+mt_status mt_comm_unique_id(uint8_t* id /* [MT_COMM_ID_BYTES] */);
+mt_status mt_comm_create(int32_t device, int32_t rank, int32_t n_ranks, const uint8_t* id, mt_comm** out);
+mt_status mt_comm_destroy(mt_comm* comm);
+/* Gather every rank's per-document checksums (mt_checksums of `eng`) to rank 0: ncclGather from
+ * HBM.  Rank 0: out[r * max_docs_per_rank + i] = rank r's document i, counts[r] = rank r's
+ * n_docs (other ranks may pass NULL). */
+mt_status mt_comm_gather_checksums(mt_comm* comm, mt_engine* eng, uint32_t max_docs_per_rank, uint64_t* out,
+                                   uint32_t* counts);
+/* max over ranks (the job's clock), and a barrier (all-reduce + device synchronize) */
+mt_status mt_comm_allreduce_max_f64(mt_comm* comm, double* v);
+mt_status mt_comm_barrier(mt_comm* comm);
 
 /* ---- deli: per-document sequence-number / MSN ticketing ----------------
  * Replaces, for many documents at once, the ordering service's per-document sequencer:
@@ -223,7 +254,8 @@ typedef struct mt_raw_msg {  /* 16 bytes */
     uint16_t client;         /* short id of the sending client, or of the joiner / leaver (< 64)   */
     uint8_t kind;            /* mt_raw_kind                                                        */
     uint8_t pad;
-    uint32_t reserved;
+    uint32_t op_index;       /* fused hand-off (mt_deli_ticket_device with d_ops): 1 + index of the op
+                                record this message carries, 0 = none (joins, leaves, no-ops)     */
 } mt_raw_msg;
 
 typedef enum mt_ticket_status {
@@ -281,18 +313,27 @@ mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_
 mt_status mt_deli_ticket(mt_deli* dl, const mt_raw_msg* msgs, uint64_t n_msgs, const uint32_t* doc_row_ptr,
                          uint32_t n_docs, mt_ticket* out);
 /* The same on device-resident buffers (HBM), asynchronous on the deli's stream.  d_ops (optional)
- * fuses the hand-off to the apply engine: message i carries op record i (a stream of op messages
- * only, 1:1), and each record gets the seq / msn / ref_seq of its ticket (seq = -1 when the
- * message was not sent, which the apply engine rejects as MT_DERR_SEQ_ORDER). */
+ * fuses the hand-off to the apply engine: a message with op_index = k + 1 carries op record k, and
+ * that record gets the seq / msn / ref_seq of its ticket (seq = -1 when the message was not sent,
+ * which the apply engine rejects as MT_DERR_SEQ_ORDER); op_index past n_ops links nothing. */
 mt_status mt_deli_ticket_device(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row_ptr, uint32_t n_docs,
-                                mt_ticket* d_out, mt_op_rec* d_ops);
+                                mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops);
 /* Bench tooling: construct documents [0, n_docs) all from the same checkpoint (device fill). */
 mt_status mt_deli_restore_all(mt_deli* dl, uint32_t n_docs, const mt_deli_checkpoint* ckpt);
 /* Bench tooling: the raw op messages behind a device op log (one MT_RAW_OP per record, client
- * sequence numbers counted per client, ref_seq copied).  With every client joined at seq 0
- * (mt_deli_restore_all), deli re-derives exactly the seq / msn the synthetic log carries. */
+ * sequence numbers counted per client, ref_seq copied, op_index = record + 1).  With every client
+ * joined at seq 0 (mt_deli_restore_all), deli re-derives exactly the seq / msn the log carries. */
 mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
                                mt_raw_msg* d_msgs);
+/* Bench tooling: a new document's whole raw stream (BASELINE config C5): the ClientJoin of clients
+ * 1..n_join (lambda.ts:286-299, each revs the sequence number) followed by the op messages of
+ * the log, their refSeq moved past the joins (+ n_join, so each op still references what its
+ * client had seen).  Document d's messages are d_msgs[msg_row_ptr[d] .. msg_row_ptr[d+1]) with
+ * msg_row_ptr[d] = d_row_ptr[d] + d * n_join (device arrays; msg_row_ptr has n_docs + 1
+ * entries).  Ticketed from new documents (mt_deli_restore with NULL) with fused stamping, the
+ * op records get seq = log seq + n_join and deli's msn. */
+mt_status mt_deli_raw_stream(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
+                             uint32_t n_join, mt_raw_msg* d_msgs, uint32_t* d_msg_row_ptr);
 mt_status mt_deli_sync(mt_deli* dl);
 /* Kernel time of the last mt_deli_ticket / mt_deli_ticket_device (HIP events around the launch). */
 mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms);

@@ -28,9 +28,9 @@ const count = (res) => res[0].forEach((r) => {
 dl.queue(0, factory("ghost").leave());
 for (let s = 0; s < 200; s++) {
     const f = factory("session-" + s);
-    dl.queue(0, f.join());
-    dl.queue(0, f.create(seq + 1));
-    dl.queue(0, f.create(seq + 1));
+    dl.queue(0, f.join());               // sequenced 4s + 1: each session revs 4 times
+    dl.queue(0, f.create(4 * s + 1));    // refSeq = the join's seq, >= the msn the joiner entered at
+    dl.queue(0, f.create(4 * s + 1));
     dl.queue(0, f.leave());
     if (s % 10 === 9) count(dl.flush());
 }

@@ -109,7 +109,7 @@ def test_deli_feeds_apply():
     dl = _seq(n)
     dl.restore_all(seq=0, clients={c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)})
     dl.raw_from_ops(d_ops, d_row, n, msgs.ptr)
-    dl.ticket_device(msgs.ptr, d_row, n, tick.ptr, d_ops)
+    dl.ticket_device(msgs.ptr, d_row, n, tick.ptr, d_ops, dev.n_ops)
     dl.sync()
     raw = msgs.download(RAW_DTYPE)
     assert np.array_equal(raw['ref_seq'], host.ops['ref_seq']) and np.all(raw['kind'] == od.OP)
@@ -120,3 +120,59 @@ def test_deli_feeds_apply():
     eng.reset()
     eng.apply_staged(dev)
     assert np.array_equal(eng.checksums(), want_cs)
+
+
+def test_c5_joins_through_deli_then_apply(oracle_lib):
+    """BASELINE config C5 as specified: per document, the ClientJoin of its 8
+    clients and then its 256 op messages -- raw messages, no pre-seeded checkpoint -- ticketed on
+    the GPU from new documents (lambda.ts:286-299: each join revs the sequence number), seq / msn /
+    refSeq stamped into the op records (fused hand-off), then applied.  Checked against the deli
+    restatement (oracle/deli.py, ticket by ticket) feeding the merge-tree oracle (oracle/mtcpu.cpp,
+    checksum by checksum) on 1,024 documents."""
+    from fluidframework_amd.deli import RAW_DTYPE, TICKET_DTYPE, batch_device_ptrs
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.hipmem import DeviceBuffer
+    from fluidframework_amd.oplog import CONFIGS
+    cfg = dict(CONFIGS['C5'])
+    cfg.pop('n_docs')
+    n, n_join = 1024, cfg['n_clients']
+    eng = MergeEngine(n, ops_per_launch=32)
+    dev = eng.synthesize(seed=5, **cfg)
+    host = dev.to_host()
+    d_ops, _, d_row = batch_device_ptrs(dev)
+    n_msgs = dev.n_ops + n * n_join
+    msgs = DeviceBuffer(n_msgs * RAW_DTYPE.itemsize)
+    mrow = DeviceBuffer((n + 1) * 4)
+    tick = DeviceBuffer(n_msgs * TICKET_DTYPE.itemsize)
+    dl = _seq(n)
+    dl.restore_all(seq=0, clients={})
+    dl.raw_stream(d_ops, d_row, n, n_join, msgs.ptr, mrow.ptr)
+    dl.ticket_device(msgs.ptr, mrow.ptr, n, tick.ptr, d_ops, dev.n_ops)
+    dl.sync()
+    raw = msgs.download(RAW_DTYPE)
+    rp = mrow.download(np.uint32)
+    assert rp[0] == 0 and rp[-1] == n_msgs
+    for d in (0, 1, n - 1):   # joins of clients 1..8 first, then the log's ops with refSeq + 8
+        seg = raw[rp[d]:rp[d + 1]]
+        assert list(seg['kind'][:n_join]) == [od.JOIN] * n_join and list(seg['client'][:n_join]) == list(range(1, 9))
+        ops = host.ops[host.row_ptr[d]:host.row_ptr[d + 1]]
+        assert np.array_equal(seg['ref_seq'][n_join:], ops['ref_seq'] + n_join)
+        assert np.array_equal(seg['op_index'][n_join:], np.arange(host.row_ptr[d], host.row_ptr[d + 1]) + 1)
+    want, _ = od.ticket_batch(raw, rp)
+    got = _tickets(tick.download(TICKET_DTYPE))
+    bad = np.nonzero(np.any(got != want, axis=1))[0]
+    assert not len(bad), f'{len(bad)} tickets differ, first {int(bad[0])}: {got[bad[0]]} vs {want[bad[0]]}'
+    assert np.all(want[:, 3] == od.SENT)
+    # the oracle's stamped log: each op record gets its message's ticket
+    stamped = host.ops.copy()
+    link = raw['op_index'] > 0
+    k = raw['op_index'][link].astype(np.int64) - 1
+    stamped['seq'][k], stamped['msn'][k], stamped['ref_seq'][k] = want[link, 0], want[link, 1], want[link, 2]
+    assert np.array_equal(dev.to_host().ops, stamped)
+    assert np.array_equal(stamped['seq'], host.ops['seq'] + n_join)
+    from fluidframework_amd.oplog import OpBatch
+    o = oracle_lib.Oracle(n).apply(OpBatch(stamped, host.payload, host.row_ptr), threads=8)
+    eng.reset()
+    eng.apply_staged(dev)
+    assert np.array_equal(eng.checksums(), o.checksums())
+    assert all(eng.error(d) == (0, 0) for d in range(0, n, 97))

@@ -49,7 +49,7 @@ ms = []
 t0 = time.perf_counter()
 for _ in range(a.steps):
     dl.restore_all(seq=0, clients=clients)
-    dl.ticket_device(msgs.ptr, d_row, a.docs, tick.ptr, d_ops if a.stamp else None)
+    dl.ticket_device(msgs.ptr, d_row, a.docs, tick.ptr, d_ops if a.stamp else None, n)
     dl.sync()
     ms.append(dl.last_ms())
 wall = time.perf_counter() - t0

@@ -1010,20 +1010,16 @@ struct RWave {
                 if (pbyte(pay, tlen + 2 * q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
             const bool ins = op.type == MT_OP_INSERT;
             if (op.pos1 < 0 || (!ins && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
+            // the window asserts (completeAndLogOp client.ts:461-464, updateSeqNumbers :826) are
+            // decided before any edit: the document halts before the failing message.  (The
+            // reference runs them after the op, so a failing insert outranks them: mt_fixup_kernel,
+            // after the apply, from the halted state.)
+            if (!(cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);
+            if (!(min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);
+            if (!(op.msn <= S)) return fail(MT_DERR_MSN_ORDER, S);
             PROF_BEGIN(t0);
-            const int L = scan(op.ref_seq, op.client);
+            scan(op.ref_seq, op.client);
             PROF_END(prof, P_SCAN, t0);
-            // the window asserts run after the op in the reference (completeAndLogOp,
-            // client.ts:461-464; updateSeqNumbers :826), so a failing insert (mergeTree.ts:2210) is
-            // reported first; all are decided here, before any edit: the document halts before
-            // the failing message
-            {
-                int wc = 0;
-                if (!(cur_seq < S)) wc = MT_DERR_SEQ_ORDER;
-                else if (!(min_seq <= op.msn) || !(op.msn <= S)) wc = MT_DERR_MSN_ORDER;
-                if (ins && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
-                if (wc) return fail(wc, S);
-            }
             // insertion steps: the boundary splits (ensureIntervalBoundary), then for an insert
             // the new segment; every step ends in the one insert_at call site
             const int nsteps = ins ? (tlen > 0 ? 2 : 1) : 2;
@@ -1062,18 +1058,15 @@ struct RWave {
             if (err) return;
         }
         const int32_t msn = op.msn;
-        if (op.type == MT_OP_NOOP) {  // every assert of the message before any edit (see the oracle)
-            if (!(cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                  // client.ts:824
-            if (!(msn <= S) || !(min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
-        }
         for (int ph = 0; ph < 2; ph++) {
             if (ph == 0) {
                 if (op.type == MT_OP_NOOP) continue;
             } else {
                 if (op.flags & MT_F_GROUP_MORE) break;
-                if (!(cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);
+                // (a non-op message's asserts, all before its edits: the document halts before it)
+                if (!(cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                   // client.ts:824
+                if (!(msn <= S) || !(min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
                 cur_seq = S;
-                if (!(msn <= S) || !(min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, S);
                 if (!(msn > min_seq)) break;
                 min_seq = msn;
             }

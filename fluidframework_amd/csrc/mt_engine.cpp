@@ -30,6 +30,7 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
                                     uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
                                          uint32_t* specs, uint32_t* counts, hipStream_t st);
 extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
@@ -312,6 +313,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
     }
+    HIP_OK(mt_launch_fixup(&e->g, b->ops, b->n_docs, e->stream));  // error precedence, see mt_service.hip
     HIP_OK(hipEventRecord(e->ev1, e->stream));
     HIP_OK(hipEventSynchronize(e->ev1));
     float kms = 0.f;

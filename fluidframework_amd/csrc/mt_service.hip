@@ -18,6 +18,7 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     sc.nlev = 1;
     sc.nb[0] = 1;
     sc.n_empty = 1;  // the root leaf block starts empty
+    sc.win_op = -1;
     g.sc[d] = sc;
     g.lbcnt[(size_t)d * g.lbcap] = 0;
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
@@ -43,6 +44,26 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         const mt_doc_scalars sc = g.sc[d];
         if (a < b && !sc.err) {
             const int nops = (int)(b - a);
+            if (ops && sc.win_op < 0) {
+                // replay the collab window over this launch's ops (client.ts:461-464, 821-828;
+                // mergeTree.ts:1718-1722) to find the first op the apply will halt on for a window
+                // assert; mt_fixup_kernel decides after the apply whether "insert failed" outranks it
+                int32_t cur = sc.cur_seq, mn = sc.min_seq;
+                for (uint32_t i = a; i < b; i++) {
+                    const mt_op_rec o = ops[i];
+                    if (o.type > MT_OP_NOOP) break;
+                    const bool bad = o.type == MT_OP_NOOP ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
+                                                          : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
+                    if (bad) {
+                        g.sc[d].win_op = (int32_t)i;
+                        break;
+                    }
+                    if (!(o.flags & MT_F_GROUP_MORE)) {
+                        cur = o.seq;
+                        mn = o.msn > mn ? o.msn : mn;
+                    }
+                }
+            }
             bool wide = sc.wide != 0;
             if (!wide && ops) {
                 for (uint32_t i = a; i < b; i++) wide = wide || ops[i].client > 32;
@@ -90,6 +111,33 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
     }
 }
 
+// After an apply: a document halted on a window assert by an insert with text reports "MergeTree
+// insert failed" instead when the insert was also past the end of its view -- the reference
+// applies the op (mergeTree.ts:2210-2216 throws) before completeAndLogOp's and updateSeqNumbers'
+// asserts (client.ts:461-464, 826).  The halted state is the state before that op, so
+// getLength(refSeq, client) is read from HBM.  One thread per document; the loop runs only for
+// such (rare) documents.
+__global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, uint32_t n_docs) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n_docs) return;
+    const mt_doc_scalars sc = g.sc[d];
+    if (sc.win_op < 0 || (sc.err != MT_DERR_SEQ_ORDER && sc.err != MT_DERR_MSN_ORDER)) return;
+    const mt_op_rec o = ops[sc.win_op];
+    const int np = o.flags >> MT_F_NPAIRS_SHIFT;
+    if (o.seq != sc.err_seq || o.type != MT_OP_INSERT || (int)o.payload_len - 2 * np <= 0) return;
+    const size_t so = (size_t)d * g.segcap;
+    const int32_t R = o.ref_seq;
+    const uint32_t C = o.client;
+    int64_t len = 0;
+    for (int i = 0; i < sc.nseg; i++) {  // nodeLength leaf branch (mergeTree.ts:1667-1697)
+        const bool seen = g.client[so + i] == C || g.seq[so + i] <= R;
+        const bool hid = (g.flags[so + i] & MT_SF_REMOVED) &&
+                         (g.rclient[so + i] == C || ((g.ovl[so + i] >> C) & 1ull) || g.rseq[so + i] <= R);
+        if (seen && !hid) len += g.len[so + i];
+    }
+    if ((int64_t)o.pos1 > len) g.sc[d].err = MT_DERR_INSERT_FAILED;
+}
+
 // checksum of the canonical state (mt_checksum.h), one wave per document
 __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n_docs, uint64_t* __restrict__ out) {
     const uint32_t d = blockIdx.x;
@@ -133,6 +181,11 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st) {
     hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
                        classes, n_classes, counts, ids, ops, acc);
+    return hipGetLastError();
+}
+extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st) {
+    if (n_docs == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_fixup_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, ops, n_docs);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st) {

@@ -36,7 +36,8 @@ struct mt_doc_scalars {      // 80 bytes
     uint32_t text_half;      // which half of the double-buffered arena is current (0/1)
     uint32_t n_empty;        // leaf blocks without children (the register engine pads one slot each)
     uint32_t wide;           // a client id above 32 was seen: the document stays on the LDS engine
-    uint32_t pad;
+    int32_t win_op;          // batch index of the first op failing a window assert (binning's
+                             // replay of the window), -1 if none: mt_fixup_kernel's input
 };
 
 // Device pointers + capacities (one allocation per array, [n_docs][capacity]).

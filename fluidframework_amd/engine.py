@@ -69,9 +69,12 @@ def lib():
         L.mt_last_apply_class_stats.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float),
                                                 ctypes.POINTER(u32), ctypes.POINTER(u64)]
         L.mt_synth_generate.argtypes = [vp, vp, u32, u32, ctypes.POINTER(vp)]
-        L.mt_synth_generate_ids.argtypes = [vp, vp, vp, u32, ctypes.POINTER(vp)]
-        L.mt_engine_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
-        L.mt_checksums_device.argtypes = [vp, vp, u32]
+        for name, at in (('mt_synth_generate_ids', [vp, vp, vp, u32, ctypes.POINTER(vp)]),
+                         ('mt_engine_info', [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+                         ('mt_checksums_device', [vp, vp, u32])):
+            if hasattr(L, name):  # (an older build loaded for an A/B lacks them)
+                getattr(L, name).argtypes = at
+                getattr(L, name).restype = ctypes.c_int
         L.mt_batch_copy_docs.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64), vp, ctypes.POINTER(u64), vp]
         L.mt_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mt_class_kernel_name.argtypes = [vp, u32, ctypes.c_char_p, u64]
@@ -83,8 +86,7 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_synth_generate_ids',
-                     'mt_engine_info', 'mt_checksums_device'):
+                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib

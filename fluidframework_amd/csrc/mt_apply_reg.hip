@@ -211,7 +211,39 @@ struct RWave {
     // ------------------------------------------------------------ leaf blocks
     MT_DEV int leaf_of(int k) const { return wave_total(__popc(bs_bits() & below(k + 1))) - 1; }
     MT_DEV int bs_slot(int b) const { return b >= nb0 ? ns : nth_slot(bs_bits(), b); }
-    MT_DEV int live_in(int a, int e) const { return wave_total(__popc(live_bits() & below(e) & ~below(a))); }
+    // ---- navigation by slot: a ballot and a readlane or two, no wave-wide scan.  A leaf block
+    // is the slot range from its start mark to the next one (or ns); slot 0 always starts block 0.
+    MT_DEV int block_start(int k) const {  // start of the leaf block holding slot k
+        const uint32_t m = bsm & below(k + 1);
+        const int l = 63 - __builtin_clzll(wave_ballot(m != 0));
+        return l * K + (31 - __builtin_clz((uint32_t)__builtin_amdgcn_readlane((int)m, l)));
+    }
+    MT_DEV int next_start(int k) const { return first_from(bsm, k + 1); }  // end of the block holding k
+    // set bits of the lanes' masks m inside slots [a, e) (a block spans one or two lanes almost always)
+    MT_DEV int count_in(uint32_t m, int a, int e) const {
+        if (e <= a) return 0;
+        const uint32_t x = m & below(e) & ~below(a);
+        const int la = a / K, lb = (e - 1) / K;
+        if (lb - la > 1) return wave_total(__popc(x));
+        int c = __popc((uint32_t)__builtin_amdgcn_readlane((int)x, la));
+        if (lb != la) c += __popc((uint32_t)__builtin_amdgcn_readlane((int)x, lb));
+        return c;
+    }
+    MT_DEV int live_in(int a, int e) const { return count_in(lvm, a, e); }
+    // slot of the r-th (0-based) set bit of m inside [a, e); -1 if there is none
+    MT_DEV int nth_in(uint32_t m, int a, int e, int r) const {
+        const uint32_t x = m & below(e) & ~below(a);
+        for (int l = a / K; l <= (e - 1) / K; l++) {
+            uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+            const int c = __popc(w);
+            if (r < c) {
+                for (; r > 0; r--) w &= w - 1;
+                return l * K + __builtin_ctz(w);
+            }
+            r -= c;
+        }
+        return -1;
+    }
 
     // ------------------------------------------------------------ element access
     MT_DEV Elem get(int k) const {  // all fields of the slot at uniform position k
@@ -378,13 +410,13 @@ struct RWave {
         }
     }
 
-    // leaf block b = slots [a, e) reached kMaxNodes live children: its child of rank 4 starts
-    // block b+1 (split, mergeTree.ts:2476-2489)
-    MT_DEV bool split_leaf(int b, int a, int e, int32_t sq) {
+    // the leaf block of slots [a, e) reached kMaxNodes live children: its child of rank 4 starts
+    // the next block (split, mergeTree.ts:2476-2489)
+    MT_DEV bool split_leaf(int a, int e, int32_t sq) {
         if (nb0 + 1 > L::LB) return fail(MT_DERR_CAPACITY, sq), false;
-        const int s4 = nth_slot(live_bits() & below(e) & ~below(a), kMaxNodes / 2);
+        const int s4 = nth_in(lvm, a, e, kMaxNodes / 2);
         int parent = -1;
-        if (nlev > 1) parent = parent_of(0, b, nullptr);
+        if (nlev > 1) parent = parent_of(0, leaf_of(a), nullptr);
         set_bs(s4, true);  // new block, needsScour undefined
         set_sc(s4, MT_SC_UNDEF);
         nb0 += 1;
@@ -404,10 +436,10 @@ struct RWave {
         return split_up(1, parent, sq);
     }
 
-    // insert e at slot k of leaf block b (insertingWalk's child insert, mergeTree.ts:2446-2470)
-    MT_DEV bool insert_at(int k, int b, Elem e, int32_t sq) {
+    // insert e at slot k (a <= k <= en) of the leaf block of slots [a, en) (insertingWalk's child
+    // insert, mergeTree.ts:2446-2470)
+    MT_DEV bool insert_at(int k, int a, int en, Elem e, int32_t sq) {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
-        const int a = bs_slot(b);
         const bool front = k == a;  // new first child: it takes over the block's marks
         shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
         if (front) {
@@ -415,8 +447,7 @@ struct RWave {
             set_sc(k + 1, MT_SC_UNDEF);
         }
         nlive += 1;
-        const int en = bs_slot(b + 1);
-        if (live_in(a, en) >= kMaxNodes) return split_leaf(b, a, en, sq);
+        if (live_in(a, en + 1) >= kMaxNodes) return split_leaf(a, en + 1, sq);
         return true;
     }
     MT_DEV int alloc_id(int32_t sq) {
@@ -485,7 +516,7 @@ struct RWave {
     // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245), first half: find the segment
     // visible to the op's view that strictly contains pos, cut it (left part in place, cum kept
     // valid for the view) and return its right part r, to be inserted at slot k1 of leaf block b.
-    MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& b) {
+    MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& ba, int& be) {
         int cs = cs0();
         int hitj = -1;
 #pragma unroll
@@ -506,7 +537,8 @@ struct RWave {
         const int t = alloc_id(sq);
         if (t < 0) return false;
         PROF_BEGIN(tb1);
-        b = leaf_of(k);
+        ba = block_start(k);
+        be = next_start(k);
         PROF_END(prof, P_B_BLK, tb1);
         PROF_BEGIN(tb2);
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
@@ -580,9 +612,8 @@ struct RWave {
         wave_sync();
         return id;
     }
-    // addToLRUSet (mergeTree.ts:1273-1283) for segment `id` in leaf block b
-    MT_DEV bool add_lru(int b, int id, int32_t sq) {
-        const int a = bs_slot(b);
+    // addToLRUSet (mergeTree.ts:1273-1283) for segment `id` in the leaf block starting at slot a
+    MT_DEV bool add_lru(int a, int id, int32_t sq) {
         if (sc_of(a) != MT_SC_TRUE && sq > cur_seq) {
             set_sc(a, MT_SC_TRUE);
             return heap_push(sq, id, sq);
@@ -775,12 +806,11 @@ struct RWave {
     }
     // pack at the leaf level: the m leaf blocks under level-1 block P (first fc; `total` live
     // children after scouring) become cc evenly filled blocks -- only block marks change
-    MT_DEV void repack_leaf(int P, int fc, int m, int total) {
+    MT_DEV void repack_leaf(int P, int fc, int m, int total, int A, int E) {
         const int half = kMaxNodes / 2;
         int cc = min(kMaxNodes - 1, total / half);
         if (cc < 1) cc = 1;
         const int base = total / cc, extra = total % cc;
-        const int A = bs_slot(fc), E = bs_slot(fc + m);
         const uint32_t lb = live_bits() & below(E) & ~below(A);
         const int c = __popc(lb);
         const int rbase = wave_incl_scan(c) - c;
@@ -822,17 +852,17 @@ struct RWave {
             if (id == (int)kDead) continue;
             const int k = slot_of_id(id);
             if (k < 0) continue;
-            const int b = leaf_of(k);
-            const int a = bs_slot(b), e = bs_slot(b + 1);
+            const int a = block_start(k), e = next_start(k);
             PROF_END(prof, P_ZPOP, tz);
             if (sc_of(a) == MT_SC_FALSE) continue;
             const int cnt = live_in(a, e);
             int P = -1, fc = 0, m = 0, total = 0;
+            int A = 0, ee = e;  // pack: the first sibling's start, and the end of the last scoured one
             for (int step = 0;; step++) {
-                int aa = a, ee = e;
-                if (step > 0) {
-                    aa = bs_slot(fc + step - 1);
-                    ee = bs_slot(fc + step);
+                int aa = a;
+                if (step > 0) {  // the siblings under the parent, left to right
+                    aa = step == 1 ? A : ee;
+                    ee = next_start(aa);
                 }
                 PROF_BEGIN(ts);
                 PROF_CNT(P_N_SCOUR, 1);
@@ -842,15 +872,16 @@ struct RWave {
                 if (step == 0) {
                     set_sc(a, MT_SC_FALSE);
                     if (!(kept < cnt && kept < kMaxNodes / 2 && nlev > 1)) break;
-                    P = parent_of(0, b, &fc);
+                    P = parent_of(0, leaf_of(a), &fc);
                     m = uni(s.ibcnt[0][P]);
+                    A = bs_slot(fc);
                 } else {
                     total += kept;
                 }
                 if (step == m) break;
             }
             PROF_BEGIN(tr);
-            if (P >= 0) repack_leaf(P, fc, m, total);
+            if (P >= 0) repack_leaf(P, fc, m, total, A, ee);
             PROF_END(prof, P_REPACK, tr);
             if (err) return;
         }
@@ -876,7 +907,7 @@ struct RWave {
     // choose its slot k in leaf block b, write its text and cold fields, build its element.
     // Returns its id (< 0 on error) and its child index inside block b before a possible split.
     MT_DEV int place_prep(const mt_op_rec op, const uint8_t* pay, int tlen, int np, Elem& en,
-                          int& k, int& b, int& idx_in) {
+                          int& k, int& ba, int& be) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, pos = op.pos1;
         // insertingWalk descends into the first block whose cumulative visible end >= pos
@@ -893,8 +924,9 @@ struct RWave {
         }
         last = wave_min(last);
         if (last == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
-        b = leaf_of(last);
-        const int a = bs_slot(b), e = last + 1;
+        const int a = block_start(last), e = last + 1;
+        ba = a;
+        be = e;
         // leaf placement: first child with pos < len, or pos == len == 0 and breakTie; else the
         // end of the block (:2431-2444)
         int best = 0x7fffffff;
@@ -913,7 +945,6 @@ struct RWave {
         }
         best = wave_min(best);
         k = best != 0x7fffffff ? best : e;
-        idx_in = live_in(a, k);
         const int t = alloc_id(S);
         if (t < 0) return -1;
         if (!arena_reserve((uint32_t)tlen, S)) return -1;
@@ -988,9 +1019,8 @@ struct RWave {
         for (;;) {
             const int k = first_from(tm, from);
             if (k >= ns) break;
-            const int b = leaf_of(k);
-            if (!add_lru(b, (int)id_of(get_li(k)), S)) return;
-            from = first_from(bs_bits(), k + 1);
+            if (!add_lru(block_start(k), (int)id_of(get_li(k)), S)) return;
+            from = next_start(k);
         }
     }
 
@@ -1027,18 +1057,17 @@ struct RWave {
                 PROF_BEGIN(t1);
                 const bool placing = ins && step == 1;
                 Elem e;
-                int k = 0, b = 0, idx_in = 0, t = -1;
+                int k = 0, ba = 0, be = 0, t = -1;
                 if (!placing) {
-                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, e, k, b)) {
+                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, e, k, ba, be)) {
                         if (err) return;
                         continue;
                     }
                 } else {
-                    t = place_prep(op, pay, tlen, np, e, k, b, idx_in);
+                    t = place_prep(op, pay, tlen, np, e, k, ba, be);
                     if (t < 0) return;
                 }
-                const int before_nb = nb0;
-                const bool ok = insert_at(k, b, e, S);
+                const bool ok = insert_at(k, ba, be, e, S);
                 if (placing) {
                     PROF_END(prof, P_INSERT, t1);
                 } else {
@@ -1046,8 +1075,8 @@ struct RWave {
                 }
                 if (!ok) return;
                 if (placing && S > min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
-                    const int bb = (nb0 > before_nb && idx_in >= kMaxNodes / 2) ? b + 1 : b;
-                    if (!add_lru(bb, t, S)) return;
+                    // the new segment's block after a possible split: the one holding slot k
+                    if (!add_lru(block_start(k), t, S)) return;
                 }
             }
             if (!ins) {

@@ -91,8 +91,7 @@ struct RLds {
     uint8_t ibcnt[MT_MAXLEV - 1][IB];  // interior levels: level L's child counts in ibcnt[L - 1]
     uint8_t lbsc[LB + 1];   // store staging: needsScour per leaf block
     int32_t nb[MT_MAXLEV];  // blocks per interior level (leaf blocks are counted by BS bits)
-    int32_t zseq[kMaxNodes], zrseq[kMaxNodes], zslot[kMaxNodes];  // scour scratch: live children
-    uint32_t zli[kMaxNodes], zcf[kMaxNodes];
+    int4 zrec[kMaxNodes];   // scour scratch: live children by rank {seq or rseq, li, cf, slot}
 };
 
 struct Elem {
@@ -685,72 +684,66 @@ struct RWave {
         const int rbase = incl - c;
         const int cnt = wave_last(incl);
         if (cnt > kMaxNodes) return fail(MT_DERR_CAPACITY, cur_seq), cnt;
-        // the live children, rank by rank, through LDS scratch: lane q gets the child of rank q
+        // the live children, rank by rank, through LDS scratch (one 16-byte record each: the
+        // removal seq of a removed child, else its seq -- the only one the decisions read)
 #pragma unroll
         for (int j = 0; j < K; j++) {
             if ((lb >> j) & 1u) {
                 const int q = rbase + __popc(lb & ((1u << j) - 1u));
-                s.zseq[q] = seq[j];
-                s.zrseq[q] = rseq[j];
-                s.zli[q] = li[j];
-                s.zcf[q] = cf[j];
-                s.zslot[q] = idx(j);
+                s.zrec[q] = make_int4((cf[j] & F_RM) ? rseq[j] : seq[j], (int)li[j], (int)cf[j], idx(j));
             }
         }
         wave_sync();
         const bool mine = lane < cnt;
-        const int32_t vseq = mine ? s.zseq[lane] : 0, vrseq = mine ? s.zrseq[lane] : 0;
-        const uint32_t vli = mine ? s.zli[lane] : 0u, vcf = mine ? s.zcf[lane] : 0u;
-        const int vslot = mine ? s.zslot[lane] : 0;
+        const int4 z = mine ? s.zrec[lane] : make_int4(0, 0, 0, 0);
+        const int32_t vsq = z.x;
+        const uint32_t vli = (uint32_t)z.y, vcf = (uint32_t)z.z;
+        const int vslot = z.w;
         const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
-        // the sequential decisions (scalar), reading child q from lane q
+        // scourNode's decisions (mergeTree.ts:1289-1365), lane-parallel: child q is unlinked if it
+        // is a tombstone at or below the MSN; it is appended to the run before it if both are live,
+        // acked at or below the MSN and non-empty, the run does not end in "\n", the props match
+        // (canAppend textSegment.ts:63-68, matchProperties properties.ts:62-93) -- the run's
+        // newline and props are those of child q-1 -- and the run or q is within
+        // TextSegmentGranularity; only that last clause depends on earlier decisions
         const int32_t minSeq = min_seq;
-        int kept = 0, prev = -1;
-        uint32_t plen = 0, pflags = 0, unlink = 0;
-        uint64_t pprops = 0;
-        int vtgt = -1;  // lane q: rank of the child it appends into, or -1
-        for (int q = 0; q < cnt; q++) {
-            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)vcf, q);
-            if (f & F_RM) {
-                if (__builtin_amdgcn_readlane(vrseq, q) > minSeq) kept++;
-                else unlink |= 1u << q;  // UNLINK
-                prev = -1;
-            } else if (__builtin_amdgcn_readlane(vseq, q) <= minSeq) {
-                const uint32_t ql = len_of((uint32_t)__builtin_amdgcn_readlane((int)vli, q));
-                const uint64_t qp = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vpr, q) |
-                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vpr >> 32), q)
-                                     << 32);
-                // canAppend + matchProperties (textSegment.ts:63-68, properties.ts:62-93)
-                const bool app = prev >= 0 && !(pflags & F_NL) &&
-                                 (plen <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
-                                 ((pflags ^ f) & F_PDEF) == 0 && pprops == qp && ql > 0;
-                if (app) {  // APPEND: segment.parent = undefined
-                    unlink |= 1u << q;
-                    if (lane == q) vtgt = prev;
-                    plen += ql;
-                    pflags = (pflags & ~F_NL) | (f & F_NL);
+        const bool rm = mine && (vcf & F_RM) != 0;
+        const uint32_t ql = len_of(vli);
+        const bool elig = mine && !rm && vsq <= minSeq && ql > 0;
+        const bool pelig = shr1(elig ? 1 : 0, 0) != 0;
+        const uint32_t pcf = (uint32_t)shr1((int)vcf, 0);
+        const uint32_t pprl = (uint32_t)shr1((int)(uint32_t)vpr, 0);
+        const uint32_t pprh = (uint32_t)shr1((int)(uint32_t)(vpr >> 32), 0);
+        const bool a0 = elig && pelig && !(pcf & F_NL) && ((pcf ^ vcf) & F_PDEF) == 0 && pprl == (uint32_t)vpr &&
+                        pprh == (uint32_t)(vpr >> 32);
+        const uint32_t a0m = (uint32_t)__ballot(a0);
+        uint32_t appm = a0m;
+        if (__ballot(a0 && ql > (uint32_t)kTextGranularity)) {
+            // a long child joins only a run still within the granularity: walk the runs in order
+            const uint32_t em = (uint32_t)__ballot(elig);
+            uint32_t plen = 0;
+            appm = 0;
+            for (int q = 0; q < cnt; q++) {
+                const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)ql, q);
+                if (((a0m >> q) & 1u) && (plen <= (uint32_t)kTextGranularity || lq <= (uint32_t)kTextGranularity)) {
+                    appm |= 1u << q;
+                    plen += lq;
                 } else {
-                    kept++;
-                    if (ql > 0) {
-                        prev = q;
-                        plen = ql;
-                        pflags = f;
-                        pprops = qp;
-                    } else {
-                        prev = -1;
-                    }
+                    plen = ((em >> q) & 1u) ? lq : 0u;
                 }
-            } else {
-                kept++;
-                prev = -1;
             }
         }
+        const uint32_t unlink = (uint32_t)__ballot(rm && vsq <= minSeq) | appm;
+        const int kept = cnt - __popc(unlink);
+        // lane q appended: the child of the run's head, the last child before q not appended
+        const uint32_t heads = ~appm & ((1u << (lane & 31)) - 1u);
+        const int vtgt = (lane < 32 && ((appm >> lane) & 1u)) ? 31 - __builtin_clz(heads) : -1;
         PROF_CNT(P_N_UNLINK, __popc(unlink));
-        uint64_t appm = __ballot(vtgt >= 0);
-        while (appm) {
-            const int p = __builtin_amdgcn_readlane(vtgt, first_lane(appm));
+        uint64_t runs = __ballot(vtgt >= 0);
+        while (runs) {
+            const int p = __builtin_amdgcn_readlane(vtgt, first_lane(runs));
             const uint64_t runm = __ballot(vtgt == p);
-            appm &= ~runm;
+            runs &= ~runm;
             PROF_CNT(P_N_APPEND, __popcll(runm));
             append_run(p, (uint32_t)runm, vli, vcf, vslot);
             if (err) return cnt;

@@ -81,8 +81,8 @@ def parse():
     p.add_argument('--comm', choices=['auto', 'rccl', 'gloo'], default='auto',
                    help='rank exchange: RCCL over xGMI (default), or gloo (ranks sharing one GPU, tests)')
     p.add_argument('--devices', default='', help='device of each local rank, e.g. "0,0" (default: rank i -> GPU i)')
-    p.add_argument('--h2d', action='store_true', help='also time a step whose op log is uploaded from host memory '
-                                                      'host memory inside the timed region (value_with_h2d)')
+    p.add_argument('--no-h2d', action='store_true', help='skip the extra step whose op log is uploaded from '
+                                                         'host memory inside the timed region (value_with_h2d)')
     return p.parse_args()
 
 
@@ -227,7 +227,7 @@ def main():
         assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
 
     value_h2d = None
-    if args.h2d:
+    if not args.no_h2d and deli is None:
         value_h2d = h2d_step(eng, dev, n_ops, barrier, comm)
 
     # final per-document checksum gather to rank 0 (RCCL ncclGather from HBM; the only collective)
@@ -309,19 +309,34 @@ def main():
 
 
 def h2d_step(eng, dev, n_ops, barrier, comm):
-    """The op log staged from host memory inside the timed region: mt_batch_upload (H2D
-    over PCIe) + apply of a copy of this rank's log.  Returns ops/s over all ranks."""
+    """One step whose op log starts in page-locked host memory ("from the first
+    H2D of the op batch"): mt_batch_upload (record validation + H2D over PCIe) and the apply,
+    timed together.  Returns ops/s over all ranks and the upload's share."""
     from fluidframework_amd.engine import DeviceBatch
+    from fluidframework_amd.hipmem import PinnedArray
+    from fluidframework_amd.oplog import OpBatch
     host = dev.to_host()
+    pins = [PinnedArray(len(host.ops), host.ops.dtype), PinnedArray(len(host.payload), np.uint8),
+            PinnedArray(len(host.row_ptr), np.uint32)]
+    for p, a in zip(pins, (host.ops, host.payload, host.row_ptr)):
+        p.a[:] = a
+    pinned = OpBatch(pins[0].a, pins[1].a, pins[2].a)
+    del host
     barrier()
     t0 = time.perf_counter()
     eng.reset()
-    staged = DeviceBatch(eng, host)
+    staged = DeviceBatch(eng, pinned)
+    t1 = time.perf_counter()
     eng.apply_staged(staged)
     barrier()
     el = comm.max(time.perf_counter() - t0)
+    up = comm.max(t1 - t0)
     staged.free()
-    return round(n_ops * comm.world / el, 1)
+    for p in pins:
+        p.free()
+    return {'value': round(n_ops * comm.world / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3),
+            'step_s': round(el, 3), 'bytes_uploaded': int(len(pinned.ops) * 32 + len(pinned.payload)),
+            'note': 'op log from page-locked host memory: validation + H2D + apply in the timed region'}
 
 
 def cpu_baseline(dev, gpu_cs, n_docs, budget_s):
@@ -350,11 +365,58 @@ def cpu_baseline(dev, gpu_cs, n_docs, budget_s):
         done_docs += d1 - d0
         ops += hb.n_ops
         d0 = d1
-    cpu = {'value': round(ops / secs, 1), 'unit': 'ops/s', 'cores': threads, 'kind': 'port',
+    cpp = {'value': round(ops / secs, 1), 'unit': 'ops/s', 'cores': threads, 'kind': 'port',
            'sample': f'docs [0, {done_docs}) of the same device-generated logs ({ops} ops, {secs:.1f} s), '
-                     f'oracle/mtcpu.cpp observer replay, {threads} threads (one per core of the host share)'}
+                     f'oracle/mtcpu.cpp observer replay (C++), {threads} threads (one per core of the host share)'}
     parity = {'docs_checked': done_docs, 'mismatches': mism, 'against': 'oracle/mtcpu.cpp'}
-    return cpu, parity
+    js = js_baseline(dev, n_docs, threads)
+    if js is None:
+        return cpp, parity
+    js['cpp_port'] = cpp
+    return js, parity
+
+
+def js_baseline(dev, n_docs, threads, docs=1536):
+    """The reference's own form of the baseline (BASELINE.json north_star: the TypeScript merge-tree
+    with one worker_thread per host core): js/observerReplay.js, a JavaScript restatement of the
+    observer path, over a sample of the same logs, scaled by r = reference / restatement measured
+    in the build container on identical logs (oracle/tsref/calibrate.py)."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which('node')
+    if not node:
+        return None
+    d1 = min(n_docs, docs)
+    path = os.path.join(tempfile.gettempdir(), f'mtgpu_js_sample_{os.getpid()}.mtlog')
+    dev.to_host(0, d1).save(path)
+    try:
+        out = subprocess.run([node, os.path.join(HERE, 'js', 'observerReplay.js'), 'bench', path, str(threads)],
+                             capture_output=True, text=True, timeout=300)
+        res = json.loads(out.stdout.strip().split('\n')[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return None
+    finally:
+        os.unlink(path)
+    cal = {}
+    try:
+        with open(os.path.join(PROFILES, f'{PMC_ROUND}_js_calibration.json')) as f:
+            cal = json.load(f)
+    except (OSError, ValueError):
+        pass
+    v = res['ops_per_sec']
+    line = {'value': round(v, 1), 'unit': 'ops/s', 'cores': threads, 'kind': 'port',
+            'sample': f'docs [0, {d1}) of the same device-generated logs ({res["ops"]} ops), js/observerReplay.js '
+                      f'(JavaScript restatement of the observer Client path, node {os.popen(node + " --version").read().strip()}), '
+                      f'{threads} worker_threads, apply-only time ({res["apply_seconds"]:.1f} s, slowest worker)'}
+    if cal.get('r'):
+        line['reference_estimate'] = round(v * cal['r'], 1)
+        line['calibration'] = {'r': round(cal['r'], 4), 'reference_ops_per_sec': round(cal['reference_ops_per_sec'], 1),
+                               'restatement_ops_per_sec': round(cal['restatement_ops_per_sec'], 1),
+                               'threads': cal['threads'], 'config': cal['config'], 'docs': cal['docs'],
+                               'source': f'profiles/{PMC_ROUND}_js_calibration.json (the transpiled reference '
+                                         'vs this restatement, build container, identical logs)'}
+    return line
 
 
 if __name__ == '__main__':

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mtgpu.h"
@@ -230,11 +231,27 @@ mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, co
         }
         b->max_ops_per_doc = std::max(b->max_ops_per_doc, doc_row_ptr[d + 1] - doc_row_ptr[d]);
     }
-    for (uint64_t i = 0; i < n_ops; i++) {  // payload bounds: the kernels trust these
-        if ((uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes) {
-            delete b;
-            return MT_ERR_ARG;
-        }
+    // payload bounds: the kernels trust these (a big batch is checked on all host cores)
+    auto bad_range = [&](uint64_t lo, uint64_t hi) {
+        bool bad = false;
+        for (uint64_t i = lo; i < hi; i++) bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
+        return bad;
+    };
+    bool bad = false;
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    if (n_ops < (1u << 20) || nt == 1) {
+        bad = bad_range(0, n_ops);
+    } else {
+        std::vector<std::thread> th;
+        std::vector<char> res(nt, 0);
+        for (unsigned t = 0; t < nt; t++)
+            th.emplace_back([&, t] { res[t] = bad_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
+        for (auto& x : th) x.join();
+        for (char r : res) bad |= r != 0;
+    }
+    if (bad) {
+        delete b;
+        return MT_ERR_ARG;
     }
     if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
         hipMalloc(&b->payload, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||

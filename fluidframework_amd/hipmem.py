@@ -23,7 +23,10 @@ def hip():
         _hip.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
         _hip.hipMemset.argtypes = [vp, ctypes.c_int, sz]
         _hip.hipDeviceSynchronize.argtypes = []
-        for f in ('hipMalloc', 'hipFree', 'hipMemcpy', 'hipMemset', 'hipDeviceSynchronize'):
+        _hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_uint]
+        _hip.hipHostFree.argtypes = [vp]
+        for f in ('hipMalloc', 'hipFree', 'hipMemcpy', 'hipMemset', 'hipDeviceSynchronize', 'hipHostMalloc',
+                  'hipHostFree'):
             getattr(_hip, f).restype = ctypes.c_int
     return _hip
 
@@ -68,3 +71,30 @@ def device_synchronize():
     """hipDeviceSynchronize on libmtgpu's runtime (bench.py's timed-region brackets)."""
     if hip().hipDeviceSynchronize() != 0:
         raise MtError('hipDeviceSynchronize failed')
+
+
+class PinnedArray:
+    """A numpy array in page-locked host memory (hipHostMalloc): H2D copies from it run at the
+    PCIe rate without a staging bounce.  .a is the array; free() (or GC) releases it."""
+
+    def __init__(self, count, dtype):
+        dtype = np.dtype(dtype)
+        nbytes = max(1, count * dtype.itemsize)
+        p = ctypes.c_void_p()
+        if hip().hipHostMalloc(ctypes.byref(p), nbytes, 0) != 0:
+            raise MtError(f'hipHostMalloc({nbytes}) failed')
+        self.ptr = p.value
+        buf = (ctypes.c_uint8 * nbytes).from_address(self.ptr)
+        self.a = np.frombuffer(buf, dtype=np.uint8)[:count * dtype.itemsize].view(dtype)
+
+    def free(self):
+        if self.ptr:
+            self.a = None
+            hip().hipHostFree(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of every kernel, from the two rocprofv3 PMC passes of
-tools/rocprof_r01.sh (FETCH_SIZE and WRITE_SIZE, in KiB per dispatch), corrected as
+tools/rocprof.sh (FETCH_SIZE and WRITE_SIZE, in KiB per dispatch), corrected as
 MI355X_MICROARCH.md's HBM section prescribes for gfx950: FETCH_SIZE reports half the bytes of
 wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is.
 
@@ -48,7 +48,7 @@ def main():
         out[short_name(k)] = {'mangled': k, 'fetch_bytes_per_launch_raw': f, 'write_bytes_per_launch': w,
                   'hbm_bytes_per_launch': 2.0 * f + w, 'launches': len(fetch.get(k, []))}
     meta = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of `bench.py --steps 1 --warmup 0 '
-                      '--no-cpu-baseline` (tools/rocprof_r01.sh)',
+                      '--no-cpu-baseline` (tools/rocprof.sh)',
             'correction': 'hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of wide reads)',
             'kernels': out}
     json.dump(meta, open(sys.argv[3], 'w'), indent=1)

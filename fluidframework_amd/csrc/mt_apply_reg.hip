@@ -199,6 +199,12 @@ struct RWave {
         for (int q = r - __builtin_amdgcn_readlane(incl - c, lk); q > 0; q--) mm &= mm - 1;
         return lk * K + (int)__builtin_ctz(mm);
     }
+    // minimum over the lanes of a per-lane slot index (0x7fffffff = none): lane l's slots all
+    // precede lane l + 1's, so it is the value of the first lane that has one
+    MT_DEV static int first_hit(int v) {
+        const uint64_t m = wave_ballot(v != 0x7fffffff);
+        return m ? __builtin_amdgcn_readlane(v, first_lane(m)) : 0x7fffffff;
+    }
     // first slot >= from whose bit is set in m; ns if none
     MT_DEV int first_from(uint32_t m, int from) const {
         const uint32_t x = m & ~below(from);
@@ -364,7 +370,7 @@ struct RWave {
             const uint64_t m = wave_ballot(p < np && incl - c <= b && b < incl);
             if (m) {
                 const int fl = first_lane(m);
-                if (first_child) *first_child = wave_bcast(incl - c, fl);
+                if (first_child) *first_child = __builtin_amdgcn_readlane(incl - c, fl);
                 return base + fl;
             }
             carry = wave_last(incl);
@@ -565,48 +571,81 @@ struct RWave {
 
     // ------------------------------------------------------------------- heap
     // Heap<LRUSegment> (collections.ts:213-265), comparer maxSeq (mergeTree.ts:923-926)
+    // Both sifts are lane-parallel with one LDS round trip per five levels: the path a sift takes
+    // depends only on the heap's values before it (the moving key is compared with them, never
+    // stored on the way), so the lanes read the candidates first and the walk runs on registers.
+    // Push: lane i holds the key's ancestor i + 1 levels up; the key rises past the ancestors
+    // while `parent - key > 0` (the exact comparison of collections.ts:228-236).
     MT_DEV bool heap_push(int32_t key, int id, int32_t sq) {
         if (heap_n + 1 >= L::H) return fail(MT_DERR_CAPACITY, sq), false;
+        const int k0 = heap_n + 1;
+        const int anc = lane < 31 ? (k0 >> (lane + 1)) : 0;
+        const bool has = anc >= 1;
+        const int32_t av = has ? s.hseq[anc] : 0;
+        const uint16_t as = has ? s.hslot[anc] : (uint16_t)0;
+        const int up = first_lane(wave_ballot(!has || av - key <= 0));  // levels the key rises
+        wave_sync();
+        if (lane < up) {  // ancestor `lane` moves one level down, into its child on the path
+            const int child = k0 >> lane;
+            s.hseq[child] = av;
+            s.hslot[child] = as;
+        }
         if (lane == 0) {
-            int k = heap_n + 1;
-            s.hseq[k] = key;
-            s.hslot[k] = (uint16_t)id;
-            while (k > 1 && s.hseq[k >> 1] - s.hseq[k] > 0) {
-                const int32_t ts = s.hseq[k >> 1];
-                const uint16_t tl = s.hslot[k >> 1];
-                s.hseq[k >> 1] = s.hseq[k];
-                s.hslot[k >> 1] = s.hslot[k];
-                s.hseq[k] = ts;
-                s.hslot[k] = tl;
-                k >>= 1;
-            }
+            s.hseq[k0 >> up] = key;
+            s.hslot[k0 >> up] = (uint16_t)id;
         }
         heap_n = heap_n + 1;
         wave_sync();
         return true;
     }
+    // Pop (collections.ts:240-263): the last entry x replaces the root and sinks along the
+    // smaller-child path (the left child unless the right one is strictly smaller) while
+    // `x - child > 0`.  Lane t < 62 holds the node t + 2 of the five-level subtree below k in
+    // heap order (relative index r at lane r - 2).
     MT_DEV int heap_pop() {
-        int id = 0;
-        if (lane == 0) {
-            id = s.hslot[1];
-            const int cnt = heap_n - 1;
-            s.hseq[1] = s.hseq[heap_n];
-            s.hslot[1] = s.hslot[heap_n];
-            int k = 1;
-            while ((k << 1) <= cnt) {
-                int j = k << 1;
-                if (j < cnt && s.hseq[j] - s.hseq[j + 1] > 0) j++;
-                if (s.hseq[k] - s.hseq[j] <= 0) break;
-                const int32_t ts = s.hseq[k];
-                const uint16_t tl = s.hslot[k];
-                s.hseq[k] = s.hseq[j];
-                s.hslot[k] = s.hslot[j];
-                s.hseq[j] = ts;
-                s.hslot[j] = tl;
+        const int id = uni(s.hslot[1]);
+        const int cnt = heap_n - 1;
+        const int32_t x = uni(s.hseq[heap_n]);
+        const uint32_t xs = uniu(s.hslot[heap_n]);
+        int k = 1;
+        for (bool more = (k << 1) <= cnt; more;) {
+            const int r = lane + 2;
+            const int dep = 31 - __builtin_clz((uint32_t)r);
+            const int node = (k << dep) + (r - (1 << dep));
+            const bool ok = lane < 62 && node <= cnt;
+            const int32_t v = ok ? s.hseq[node] : 0;
+            const uint32_t sl = ok ? (uint32_t)s.hslot[node] : 0u;
+            wave_sync();
+            int rr = 1;
+            more = false;
+            for (int lv = 0; lv < 5; lv++) {
+                if ((k << 1) > cnt) break;
+                int j = k << 1, jr = rr << 1;
+                int32_t vj = __builtin_amdgcn_readlane(v, jr - 2);
+                if (j < cnt) {
+                    const int32_t v1 = __builtin_amdgcn_readlane(v, jr - 1);
+                    if (vj - v1 > 0) {
+                        j++;
+                        jr++;
+                        vj = v1;
+                    }
+                }
+                if (x - vj <= 0) break;
+                const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)sl, jr - 2);
+                if (lane == 0) {  // the child moves up into k
+                    s.hseq[k] = vj;
+                    s.hslot[k] = (uint16_t)sj;
+                }
                 k = j;
+                rr = jr;
+                more = lv == 4 && (k << 1) <= cnt;
             }
+            wave_sync();
         }
-        id = __builtin_amdgcn_readlane(id, 0);
+        if (lane == 0) {
+            s.hseq[k] = x;
+            s.hslot[k] = (uint16_t)xs;
+        }
         heap_n = heap_n - 1;
         wave_sync();
         return id;
@@ -915,7 +954,7 @@ struct RWave {
             const bool ends = (j + 1 < K ? ((bm >> (j + 1)) & 1u) != 0 : nxt != 0) || i == ns - 1;
             last = (i < ns && ends && cum[j] >= pos) ? i : last;
         }
-        last = wave_min(last);
+        last = first_hit(last);  // slots are blocked by lane: the first lane with a hit has the minimum
         if (last == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
         const int a = block_start(last), e = last + 1;
         ba = a;
@@ -936,7 +975,7 @@ struct RWave {
                 best = h ? i : best;
             }
         }
-        best = wave_min(best);
+        best = first_hit(best);
         k = best != 0x7fffffff ? best : e;
         const int t = alloc_id(S);
         if (t < 0) return -1;
@@ -1461,20 +1500,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K >= 12 ? MT
     // while op i is applied
     uint32_t blk0 = load_op_block(ops, a, b, wv.lane);
     uint32_t blk1 = load_op_block(ops, a + 8, b, wv.lane);
-    mt_op_rec nx = op_from_block(blk0, 0);
-    uint32_t pb0 = wv.lane < (int)nx.payload_len ? payload[nx.payload_off + wv.lane] : 0u;
+    uint32_t pb0;
+    {
+        const uint32_t poff = (uint32_t)__builtin_amdgcn_readlane((int)blk0, 6);
+        const uint32_t plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, 7);
+        pb0 = wv.lane < (int)plen ? payload[poff + wv.lane] : 0u;
+    }
     for (uint32_t i = a; i < b; i++) {
         if (wv.err) break;
-        const mt_op_rec op = nx;
+        // op i's fields are taken from its block here (not carried over from the previous
+        // iteration: ten fewer scalars live across the apply)
+        const mt_op_rec op = op_from_block(blk0, (i - a) & 7u);
         wv.pb = pb0;
         const uint32_t j = (i + 1 - a) & 7u;  // op i+1's record in its block
         if (j == 0) {
             blk0 = blk1;
             blk1 = load_op_block(ops, i + 9, b, wv.lane);
         }
-        if (i + 1 < b) {
-            nx = op_from_block(blk0, j);
-            pb0 = wv.lane < (int)nx.payload_len ? payload[nx.payload_off + wv.lane] : 0u;
+        if (i + 1 < b) {  // payload prefetch of op i+1
+            const uint32_t poff = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j * 8 + 6));
+            const uint32_t plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j * 8 + 7));
+            pb0 = wv.lane < (int)plen ? payload[poff + wv.lane] : 0u;
         }
         wv.apply(op, payload);
 #ifdef MT_PROF

@@ -285,6 +285,7 @@ def main():
                 'measured_in': 'an extra untimed step with the capacity classes serialized'
                                if rcls is not cls else 'the timed steps (classes serialized)',
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
+                'class_ms_serialized': {str(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
                 'all_apply_kernels': {'launches': launches, 'kernel_ms': round(kern_ms, 2),
                                       'achieved_GBps': round(all_achieved, 1),
                                       'apply_wall_ms': round(wall_ms, 2),

@@ -82,7 +82,8 @@ struct Wave {
         const bool seen = (s.client[slot] == C) || (s.seq[slot] <= R);
         if (!seen) return 0;
         if (s.flags[slot] & MT_SF_REMOVED) {
-            if (s.rclient[slot] == C || ((s.ovl[slot] >> C) & 1ull) || s.rseq[slot] <= R) return 0;
+            // (C = NonCollabClient for a snapshot body append: no overlap bit, MT_OP_LOAD)
+            if (s.rclient[slot] == C || (C < 64 && ((s.ovl[slot] >> C) & 1ull)) || s.rseq[slot] <= R) return 0;
         }
         return (int)s.len[slot];
     }
@@ -616,7 +617,7 @@ struct Wave {
 
     MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np) {
         const int32_t S = op.seq, R = op.ref_seq;
-        const int C = op.client, pos = op.pos1;
+        const int C = op.client & 0xFF, pos = op.pos1;  // (MT_OP_LOAD: removedClient in the high byte)
         if (!boundary(pos, R, C, S)) return;  // cum: apply() scanned for (R, C)
         if (tlen > 0) {  // blockInsert (mergeTree.ts:2141-2224)
             block_starts();
@@ -667,14 +668,17 @@ struct Wave {
             }
             __threadfence_block();
             if (lane == 0) {
+                // a snapshot body segment may arrive removed (SnapshotLoader.specToSegment,
+                // snapshotLoader.ts:101-106): MT_OP_LOAD carries removedSeq in pos2
+                const bool lrm = op.type == MT_OP_LOAD && op.pos2 >= 0;
                 s.seq[t] = S;
                 s.client[t] = (uint8_t)C;
-                s.rseq[t] = 0;
-                s.rclient[t] = 0;
+                s.rseq[t] = lrm ? op.pos2 : 0;
+                s.rclient[t] = lrm ? (uint8_t)(op.client >> 8) : 0;
                 s.ovl[t] = 0;
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
-                uint8_t f = (pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0);
+                uint8_t f = (pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0) | (lrm ? MT_SF_REMOVED : 0);
                 uint64_t p = 0;
                 if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
                     f |= MT_SF_PDEF;
@@ -777,8 +781,17 @@ struct Wave {
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
         const int np = op.flags >> MT_F_NPAIRS_SHIFT;
         const int32_t S = op.seq;
-        if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
-        if (op.type != MT_OP_NOOP) {
+        if (op.type > MT_OP_LOAD) return fail(MT_DERR_BAD_OP, S);
+        // MT_OP_LOAD: MergeTree.insertSegments from SnapshotLoader.loadBody (snapshotLoader.ts:192-224),
+        // no Client around it: no window asserts and no updateSeqNumbers
+        const bool load = op.type == MT_OP_LOAD;
+        const int C = op.client & 0xFF;
+        if (load) {
+            const bool ok = (C == MT_CLIENT_NONCOLLAB || (C >= 1 && C < MT_MAX_CLIENTS)) &&
+                            (op.pos2 < 0 || ((op.client >> 8) >= 1 && (op.client >> 8) < MT_MAX_CLIENTS));
+            if (!ok) return fail(MT_DERR_LIMITS, S);
+            if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+        } else if (op.type != MT_OP_NOOP) {
             if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
         } else {  // every assert of the message before any edit: the document halts before it
@@ -791,21 +804,22 @@ struct Wave {
         for (int q = 0; q < np; q++)
             if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
         if (op.type != MT_OP_NOOP) {
-            if (op.pos1 < 0 || (op.type != MT_OP_INSERT && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
-            const int L = scan(op.ref_seq, op.client);  // cum for the op's view (no edit yet)
+            if (op.pos1 < 0 || (op.type != MT_OP_INSERT && !load && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
+            const int L = scan(op.ref_seq, C);  // cum for the op's view (no edit yet)
             // the window asserts run after the op in the reference (completeAndLogOp, client.ts:461-464;
             // updateSeqNumbers :826), so a failing insert (mergeTree.ts:2210) is reported first; all of
             // them are decided here, before any edit: the document halts before the failing message
             int wc = 0;
-            if (!(s.cur_seq < S)) wc = MT_DERR_SEQ_ORDER;
+            if (load) wc = 0;
+            else if (!(s.cur_seq < S)) wc = MT_DERR_SEQ_ORDER;
             else if (!(s.min_seq <= op.msn) || !(op.msn <= S)) wc = MT_DERR_MSN_ORDER;
-            if (op.type == MT_OP_INSERT && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
+            if ((op.type == MT_OP_INSERT || load) && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
             if (wc) return fail(wc, S);
-            if (op.type == MT_OP_INSERT) op_insert(op, pay, tlen, pairs, np);
+            if (op.type == MT_OP_INSERT || load) op_insert(op, pay, tlen, pairs, np);
             else op_range(op, pairs, np);
         }
         if (s.err) return;
-        if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
+        if (!load && !(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
     }
 
     // ---------------------------------------------------------------- generator

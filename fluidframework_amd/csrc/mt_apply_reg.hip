@@ -20,9 +20,10 @@
 //     (K predicated moves per field per lane, DPP wave_shr:1 across lanes);
 //   * cold fields (property set, text offset) stay in LDS indexed by a segment id that never
 //     changes while the segment is linked; the zamboni heap holds those ids.
-// Capacity classes K = 2, 4, 8, 12, 16 (128..1024 slots).  Bigger documents, and documents that
-// ever see a client id above 32 (the register overlap set is 32 bits wide), run on mt_apply.hip's
-// LDS engine; both engines share the HBM layout of mt_state.h.
+// Capacity classes K = 2, 4, 8, 12, 16 (128..1024 slots).  Bigger documents, documents that ever
+// see a client id above 32 (the register overlap set is 32 bits wide), and a launch that carries
+// snapshot body appends (MT_OP_LOAD, once in a document's life) run on mt_apply.hip's LDS engine;
+// both engines share the HBM layout of mt_state.h.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

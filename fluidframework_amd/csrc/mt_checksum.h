@@ -19,6 +19,8 @@ MT_HD static inline uint64_t mt_seg_hash(uint64_t idx, uint64_t text_hash, int32
     h = mt_mix64(h ^ props_lo ^ ((uint64_t)props_defined << 63));
     return h;
 }
+// canonical client id of a stored short id: NonCollabClient (snapshot loads) is -2
+MT_HD static inline int32_t mt_canon_client(uint32_t c) { return c == 0xFEu ? -2 : (int32_t)c; }
 MT_HD static inline uint64_t mt_tree_term(uint64_t count, uint64_t b, uint64_t depth) {
     return mt_mix64(count ^ (b << 8) ^ (depth << 56));
 }

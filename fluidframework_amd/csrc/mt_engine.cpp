@@ -27,6 +27,9 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
+extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
+                                     const mt_load_seg* segs, const uint8_t* text, const int32_t* min_seq,
+                                     const int32_t* cur_seq, hipStream_t st);
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
                                     uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st);
@@ -118,6 +121,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     if (!cfg || !out || cfg->max_docs == 0) return MT_ERR_ARG;
     // the register / LDS classes reach 2048 slots and read whole rows of that size
     if (cfg->seg_capacity != 0 && cfg->seg_capacity < 2048) return MT_ERR_ARG;
+    if (cfg->text_capacity > MT_MAX_TEXTCAP) return MT_ERR_ARG;  // li packs len into 20 bits (mt_apply_reg.hip)
     HIP_OK(hipSetDevice(cfg->device));
     auto* e = new mt_engine();
     e->cfg = *cfg;
@@ -210,6 +214,55 @@ mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
     HIP_OK(mt_launch_init(&e->g, n_docs, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return MT_OK;
+}
+
+mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const uint32_t* seg_row_ptr,
+                       const mt_load_seg* segs, const uint8_t* text, uint64_t text_bytes, const int32_t* min_seq,
+                       const int32_t* cur_seq) {
+    static_assert(sizeof(mt_load_seg) == 32, "mt_load_seg is 32 bytes");
+    if (!e || (n && (!doc_ids || !seg_row_ptr || !min_seq || !cur_seq))) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    const uint64_t n_segs = seg_row_ptr[n] - seg_row_ptr[0];
+    if (n_segs && !segs) return MT_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++) {
+        if (doc_ids[i] >= e->n_docs || seg_row_ptr[i + 1] < seg_row_ptr[i]) return MT_ERR_ARG;
+        if (!(min_seq[i] <= cur_seq[i])) return MT_ERR_ARG;
+    }
+    for (uint64_t k = 0; k < n_segs; k++) {  // every text range inside `text`, ids in range
+        const mt_load_seg& sg = segs[seg_row_ptr[0] + k];
+        if ((uint64_t)sg.text_off + sg.text_len > text_bytes) return MT_ERR_ARG;
+        if (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) return MT_ERR_ARG;
+        if (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS) return MT_ERR_ARG;
+    }
+    HIP_OK(hipSetDevice(e->cfg.device));
+    // one staging allocation: ids, rebased row pointers, windows, segments, text
+    std::vector<uint32_t> rp(n + 1);
+    for (uint32_t i = 0; i <= n; i++) rp[i] = seg_row_ptr[i] - seg_row_ptr[0];
+    const size_t o_ids = 0, o_rp = o_ids + 4ull * n, o_mn = o_rp + 4ull * (n + 1), o_cs = o_mn + 4ull * n;
+    const size_t o_sg = (o_cs + 4ull * n + 31) & ~size_t(31), o_tx = o_sg + sizeof(mt_load_seg) * n_segs;
+    const size_t total = o_tx + text_bytes;
+    uint8_t* buf = nullptr;
+    if (hipMalloc(&buf, total ? total : 1) != hipSuccess) return MT_ERR_NOMEM;
+    mt_status st = MT_OK;
+    do {
+        if (hipMemcpyAsync(buf + o_ids, doc_ids, 4ull * n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            hipMemcpyAsync(buf + o_rp, rp.data(), 4ull * (n + 1), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            hipMemcpyAsync(buf + o_mn, min_seq, 4ull * n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            hipMemcpyAsync(buf + o_cs, cur_seq, 4ull * n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            (n_segs && hipMemcpyAsync(buf + o_sg, segs + seg_row_ptr[0], sizeof(mt_load_seg) * n_segs,
+                                      hipMemcpyHostToDevice, e->stream) != hipSuccess) ||
+            (text_bytes && hipMemcpyAsync(buf + o_tx, text, text_bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)) {
+            st = MT_ERR_HIP;
+            break;
+        }
+        if (mt_launch_load(&e->g, n, reinterpret_cast<uint32_t*>(buf + o_ids), reinterpret_cast<uint32_t*>(buf + o_rp),
+                           reinterpret_cast<mt_load_seg*>(buf + o_sg), buf + o_tx, reinterpret_cast<int32_t*>(buf + o_mn),
+                           reinterpret_cast<int32_t*>(buf + o_cs), e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            st = MT_ERR_HIP;
+    } while (0);
+    hipFree(buf);
+    return st;
 }
 
 mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
@@ -654,7 +707,7 @@ std::string state_json(const HostDoc& h) {
         o += '[';
         json_str(o, h.text.data() + h.toff[i], h.len[i]);
         const bool rm = h.flags[i] & MT_SF_REMOVED;
-        o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(h.client[i]) + ',';
+        o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(mt_canon_client(h.client[i])) + ',';
         o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient[i]) : "-1") + ",[";
         bool f = true;
         for (int c = 0; c < 64; c++)
@@ -751,6 +804,7 @@ void seg_json(std::string& o, const HostDoc& h, int i, const std::string& text) 
 }
 
 std::string client_name(const char* const* names, uint32_t n_names, uint32_t c) {
+    if (c == MT_CLIENT_NONCOLLAB) return "original";  // Client.getLongClientId of a negative id (client.ts:645-652)
     if (names && c < n_names && names[c]) return names[c];
     return std::to_string(c);
 }

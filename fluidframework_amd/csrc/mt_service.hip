@@ -24,6 +24,119 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
 }
 
+// SnapshotLoader.loadHeader (snapshotLoader.ts:119-157) for a batch of documents, one wave per
+// document: the header chunk's segments become the document in order (specToSegment, :85-117:
+// NonCollabClient / UniversalSequenceNumber without merge info), texts packed into the arena's
+// first half; MergeTree.reloadFromSegments (mergeTree.ts:1195-1251) shapes the tree bottom-up with
+// MaxNodesInBlock - 1 = 7 children per block (the last block of a level takes the rest) until one
+// block is left; startOrUpdateCollaboration (client.ts:1051-1071, mergeTree.ts:1254-1271) sets the
+// window and an empty LRU heap.  Every block's needsScour is undefined.
+__global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, const uint32_t* __restrict__ doc_ids,
+                                                     const uint32_t* __restrict__ row_ptr,
+                                                     const mt_load_seg* __restrict__ segs,
+                                                     const uint8_t* __restrict__ text,
+                                                     const int32_t* __restrict__ min_seq,
+                                                     const int32_t* __restrict__ cur_seq) {
+    const uint32_t w = blockIdx.x;
+    if (w >= n) return;
+    const uint32_t d = doc_ids[w];
+    const int lane = lane_id();
+    const uint32_t r0 = row_ptr[w];
+    const int ns = (int)(row_ptr[w + 1] - r0);
+    constexpr int kPerBlock = 7;  // MaxNodesInBlock - 1
+    int nb[MT_MAXLEV] = {0};
+    int nlev = 0;
+    int err = 0;
+    {
+        int m = ns;
+        do {
+            const int blocks = m == 0 ? 1 : (m + kPerBlock - 1) / kPerBlock;
+            if (nlev >= MT_MAXLEV || blocks > (int)(nlev == 0 ? g.lbcap : g.ibcap)) {
+                err = MT_DERR_CAPACITY;
+                break;
+            }
+            nb[nlev++] = blocks;
+            m = blocks;
+        } while (m > 1);
+    }
+    if (ns > (int)g.segcap) err = MT_DERR_CAPACITY;
+    const size_t so = (size_t)d * g.segcap;
+    uint8_t* arena = g.text + (size_t)d * 2 * g.textcap;  // half 0
+    uint32_t carry = 0;
+    bool wide = false;
+    for (int base = 0; base < ns && !err; base += 64) {
+        const int i = base + lane;
+        mt_load_seg sg{};
+        if (i < ns) sg = segs[r0 + i];
+        const uint32_t l = i < ns ? sg.text_len : 0u;
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)l);
+        const uint32_t at = carry + incl - l;
+        carry += (uint32_t)wave_last((int)incl);
+        if (carry > g.textcap) {
+            err = MT_DERR_TEXT_ARENA;
+            break;
+        }
+        wide = wide || __ballot(i < ns && ((sg.client > 32 && sg.client < MT_MAX_CLIENTS) ||
+                                           (sg.rseq >= 0 && sg.rclient > 32))) != 0;
+        if (i < ns) {
+            bool nl = false;
+            for (uint32_t q = 0; q < l; q++) {
+                const uint8_t c = text[sg.text_off + q];
+                arena[at + q] = c;
+                nl = nl || c == '\n';
+            }
+            const bool rm = sg.rseq >= 0;
+            uint8_t fl = (uint8_t)((rm ? MT_SF_REMOVED : 0u) | (sg.flags & MT_SF_PDEF) | (nl ? MT_SF_HASNL : 0u));
+            if (l && text[sg.text_off + l - 1] == '\n') fl |= MT_SF_NL;
+            g.seq[so + i] = sg.seq;
+            g.rseq[so + i] = rm ? sg.rseq : 0;
+            g.len[so + i] = l;
+            g.toff[so + i] = at;
+            g.ovl[so + i] = 0;  // removedClientOverlap is not part of a snapshot
+            g.props[so + i] = sg.props;
+            g.client[so + i] = sg.client;
+            g.rclient[so + i] = rm ? sg.rclient : 0;
+            g.flags[so + i] = fl;
+        }
+    }
+    if (!err) {
+        // block shape, level by level: block b of a level has min(7, m - 7b) children
+        int m = ns;
+        for (int L = 0; L < nlev; L++) {
+            uint8_t* cnt = L == 0 ? g.lbcnt + (size_t)d * g.lbcap
+                                  : g.ibcnt + ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
+            for (int b = lane; b < nb[L]; b += 64) {
+                cnt[b] = (uint8_t)min(kPerBlock, m - kPerBlock * b);
+                if (L == 0) g.lbscour[(size_t)d * g.lbcap + b] = MT_SC_UNDEF;
+            }
+            m = nb[L];
+        }
+    }
+    if (lane == 0) {
+        mt_doc_scalars sc{};
+        sc.win_op = -1;
+        if (err) {  // the document keeps an empty tree and reports the error
+            sc.nlev = 1;
+            sc.nb[0] = 1;
+            sc.n_empty = 1;
+            sc.err = err;
+            sc.err_seq = cur_seq[w];
+            g.lbcnt[(size_t)d * g.lbcap] = 0;
+            g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
+        } else {
+            sc.nseg = ns;
+            sc.nlev = nlev;
+            for (int L = 0; L < nlev; L++) sc.nb[L] = nb[L];
+            sc.n_empty = ns == 0 ? 1u : 0u;
+            sc.text_top = carry;
+            sc.wide = wide ? 1u : 0u;
+        }
+        sc.cur_seq = cur_seq[w];
+        sc.min_seq = min_seq[w];
+        g.sc[d] = sc;
+    }
+}
+
 // Bin the documents that have ops in this launch by the capacity class they need.  Each op
 // adds at most 2 segments (a boundary split + an insert, or two boundary splits), at most 2 leaf
 // blocks, and a handful of heap entries; the register engine also pads one slot per empty leaf
@@ -51,7 +164,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 int32_t cur = sc.cur_seq, mn = sc.min_seq;
                 for (uint32_t i = a; i < b; i++) {
                     const mt_op_rec o = ops[i];
-                    if (o.type > MT_OP_NOOP) break;
+                    if (o.type == MT_OP_LOAD) continue;  // snapshot body append: no window update
+                    if (o.type > MT_OP_LOAD) break;
                     const bool bad = o.type == MT_OP_NOOP ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
                                                           : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
                     if (bad) {
@@ -65,14 +179,25 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 }
             }
             bool wide = sc.wide != 0;
+            // snapshot body appends (MT_OP_LOAD, SnapshotLoader.loadBody) are applied by the LDS
+            // engine only: the register engine's hot loop stays free of them
+            bool lds_only = false;
+            if (ops)
+                for (uint32_t i = a; i < b && !lds_only; i++) lds_only = ops[i].type == MT_OP_LOAD;
             if (!wide && ops) {
-                for (uint32_t i = a; i < b; i++) wide = wide || ops[i].client > 32;
+                for (uint32_t i = a; i < b; i++) {
+                    const uint32_t c = ops[i].client;
+                    wide = wide || (ops[i].type == MT_OP_LOAD
+                                        ? (((c & 0xFFu) > 32 && (c & 0xFFu) != MT_CLIENT_NONCOLLAB) ||
+                                           (ops[i].pos2 >= 0 && (c >> 8) > 32))
+                                        : c > 32);
+                }
                 if (wide) g.sc[d].wide = 1u;
             }
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
             c = n_classes - 1;
-            for (int k = 0; k < n_classes && !wide; k++) {
+            for (int k = 0; k < n_classes && !wide && !lds_only; k++) {
                 const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
                           h = classes[4 * k + 3];
                 if (sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb &&
@@ -153,7 +278,7 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
         for (uint32_t q = 0; q < tl; q++) h = mt_fnv1a_step(h, text[t0 + q]);
         const uint8_t f = g.flags[so + i];
         const bool rm = f & MT_SF_REMOVED;
-        seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], g.client[so + i], rm ? g.rseq[so + i] : -1,
+        seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(g.client[so + i]), rm ? g.rseq[so + i] : -1,
                                rm ? (int32_t)g.rclient[so + i] : -1, g.ovl[so + i], g.props[so + i],
                                (f & MT_SF_PDEF) ? 1u : 0u);
     }
@@ -174,6 +299,14 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
 
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st) {
     hipLaunchKernelGGL(mt_init_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, n_docs);
+    return hipGetLastError();
+}
+extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
+                                     const mt_load_seg* segs, const uint8_t* text, const int32_t* min_seq,
+                                     const int32_t* cur_seq, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_load_kernel, dim3(n), dim3(64), 0, st, *g, n, doc_ids, row_ptr, segs, text, min_seq,
+                       cur_seq);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,

@@ -1,0 +1,230 @@
+"""Snapshot load on the host side of the engine: the reference's SnapshotLoader
+(packages/dds/merge-tree/src/snapshotLoader.ts:24-253) for many documents at once.
+
+A merge-tree snapshot is a tree of blobs: the header chunk (snapshotLegacy.ts:45-47 `header`) and,
+for long documents, body chunks (`body_0`.. in v1, `body` in the legacy format), plus an optional
+`catchupOps` blob (legacy).  The chunks are parsed and brought to the v1 shape exactly as
+toLatestVersion does (snapshotChunks.ts:133-185); then
+
+  * the header's segments become the document through mt_docs_load -- reloadFromSegments
+    (mergeTree.ts:1195-1251) + startOrUpdateCollaboration(minSeq, seq) on the device;
+  * every body segment becomes an MT_OP_LOAD record, applied by the engine's own insert path as
+    loadBody's insertSegments(root.cachedLength, ...) (snapshotLoader.ts:192-224) does;
+  * catch-up ops are returned to the caller, to be submitted like any other sequenced ops.
+
+Segment specs (IJSONSegment / IJSONSegmentWithMergeInfo, snapshotChunks.ts:60-73) map as
+SnapshotLoader.specToSegment (snapshotLoader.ts:85-117) does: without merge info a segment is
+(UniversalSequenceNumber 0, NonCollabClient); with it, its seq / client / removedSeq / removedClient.
+Long client ids and property keys / values are interned per document by the caller's interners.
+Markers are not part of the device representation and are refused (ValueError), like text beyond
+U+00FF (one byte per UTF-16 code unit, textSegment.ts:45).
+"""
+import ctypes
+import json
+
+import numpy as np
+
+from .engine import _check, _ptr, lib
+from .oplog import F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OpBatch
+
+MT_OP_LOAD = 4
+NONCOLLAB = 0xFE            # MT_CLIENT_NONCOLLAB: NonCollabClient (constants.ts:15)
+UNIVERSAL_SEQ = 0           # UniversalSequenceNumber (constants.ts:11)
+SF_PDEF = 2
+
+LOAD_SEG_DTYPE = np.dtype([('seq', '<i4'), ('rseq', '<i4'), ('client', 'u1'), ('rclient', 'u1'), ('flags', 'u1'),
+                           ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('pad2', '<u4'),
+                           ('props', '<u8')])
+assert LOAD_SEG_DTYPE.itemsize == 32
+
+
+class Interner:
+    """First-appearance ids (Client.getOrAddShortClientId order, client.ts:636-660); `first` is the
+    first id handed out (1 for clients: 0 is the document's own observer)."""
+
+    def __init__(self, first=1, limit=64):
+        self.ids = {}
+        self.first, self.limit = first, limit
+
+    def __call__(self, key):
+        k = json.dumps(key, sort_keys=True)  # (a value "true" and a value true are different ids)
+        if k not in self.ids:
+            if self.first + len(self.ids) >= self.limit:
+                raise ValueError(f'more than {self.limit - self.first} distinct ids in one document')
+            self.ids[k] = self.first + len(self.ids)
+        return self.ids[k]
+
+
+class DocInterners:
+    """Per-document id spaces: long client ids -> short ids (1..63), property keys -> 0..7,
+    property values -> 1..255 (0 = absent)."""
+
+    def __init__(self):
+        self.client = Interner(1, 64)
+        self.key = Interner(0, 8)
+        self.value = Interner(1, 256)
+
+
+def _blobs(tree):
+    """{path: contents str or parsed} of a snapshot: an ITree ({"entries": [...]}, e.g. the
+    reference's sequence/src/test/snapshots/*.json; a SharedString keeps the merge-tree under
+    "content"), or the {path: parsed chunk} form mt_get_snapshot / SnapshotV1.emit produce."""
+    if isinstance(tree, dict) and 'entries' in tree:
+        entries = tree['entries']
+        content = [e for e in entries if e.get('path') == 'content' and e.get('type') == 'Tree']
+        if content:
+            entries = content[0]['value']['entries']
+        return {e['path']: e['value']['contents'] for e in entries if e.get('type') == 'Blob'}
+    return dict(tree)
+
+
+def _parse(x):
+    return json.loads(x) if isinstance(x, str) else x
+
+
+def to_latest_version(path, chunk):
+    """snapshotChunks.ts:133-185: a legacy chunk (version undefined) in the v1 shape."""
+    if chunk.get('version') == '1':
+        return chunk
+    if chunk.get('version') is not None:
+        raise ValueError(f'Unsupported chunk path: {path} version: {chunk.get("version")}')
+    meta = None
+    if path == 'header':
+        meta = chunk.get('headerMetadata')
+        if meta is None:
+            ids = [{'id': 'header'}]
+            if chunk['chunkLengthChars'] < chunk['totalLengthChars']:
+                ids.append({'id': 'body'})
+            meta = {'orderedChunkMetadata': ids, 'minSequenceNumber': chunk.get('chunkMinSequenceNumber'),
+                    'sequenceNumber': chunk.get('chunkSequenceNumber'), 'totalLength': chunk['totalLengthChars'],
+                    'totalSegmentCount': chunk['totalSegmentCount']}
+    return {'version': '1', 'length': chunk['chunkLengthChars'], 'segmentCount': chunk['chunkSegmentCount'],
+            'headerMetadata': meta, 'segments': chunk['segmentTexts'], 'startIndex': chunk['chunkStartSegmentIndex']}
+
+
+class LoadedDoc:
+    """One document's snapshot, parsed: header specs, body specs, window, catch-up ops."""
+
+    def __init__(self, tree):
+        blobs = _blobs(tree)
+        header = to_latest_version('header', _parse(blobs['header']))
+        meta = header.get('headerMetadata')
+        if meta is None:
+            raise ValueError('header metadata not available')
+        # snapshotLoader.ts:159-190: every further chunk in orderedChunkMetadata order
+        self.header = list(header['segments'])
+        self.body = []
+        if header['segmentCount'] != meta['totalSegmentCount']:
+            for md in meta['orderedChunkMetadata'][1:]:
+                self.body.extend(to_latest_version(md['id'], _parse(blobs[md['id']]))['segments'])
+        known = {md['id'] for md in meta['orderedChunkMetadata']}
+        rest = [p for p in blobs if p not in known]
+        self.catchup = _parse(blobs[rest[0]]) if len(rest) == 1 and blobs[rest[0]] else []
+        if len(rest) > 1:
+            raise ValueError('Unexpected blobs in snapshot')
+        self.seq = meta['sequenceNumber']
+        self.min_seq = meta['minSequenceNumber'] if meta.get('minSequenceNumber') is not None else self.seq
+
+
+def _spec(spec, it):
+    """specToSegment (snapshotLoader.ts:85-117) -> (text bytes, seq, client, rseq, rclient, pdef, props)"""
+    merge = isinstance(spec, dict) and 'json' in spec
+    js = spec['json'] if merge else spec
+    if isinstance(js, str):
+        text, props = js, None
+    elif isinstance(js, dict) and 'text' in js:
+        text, props = js['text'], js.get('props')
+    else:
+        raise ValueError(f'only text segments are device-representable (got {json.dumps(js)[:80]})')
+    try:
+        tb = text.encode('latin-1')
+    except UnicodeEncodeError:
+        raise ValueError('text beyond U+00FF is not device-representable') from None
+    pv = 0
+    if props is not None:
+        for k, v in props.items():
+            if v is None:  # a null value never reaches a stored property set
+                continue
+            pv |= it.value(v) << (8 * it.key(k))
+    if merge:
+        seq = spec['seq'] if spec.get('seq') is not None else UNIVERSAL_SEQ
+        client = it.client(spec['client']) if spec.get('client') is not None else NONCOLLAB
+        rseq = spec['removedSeq'] if spec.get('removedSeq') is not None else -1
+        rclient = it.client(spec['removedClient']) if spec.get('removedClient') is not None else 0
+    else:
+        seq, client, rseq, rclient = UNIVERSAL_SEQ, NONCOLLAB, -1, 0
+    return tb, seq, client, rseq, rclient, props is not None, pv
+
+
+def build_load(docs, interners=None):
+    """Device inputs for a batch of parsed documents: (segs, text, row_ptr, min_seq, cur_seq,
+    body OpBatch of MT_OP_LOAD records, interners)."""
+    interners = interners or [DocInterners() for _ in docs]
+    segs, text, row_ptr = [], bytearray(), [0]
+    recs, payload, body_rp = [], bytearray(), [0]
+    for doc, it in zip(docs, interners):
+        local = 0  # root.cachedLength: the local (non-removed) length
+        for spec in doc.header:
+            tb, seq, client, rseq, rclient, pdef, pv = _spec(spec, it)
+            segs.append((seq, rseq, client, rclient, SF_PDEF if pdef else 0, 0, len(text), len(tb), 0, pv))
+            text += tb
+            local += 0 if rseq >= 0 else len(tb)
+        row_ptr.append(len(segs))
+        # loadBody (snapshotLoader.ts:192-224): a run of segments without merge info is one
+        # insertSegments at root.cachedLength, each next one at insertPos += cachedLength
+        # (mergeTree.ts:2219); any other segment is its own insertSegments call
+        batch_pos = None
+        for spec in doc.body:
+            tb, seq, client, rseq, rclient, pdef, pv = _spec(spec, it)
+            batched = client == NONCOLLAB and seq == UNIVERSAL_SEQ
+            if batched:
+                pos = local if batch_pos is None else batch_pos
+                batch_pos = pos + len(tb)
+            else:
+                pos = local
+                batch_pos = None
+            local += 0 if rseq >= 0 else len(tb)
+            pairs = b''
+            flags = 0
+            if pdef:
+                for k in range(8):
+                    v = (pv >> (8 * k)) & 0xFF
+                    if v:
+                        pairs += bytes([k, v])
+                flags = F_PROPS | ((len(pairs) // 2) << NPAIRS_SHIFT)
+            data = tb + pairs
+            recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8), MT_OP_LOAD, flags,
+                         pos, rseq, len(payload), len(data)))
+            payload += data
+        body_rp.append(len(recs))
+    segs_a = np.array(segs, dtype=LOAD_SEG_DTYPE) if segs else np.zeros(0, dtype=LOAD_SEG_DTYPE)
+    body = OpBatch(np.array(recs, dtype=OP_DTYPE) if recs else np.zeros(0, dtype=OP_DTYPE),
+                   np.frombuffer(bytes(payload), dtype=np.uint8).copy(), np.array(body_rp, dtype=np.uint32))
+    return (segs_a, np.frombuffer(bytes(text), dtype=np.uint8).copy(), np.array(row_ptr, dtype=np.uint32),
+            np.array([d.min_seq for d in docs], dtype=np.int32), np.array([d.seq for d in docs], dtype=np.int32),
+            body, interners)
+
+
+def load_docs(engine, trees, doc_ids=None, interners=None):
+    """Load one snapshot per document into `engine` (documents doc_ids, default 0..n-1): the
+    header through mt_docs_load, then the body appends through the engine's apply (documents
+    without a snapshot in the batch get no ops).  Returns (interners, catch-up ops per doc)."""
+    docs = [LoadedDoc(t) for t in trees]
+    ids = np.arange(len(docs), dtype=np.uint32) if doc_ids is None else np.ascontiguousarray(doc_ids, np.uint32)
+    segs, text, rp, mn, cs, body, its = build_load(docs, interners)
+    L = lib()
+    L.mt_docs_load.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    L.mt_docs_load.restype = ctypes.c_int
+    _check(L.mt_docs_load(engine.h, len(docs), _ptr(ids), _ptr(rp), _ptr(segs), _ptr(text), len(text), _ptr(mn),
+                          _ptr(cs)), 'mt_docs_load')
+    if body.n_ops:
+        # the engine applies a batch over all its documents: scatter the body rows to doc_ids
+        counts = np.zeros(engine.n_docs, dtype=np.int64)
+        counts[ids] = np.diff(body.row_ptr)
+        row_ptr = np.zeros(engine.n_docs + 1, dtype=np.uint32)
+        row_ptr[1:] = np.cumsum(counts)
+        order = np.argsort(ids, kind='stable')
+        ops = np.concatenate([body.ops[body.row_ptr[i]:body.row_ptr[i + 1]] for i in order]) if len(order) else body.ops
+        engine.apply(OpBatch(ops, body.payload, row_ptr))
+    return its, [d.catchup for d in docs]

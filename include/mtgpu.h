@@ -30,7 +30,12 @@ enum mt_op_type {
     MT_OP_INSERT = 0,   /* ops.ts:29-34 MergeTreeDeltaType.INSERT   (client.ts:393-441)      */
     MT_OP_REMOVE = 1,   /* MergeTreeDeltaType.REMOVE                (client.ts:320-351)      */
     MT_OP_ANNOTATE = 2, /* MergeTreeDeltaType.ANNOTATE              (client.ts:358-386)      */
-    MT_OP_NOOP = 3      /* non-op message: only updateSeqNumbers(msn, seq) (client.ts:818)  */
+    MT_OP_NOOP = 3,     /* non-op message: only updateSeqNumbers(msn, seq) (client.ts:818)  */
+    MT_OP_LOAD = 4      /* snapshot body segment: MergeTree.insertSegments(pos1, [seg], ref_seq,
+                           client, seq) as SnapshotLoader.loadBody appends it (snapshotLoader.ts:
+                           192-224) -- no collab-window asserts, no updateSeqNumbers.  The segment
+                           may arrive removed: pos2 = its removedSeq (-1: not removed) and the
+                           high byte of `client` its removedClient.  See mt_docs_load. */
 };
 enum mt_op_flags {
     MT_F_REWRITE = 1u << 0,    /* annotate with combiningOp {name:"rewrite"} (properties.ts:118-124) */
@@ -53,10 +58,15 @@ typedef struct mt_op_rec {
     uint32_t payload_len; /* text bytes + 2*npairs: [text][key u8, value u8]*; value 0 = null   */
 } mt_op_rec;
 
+/* NonCollabClient (constants.ts:15): the client of a segment loaded from a snapshot below the
+ * MSN (snapshotLoader.ts:107-114); canonical state and checksum report it as -2 */
+#define MT_CLIENT_NONCOLLAB 0xFE
+
 /* ---- limits of the device representation (checked; violations become per-doc errors) ------ */
 #define MT_MAX_CLIENTS 64      /* short client ids 0..63 (overlap set is a u64 bitmask)          */
 #define MT_MAX_KEYS 8          /* property keys per document (u8 value id per key)              */
 #define MT_MAX_VALUES 255      /* property value ids 1..255 per document (0 = absent/null)      */
+#define MT_MAX_TEXTCAP (512u * 1024u) /* text arena bytes per document half (mt_cfg.text_capacity) */
 
 typedef enum mt_status {
     MT_OK = 0,
@@ -93,7 +103,11 @@ typedef struct mt_engine mt_engine;
 typedef struct mt_batch mt_batch;
 
 /* seg_capacity: 0 = 2048; values below 2048 are rejected (MT_ERR_ARG) -- the capacity classes
- * go up to 2048 segments and every document's slot rows must hold the largest one. */
+ * go up to 2048 segments and every document's slot rows must hold the largest one.
+ * text_capacity: 0 = 64 KiB; at most MT_MAX_TEXTCAP (MT_ERR_ARG above).  Each document has two
+ * halves of this size (compaction copies the live text into the other half); a zamboni append
+ * copies its run to the top of the arena, so documents whose live text approaches the capacity
+ * stop with MT_DERR_TEXT_ARENA -- size it at a few times the largest expected document. */
 mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out);
 mt_status mt_engine_destroy(mt_engine* eng);
 /* documents started by the last mt_docs_init, and the engine's max_docs (either may be NULL) */
@@ -102,6 +116,34 @@ mt_status mt_engine_info(const mt_engine* eng, uint32_t* n_docs, uint32_t* max_d
 /* Start `n_docs` empty documents: Client + startOrUpdateCollaboration(observer, 0, 0)
  * (client.ts:1051-1071, mergeTree.ts:1254-1271). */
 mt_status mt_docs_init(mt_engine* eng, uint32_t n_docs);
+
+/* ---- snapshot load ---------------------------------------------------
+ * One segment of a snapshot's header chunk (IJSONSegmentWithMergeInfo, snapshotChunks.ts:60-66,
+ * after SnapshotLoader.specToSegment, snapshotLoader.ts:85-117): 32 bytes. */
+typedef struct mt_load_seg {
+    int32_t seq;          /* spec.seq, or UniversalSequenceNumber (0) without merge info            */
+    int32_t rseq;         /* spec.removedSeq; -1 = not removed                                      */
+    uint8_t client;       /* short id of spec.client, or MT_CLIENT_NONCOLLAB                        */
+    uint8_t rclient;      /* short id of spec.removedClient (when removed)                          */
+    uint8_t flags;        /* MT_SF_PDEF (from mt_state.h: 2) when the spec carries props             */
+    uint8_t pad;
+    uint32_t text_off;    /* the segment's text in the batch's text bytes                           */
+    uint32_t text_len;
+    uint32_t pad2;
+    uint64_t props;       /* 8 keys x u8 value id (0 = absent)                                       */
+} mt_load_seg;
+
+/* SnapshotLoader.loadHeader for documents doc_ids[0..n): MergeTree.reloadFromSegments (mergeTree.ts:
+ * 1195-1251: the leaves in blocks of MaxNodesInBlock - 1 = 7, levels built bottom-up until one
+ * block is left) then startOrUpdateCollaboration(id, min_seq[i], cur_seq[i]) (snapshotLoader.ts:
+ * 138-154, client.ts:1051-1071; an empty LRU heap, every block's needsScour undefined).  Document
+ * i's segments are segs[seg_row_ptr[i] .. seg_row_ptr[i+1]) in order; texts are byte ranges of
+ * `text` (Latin-1, one byte per UTF-16 unit).  Built on the device, one wave per document.
+ * The body chunks (and catch-up ops) follow through mt_submit as MT_OP_LOAD records (and normal
+ * ops).  A document over the engine's capacities gets MT_DERR_CAPACITY / MT_DERR_TEXT_ARENA. */
+mt_status mt_docs_load(mt_engine* eng, uint32_t n, const uint32_t* doc_ids, const uint32_t* seg_row_ptr,
+                       const mt_load_seg* segs, const uint8_t* text, uint64_t text_bytes, const int32_t* min_seq,
+                       const int32_t* cur_seq);
 
 /* Host -> device staging of a CSR op batch.  Ops are grouped by document (doc_row_ptr has
  * n_docs+1 entries) and seq-ascending within a document.  Buffers are caller-owned and copied

@@ -113,7 +113,7 @@ struct Doc {
     static int segLen(const Seg* s, int32_t R, int32_t C) {
         if (s->client == C || s->seq <= R) {
             if (s->removed) {
-                if (s->rclient == C || ((s->overlap >> C) & 1) || s->rseq <= R) return 0;
+                if (s->rclient == C || (C >= 0 && ((s->overlap >> C) & 1)) || s->rseq <= R) return 0;
             }
             return s->len();
         }
@@ -398,8 +398,55 @@ struct Doc {
         }
     }
 
+    // SnapshotLoader.loadHeader (snapshotLoader.ts:119-157): specToSegment for every spec, then
+    // MergeTree.reloadFromSegments (mergeTree.ts:1195-1251: blocks of MaxNodesInBlock - 1 children,
+    // built bottom-up until one block is left) and startOrUpdateCollaboration(minSeq, currentSeq)
+    // (client.ts:1051-1071, mergeTree.ts:1254-1271: an empty LRU heap)
+    void reload(const mt_load_seg* segs, uint32_t n, const uint8_t* text, int32_t min_seq, int32_t cur_seq) {
+        std::vector<Node*> nodes;
+        for (uint32_t i = 0; i < n; i++) {
+            const mt_load_seg& sg = segs[i];
+            Seg* sx = newSeg();
+            sx->text.assign(reinterpret_cast<const char*>(text + sg.text_off), sg.text_len);
+            sx->seq = sg.seq;
+            sx->client = sg.client == MT_CLIENT_NONCOLLAB ? -2 : sg.client;
+            if (sg.rseq >= 0) {
+                sx->removed = true;
+                sx->rseq = sg.rseq;
+                sx->rclient = sg.rclient;
+            }
+            if (sg.flags & 2u) {  // MT_SF_PDEF
+                sx->props_defined = true;
+                for (int k = 0; k < 8; k++) sx->props[k] = (uint8_t)(sg.props >> (8 * k));
+            }
+            nodes.push_back(sx);
+        }
+        const int per = kMaxNodes - 1;
+        if (nodes.empty()) {
+            root = newBlock();
+        } else {
+            for (;;) {
+                std::vector<Node*> blocks;
+                for (size_t i = 0; i < nodes.size(); i += per) {
+                    Block* b = newBlock();
+                    for (size_t j = i; j < std::min(nodes.size(), i + per); j++) assign(b, nodes[j], b->childCount++);
+                    blocks.push_back(b);
+                }
+                if (blocks.size() == 1) {
+                    root = static_cast<Block*>(blocks[0]);
+                    break;
+                }
+                nodes.swap(blocks);
+            }
+        }
+        root->parent = nullptr;
+        minSeq = min_seq;
+        currentSeq = cur_seq;
+    }
+
     void applyOp(const mt_op_rec& op, const uint8_t* payload, bool last_member) {
         if (err) return;
+        if (op.type == MT_OP_LOAD) return loadInsert(op, payload);
         const int32_t S = op.seq, R = op.ref_seq, C = op.client;
         const int np = op.flags >> MT_F_NPAIRS_SHIFT;
         // Every assert the reference raises for this message is checked BEFORE anything is
@@ -488,6 +535,46 @@ struct Doc {
                 return fail(MT_DERR_BAD_OP, S);
         }
         if (last_member) updateSeqNumbers(op.msn, S);
+    }
+
+    // SnapshotLoader.loadBody's append (snapshotLoader.ts:192-224): MergeTree.insertSegments(pos,
+    // [seg], refSeq, client, seq) (mergeTree.ts:1968-1998) outside any Client -- no window asserts,
+    // no updateSeqNumbers; the segment may carry removedSeq / removedClient from its spec
+    void loadInsert(const mt_op_rec& op, const uint8_t* payload) {
+        const int32_t S = op.seq, R = op.ref_seq;
+        const int c = op.client & 0xFF, rc = op.client >> 8;
+        const int32_t C = c == MT_CLIENT_NONCOLLAB ? -2 : c;
+        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        if (!(c == MT_CLIENT_NONCOLLAB || (c >= 1 && c < MT_MAX_CLIENTS)) ||
+            (op.pos2 >= 0 && !(rc >= 1 && rc < MT_MAX_CLIENTS)))
+            return fail(MT_DERR_LIMITS, S);
+        if (op.payload_len < (uint32_t)(2 * np) || op.pos1 < 0) return fail(MT_DERR_BAD_OP, S);
+        const uint8_t* pay = payload + op.payload_off;
+        const int tlen = (int)op.payload_len - 2 * np;
+        const uint8_t* pairs = pay + tlen;
+        for (int q = 0; q < np; q++)
+            if (pairs[2 * q] >= kMaxKeys) return fail(MT_DERR_LIMITS, S);
+        ensureIntervalBoundary(op.pos1, R, C);
+        if (tlen > 0) {
+            Seg* sx = newSeg();
+            sx->text.assign(reinterpret_cast<const char*>(pay), tlen);
+            if (op.flags & MT_F_PROPS) {
+                sx->props_defined = true;
+                for (int q = 0; q < np; q++) sx->props[pairs[2 * q]] = pairs[2 * q + 1];
+            }
+            sx->seq = S;
+            sx->client = C;
+            if (op.pos2 >= 0) {
+                sx->removed = true;
+                sx->rseq = op.pos2;
+                sx->rclient = rc;
+            }
+            Block* sp = insertingWalk(root, op.pos1, R, C, sx);
+            if (!sx->parent) return fail(MT_DERR_INSERT_FAILED, S);
+            updateRoot(sp);
+            if (S > minSeq) addToLRUSet(sx, S);
+        }
+        zamboni();
     }
 
     // Client.updateSeqNumbers + MergeTree.setMinSeq (client.ts:821-828, mergeTree.ts:1718-1736)
@@ -732,6 +819,14 @@ int mto_apply(mto_engine* e, const mt_op_rec* ops, const uint8_t* payload, const
 
 void mto_checksums(mto_engine* e, uint64_t* out, uint32_t n_docs) {
     for (uint32_t d = 0; d < n_docs && d < e->docs.size(); d++) out[d] = doc_checksum(e->docs[d]);
+}
+
+int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_segs, const uint8_t* text,
+             int32_t min_seq, int32_t cur_seq) {
+    if (doc >= e->docs.size()) return -1;
+    e->docs[doc] = Doc();
+    e->docs[doc].reload(segs, n_segs, text, min_seq, cur_seq);
+    return 0;
 }
 
 int mto_doc_error(mto_engine* e, uint32_t doc, int32_t* seq) {

@@ -19,6 +19,9 @@ int mto_apply(mto_engine* e, const mt_op_rec* ops, const uint8_t* payload, const
               uint32_t n_docs, int n_threads);
 void mto_checksums(mto_engine* e, uint64_t* out, uint32_t n_docs);
 int mto_doc_error(mto_engine* e, uint32_t doc, int32_t* seq);
+/* SnapshotLoader.loadHeader of one document (reloadFromSegments + the collab window) */
+int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_segs, const uint8_t* text,
+             int32_t min_seq, int32_t cur_seq);
 uint64_t mto_doc_state(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
 uint64_t mto_doc_text(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
 uint32_t mto_doc_nsegs(mto_engine* e, uint32_t doc);

@@ -52,6 +52,8 @@ def lib():
         L.mto_doc_nsegs.argtypes = [vp, u32]
         L.mto_generate.restype = ctypes.c_int
         L.mto_generate.argtypes = [vp, u32, u32, vp, vp, vp, vp, ctypes.c_int]
+        L.mto_load.restype = ctypes.c_int
+        L.mto_load.argtypes = [vp, u32, vp, u32, vp, i32, i32]
         L.mto_seg_hash.restype = u64
         L.mto_seg_hash.argtypes = [u64, u64, i32, i32, i32, i32, u64, u64, u32]
         _lib = L
@@ -92,6 +94,17 @@ class Oracle:
         rc = lib().mto_apply(self.h, _ptr(batch.ops), _ptr(batch.payload), _ptr(batch.row_ptr), batch.n_docs,
                              threads)
         assert rc == 0
+        return self
+
+    def load(self, segs, text, row_ptr, min_seq, cur_seq, doc_ids=None):
+        """SnapshotLoader.loadHeader for documents doc_ids (default 0..n-1): the mt_docs_load inputs."""
+        n = len(row_ptr) - 1
+        ids = range(n) if doc_ids is None else doc_ids
+        for i, d in enumerate(ids):
+            a, b = int(row_ptr[i]), int(row_ptr[i + 1])
+            part = np.ascontiguousarray(segs[a:b])
+            rc = lib().mto_load(self.h, int(d), _ptr(part), b - a, _ptr(text), int(min_seq[i]), int(cur_seq[i]))
+            assert rc == 0
         return self
 
     def checksums(self):

@@ -13,6 +13,13 @@
 //   node replay_ref.js bench <log.mtlog> <threads>   -> ops/sec over all docs (worker_threads)
 //   node replay_ref.js snapshot <log.mtlog> [d0 d1 [chunk]]  -> JSON lines {doc, err, snapshot}: the
 //        entries SnapshotV1.extractSync() + emit() write (snapshotV1.ts:85-246), path -> contents
+//   node replay_ref.js load <log.mtlog> <k> [chunk]  -> JSON lines {doc, err, snapshot, state}: messages
+//        [0, k) replayed on an observer, its SnapshotV1 tree loaded into a fresh Client through the
+//        reference's SnapshotLoader (snapshotLoader.ts:35-225, MockStorage), then messages [k, n)
+//        applied to the loaded Client; state = its canonical state
+//   node replay_ref.js loadtree <snapshot.json> [log.mtlog]  -> one JSON line {err, state}: a stored
+//        SharedString snapshot tree (its "content" subtree, e.g. sequence/src/test/snapshots/*) loaded
+//        the same way, then the log's document 0 applied
 const fs = require("fs");
 const path = require("path");
 const { Worker, isMainThread, parentPort, workerData } = require("worker_threads");
@@ -22,6 +29,9 @@ const { Client } = require(path.join(ROOT, "client.js"));
 const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
 const { MergeTree } = require(path.join(ROOT, "mergeTree.js"));
 const { SnapshotV1 } = require(path.join(ROOT, "snapshotV1.js"));
+const { SnapshotLoader } = require(path.join(ROOT, "snapshotLoader.js"));
+const { MockStorage } = require(path.join(__dirname, "..", "_tsref", "node_modules", "@fluidframework",
+    "test-runtime-utils", "mockStorage.js"));
 
 const { loadLog, messages } = require(path.join(__dirname, "..", "..", "js", "mtlog.js"));
 
@@ -35,6 +45,7 @@ function newObserver() {
 }
 
 function logId(client, shortId) {
+    if (shortId < 0) return -2;  // NonCollabClient (constants.ts:15): segments loaded below the MSN
     const long = client.getLongClientId(shortId);
     return long === "observer" ? 0 : parseInt(long.slice(1), 10);
 }
@@ -83,7 +94,93 @@ function replayDoc(log, d) {
     return { c, err };
 }
 
+// SharedSegmentSequence.loadCore's view of the merge-tree content (a fresh Client, SnapshotLoader
+// .initialize over the "content" blobs, then the catch-up ops), with the runtime pieces the loader
+// reads stubbed: options, documentId, clientId (-> "snapshot", snapshotLoader.ts:145), attached.
+async function loadClient(tree) {
+    const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {},
+        shipAssert(c, e) { if (!c) throw new Error(`shipAssert ${JSON.stringify(e)}`); } };
+    const c = new Client(specToSegment, logger);
+    const runtime = { options: {}, documentId: "doc", clientId: undefined, attachState: "Attached", logger,
+        IFluidSerializer: undefined };
+    const loader = new SnapshotLoader(runtime, c, c.mergeTree, logger);
+    const { catchupOpsP } = await loader.initialize("doc", new MockStorage(tree));
+    const catchup = await catchupOpsP;
+    for (const m of catchup) c.applyMsg(m);
+    return c;
+}
+
+function emitTree(c, chunk) {
+    const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+    if (chunk) {
+        c.mergeTree.options = Object.assign({}, c.mergeTree.options, { mergeTreeSnapshotChunkSize: chunk });
+    }
+    const snap = new SnapshotV1(c.mergeTree, logger);
+    snap.extractSync();
+    return snap.emit();
+}
+
+async function mainAsync(mode) {
+    if (mode === "load") {
+        const log = loadLog(process.argv[3]);
+        const k = parseInt(process.argv[4], 10);
+        const chunk = process.argv[5] ? parseInt(process.argv[5], 10) : 0;
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const msgs = Array.from(messages(log, d));
+            const c0 = newObserver();
+            let err = null, snapshot = null, state = null;
+            try {
+                for (let i = 0; i < Math.min(k, msgs.length); i++) c0.applyMsg(msgs[i]);
+                const tree = emitTree(c0, chunk);
+                snapshot = {};
+                for (const e of tree.entries) snapshot[e.path] = JSON.parse(e.value.contents);
+                let c = await loadClient(tree), at = -1;
+                for (let i = k; i < msgs.length && at < 0; i++) {
+                    try {
+                        c.applyMsg(msgs[i]);
+                    } catch (e) {
+                        err = String(e.message || e);
+                        at = i;
+                    }
+                }
+                if (at >= 0) {  // the state before the failing message (the engine halts there)
+                    c = await loadClient(tree);
+                    for (let i = k; i < at; i++) c.applyMsg(msgs[i]);
+                }
+                state = canonical(c);
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            out.push(JSON.stringify({ doc: d, err, snapshot, state }));  // (err: the message [k, n) that threw)
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
+    if (mode === "loadtree") {
+        const stored = JSON.parse(fs.readFileSync(process.argv[3], "utf8"));
+        const content = stored.entries.find((e) => e.path === "content" && e.type === "Tree");
+        const c = await loadClient(content ? content.value : stored);
+        let err = null;
+        if (process.argv[4]) {
+            const log = loadLog(process.argv[4]);
+            try {
+                for (const m of messages(log, 0)) c.applyMsg(m);
+            } catch (e) {
+                err = String(e.message || e);
+            }
+        }
+        process.stdout.write(JSON.stringify({ err, state: canonical(c) }) + "\n");
+        return;
+    }
+    throw new Error("mode: state | errstate | snapshot | load | loadtree | bench");
+}
+
 function main() {
+    if (process.argv[2] === "load" || process.argv[2] === "loadtree") {
+        mainAsync(process.argv[2]).catch((e) => { console.error(e); process.exit(1); });
+        return;
+    }
     const mode = process.argv[2];
     const log = loadLog(process.argv[3]);
     if (mode === "state") {
@@ -161,7 +258,7 @@ function main() {
         }
         return;
     }
-    throw new Error("mode: state | errstate | snapshot | bench");
+    throw new Error("mode: state | errstate | snapshot | load | loadtree | bench");
 }
 
 if (isMainThread) {

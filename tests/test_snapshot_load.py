@@ -1,0 +1,231 @@
+"""Snapshot LOAD: SnapshotLoader (snapshotLoader.ts:24-253) into a fresh
+document -- reloadFromSegments' 7-per-block tree (mergeTree.ts:1195-1251), the collab window of the
+header, the body chunks appended through insertSegments -- then more sequenced ops.
+
+Pinned by the reference itself (tests/golden/make_load.py):
+  * load_<set>.jsonl: a snapshot the reference emitted after messages [0, k) of a golden log,
+    loaded by the reference's SnapshotLoader, then messages [k, n) applied; the expected canonical
+    state (before the failing message when the reference throws -- a snapshot drops the
+    removedClientOverlap sets, so later views can differ from the unloaded document's);
+  * ref_snapshots/: the reference's own snapshot test data (sequence/src/test/snapshots, v1 and
+    legacy formats, header-only and header + body chunks, annotated), loaded, then the edits of
+    snapshotVersion.spec.ts:53-73 as remote ops.
+CPU tests run the oracle's restatement (oracle/mtcpu.cpp reload + loadInsert) and the host loader
+(fluidframework_amd/snapshot.py); the gpu tests run libmtgpu (mt_docs_load + MT_OP_LOAD)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+LOAD_SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny']
+REF_DIR = os.path.join(GOLDEN, 'ref_snapshots')
+ERRS = {'MergeTree insert failed': 3, 'sequence#': 1, 'minSequence#': 2}
+
+
+class LogIds:
+    """The golden logs' id spaces: client "c<k>" is short id k, key "k<n>" is key n, values are ids."""
+
+    def __init__(self):
+        self.client = lambda s: int(s[1:])
+        self.key = lambda k: int(k[1:])
+        self.value = lambda v: int(v)
+
+
+def err_code(msg):
+    if msg is None:
+        return 0
+    for k, v in ERRS.items():
+        if k in msg:
+            return v
+    raise AssertionError(msg)
+
+
+def load_set(name):
+    with open(os.path.join(GOLDEN, f'load_{name}.jsonl')) as f:
+        return [json.loads(x) for x in f if x.strip()]
+
+
+def tail_batch(batch, k):
+    """The records of every document from its k-th message on (GROUP members are one message)."""
+    from fluidframework_amd.oplog import F_GROUP_MORE, OpBatch
+    keep, rp = [], [0]
+    for d in range(batch.n_docs):
+        a, b = int(batch.row_ptr[d]), int(batch.row_ptr[d + 1])
+        m, start = 0, b
+        for i in range(a, b):
+            if m == k:
+                start = i
+                break
+            if not (batch.ops[i]['flags'] & F_GROUP_MORE):
+                m += 1
+        keep.append(np.arange(start, b))
+        rp.append(rp[-1] + b - start)
+    idx = np.concatenate(keep) if keep else np.zeros(0, dtype=np.int64)
+    return OpBatch(batch.ops[idx], batch.payload, np.array(rp, dtype=np.uint32))
+
+
+def head_batch(batch, k):
+    """The first k records of every document (logs without GROUP messages)."""
+    from fluidframework_amd.oplog import OpBatch
+    a = batch.row_ptr[:-1].astype(np.int64)
+    b = np.minimum(a + k, batch.row_ptr[1:])
+    idx = np.concatenate([np.arange(x, y) for x, y in zip(a, b)])
+    rp = np.zeros(batch.n_docs + 1, dtype=np.uint32)
+    rp[1:] = np.cumsum(b - a)
+    return OpBatch(batch.ops[idx], batch.payload, rp)
+
+
+def load_inputs(rows, ids_factory=LogIds):
+    from fluidframework_amd import snapshot
+    docs = [snapshot.LoadedDoc(r['snapshot']) for r in rows]
+    return snapshot.build_load(docs, [ids_factory() for _ in rows])
+
+
+def translate_props(state, it):
+    """The reference's property names / values as the loader's interned ids ({"k<key>": value})."""
+    if state is None:
+        return None
+    out = dict(state)
+    segs = []
+    for s in state['segs']:
+        s = list(s)
+        if s[6] is not None:
+            s[6] = {f'k{it.key.ids[json.dumps(k)]}': it.value.ids[json.dumps(v)] for k, v in s[6].items()
+                    if v is not None}
+            s[6] = dict(sorted(s[6].items(), key=lambda kv: int(kv[0][1:])))
+        segs.append(s)
+    out['segs'] = segs
+    return out
+
+
+def ref_cases():
+    with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
+        return [json.loads(x) for x in f if x.strip()]
+
+
+# ----------------------------------------------------------------------------------- CPU (oracle)
+def test_chunk_formats_agree():
+    """v1, legacy and legacy-with-catch-up snapshots of the same string parse to the same specs
+    (toLatestVersion, snapshotChunks.ts:133-185)."""
+    from fluidframework_amd import snapshot
+    by = {}
+    for c in ref_cases():
+        with open(os.path.join(REF_DIR, c['file'])) as f:
+            d = snapshot.LoadedDoc(json.load(f))
+        kind = c['file'].split('_', 1)[1]
+        by.setdefault(kind, []).append((d.header + d.body, d.seq, d.min_seq, d.catchup))
+    for kind, v in by.items():
+        assert all(x == v[0] for x in v), kind
+
+
+@pytest.mark.parametrize('name', LOAD_SETS)
+def test_oracle_load_matches_reference(oracle_lib, name):
+    from fluidframework_amd.oplog import OpBatch
+    rows = load_set(name)
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    segs, text, rp, mn, cs, body, _ = load_inputs(rows)
+    o = oracle_lib.Oracle(batch.n_docs).load(segs, text, rp, mn, cs)
+    if body.n_ops:
+        o.apply(body)
+    o.apply(tail_batch(batch, rows[0]['k']))
+    for r in rows:
+        d = r['doc']
+        assert o.error(d)[0] == err_code(r['err']), (name, d, o.error(d), r['err'])
+        if r['state'] is not None:  # (None: the reference's load itself threw -- loadBody's append
+            assert o.state(d) == r['state'], (name, d)  # fell outside what its view sees)
+
+
+def test_oracle_loads_reference_snapshot_files(oracle_lib):
+    from fluidframework_amd import snapshot
+    from fluidframework_amd.oplog import OpBatch
+    for c in ref_cases():
+        with open(os.path.join(REF_DIR, c['file'])) as f:
+            doc = snapshot.LoadedDoc(json.load(f))
+        segs, text, rp, mn, cs, body, its = snapshot.build_load([doc])
+        o = oracle_lib.Oracle(1).load(segs, text, rp, mn, cs)
+        if body.n_ops:
+            o.apply(body)
+        assert o.state(0) == translate_props(c['loaded'], its[0]), c['file']
+        o.apply(OpBatch.load(os.path.join(REF_DIR, c['file'].replace('.json', '.mtlog'))))
+        assert o.error(0)[0] == err_code(c['err'])
+        assert o.state(0) == translate_props(c['state'], its[0]), c['file']
+
+
+# ----------------------------------------------------------------------------------- GPU (libmtgpu)
+@pytest.mark.gpu
+@pytest.mark.parametrize('b', [0, 32])
+@pytest.mark.parametrize('name', LOAD_SETS)
+def test_engine_load_matches_reference(name, b):
+    from fluidframework_amd import snapshot
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    rows = load_set(name)
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=b)
+    snapshot.load_docs(eng, [r['snapshot'] for r in rows], interners=[LogIds() for _ in rows])
+    eng.apply(tail_batch(batch, rows[0]['k']))
+    for r in rows:
+        d = r['doc']
+        assert eng.error(d)[0] == err_code(r['err']), (name, d, eng.error(d), r['err'])
+        if r['state'] is not None:
+            assert eng.state(d) == r['state'], (name, d)
+
+
+@pytest.mark.gpu
+def test_engine_loads_reference_snapshot_files(oracle_lib):
+    """All the reference's text-only snapshot files in one engine (one document each, loaded in one
+    mt_docs_load + one body batch), then the spec's edits; checksums against the oracle too."""
+    from fluidframework_amd import snapshot
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    cases = ref_cases()
+    trees = []
+    for c in cases:
+        with open(os.path.join(REF_DIR, c['file'])) as f:
+            trees.append(json.load(f))
+    # (a 38,890-character document whose appends copy runs of up to its whole text: a larger arena)
+    eng = MergeEngine(len(cases), ops_per_launch=32, text_capacity=256 * 1024)
+    its, catchup = snapshot.load_docs(eng, trees)
+    assert all(x == [] for x in catchup)
+    for d, c in enumerate(cases):
+        assert eng.state(d) == translate_props(c['loaded'], its[d]), c['file']
+    logs = [OpBatch.load(os.path.join(REF_DIR, c['file'].replace('.json', '.mtlog'))) for c in cases]
+    eng.apply(OpBatch.concat(logs))
+    for d, c in enumerate(cases):
+        assert eng.error(d)[0] == err_code(c['err'])
+        assert eng.state(d) == translate_props(c['state'], its[d]), c['file']
+
+
+@pytest.mark.gpu
+def test_engine_load_checksums_match_oracle_at_scale(oracle_lib):
+    """Larger property-based check: 512 synthetic documents replayed on the oracle, their snapshots
+    (the oracle's restatement of SnapshotV1 emit, chunked small so bodies exist) loaded into both
+    the engine and the oracle, then 256 more synthetic ops each; checksums must agree."""
+    from fluidframework_amd import snapshot
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import CONFIGS
+    from oracle import snapshot as osnap
+    cfg = dict(CONFIGS['C4'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 768
+    n = 512
+    full = oracle_lib.generate(n, seed=77, **cfg)
+    head, tail = head_batch(full, 512), tail_batch(full, 512)
+    o0 = oracle_lib.Oracle(n).apply(head, threads=8)
+    trees = [osnap.emit(o0.state(d), 200) for d in range(n)]
+    eng = MergeEngine(n, ops_per_launch=32)
+    snapshot.load_docs(eng, trees, interners=[LogIds() for _ in range(n)])
+    segs, text, rp, mn, cs, body, _ = snapshot.build_load([snapshot.LoadedDoc(t) for t in trees],
+                                                          [LogIds() for _ in range(n)])
+    o = oracle_lib.Oracle(n).load(segs, text, rp, mn, cs)
+    if body.n_ops:
+        o.apply(body, threads=8)
+    np.testing.assert_array_equal(eng.checksums(), o.checksums())
+    eng.apply(tail)
+    o.apply(tail, threads=8)
+    got, want = eng.checksums(), o.checksums()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (bad[:8], [eng.error(int(d)) for d in bad[:4]], [o.error(int(d)) for d in bad[:4]])

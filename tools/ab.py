@@ -30,8 +30,10 @@ for r in range(a.reps):
         line = json.loads([x for x in out.stdout.split('\n') if x.startswith('{')][0])
         rf = line['roofline']
         res[lib].append((line['value'], rf['avg_launch_ms'], rf['kernel'], line['checksum_digest']))
+        ak = rf.get('all_apply_kernels', {})
         print(f'rep {r} {os.path.basename(lib)}: {line["value"] / 1e6:.1f} M ops/s, {rf["kernel"]} '
-              f'{rf["avg_launch_ms"]:.3f} ms, digest {line["checksum_digest"]}', flush=True)
+              f'{rf["avg_launch_ms"]:.3f} ms, all apply kernels {ak.get("kernel_ms")} ms / {ak.get("launches")}, '
+              f'classes {rf.get("class_ms_serialized")}, digest {line["checksum_digest"]}', flush=True)
 for lib, v in res.items():
     print(f'{os.path.basename(lib)}: median {statistics.median(x[0] for x in v) / 1e6:.2f} M ops/s, '
           f'kernel {statistics.median(x[1] for x in v):.3f} ms')

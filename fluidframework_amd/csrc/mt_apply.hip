@@ -57,9 +57,22 @@ struct Lds {
     uint32_t gpay;          // generator: payload bytes used in this document's region
 };
 
-template <int CAP>
+// G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
+// SURVEY.md §8 a9 "unbounded B-tree"): the same structure lives in a per-wave workspace in HBM
+// (mt_launch_apply_big); lanes exchange it through the vector L1 / L2, so a pass boundary also
+// waits for the wave's outstanding stores (workgroup scope = the wave's CU).
+template <int CAP, bool G = false>
 struct Wave {
     using L = Lds<CAP>;
+    MT_DEV static void sync() {
+        if (G) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        } else {
+            wave_sync();
+        }
+    }
     L& s;
     const int lane;
     uint8_t* const abase;   // document's double-buffered arena: [2][textcap]
@@ -73,7 +86,7 @@ struct Wave {
             s.err = code;
             s.err_seq = seq;
         }
-        wave_sync();
+        sync();
     }
 
     // -------------------------------------------------------------- visibility
@@ -99,7 +112,7 @@ struct Wave {
             if (i < n) s.cum[i] = incl;
             carry = wave_last(incl);
         }
-        wave_sync();
+        sync();
         return carry;
     }
     MT_DEV int cstart(int k) const { return k > 0 ? s.cum[k - 1] : 0; }
@@ -112,9 +125,9 @@ struct Wave {
             T v{};
             const bool ok = i >= from;
             if (ok) v = a[i];
-            wave_sync();
+            sync();
             if (ok) a[i + 1] = v;
-            wave_sync();
+            sync();
         }
     }
     template <class T>
@@ -124,9 +137,9 @@ struct Wave {
             T v{};
             const bool ok = i < count_end;
             if (ok) v = a[i];
-            wave_sync();
+            sync();
             if (ok) a[i - by] = v;
-            wave_sync();
+            sync();
         }
     }
 
@@ -146,7 +159,7 @@ struct Wave {
             carry = wave_last(incl);
         }
         if (lane == 0) s.bst[nb] = carry;
-        wave_sync();
+        sync();
     }
 
     // leaf block containing position k (first non-empty block whose range holds k); needs bst
@@ -193,7 +206,7 @@ struct Wave {
             if (L == 0) s.lbscour[b + 1] = MT_SC_UNDEF;
         }
         s.nb[L] = nb + 1;
-        wave_sync();
+        sync();
         return true;
     }
 
@@ -205,7 +218,7 @@ struct Wave {
             int parent = -1;
             if (L < s.nlev - 1) parent = parent_of(L, b, nullptr);
             if (lane == 0) lvl(L)[b] = (uint8_t)half;
-            wave_sync();
+            sync();
             if (!insert_block_after(L, b, half)) return fail(MT_DERR_CAPACITY, seq), false;
             if (L == s.nlev - 1) {  // split the root: new root with 2 children
                 if (s.nlev + 1 > MT_MAXLEV) return fail(MT_DERR_CAPACITY, seq), false;
@@ -213,13 +226,13 @@ struct Wave {
                 if (lane == 0) lvl(nl)[0] = 2;
                 s.nb[nl] = 1;
                 s.nlev = nl + 1;
-                wave_sync();
+                sync();
                 return true;
             }
             uint8_t* pc = lvl(L + 1);
             const int c = (int)pc[parent] + 1;
             if (lane == 0) pc[parent] = (uint8_t)c;
-            wave_sync();
+            sync();
             if (c < kMaxNodes) return true;
             L = L + 1;
             b = parent;
@@ -231,7 +244,7 @@ struct Wave {
         int sl;
         if (s.nfree > 0) {
             sl = s.freel[s.nfree - 1];
-            wave_sync();
+            sync();
             s.nfree = s.nfree - 1;
         } else {
             sl = s.next_slot;
@@ -241,7 +254,7 @@ struct Wave {
             }
             s.next_slot = sl + 1;
         }
-        wave_sync();
+        sync();
         return sl;
     }
     // unlink: free the slot and kill heap entries that still point at it
@@ -252,9 +265,9 @@ struct Wave {
             if (i <= hn && s.hslot[i] == sl) s.hslot[i] = MT_DEAD_SLOT;
         }
         if (lane == 0) s.freel[s.nfree] = (uint16_t)sl;
-        wave_sync();
+        sync();
         s.nfree = s.nfree + 1;
-        wave_sync();
+        sync();
     }
 
     // insert slot `sl` at document position k of leaf block b; splits blocks as needed.
@@ -270,9 +283,9 @@ struct Wave {
         }
         s.n = n + 1;
         const int c = (int)s.lbcnt[b] + 1;
-        wave_sync();
+        sync();
         if (lane == 0) s.lbcnt[b] = (uint8_t)c;
-        wave_sync();
+        sync();
         if (c >= kMaxNodes) return split_up(0, b, seq);
         return true;
     }
@@ -306,7 +319,7 @@ struct Wave {
                 const uint8_t* src = arena + s.toff[sl];
                 for (int q = 0; q < l; q++) dst[at + q] = src[q];
             }
-            wave_sync();
+            sync();
             if (i < n) s.toff[sl] = at;
             carry += (uint32_t)wave_last(incl);
         }
@@ -314,7 +327,7 @@ struct Wave {
         s.text_half = s.text_half ^ 1u;
         s.text_top = carry;
         arena = dst;
-        wave_sync();
+        sync();
     }
     MT_DEV bool arena_reserve(uint32_t need, int32_t seq) {
         if (s.text_top + need <= textcap) return true;
@@ -361,9 +374,9 @@ struct Wave {
             s.flags[sl] = (uint8_t)((s.flags[sl] & ~MT_SF_NL) | (last == '\n' ? MT_SF_NL : 0));
         }
         const int old_end = s.cum[k];
-        wave_sync();
+        sync();
         if (lane == 0) s.cum[k] = pos;
-        wave_sync();
+        sync();
         return insert_at(k + 1, b, t, old_end, seq);
     }
 
@@ -386,9 +399,9 @@ struct Wave {
             }
         }
         const int hn = s.heap_n + 1;
-        wave_sync();
+        sync();
         s.heap_n = hn;
-        wave_sync();
+        sync();
         return true;
     }
     MT_DEV int heap_pop() {
@@ -413,18 +426,18 @@ struct Wave {
             }
         }
         sl = wave_bcast(sl, 0);
-        wave_sync();
+        sync();
         s.heap_n = s.heap_n - 1;
-        wave_sync();
+        sync();
         return sl;
     }
 
     // addToLRUSet (mergeTree.ts:1273-1283) for a segment in leaf block b
     MT_DEV bool add_lru(int b, int sl, int32_t seq) {
         if (s.lbscour[b] != MT_SC_TRUE && seq > s.cur_seq) {
-            wave_sync();
+            sync();
             if (lane == 0) s.lbscour[b] = MT_SC_TRUE;
-            wave_sync();
+            sync();
             return heap_push(seq, sl, seq);
         }
         return true;
@@ -471,12 +484,12 @@ struct Wave {
             }
         }
         if (kept < cnt) {
-            wave_sync();
+            sync();
             if (lane < kept) s.order[st + lane] = keep[lane];
-            wave_sync();
+            sync();
             shift_left(s.order, st + cnt, s.n, cnt - kept);
             s.n = s.n - (cnt - kept);
-            wave_sync();
+            sync();
             if (lane == 0) s.lbcnt[b] = (uint8_t)kept;
             // later block starts move left
             const int nb = s.nb[0];
@@ -484,7 +497,7 @@ struct Wave {
                 const int j = base + lane;
                 if (j <= nb) s.bst[j] -= (cnt - kept);
             }
-            wave_sync();
+            sync();
         }
         return kept;
     }
@@ -509,13 +522,13 @@ struct Wave {
             if (lane == 0) s.toff[prev] = top;
             top += pl + ql;
         }
-        wave_sync();
+        sync();
         if (lane == 0) {
             s.len[prev] = pl + ql;
             s.flags[prev] = (uint8_t)((s.flags[prev] & ~MT_SF_NL) | (s.flags[sl] & (MT_SF_NL | MT_SF_HASNL)));
         }
         s.text_top = top;
-        wave_sync();
+        sync();
     }
 
     // pack (mergeTree.ts:1368-1420): repack the children of block P at level L+1, recursing up
@@ -535,7 +548,7 @@ struct Wave {
             const int base = total / cc, extra = total % cc;
             uint8_t* a = lvl(L);
             const int nb = s.nb[L];
-            wave_sync();
+            sync();
             if (cc < m) {
                 shift_left(a, first_child + m, nb, m - cc);
                 if (L == 0) shift_left(s.lbscour, first_child + m, nb, m - cc);
@@ -550,9 +563,9 @@ struct Wave {
                 if (L == 0) s.lbscour[first_child + lane] = MT_SC_UNDEF;
             }
             s.nb[L] = nb + cc - m;
-            wave_sync();
+            sync();
             if (lane == 0) lvl(L + 1)[P] = (uint8_t)cc;
-            wave_sync();
+            sync();
             if (L == 0) block_starts();
             // underflow(parent) && parent.parent
             if (cc < kMaxNodes / 2 && (L + 1) < s.nlev - 1) {
@@ -582,7 +595,7 @@ struct Wave {
     MT_DEV void zamboni() {
         for (int it = 0; it < 2; it++) {
             if (s.heap_n == 0 || s.hseq[1] > s.min_seq) break;
-            wave_sync();
+            sync();
             const int sl = heap_pop();
             if (sl == (int)MT_DEAD_SLOT) continue;
             const int k = pos_of_slot(sl);
@@ -592,9 +605,9 @@ struct Wave {
             if (s.lbscour[b] == MT_SC_FALSE) continue;
             const int cnt = s.lbcnt[b];
             const int kept = scour(b);
-            wave_sync();
+            sync();
             if (lane == 0) s.lbscour[b] = MT_SC_FALSE;
-            wave_sync();
+            sync();
             if (kept < cnt && kept < kMaxNodes / 2 && s.nlev > 1) {
                 int fc = 0;
                 const int P = parent_of(0, b, &fc);
@@ -688,7 +701,7 @@ struct Wave {
                 s.props[t] = p;
             }
             s.text_top = top + (uint32_t)tlen;
-            wave_sync();
+            sync();
             const int idx = k - st;  // index inside block b before a possible split
             const int before_nb = s.nb[0];
             if (!insert_at(k, b, t, -1, S)) return;
@@ -733,7 +746,7 @@ struct Wave {
                 }
             }
         }
-        wave_sync();
+        sync();
         // addToLRUSet for touched segments in document order: one heap push per leaf block
         // whose needsScour is not already true, for its first touched segment
         block_starts();
@@ -766,14 +779,14 @@ struct Wave {
     // Client.updateSeqNumbers + MergeTree.setMinSeq (client.ts:821-828, mergeTree.ts:1718-1736)
     MT_DEV void update_seq(int32_t msn, int32_t seq) {
         if (!(s.cur_seq <= seq)) return fail(MT_DERR_SEQ_ORDER, seq);
-        wave_sync();
+        sync();
         s.cur_seq = seq;
-        wave_sync();
+        sync();
         if (!(msn <= seq) || !(s.min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, seq);
         if (msn > s.min_seq) {
-            wave_sync();
+            sync();
             s.min_seq = msn;
-            wave_sync();
+            sync();
             zamboni();
         }
     }
@@ -837,15 +850,15 @@ struct Wave {
             if (seq < s.gstall) {
                 want = s.gcref[1];
             } else if (mt_ru(key, i, MT_R_STALL, 1, cfg.stall_ops) == 1) {
-                wave_sync();
+                sync();
                 s.gstall = seq + (int32_t)cfg.stall_ops;
             }
         }
         int32_t R = s.gcref[c] > want ? s.gcref[c] : want;
         if (R > seq) R = seq;
-        wave_sync();
+        sync();
         if (lane == 0) s.gcref[c] = R;
-        wave_sync();
+        sync();
         const int32_t mine = (lane >= 1 && lane <= (int)C) ? s.gcref[lane] : 0x7fffffff;
         const int32_t msn = min(R, wave_min(mine));
         const int L = scan(R, c);
@@ -951,7 +964,7 @@ struct Wave {
         rec.flags |= (uint8_t)(np << MT_F_NPAIRS_SHIFT);
         rec.payload_len = n + 2 * np;
         rec.payload_off = 0;  // caller rebases
-        wave_sync();
+        sync();
         return rec;
     }
 
@@ -1000,7 +1013,7 @@ struct Wave {
             s.text_top = sc.text_top;
             s.text_half = sc.text_half;
         }
-        wave_sync();
+        sync();
         arena = abase + (size_t)s.text_half * textcap;
     }
 
@@ -1022,7 +1035,7 @@ struct Wave {
             g.flags[so + i] = s.flags[sl];
             s.cum[sl] = i;  // slot -> position for the heap remap
         }
-        wave_sync();
+        sync();
         const size_t lo = (size_t)d * g.lbcap;
         int nempty = 0;
         for (int i = lane; i < min(s.nb[0], (int)g.lbcap); i += 64) {
@@ -1120,6 +1133,33 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     wv.store(g, d);
 }
 
+// Documents above 2048 segments: the same engine with the document's structure in a per-wave
+// HBM workspace (ws + w * sizeof(Lds<CAP>)) instead of LDS.  Latency-bound like the LDS form but
+// without its 160 KiB-per-CU ceiling; such documents are rare, so a handful of waves serve them.
+template <int CAP>
+__global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_rec* __restrict__ ops,
+                                                     const uint8_t* __restrict__ payload,
+                                                     const uint32_t* __restrict__ row_ptr,
+                                                     const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
+                                                     uint32_t op_lo, uint32_t op_cnt, uint8_t* __restrict__ ws) {
+    const uint32_t w = blockIdx.x;
+    if (w >= n_docs) return;
+    const uint32_t d = doc_ids ? doc_ids[w] : w;
+    Lds<CAP>& st = *reinterpret_cast<Lds<CAP>*>(ws + (size_t)w * sizeof(Lds<CAP>));
+    Wave<CAP, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap);
+    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+    const uint32_t a = min(r1, r0 + op_lo);
+    const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
+    if (a >= b) return;
+    wv.load(g, d);
+    for (uint32_t i = a; i < b; i++) {
+        if (st.err) break;
+        const mt_op_rec op = ops[i];
+        wv.apply(op, payload);
+    }
+    wv.store(g, d);
+}
+
 }  // namespace mt
 
 // ------------------------------------------------------------------------------------------
@@ -1168,8 +1208,33 @@ extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_
     return launch_any(cap_class, true, g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga, stream);
 }
 
+// classes above 2048 segments (workspace: n_docs * mt_lds_bytes(cap_class) bytes of HBM)
+extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                          const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                          uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
+                                          hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    dim3 grid(n_docs), block(64);
+#define MT_LAUNCH_BIG(CAPV)                                                                                  \
+    case CAPV:                                                                                               \
+        hipLaunchKernelGGL((mt::apply_kernel_g<CAPV>), grid, block, 0, stream, *g, ops, payload, row_ptr,     \
+                           doc_ids, n_docs, op_lo, op_cnt, ws);                                              \
+        return hipGetLastError();
+    switch (cap_class) {
+        MT_LAUNCH_BIG(4096)
+        MT_LAUNCH_BIG(8192)
+        MT_LAUNCH_BIG(16384)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef MT_LAUNCH_BIG
+}
+
 extern "C" size_t mt_lds_bytes(int cap_class) {
     switch (cap_class) {
+        case 4096: return sizeof(mt::Lds<4096>);
+        case 8192: return sizeof(mt::Lds<8192>);
+        case 16384: return sizeof(mt::Lds<16384>);
         case 128: return sizeof(mt::Lds<128>);
         case 256: return sizeof(mt::Lds<256>);
         case 512: return sizeof(mt::Lds<512>);

@@ -26,13 +26,18 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
+extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                          const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                          uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
+                                          hipStream_t stream);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
                                      const mt_load_seg* segs, const uint8_t* text, const int32_t* min_seq,
                                      const int32_t* cur_seq, hipStream_t st);
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
-                                    uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
-                                    uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st);
+                                    uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
+                                    uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
+                                    hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
@@ -44,11 +49,16 @@ extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_
                                     uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 
 namespace {
-const int32_t kClasses[] = {128, 256, 512, 768, 1024, 2048};
-constexpr int kNumClasses = 6;
+// register engine <= 1024, LDS engine 2048, the LDS engine's HBM-workspace form above (only the
+// classes with CAP <= the engine's seg_capacity are used: mt_engine::n_classes)
+const int32_t kClasses[] = {128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384};
+constexpr int kNumClasses = 9;
+constexpr int kLdsClasses = 6;   // classes an LDS-resident kernel serves (the generator's)
+constexpr int kMaxSegCap = 16384;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
-const int32_t kClassParams[kNumClasses * 4] = {128,  64,  24,  128, 256,  128, 40,  192, 512,  256,  72,  320,
-                                               768,  384, 104, 448, 1024, 512, 136, 576, 2048, 1024, 264, 1088};
+const int32_t kClassParams[kNumClasses * 4] = {128,  64,   24,   128,  256,  128,  40,   192,  512,   256,  72,   320,
+                                               768,  384,  104,  448,  1024, 512,  136,  576,  2048,  1024, 264,  1088,
+                                               4096, 2048, 520,  2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256};
 // the LDS engine has no 768 instantiation: its 1024 kernel serves that class
 int lds_cap(int cap) { return cap == 768 ? 1024 : cap; }
 }  // namespace
@@ -85,6 +95,10 @@ struct mt_engine {
     // register-resident engine (mt_apply_reg.hip) for classes up to kRegMaxCap segments; the
     // LDS engine (mt_apply.hip) above that, or everywhere with MTGPU_ENGINE=lds
     bool use_reg = true;
+    int n_classes = kLdsClasses;   // classes with CAP <= seg_capacity
+    int first_lds = 5;             // first class not served by the register engine
+    uint8_t* ws = nullptr;         // HBM workspace of the classes above 2048 segments
+    size_t ws_bytes = 0;
     // the capacity classes of one tick touch disjoint documents: each runs on its own stream
     // (fork/join around the tick) so the small classes and every class's tail overlap;
     // MTGPU_SERIAL=1 keeps them on the engine stream, one after another
@@ -120,15 +134,17 @@ const char* mt_version(void) { return "libmtgpu 0.1 (gfx950)"; }
 mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     if (!cfg || !out || cfg->max_docs == 0) return MT_ERR_ARG;
     // the register / LDS classes reach 2048 slots and read whole rows of that size
-    if (cfg->seg_capacity != 0 && cfg->seg_capacity < 2048) return MT_ERR_ARG;
+    if (cfg->seg_capacity != 0 && (cfg->seg_capacity < 2048 || cfg->seg_capacity > (uint32_t)kMaxSegCap))
+        return MT_ERR_ARG;
     if (cfg->text_capacity > MT_MAX_TEXTCAP) return MT_ERR_ARG;  // li packs len into 20 bits (mt_apply_reg.hip)
     HIP_OK(hipSetDevice(cfg->device));
     auto* e = new mt_engine();
     e->cfg = *cfg;
     if (e->cfg.seg_capacity == 0) e->cfg.seg_capacity = 2048;
     if (e->cfg.text_capacity == 0) e->cfg.text_capacity = 64 * 1024;
-    if (e->cfg.heap_capacity == 0) e->cfg.heap_capacity = 1088;
-    e->cfg.seg_capacity = std::min<uint32_t>(e->cfg.seg_capacity, 2048);
+    if (e->cfg.heap_capacity == 0) e->cfg.heap_capacity = std::max<uint32_t>(1088, e->cfg.seg_capacity / 2 + 64);
+    e->n_classes = 0;
+    while (e->n_classes < kNumClasses && kClasses[e->n_classes] <= (int32_t)e->cfg.seg_capacity) e->n_classes++;
     mt_gstate& g = e->g;
     const size_t D = cfg->max_docs;
     g.segcap = e->cfg.seg_capacity;
@@ -160,6 +176,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         const char* v = getenv("MTGPU_ENGINE");
         // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
         e->use_reg = !(v && strcmp(v, "lds") == 0) && e->cfg.text_capacity <= 65536;
+        e->first_lds = e->use_reg ? 5 : 0;
         const char* sv = getenv("MTGPU_SERIAL");
         e->concurrent = !(sv && strcmp(sv, "1") == 0);
     }
@@ -183,6 +200,7 @@ mt_status mt_engine_destroy(mt_engine* e) {
     hipSetDevice(e->cfg.device);
     if (e->stream) hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) hipFree(p);
+    if (e->ws) (void)hipFree(e->ws);
     if (e->h_counts) hipHostFree(e->h_counts);
     for (auto ev : e->kev) (void)hipEventDestroy(ev);
     if (e->ev0) hipEventDestroy(e->ev0);
@@ -345,11 +363,26 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
         HIP_OK(hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream));
-        HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
-                             b->ops, e->d_acc, e->stream));
+        HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, e->n_classes, e->first_lds,
+                             e->d_counts, e->d_ids, b->ops, e->d_acc, e->stream));
         HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
+        // the classes above 2048 segments keep each document's structure in an HBM workspace
+        // (one region per class: their kernels may run concurrently)
+        size_t ws_off[kNumClasses] = {}, need = 0;
+        for (int c = kLdsClasses; c < e->n_classes; c++) {
+            ws_off[c] = need;
+            need += (size_t)e->h_counts[c] * mt_lds_bytes(kClasses[c]);
+        }
+        if (need > e->ws_bytes) {
+            HIP_OK(hipDeviceSynchronize());
+            if (e->ws) HIP_OK(hipFree(e->ws));
+            e->ws = nullptr;
+            e->ws_bytes = 0;
+            if (hipMalloc(&e->ws, need) != hipSuccess) return MT_ERR_NOMEM;
+            e->ws_bytes = need;
+        }
         if (e->concurrent) HIP_OK(hipEventRecord(e->fork_ev, e->stream));
         bool joined[kNumClasses] = {};
         for (int c = 0; c < kNumClasses; c++) {
@@ -370,6 +403,9 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             if (e->use_reg && kClasses[c] <= kRegMaxCap)
                 HIP_OK(mt_launch_apply_reg(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
                                            e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
+            else if (c >= kLdsClasses)
+                HIP_OK(mt_launch_apply_big(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                           e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, e->ws + ws_off[c], st));
             else
                 HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
                                        e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
@@ -454,8 +490,8 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
     for (uint32_t lo = 0; r == hipSuccess && lo < per; lo += tick) {
         r = hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream);
         if (r == hipSuccess)
-            r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, kNumClasses, e->d_counts, e->d_ids,
-                              nullptr, nullptr, e->stream);
+            r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, std::min(e->n_classes, kLdsClasses), 0,
+                              e->d_counts, e->d_ids, nullptr, nullptr, e->stream);
         if (r == hipSuccess)
             r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                e->stream);
@@ -588,6 +624,8 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
     char tmp[96];
     if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)
         snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel<%u>", capacity / 64);
+    else if (capacity > 2048)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u>", capacity);
     else
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)capacity));
     const size_t n = std::min<size_t>(cap - 1, strlen(tmp));

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // last class (the LDS engine, 64-client overlap sets).  Binning is wave-aggregated: one atomic
 // per (wave, class).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
-                              uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes,
+                              uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
                               uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
                               const mt_op_rec* __restrict__ ops, unsigned long long* __restrict__ acc) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -197,7 +197,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
             c = n_classes - 1;
-            for (int k = 0; k < n_classes && !wide && !lds_only; k++) {
+            // (wide documents and snapshot appends start at the first class the LDS engine serves)
+            for (int k = (wide || lds_only) ? first_lds : 0; k < n_classes; k++) {
                 const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
                           h = classes[4 * k + 3];
                 if (sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb &&
@@ -310,10 +311,11 @@ extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint3
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
-                                    uint32_t op_cnt, const int32_t* classes, int n_classes, uint32_t* counts,
-                                    uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc, hipStream_t st) {
+                                    uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
+                                    uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
+                                    hipStream_t st) {
     hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
-                       classes, n_classes, counts, ids, ops, acc);
+                       classes, n_classes, first_lds, counts, ids, ops, acc);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st) {

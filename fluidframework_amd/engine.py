@@ -147,7 +147,7 @@ class DeviceBatch:
 
 
 class MergeEngine:
-    def __init__(self, n_docs, device=0, seg_capacity=2048, text_capacity=64 * 1024, heap_capacity=1088,
+    def __init__(self, n_docs, device=0, seg_capacity=2048, text_capacity=64 * 1024, heap_capacity=0,
                  ops_per_launch=0):
         cfg = _Cfg(device, n_docs, seg_capacity, text_capacity, heap_capacity, ops_per_launch)
         self.h = ctypes.c_void_p()

@@ -1,0 +1,58 @@
+"""Documents beyond the LDS-resident classes (the reference's B-tree is unbounded,
+mergeTree.ts:330-334): an engine created with seg_capacity up to 16384 serves the 4096 / 8192 /
+16384-segment classes with the LDS engine's HBM-workspace form (mt::apply_kernel_g), and text
+arenas above 64 KiB with the LDS engine.  Documents grow through every class inside one replay;
+bit-exact against the CPU oracle (state and checksum)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# inserts dominate and almost every insert carries its own property value, so zamboni can seldom
+# append neighbours: segment counts grow with the op count
+GROW = dict(n_clients=8, max_lag=8, n_keys=2, n_values=250, p_insert=0.92, p_remove=0.04, p_overlap=0.3,
+            p_null=0.05, p_rewrite=0.02, p_insert_props=1.0)
+
+
+def _check(eng, o, n, docs):
+    got, want = eng.checksums(), o.checksums()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (bad[:8], [eng.error(int(d)) for d in bad[:4]])
+    for d in docs:
+        assert eng.error(d) == (0, 0), eng.error(d)
+        assert eng.state(d) == o.state(d), d
+
+
+def test_documents_grow_past_8k_segments(oracle_lib):
+    """4 documents x 12,000 ops (97 % inserts): three end above 8,192 segments (the 16384 class,
+    up to ~13 K segments and ~100 KB of text: a 512 KiB arena, every class on the LDS engine)."""
+    from fluidframework_amd.engine import MergeEngine
+    n = 4
+    cfg = dict(GROW, p_insert=0.97, p_remove=0.02)
+    batch = oracle_lib.generate(n, seed=4242, ops_per_doc=12000, **cfg)
+    o = oracle_lib.Oracle(n).apply(batch, threads=4)
+    segs = [o.nsegs(d) for d in range(n)]
+    assert sum(1 for x in segs if x > 8192) >= 2, segs
+    eng = MergeEngine(n, seg_capacity=16384, text_capacity=512 * 1024, ops_per_launch=32)
+    eng.apply(batch)
+    assert list(eng.seg_counts()) == segs
+    _check(eng, o, n, range(n))
+    names = {c: eng.class_kernel(c) for c in (2048, 4096, 16384)}
+    assert names[16384] == 'mt::apply_kernel_g<16384>', names
+
+
+def test_register_engine_hands_over_to_the_big_classes(oracle_lib):
+    """64 KiB arenas keep the register engine for the small classes; documents grow from it
+    through the 2048 LDS class into the 4096 / 8192 HBM-workspace classes within one replay."""
+    from fluidframework_amd.engine import MergeEngine
+    n = 24
+    batch = oracle_lib.generate(n, seed=99, ops_per_doc=3400, **GROW)
+    o = oracle_lib.Oracle(n).apply(batch, threads=8)
+    segs = [o.nsegs(d) for d in range(n)]
+    assert max(segs) > 2048, segs
+    eng = MergeEngine(n, seg_capacity=8192, text_capacity=64 * 1024, ops_per_launch=32)
+    assert eng.class_kernel(1024).startswith('mtr::reg_apply_kernel')
+    eng.apply(batch)
+    used = {cap: k for cap, ms, k, b in eng.last_class_stats() if k}
+    assert 4096 in used and 1024 in used, used
+    _check(eng, o, n, range(0, n, 5))

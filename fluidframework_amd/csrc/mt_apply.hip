@@ -468,7 +468,10 @@ struct Wave {
                 bool app = false;
                 if (prev >= 0) {
                     const uint32_t pl = s.len[prev], ql = s.len[sl];
-                    app = !(s.flags[prev] & MT_SF_NL) && (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
+                    // TextSegment.canAppend: two text segments (a Marker never appends, nor is
+                    // appended to: Marker.canAppend, TextSegment.is, mergeTree.ts:793; textSegment.ts:63-68)
+                    app = !((s.flags[prev] | f) & MT_SF_MARKER) && !(s.flags[prev] & MT_SF_NL) &&
+                          (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
                           props_match(s.flags[prev], s.props[prev], f, s.props[sl]) && ql > 0;
                 }
                 if (app) {
@@ -691,7 +694,10 @@ struct Wave {
                 s.ovl[t] = 0;
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
-                uint8_t f = (pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0) | (lrm ? MT_SF_REMOVED : 0);
+                // a Marker (MT_F_MARKER): length 1, its arena byte is its ReferenceType
+                uint8_t f = (op.flags & MT_F_MARKER) ? MT_SF_MARKER
+                                                     : ((pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0));
+                f |= lrm ? MT_SF_REMOVED : 0;
                 uint64_t p = 0;
                 if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
                     f |= MT_SF_PDEF;
@@ -792,7 +798,7 @@ struct Wave {
     }
 
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
-        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
         if (op.type > MT_OP_LOAD) return fail(MT_DERR_BAD_OP, S);
         // MT_OP_LOAD: MergeTree.insertSegments from SnapshotLoader.loadBody (snapshotLoader.ts:192-224),
@@ -874,10 +880,16 @@ struct Wave {
         uint8_t pr[4] = {0, 0, 0, 0};
         if (type == 0) {
             rec.pos1 = (int32_t)mt_ru(key, i, MT_R_POS1, 0, (uint32_t)L);
-            const uint32_t tl = mt_gen_text_len(key, i);
+            const bool mk = mt_gen_is_marker(cfg, key, i);
+            const uint32_t tl = mk ? 1u : mt_gen_text_len(key, i);
             if (pay_off + tl + 2 <= paycap) {
-                for (uint32_t t = lane; t < tl; t += 64) pay[t] = mt_gen_char(key, i, t);
+                if (mk) {
+                    if (lane == 0) pay[0] = mt_gen_ref_type(key, i);
+                } else {
+                    for (uint32_t t = lane; t < tl; t += 64) pay[t] = mt_gen_char(key, i, t);
+                }
             }
+            if (mk) rec.flags |= MT_F_MARKER;
             n = tl;
             if (cfg.n_keys && mt_rp(key, i, MT_R_IPROPS, cfg.p_insert_props)) {
                 rec.flags |= MT_F_PROPS;

@@ -45,6 +45,7 @@ constexpr uint32_t F_RM = (uint32_t)MT_SF_REMOVED << 16;
 constexpr uint32_t F_PDEF = (uint32_t)MT_SF_PDEF << 16;
 constexpr uint32_t F_NL = (uint32_t)MT_SF_NL << 16;
 constexpr uint32_t F_HASNL = (uint32_t)MT_SF_HASNL << 16;
+constexpr uint32_t F_MARKER = (uint32_t)MT_SF_MARKER << 16;
 constexpr uint32_t kEmptyCf = 0xFFu;     // padding: client 255 never matches (and the slot is dead)
 constexpr uint16_t kDead = 0xFFFFu;
 
@@ -754,7 +755,9 @@ struct RWave {
         const uint32_t pcf = (uint32_t)shr1((int)vcf, 0);
         const uint32_t pprl = (uint32_t)shr1((int)(uint32_t)vpr, 0);
         const uint32_t pprh = (uint32_t)shr1((int)(uint32_t)(vpr >> 32), 0);
-        const bool a0 = elig && pelig && !(pcf & F_NL) && ((pcf ^ vcf) & F_PDEF) == 0 && pprl == (uint32_t)vpr &&
+        // (canAppend needs two text segments: a Marker neither appends nor is appended to,
+        // mergeTree.ts:793, textSegment.ts:63-68)
+        const bool a0 = elig && pelig && !((pcf | vcf) & F_MARKER) && !(pcf & F_NL) && ((pcf ^ vcf) & F_PDEF) == 0 && pprl == (uint32_t)vpr &&
                         pprh == (uint32_t)(vpr >> 32);
         const uint32_t a0m = (uint32_t)__ballot(a0);
         uint32_t appm = a0m;
@@ -990,7 +993,9 @@ struct RWave {
             hasnl = hasnl || __ballot(i < tlen && c == '\n') != 0;
         }
         dirty = true;
-        uint32_t fl = (pbyte(pay, tlen - 1) == '\n' ? F_NL : 0u) | (hasnl ? F_HASNL : 0u);
+        // a Marker (MT_F_MARKER): length 1, its one arena byte is its ReferenceType, no newline
+        uint32_t fl = (op.flags & MT_F_MARKER) ? F_MARKER
+                                               : ((pbyte(pay, tlen - 1) == '\n' ? F_NL : 0u) | (hasnl ? F_HASNL : 0u));
         uint64_t p = 0;
         if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
             fl |= F_PDEF;
@@ -1061,7 +1066,7 @@ struct RWave {
     // (client.ts:821-828, MergeTree.setMinSeq mergeTree.ts:1718-1736).  Every register-heavy
     // routine has exactly one call site.
     MT_DEV void apply(const mt_op_rec op, const uint8_t* payload) {
-        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
         if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
         const uint8_t* pay = payload + op.payload_off;
@@ -1285,7 +1290,7 @@ struct RWave {
                 for (int j = 0; j < K; j++) {
                     const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
                     const bool in = i0 + j < n;
-                    cf[j] = in ? (bc[j] | (br[j] << 8) | ((bf[j] & 0xFu) << 16)) : kEmptyCf;
+                    cf[j] = in ? (bc[j] | (br[j] << 8) | ((bf[j] & 0x1Fu) << 16)) : kEmptyCf;
                     const uint32_t bit = in ? (1u << j) : 0u;
                     lvm |= bit;
                     bsm |= (mk & 1) ? bit : 0u;
@@ -1355,7 +1360,7 @@ struct RWave {
         store_field(cf, lb, pbase, nn, [&](int i, uint32_t v) {
             g.client[so + i] = (uint8_t)(v & 0xFFu);
             g.rclient[so + i] = (uint8_t)((v >> 8) & 0xFFu);
-            g.flags[so + i] = (uint8_t)((v >> 16) & 0xFu);
+            g.flags[so + i] = (uint8_t)((v >> 16) & 0x1Fu);
         });
         store_field(li, lb, pbase, nn, [&](int i, uint32_t v) {
             const uint32_t id = id_of(v);

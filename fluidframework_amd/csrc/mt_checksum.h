@@ -7,6 +7,8 @@
 
 MT_HD static inline uint64_t mt_fnv1a_step(uint64_t h, uint8_t c) { return (h ^ c) * 0x100000001B3ull; }
 #define MT_FNV_INIT 0xCBF29CE484222325ull
+// a Marker's "text hash": the fnv1a of its one ReferenceType byte, xor this tag
+#define MT_MARKER_TAG 0x4D41524B45520000ull
 
 MT_HD static inline uint64_t mt_seg_hash(uint64_t idx, uint64_t text_hash, int32_t seq, int32_t client, int32_t rseq,
                                          int32_t rclient, uint64_t overlap, uint64_t props_lo, uint32_t props_defined) {

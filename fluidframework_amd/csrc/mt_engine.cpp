@@ -743,7 +743,10 @@ std::string state_json(const HostDoc& h) {
     for (int i = 0; i < h.sc.nseg; i++) {
         if (i) o += ',';
         o += '[';
-        json_str(o, h.text.data() + h.toff[i], h.len[i]);
+        if (h.flags[i] & MT_SF_MARKER)  // a Marker: {"marker": refType}
+            o += "{\"marker\":" + std::to_string(h.text[h.toff[i]]) + "}";
+        else
+            json_str(o, h.text.data() + h.toff[i], h.len[i]);
         const bool rm = h.flags[i] & MT_SF_REMOVED;
         o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(mt_canon_client(h.client[i])) + ',';
         o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient[i]) : "-1") + ",[";
@@ -828,9 +831,17 @@ void props_json(std::string& o, uint64_t props) {
     o += '}';
 }
 
-// TextSegment.toJSONObject (textSegment.ts:47-53) of `text` with the props of segment i
+// TextSegment.toJSONObject (textSegment.ts:47-53) of `text` with the props of segment i;
+// Marker.toJSONObject (mergeTree.ts:652-656) for a marker: {marker: {refType}, props?}
 void seg_json(std::string& o, const HostDoc& h, int i, const std::string& text) {
-    if (h.flags[i] & MT_SF_PDEF) {
+    if (h.flags[i] & MT_SF_MARKER) {
+        o += "{\"marker\":{\"refType\":" + std::to_string(h.text[h.toff[i]]) + "}";
+        if (h.flags[i] & MT_SF_PDEF) {
+            o += ",\"props\":";
+            props_json(o, h.props[i]);
+        }
+        o += '}';
+    } else if (h.flags[i] & MT_SF_PDEF) {
         o += "{\"text\":";
         js_str(o, (const uint8_t*)text.data(), text.size());
         o += ",\"props\":";
@@ -994,7 +1005,8 @@ mt_status mt_get_text(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint6
     if (st) return st;
     std::string t;
     for (int i = 0; i < h.sc.nseg; i++)
-        if (!(h.flags[i] & MT_SF_REMOVED)) t.append((const char*)h.text.data() + h.toff[i], h.len[i]);
+        if (!(h.flags[i] & (MT_SF_REMOVED | MT_SF_MARKER)))  // gatherText: text segments only
+            t.append((const char*)h.text.data() + h.toff[i], h.len[i]);
     return copy_out(t, buf, cap, len);
 }
 

@@ -86,8 +86,10 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
                 nl = nl || c == '\n';
             }
             const bool rm = sg.rseq >= 0;
-            uint8_t fl = (uint8_t)((rm ? MT_SF_REMOVED : 0u) | (sg.flags & MT_SF_PDEF) | (nl ? MT_SF_HASNL : 0u));
-            if (l && text[sg.text_off + l - 1] == '\n') fl |= MT_SF_NL;
+            const bool mk = sg.flags & MT_SF_MARKER;  // a Marker spec: one byte, its ReferenceType
+            uint8_t fl = (uint8_t)((rm ? MT_SF_REMOVED : 0u) | (sg.flags & (MT_SF_PDEF | MT_SF_MARKER)) |
+                                   (nl && !mk ? MT_SF_HASNL : 0u));
+            if (!mk && l && text[sg.text_off + l - 1] == '\n') fl |= MT_SF_NL;
             g.seq[so + i] = sg.seq;
             g.rseq[so + i] = rm ? sg.rseq : 0;
             g.len[so + i] = l;
@@ -249,7 +251,7 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const mt_doc_scalars sc = g.sc[d];
     if (sc.win_op < 0 || (sc.err != MT_DERR_SEQ_ORDER && sc.err != MT_DERR_MSN_ORDER)) return;
     const mt_op_rec o = ops[sc.win_op];
-    const int np = o.flags >> MT_F_NPAIRS_SHIFT;
+    const int np = MT_OP_NPAIRS(o.flags);
     if (o.seq != sc.err_seq || o.type != MT_OP_INSERT || (int)o.payload_len - 2 * np <= 0) return;
     const size_t so = (size_t)d * g.segcap;
     const int32_t R = o.ref_seq;
@@ -278,6 +280,7 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
         const uint32_t t0 = g.toff[so + i], tl = g.len[so + i];
         for (uint32_t q = 0; q < tl; q++) h = mt_fnv1a_step(h, text[t0 + q]);
         const uint8_t f = g.flags[so + i];
+        if (f & MT_SF_MARKER) h ^= MT_MARKER_TAG;  // a Marker: its ReferenceType byte, tagged
         const bool rm = f & MT_SF_REMOVED;
         seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(g.client[so + i]), rm ? g.rseq[so + i] : -1,
                                rm ? (int32_t)g.rclient[so + i] : -1, g.ovl[so + i], g.props[so + i],
@@ -389,7 +392,8 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
             const uint32_t fj = (uint32_t)__builtin_amdgcn_readlane((int)fl, j);
             const uint64_t pj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pr, j) |
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), j) << 32);
-            if (have && !(pfl & MT_SF_NL) && (plen <= 256u || lj <= 256u) && ((pfl ^ fj) & MT_SF_PDEF) == 0 &&
+            if (have && !((pfl | fj) & MT_SF_MARKER) && !(pfl & MT_SF_NL) && (plen <= 256u || lj <= 256u) &&
+                ((pfl ^ fj) & MT_SF_PDEF) == 0 &&
                 pprops == pj) {
                 pc = base + j - ps + 1;  // span from the run's first segment (elided ones inside it skipped by the reader)
                 plen += lj;

@@ -25,7 +25,8 @@ enum {
     MT_R_CLIENT = 0, MT_R_LAG = 1, MT_R_STALL = 2, MT_R_TYPE = 3, MT_R_POS1 = 4, MT_R_BIGLEN = 5,
     MT_R_LEN = 6, MT_R_AIM = 7, MT_R_AIMPICK = 8, MT_R_AIMPRE = 9, MT_R_AIMPOST = 10, MT_R_NKEYS = 11,
     MT_R_KEY0 = 12, MT_R_VAL0 = 13, MT_R_NULL0 = 14, MT_R_VAL1 = 15, MT_R_NULL1 = 16, MT_R_REWRITE = 17,
-    MT_R_IPROPS = 18, MT_R_IKEY = 19, MT_R_IVAL = 20, MT_R_TBIG = 21, MT_R_TLEN = 22, MT_R_CHAR0 = 64
+    MT_R_IPROPS = 18, MT_R_IKEY = 19, MT_R_IVAL = 20, MT_R_TBIG = 21, MT_R_TLEN = 22, MT_R_MARKER = 23,
+    MT_R_MREF = 24, MT_R_CHAR0 = 64
 };
 
 MT_HD static inline uint64_t mt_mix64(uint64_t z) {  /* splitmix64 */
@@ -49,6 +50,14 @@ MT_HD static inline int mt_rp(uint64_t key, uint32_t op, uint32_t slot, uint32_t
 /* text of an insert: length 1..16 (300 with p = 1/256); chars [a-z0-9], '\n' with p = 1/64 */
 MT_HD static inline uint32_t mt_gen_text_len(uint64_t key, uint32_t op) {
     return (mto_rng(key, op, MT_R_TBIG) & 255) == 0 ? 300u : mt_ru(key, op, MT_R_TLEN, 1, 16);
+}
+/* a marker insert (p_marker): its ReferenceType, Tile / NestBegin / NestEnd (ops.ts:6-16) */
+MT_HD static inline int mt_gen_is_marker(const mt_synth_cfg& cfg, uint64_t key, uint32_t op) {
+    return cfg.p_marker && (uint32_t)mto_rng(key, op, MT_R_MARKER) < cfg.p_marker;
+}
+MT_HD static inline uint8_t mt_gen_ref_type(uint64_t key, uint32_t op) {
+    const uint32_t k = (uint32_t)(mto_rng(key, op, MT_R_MREF) >> 40) % 3u;
+    return (uint8_t)(k == 0 ? 1u : (k == 1 ? 2u : 4u));
 }
 MT_HD static inline uint8_t mt_gen_char(uint64_t key, uint32_t op, uint32_t t) {
     uint64_t r = mto_rng(key, op, MT_R_CHAR0 + t);
@@ -92,8 +101,13 @@ static inline uint32_t mto_gen_op(const mt_synth_cfg& cfg, uint64_t key, uint32_
     uint32_t n = 0, np = 0;
     if (type == 0) {
         rec.pos1 = (int32_t)mt_ru(key, i, MT_R_POS1, 0, (uint32_t)L);
-        uint32_t tl = mt_gen_text_len(key, i);
-        for (uint32_t t = 0; t < tl; t++) buf[n++] = mt_gen_char(key, i, t);
+        if (mt_gen_is_marker(cfg, key, i)) {
+            rec.flags |= MT_F_MARKER;
+            buf[n++] = mt_gen_ref_type(key, i);
+        } else {
+            uint32_t tl = mt_gen_text_len(key, i);
+            for (uint32_t t = 0; t < tl; t++) buf[n++] = mt_gen_char(key, i, t);
+        }
         if (cfg.n_keys && mt_rp(key, i, MT_R_IPROPS, cfg.p_insert_props)) {
             rec.flags |= 2; /* MT_F_PROPS */
             buf[n++] = (uint8_t)mt_ru(key, i, MT_R_IKEY, 0, cfg.n_keys - 1);

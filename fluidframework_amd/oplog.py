@@ -17,7 +17,13 @@ assert OP_DTYPE.itemsize == 32
 
 INSERT, REMOVE, ANNOTATE, NOOP = 0, 1, 2, 3
 F_REWRITE, F_PROPS, F_GROUP_MORE = 1, 2, 4
-NPAIRS_SHIFT = 3
+F_MARKER = 128          # insert of a Marker: the one text byte is its ReferenceType (ops.ts:6-16)
+NPAIRS_SHIFT = 3        # bits 3..6: property pairs in the payload
+REF_TILE, REF_NEST_BEGIN, REF_NEST_END = 1, 2, 4
+
+
+def npairs(flags):
+    return (int(flags) >> NPAIRS_SHIFT) & 15
 
 MAGIC = b'MTLOG001'
 
@@ -108,12 +114,14 @@ class OpBatch:
 
 
 def synth_cfg_array(seed=1, n_clients=8, ops_per_doc=1024, max_lag=8, stall_ops=0, n_keys=0, n_values=16,
-                    p_insert=0.6, p_remove=0.4, p_overlap=0.0, p_null=0.05, p_rewrite=0.0, p_insert_props=0.0):
+                    p_insert=0.6, p_remove=0.4, p_overlap=0.0, p_null=0.05, p_rewrite=0.0, p_insert_props=0.0,
+                    p_marker=0.0):
     """mt_synth_cfg (fluidframework_amd/csrc/mt_synth.h) as raw little-endian bytes."""
     def fx(p):
         return min(int(round(p * 4294967296.0)), 0xFFFFFFFF)
-    return struct.pack('<13I', seed, n_clients, ops_per_doc, max_lag, stall_ops, n_keys, n_values,
-                       fx(p_insert), fx(p_remove), fx(p_overlap), fx(p_null), fx(p_rewrite), fx(p_insert_props))
+    return struct.pack('<14I', seed, n_clients, ops_per_doc, max_lag, stall_ops, n_keys, n_values,
+                       fx(p_insert), fx(p_remove), fx(p_overlap), fx(p_null), fx(p_rewrite), fx(p_insert_props),
+                       fx(p_marker))
 
 
 # The BASELINE.json configurations (SURVEY.md §8d), as synthetic-workload parameters.

@@ -16,8 +16,9 @@ Segment specs (IJSONSegment / IJSONSegmentWithMergeInfo, snapshotChunks.ts:60-73
 SnapshotLoader.specToSegment (snapshotLoader.ts:85-117) does: without merge info a segment is
 (UniversalSequenceNumber 0, NonCollabClient); with it, its seq / client / removedSeq / removedClient.
 Long client ids and property keys / values are interned per document by the caller's interners.
-Markers are not part of the device representation and are refused (ValueError), like text beyond
-U+00FF (one byte per UTF-16 code unit, textSegment.ts:45).
+Marker specs ({marker: {refType}, props}, Marker.toJSONObject mergeTree.ts:652-656) load as markers
+(one byte, the ReferenceType, up to 255).  Text beyond U+00FF is refused (ValueError): one byte per
+UTF-16 code unit (textSegment.ts:45).
 """
 import ctypes
 import json
@@ -25,12 +26,13 @@ import json
 import numpy as np
 
 from .engine import _check, _ptr, lib
-from .oplog import F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OpBatch
+from .oplog import F_MARKER, F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OpBatch
 
 MT_OP_LOAD = 4
 NONCOLLAB = 0xFE            # MT_CLIENT_NONCOLLAB: NonCollabClient (constants.ts:15)
 UNIVERSAL_SEQ = 0           # UniversalSequenceNumber (constants.ts:11)
 SF_PDEF = 2
+SF_MARKER = 16
 
 LOAD_SEG_DTYPE = np.dtype([('seq', '<i4'), ('rseq', '<i4'), ('client', 'u1'), ('rclient', 'u1'), ('flags', 'u1'),
                            ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('pad2', '<u4'),
@@ -127,15 +129,22 @@ class LoadedDoc:
 
 
 def _spec(spec, it):
-    """specToSegment (snapshotLoader.ts:85-117) -> (text bytes, seq, client, rseq, rclient, pdef, props)"""
+    """specToSegment (snapshotLoader.ts:85-117) -> (text bytes, seq, client, rseq, rclient, pdef, props,
+    marker)"""
     merge = isinstance(spec, dict) and 'json' in spec
     js = spec['json'] if merge else spec
+    marker = False
     if isinstance(js, str):
         text, props = js, None
     elif isinstance(js, dict) and 'text' in js:
         text, props = js['text'], js.get('props')
+    elif isinstance(js, dict) and 'marker' in js:    # Marker.fromJSONObject (mergeTree.ts:658-665)
+        rt = js['marker'].get('refType', 0)
+        if not 0 <= rt <= 255:
+            raise ValueError(f'marker refType {rt} is not device-representable')
+        text, props, marker = chr(rt), js.get('props'), True
     else:
-        raise ValueError(f'only text segments are device-representable (got {json.dumps(js)[:80]})')
+        raise ValueError(f'not a text or marker segment spec: {json.dumps(js)[:80]}')
     try:
         tb = text.encode('latin-1')
     except UnicodeEncodeError:
@@ -153,7 +162,7 @@ def _spec(spec, it):
         rclient = it.client(spec['removedClient']) if spec.get('removedClient') is not None else 0
     else:
         seq, client, rseq, rclient = UNIVERSAL_SEQ, NONCOLLAB, -1, 0
-    return tb, seq, client, rseq, rclient, props is not None, pv
+    return tb, seq, client, rseq, rclient, props is not None, pv, marker
 
 
 def build_load(docs, interners=None):
@@ -165,8 +174,9 @@ def build_load(docs, interners=None):
     for doc, it in zip(docs, interners):
         local = 0  # root.cachedLength: the local (non-removed) length
         for spec in doc.header:
-            tb, seq, client, rseq, rclient, pdef, pv = _spec(spec, it)
-            segs.append((seq, rseq, client, rclient, SF_PDEF if pdef else 0, 0, len(text), len(tb), 0, pv))
+            tb, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
+            segs.append((seq, rseq, client, rclient, (SF_PDEF if pdef else 0) | (SF_MARKER if mk else 0), 0,
+                         len(text), len(tb), 0, pv))
             text += tb
             local += 0 if rseq >= 0 else len(tb)
         row_ptr.append(len(segs))
@@ -175,7 +185,7 @@ def build_load(docs, interners=None):
         # (mergeTree.ts:2219); any other segment is its own insertSegments call
         batch_pos = None
         for spec in doc.body:
-            tb, seq, client, rseq, rclient, pdef, pv = _spec(spec, it)
+            tb, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
             batched = client == NONCOLLAB and seq == UNIVERSAL_SEQ
             if batched:
                 pos = local if batch_pos is None else batch_pos
@@ -192,6 +202,8 @@ def build_load(docs, interners=None):
                     if v:
                         pairs += bytes([k, v])
                 flags = F_PROPS | ((len(pairs) // 2) << NPAIRS_SHIFT)
+            if mk:
+                flags |= F_MARKER
             data = tb + pairs
             recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8), MT_OP_LOAD, flags,
                          pos, rseq, len(payload), len(data)))

@@ -40,10 +40,15 @@ enum mt_op_type {
 enum mt_op_flags {
     MT_F_REWRITE = 1u << 0,    /* annotate with combiningOp {name:"rewrite"} (properties.ts:118-124) */
     MT_F_PROPS = 1u << 1,      /* insert spec carries a props object (TextSegment.make, textSegment.ts:24-30) */
-    MT_F_GROUP_MORE = 1u << 2  /* GROUP member: next record is the next member of the same message
+    MT_F_GROUP_MORE = 1u << 2, /* GROUP member: next record is the next member of the same message
                                   (client.ts:782-790); the window update waits for the last member */
+    MT_F_MARKER = 1u << 7      /* insert of a Marker (mergeTree.ts:630-798, IJSONMarkerSegment): the
+                                  payload's text part is one byte, its ReferenceType (ops.ts:6-16;
+                                  Simple/Tile/NestBegin/NestEnd/RangeBegin/RangeEnd/Slide/Stay); the
+                                  segment has length 1 and never appends (Marker.canAppend) */
 };
-#define MT_F_NPAIRS_SHIFT 3    /* bits 3..7: number of (key,value) property pairs in the payload */
+#define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload */
+#define MT_OP_NPAIRS(flags) (((flags) >> MT_F_NPAIRS_SHIFT) & 0xF)
 
 typedef struct mt_op_rec {
     int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */
@@ -125,7 +130,8 @@ typedef struct mt_load_seg {
     int32_t rseq;         /* spec.removedSeq; -1 = not removed                                      */
     uint8_t client;       /* short id of spec.client, or MT_CLIENT_NONCOLLAB                        */
     uint8_t rclient;      /* short id of spec.removedClient (when removed)                          */
-    uint8_t flags;        /* MT_SF_PDEF (from mt_state.h: 2) when the spec carries props             */
+    uint8_t flags;        /* MT_SF_PDEF (2) when the spec carries props, MT_SF_MARKER (16) for a
+                             Marker spec (text_len 1: its ReferenceType byte)  (mt_state.h)        */
     uint8_t pad;
     uint32_t text_off;    /* the segment's text in the batch's text bytes                           */
     uint32_t text_len;
@@ -222,6 +228,7 @@ typedef struct mt_synth_cfg {
     uint32_t p_null;         /* annotate value null = delete the key                         */
     uint32_t p_rewrite;      /* annotate with combiningOp "rewrite"                          */
     uint32_t p_insert_props; /* insert carries a props object                                */
+    uint32_t p_marker;       /* an insert is a Marker (refType Tile, NestBegin or NestEnd)    */
 } mt_synth_cfg;
 
 /* doc_id_base: global id of the engine's document 0 (a rank's shard of a multi-GPU job) */

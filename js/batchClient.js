@@ -15,7 +15,7 @@ const path = require("path");
 const native = require(path.join(__dirname, "mtgpu.node"));
 
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
-const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4;
+const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const MAX_CLIENTS = 64, MAX_KEYS = 8, MAX_VALUES = 255;
 const REC = 32;
 
@@ -162,7 +162,14 @@ class BatchClient {
             else if (op.seg && typeof op.seg === "object" && "text" in op.seg) {
                 text = op.seg.text;
                 if (op.seg.props) { r.flags |= F_PROPS; pairs = this._pairs(op.seg.props); }
-            } else throw new Error("BatchClient: only text segments are supported (markers: SURVEY §8f)");
+            } else if (op.seg && typeof op.seg === "object" && "marker" in op.seg) {
+                // Marker.fromJSONObject (mergeTree.ts:658-665): length 1, its ReferenceType as the one byte
+                const rt = op.seg.marker.refType;
+                if (!(Number.isInteger(rt) && rt >= 0 && rt <= 255)) throw new Error("BatchClient: marker refType out of range");
+                text = String.fromCharCode(rt);
+                r.flags |= F_MARKER;
+                if (op.seg.props) { r.flags |= F_PROPS; pairs = this._pairs(op.seg.props); }
+            } else throw new Error("BatchClient: only text and marker segments are supported");
             if (typeof text !== "string") throw new Error("BatchClient: segment text must be a string");
             // the device arena holds one byte per UTF-16 code unit, so lengths and positions equal the
             // reference's cachedLength = text.length (textSegment.ts:45) only up to U+00FF: anything

@@ -1,7 +1,8 @@
 "use strict";
 // mtlog.js -- read MTLOG op-log files (fluidframework_amd/oplog.py) as ISequencedDocumentMessage
 // objects (protocol.ts:132-172) carrying IMergeTreeOp contents (ops.ts:63-110).  Client long ids
-// are "c<id>" for record client <id>; property keys "k<id>", values the value ids.
+// are "c<id>" for record client <id>; property keys "k<id>", values the value ids.  A marker insert
+// (flags bit 7) carries its ReferenceType as the one text byte: seg = {marker: {refType}, props?}.
 const fs = require("fs");
 
 function loadLog(file) {
@@ -27,7 +28,7 @@ function readOp(log, i) {
 }
 
 function propsOf(log, r) {
-    const np = r.flags >> 3;
+    const np = (r.flags >> 3) & 15;
     const start = log.payOff + r.poff + r.plen - 2 * np;
     const props = {};
     for (let q = 0; q < np; q++) {
@@ -38,7 +39,12 @@ function propsOf(log, r) {
 }
 
 function toOp(log, r) {
-    const np = r.flags >> 3;
+    const np = (r.flags >> 3) & 15;
+    if (r.type === 0 && (r.flags & 128)) {
+        const seg = { marker: { refType: log.buf.readUInt8(log.payOff + r.poff) } };
+        if (r.flags & 2) seg.props = propsOf(log, r);
+        return { type: 0, pos1: r.pos1, seg };
+    }
     if (r.type === 0) {
         const text = log.buf.toString("latin1", log.payOff + r.poff, log.payOff + r.poff + r.plen - 2 * np);
         return { type: 0, pos1: r.pos1, seg: (r.flags & 2) ? { text, props: propsOf(log, r) } : text };

@@ -24,7 +24,7 @@ const { loadLog } = require("./mtlog.js");
 
 const MAX_NODES = 8, TEXT_GRANULARITY = 256, ZAMBONI_MAX = 2;
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, NOOP = 3;
-const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4;
+const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const SC_UNDEF = 0, SC_TRUE = 1, SC_FALSE = 2;
 const E_SEQ = 1, E_MSN = 2, E_INSERT = 3, E_LIMITS = 6, E_BADOP = 7;
 
@@ -33,6 +33,7 @@ class Seg {
         this.leaf = true; this.parent = undefined; this.text = text;
         this.seq = 0; this.client = 0; this.removed = false; this.rseq = 0; this.rclient = 0;
         this.overlap = 0n; this.props = undefined;  // undefined | array of value ids by key id
+        this.marker = false;  // a Marker (mergeTree.ts:630-798): text = its one refType character
     }
 }
 class Block {
@@ -90,7 +91,7 @@ class Doc {
         s.text = s.text.substring(0, pos);
         r.props = s.props === undefined ? undefined : s.props.slice();
         r.removed = s.removed; r.rseq = s.rseq; r.rclient = s.rclient; r.seq = s.seq; r.client = s.client;
-        r.overlap = s.overlap;
+        r.overlap = s.overlap; r.marker = s.marker;
         return r;
     }
     insertingWalk(b, pos, R, C, cand) {  // mergeTree.ts:2345-2474
@@ -161,7 +162,7 @@ class Doc {
                 if (s.rseq > this.minSeq) hold.push(s); else s.parent = undefined;
                 prev = undefined;
             } else if (s.seq <= this.minSeq) {
-                const app = prev && !prev.text.endsWith("\n") &&
+                const app = prev && !prev.marker && !s.marker && !prev.text.endsWith("\n") &&
                     (prev.text.length <= TEXT_GRANULARITY || s.text.length <= TEXT_GRANULARITY) &&
                     sameProps(prev, s) && s.text.length > 0;
                 if (app) {
@@ -250,7 +251,7 @@ class Doc {
                     s.props = [];
                     for (let q = 0; q < pairs.length; q += 2) s.props[pairs[q]] = pairs[q + 1];
                 }
-                s.seq = S; s.client = C;
+                s.seq = S; s.client = C; s.marker = (r.flags & F_MARKER) !== 0;
                 const sp = this.insertingWalk(this.root, r.pos1, R, C, s);
                 if (!s.parent) return this.fail(E_INSERT, S);
                 this.updateRoot(sp);
@@ -294,7 +295,8 @@ class Doc {
                     props = {};
                     n.props.forEach((v, k) => { if (v) props["k" + k] = v; });
                 }
-                segs.push([n.text, n.seq, n.client, n.removed ? n.rseq : -1, n.removed ? n.rclient : -1, ov, props]);
+                segs.push([n.marker ? { marker: n.text.charCodeAt(0) } : n.text, n.seq, n.client,
+                    n.removed ? n.rseq : -1, n.removed ? n.rclient : -1, ov, props]);
                 return;
             }
             for (const ch of n.children) walk(ch);
@@ -321,7 +323,7 @@ function records(log, d) {
             client: b.readUInt16LE(o + 12), type: b.readUInt8(o + 14), flags: b.readUInt8(o + 15),
             pos1: b.readInt32LE(o + 16), pos2: b.readInt32LE(o + 20) };
         const poff = log.payOff + b.readUInt32LE(o + 24), plen = b.readUInt32LE(o + 28);
-        const np = r.flags >> 3;
+        const np = (r.flags >> 3) & 15;
         const text = b.toString("latin1", poff, poff + plen - 2 * np);
         const pairs = [];
         for (let q = 0; q < 2 * np; q++) pairs.push(b.readUInt8(poff + plen - 2 * np + q));

@@ -3,6 +3,7 @@ the checksum definition in DESIGN.md; checks the C++ oracle and device checksums
 TEST INFRASTRUCTURE ONLY."""
 
 M64 = (1 << 64) - 1
+MARKER_TAG = 0x4D41524B45520000
 
 
 def mix64(z):
@@ -44,7 +45,11 @@ def checksum(state):
                 kid = int(k[1:])
                 if kid < 8:
                     props_lo |= (int(v) & 0xFF) << (8 * kid)
-        seg_sum = (seg_sum + seg_hash(i, fnv1a(text.encode()), seq, client, rseq, rclient, overlap, props_lo,
+        if isinstance(text, dict):  # a Marker {"marker": refType}: its refType byte, tagged
+            th = fnv1a(bytes([text['marker']])) ^ MARKER_TAG
+        else:
+            th = fnv1a(text.encode('latin-1'))
+        seg_sum = (seg_sum + seg_hash(i, th, seq, client, rseq, rclient, overlap, props_lo,
                                       props is not None)) & M64
     tree_sum = 0
     for level, counts in enumerate(state['tree']):
@@ -56,4 +61,4 @@ def checksum(state):
 
 
 def text_of(state):
-    return ''.join(s[0] for s in state['segs'] if s[3] == -1)
+    return ''.join(s[0] for s in state['segs'] if s[3] == -1 and not isinstance(s[0], dict))

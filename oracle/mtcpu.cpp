@@ -70,6 +70,7 @@ struct Seg : Node {
     uint64_t overlap = 0;             // removedClientOverlap as a set (clients < 64)
     bool props_defined = false;
     uint8_t props[kMaxKeys] = {0};    // value id per key (0 = absent)
+    bool marker = false;              // a Marker (mergeTree.ts:630-798): text = its one refType byte
     Seg() : Node(true) {}
     int len() const { return (int)text.size(); }
 };
@@ -190,6 +191,7 @@ struct Doc {
         r->seq = s->seq;
         r->client = s->client;
         r->overlap = s->overlap;
+        r->marker = s->marker;
         return r;
     }
 
@@ -276,7 +278,10 @@ struct Doc {
         if (a->props_defined != b->props_defined) return false;
         return std::memcmp(a->props, b->props, sizeof(a->props)) == 0;
     }
+    // TextSegment.canAppend (textSegment.ts:63-68): both text segments (Marker.canAppend is false,
+    // and a marker is not TextSegment.is, mergeTree.ts:793)
     static bool canAppend(const Seg* prev, const Seg* s) {
+        if (prev->marker || s->marker) return false;
         if (!prev->text.empty() && prev->text.back() == '\n') return false;
         return prev->len() <= kTextGranularity || s->len() <= kTextGranularity;
     }
@@ -415,6 +420,7 @@ struct Doc {
                 sx->rseq = sg.rseq;
                 sx->rclient = sg.rclient;
             }
+            sx->marker = (sg.flags & 16u) != 0;  // MT_SF_MARKER
             if (sg.flags & 2u) {  // MT_SF_PDEF
                 sx->props_defined = true;
                 for (int k = 0; k < 8; k++) sx->props[k] = (uint8_t)(sg.props >> (8 * k));
@@ -448,7 +454,7 @@ struct Doc {
         if (err) return;
         if (op.type == MT_OP_LOAD) return loadInsert(op, payload);
         const int32_t S = op.seq, R = op.ref_seq, C = op.client;
-        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        const int np = MT_OP_NPAIRS(op.flags);
         // Every assert the reference raises for this message is checked BEFORE anything is
         // applied, in the reference's order: the document halts in the state of the messages
         // before it (the reference throws after the op's tree edits, leaving them half-done).
@@ -490,6 +496,7 @@ struct Doc {
                     }
                     s->seq = S;
                     s->client = C;
+                    s->marker = (op.flags & MT_F_MARKER) != 0;
                     Block* sp = insertingWalk(root, op.pos1, R, C, s);
                     if (!s->parent) return fail(MT_DERR_INSERT_FAILED, S);
                     updateRoot(sp);
@@ -544,7 +551,7 @@ struct Doc {
         const int32_t S = op.seq, R = op.ref_seq;
         const int c = op.client & 0xFF, rc = op.client >> 8;
         const int32_t C = c == MT_CLIENT_NONCOLLAB ? -2 : c;
-        const int np = op.flags >> MT_F_NPAIRS_SHIFT;
+        const int np = MT_OP_NPAIRS(op.flags);
         if (!(c == MT_CLIENT_NONCOLLAB || (c >= 1 && c < MT_MAX_CLIENTS)) ||
             (op.pos2 >= 0 && !(rc >= 1 && rc < MT_MAX_CLIENTS)))
             return fail(MT_DERR_LIMITS, S);
@@ -564,6 +571,7 @@ struct Doc {
             }
             sx->seq = S;
             sx->client = C;
+            sx->marker = (op.flags & MT_F_MARKER) != 0;
             if (op.pos2 >= 0) {
                 sx->removed = true;
                 sx->rseq = op.pos2;
@@ -602,7 +610,7 @@ struct Doc {
     std::string text() const {
         std::string t;
         walkSegs(root, [&](const Seg* s) {
-            if (!s->removed) t += s->text;
+            if (!s->removed && !s->marker) t += s->text;  // gatherText: text segments only
         });
         return t;
     }
@@ -659,7 +667,8 @@ uint64_t doc_checksum(const Doc& doc) {
     Doc::walkSegs(doc.root, [&](const Seg* s) {
         uint64_t props_lo = 0;
         for (int k = 0; k < 8; k++) props_lo |= (uint64_t)s->props[k] << (8 * k);
-        d.seg_sum += mto_seg_hash(idx++, fnv1a(s->text.data(), s->text.size()), s->seq, s->client,
+        const uint64_t th = fnv1a(s->text.data(), s->text.size()) ^ (s->marker ? 0x4D41524B45520000ull : 0ull);
+        d.seg_sum += mto_seg_hash(idx++, th, s->seq, s->client,
                                   s->removed ? s->rseq : -1, s->removed ? s->rclient : -1,
                                   s->overlap, props_lo, s->props_defined);
     });
@@ -705,7 +714,10 @@ std::string doc_state_json(const Doc& doc) {
         if (!first) o += ',';
         first = false;
         o += '[';
-        json_escape(o, s->text);
+        if (s->marker)  // {"marker": refType}
+            o += "{\"marker\":" + std::to_string((unsigned char)s->text[0]) + "}";
+        else
+            json_escape(o, s->text);
         o += ',' + std::to_string(s->seq) + ',' + std::to_string(s->client) + ',';
         o += (s->removed ? std::to_string(s->rseq) : "-1") + ',';
         o += (s->removed ? std::to_string(s->rclient) : "-1") + ",[";

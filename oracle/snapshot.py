@@ -21,6 +21,11 @@ def client_name(c):
 
 
 def _json(text, props):
+    if isinstance(text, dict):                       # Marker.toJSONObject (mergeTree.ts:652-656)
+        spec = {'marker': {'refType': text['marker']}}
+        if props is not None:
+            spec['props'] = props
+        return spec
     return text if props is None else {'text': text, 'props': props}       # toJSONObject
 
 
@@ -32,17 +37,18 @@ def extract(state, name=client_name):
 
     def push(p):
         specs.append(_json(p[0], p[1]))
-        lens.append(len(p[0]))
+        lens.append(1 if isinstance(p[0], dict) else len(p[0]))
 
     for text, seq, c, rseq, rc, _ov, props in state['segs']:
         removed = rseq != -1
         if removed and rseq <= msn:                  # removed at or below the MSN: elided
             continue
         if seq <= msn and not removed:               # below the MSN: coalesce
+            mk = isinstance(text, dict) or (prev is not None and isinstance(prev[0], dict))
             if prev is None:
                 prev = [text, props]
-            elif (not prev[0].endswith('\n') and (len(prev[0]) <= TEXT_GRANULARITY or len(text) <= TEXT_GRANULARITY)
-                  and prev[1] == props):
+            elif (not mk and not prev[0].endswith('\n')       # canAppend: text segments only
+                  and (len(prev[0]) <= TEXT_GRANULARITY or len(text) <= TEXT_GRANULARITY) and prev[1] == props):
                 prev[0] += text                      # clone + append
             else:
                 push(prev)
@@ -59,7 +65,7 @@ def extract(state, name=client_name):
                 raw['removedSeq'] = rseq
                 raw['removedClient'] = name(rc)
             specs.append(raw)
-            lens.append(len(text))
+            lens.append(1 if isinstance(text, dict) else len(text))
     if prev is not None:
         push(prev)
     return specs, lens

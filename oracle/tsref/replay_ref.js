@@ -27,7 +27,7 @@ const { Worker, isMainThread, parentPort, workerData } = require("worker_threads
 const ROOT = path.join(__dirname, "..", "_tsref", "merge-tree", "src");
 const { Client } = require(path.join(ROOT, "client.js"));
 const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
-const { MergeTree } = require(path.join(ROOT, "mergeTree.js"));
+const { MergeTree, Marker } = require(path.join(ROOT, "mergeTree.js"));
 const { SnapshotV1 } = require(path.join(ROOT, "snapshotV1.js"));
 const { SnapshotLoader } = require(path.join(ROOT, "snapshotLoader.js"));
 const { MockStorage } = require(path.join(__dirname, "..", "_tsref", "node_modules", "@fluidframework",
@@ -35,7 +35,8 @@ const { MockStorage } = require(path.join(__dirname, "..", "_tsref", "node_modul
 
 const { loadLog, messages } = require(path.join(__dirname, "..", "..", "js", "mtlog.js"));
 
-function specToSegment(spec) { return TextSegment.fromJSONObject(spec); }
+// the segment factory a SharedString uses (sequence/src/sharedString.ts segmentFromSpec): text or marker
+function specToSegment(spec) { return TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec); }
 
 function newObserver() {
     const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
@@ -66,7 +67,7 @@ function canonical(client) {
                     props[k] = ch.properties[k];
                 }
             }
-            segs.push([ch.text, ch.seq, logId(client, ch.clientId), removed ? ch.removedSeq : -1,
+            segs.push([Marker.is(ch) ? { marker: ch.refType } : ch.text, ch.seq, logId(client, ch.clientId), removed ? ch.removedSeq : -1,
                 removed ? logId(client, ch.removedClientId) : -1, ov, props]);
         }
     };

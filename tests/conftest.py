@@ -14,7 +14,7 @@ def pytest_configure(config):
 
 
 GOLDEN = os.path.join(REPO, 'tests', 'golden')
-GOLDEN_SETS = ['scenarios', 'synth_c1', 'synth_c2', 'synth_c3', 'synth_c4', 'synth_tiny']
+GOLDEN_SETS = ['scenarios', 'markers', 'synth_c1', 'synth_c2', 'synth_c3', 'synth_c4', 'synth_tiny', 'synth_markers']
 
 
 def load_golden(name):

@@ -10,7 +10,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
-SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny']
+SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny', 'markers', 'synth_markers']
 CHUNKED = {'synth_c3': 300}   # a small mergeTreeSnapshotChunkSize: multi-chunk (header + body_i) trees
 
 

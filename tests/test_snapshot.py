@@ -10,6 +10,7 @@ import pytest
 from conftest import GOLDEN
 
 SETS = [('scenarios', None), ('synth_c1', None), ('synth_c3', None), ('synth_c4', None), ('synth_tiny', None),
+        ('markers', None), ('synth_markers', None),
         ('synth_c3', 300)]
 
 

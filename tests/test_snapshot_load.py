@@ -20,7 +20,7 @@ import pytest
 
 from conftest import GOLDEN
 
-LOAD_SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny']
+LOAD_SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny', 'markers', 'synth_markers']
 REF_DIR = os.path.join(GOLDEN, 'ref_snapshots')
 ERRS = {'MergeTree insert failed': 3, 'sequence#': 1, 'minSequence#': 2}
 
@@ -101,9 +101,23 @@ def translate_props(state, it):
     return out
 
 
-def ref_cases():
+def ref_cases(representable=True):
+    """The reference snapshot files; representable=True: those the device holds (withMarkers gives
+    each of its 564 markers its own markerId value, past the 255 value ids of a document)."""
     with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
-        return [json.loads(x) for x in f if x.strip()]
+        cases = [json.loads(x) for x in f if x.strip()]
+    return [c for c in cases if ('withMarkers' not in c['file']) == representable]
+
+
+def test_loader_refuses_more_values_than_the_device_holds():
+    """Property values are interned per document into u8 ids: the reference's withMarkers files
+    (a distinct markerId per marker) are refused loudly, never truncated."""
+    from fluidframework_amd import snapshot
+    for c in ref_cases(representable=False):
+        with open(os.path.join(REF_DIR, c['file'])) as f:
+            doc = snapshot.LoadedDoc(json.load(f))
+        with pytest.raises(ValueError, match='distinct ids'):
+            snapshot.build_load([doc])
 
 
 # ----------------------------------------------------------------------------------- CPU (oracle)

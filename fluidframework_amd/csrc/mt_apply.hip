@@ -50,6 +50,7 @@ struct Lds {
     uint8_t lbscour[LB];
     uint8_t ibcnt[MT_MAXLEV - 1][IB];
     int32_t n, nlev, heap_n, cur_seq, min_seq, err, err_seq, nfree, next_slot;
+    int32_t evn, evseq;     // delta events recorded (mt_events_enable) / seq of the message applying
     int32_t nb[MT_MAXLEV];
     uint32_t text_top, text_half;
     int32_t gcref[64];      // generator: latest refSeq per client (deli clientSeqManager)
@@ -78,8 +79,114 @@ struct Wave {
     uint8_t* const abase;   // document's double-buffered arena: [2][textcap]
     uint8_t* arena;         // current half
     const uint32_t textcap;
+    mt_event* const ev;     // the document's delta-event records (null: not recording)
+    const uint32_t evcap;
 
-    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc) : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc) {}
+    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc, mt_event* e = nullptr, uint32_t ec = 0)
+        : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc), ev(e), evcap(ec) {}
+
+    // ------------------------------------------------------------ delta events
+    // One callback record (mt_event, include/mtgpu.h), written by lane 0 in firing order: the
+    // reference's mergeTreeDeltaCallback / mergeTreeMaintenanceCallback (mergeTreeDeltaCallback.ts).
+    MT_DEV void emit(int op, unsigned flags, int leaf, int pos, uint32_t len, uint8_t pmask = 0, uint64_t pvals = 0) {
+        if (!ev) return;
+        const int n = s.evn;
+        if (lane == 0 && n < (int)evcap) {
+            mt_event e{};
+            e.seq = s.evseq;
+            e.op = (int8_t)op;
+            e.flags = (uint8_t)flags;
+            e.pmask = pmask;
+            e.leaf = leaf;
+            e.pos = pos;
+            e.len = len;
+            e.pvals = pvals;
+            ev[n] = e;
+        }
+        sync();
+        s.evn = n + 1;
+        sync();
+    }
+    // characters of unremoved segments before document position k (the local view's position)
+    MT_DEV int local_prefix(int k) {
+        int t = 0;
+        for (int base = 0; base < k; base += 64) {
+            const int i = base + lane;
+            if (i < k) {
+                const int sl = s.order[i];
+                t += (s.flags[sl] & MT_SF_REMOVED) ? 0 : (int)s.len[sl];
+            }
+        }
+        return wave_sum(t);
+    }
+    // The REMOVE / ANNOTATE callback (mergeTree.ts:2705-2712 / 2592-2600): its delta segments in
+    // document order, lane-parallel.  REMOVE runs after the edits (segments this op removed: rseq
+    // == S by C; their local position with the removal applied), ANNOTATE before them (the
+    // propertyDeltas need the previous values; annotate does not move the local view).
+    MT_DEV void emit_range(bool is_remove, int32_t S, int C, int start, int end, const uint8_t* pairs, int np,
+                           bool rewrite) {
+        if (!ev) return;
+        const int n = s.n, e0 = s.evn;
+        int cnt = 0, lpos = 0;
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            bool hit = false;
+            int ll = 0;
+            uint32_t ln = 0;
+            uint8_t pm = 0;
+            uint64_t pv = 0;
+            if (i < n) {
+                const int sl = s.order[i];
+                const uint8_t f = s.flags[sl];
+                ln = s.len[sl];
+                ll = (f & MT_SF_REMOVED) ? 0 : (int)ln;
+                const int ce = s.cum[i], cs = cstart(i);
+                hit = ce > cs && cs < end && ce > start;
+                if (is_remove) {
+                    hit = hit && (f & MT_SF_REMOVED) && s.rseq[sl] == S && s.rclient[sl] == C;
+                } else if (hit) {
+                    // SegmentPropertiesManager.addProperties' deltas (segmentPropertiesManager.ts:60-108):
+                    // a rewrite records each key it deletes with its old value; every key of the op
+                    // records the value before it is set (null when absent, and null for a rewrite's
+                    // null-valued key, deleted a moment earlier)
+                    const uint64_t old = (f & MT_SF_PDEF) ? s.props[sl] : 0;
+                    if (rewrite) {
+                        for (int k = 0; k < 8; k++)
+                            if ((old >> (8 * k)) & 0xFF) pm |= (uint8_t)(1u << k);
+                        pv = old;
+                    }
+                    for (int q = 0; q < np; q++) {
+                        const int k = pairs[2 * q];
+                        const uint64_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : ((old >> (8 * k)) & 0xFF);
+                        pm |= (uint8_t)(1u << k);
+                        pv = (pv & ~(0xFFull << (8 * k))) | (prev << (8 * k));
+                    }
+                }
+            }
+            const int incl = wave_incl_scan(ll);
+            const uint64_t m = wave_ballot(hit);
+            const int idx = cnt + __popcll(m & below);
+            if (hit && e0 + idx < (int)evcap) {
+                mt_event e{};
+                e.seq = s.evseq;
+                e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
+                e.flags = (uint8_t)(idx == 0 ? MT_EVF_FIRST : 0);
+                e.pmask = pm;
+                e.leaf = i;
+                e.pos = lpos + incl - ll;
+                e.len = ln;
+                e.pvals = pv;
+                ev[e0 + idx] = e;
+            }
+            cnt += __popcll(m);
+            lpos += wave_last(incl);
+        }
+        sync();
+        if (cnt == 0) return emit(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE, MT_EVF_FIRST | MT_EVF_EMPTY, -1, -1, 0);
+        s.evn = e0 + cnt;
+        sync();
+    }
 
     MT_DEV void fail(int code, int32_t seq) {
         if (s.err == 0) {
@@ -377,6 +484,9 @@ struct Wave {
         sync();
         if (lane == 0) s.cum[k] = pos;
         sync();
+        // MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2231-2236): [segment, next-to-be-linked]
+        emit(MT_EV_SPLIT, MT_EVF_FIRST, k, -1, (uint32_t)off);
+        emit(MT_EV_SPLIT, 0, k + 1, -1, s.len[t]);
         return insert_at(k + 1, b, t, old_end, seq);
     }
 
@@ -455,14 +565,18 @@ struct Wave {
         const int st = s.bst[b];
         const int cnt = s.lbcnt[b];
         const int32_t minSeq = s.min_seq;
-        int kept = 0, prev = -1;
+        int kept = 0, prev = -1, prevk = -1;  // prevk: prev's leaf ordinal
         uint16_t keep[kMaxNodes];
         for (int q = 0; q < cnt; q++) {
             const int sl = s.order[st + q];
             const uint8_t f = s.flags[sl];
             if (f & MT_SF_REMOVED) {
-                if (s.rseq[sl] > minSeq) keep[kept++] = (uint16_t)sl;
-                else free_slot(sl);  // UNLINK
+                if (s.rseq[sl] > minSeq) {
+                    keep[kept++] = (uint16_t)sl;
+                } else {
+                    emit(MT_EV_UNLINK, MT_EVF_FIRST, st + kept, -1, s.len[sl]);  // mergeTree.ts:1310-1315
+                    free_slot(sl);  // UNLINK
+                }
                 prev = -1;
             } else if (s.seq[sl] <= minSeq) {
                 bool app = false;
@@ -476,10 +590,13 @@ struct Wave {
                 }
                 if (app) {
                     append_text(prev, sl);
+                    emit(MT_EV_APPEND, MT_EVF_FIRST, prevk, -1, s.len[prev]);  // mergeTree.ts:1335-1340
+                    emit(MT_EV_APPEND, 0, st + kept, -1, s.len[sl]);
                     free_slot(sl);  // APPEND: segment.parent = undefined
                 } else {
                     keep[kept++] = (uint16_t)sl;
                     prev = s.len[sl] > 0 ? sl : -1;
+                    prevk = st + kept - 1;
                 }
             } else {
                 keep[kept++] = (uint16_t)sl;
@@ -715,6 +832,10 @@ struct Wave {
             if (S > s.min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
                 if (!add_lru(bb, t, S)) return;
             }
+            // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988); a snapshot body append has no opArgs
+            if (ev && op.type != MT_OP_LOAD) emit(MT_EV_INSERT, MT_EVF_FIRST, k, local_prefix(k), (uint32_t)tlen);
+        } else if (op.type != MT_OP_LOAD) {
+            emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
         }
         zamboni();
     }
@@ -729,6 +850,7 @@ struct Wave {
         const int n = s.n;
         const uint64_t cbit = 1ull << C;
         const bool rewrite = op.flags & MT_F_REWRITE;
+        if (!is_remove) emit_range(false, S, C, start, end, pairs, np, rewrite);
         for (int base = 0; base < n; base += 64) {
             const int i = base + lane;
             if (i < n) {
@@ -753,6 +875,7 @@ struct Wave {
             }
         }
         sync();
+        if (is_remove) emit_range(true, S, C, start, end, pairs, np, rewrite);
         // addToLRUSet for touched segments in document order: one heap push per leaf block
         // whose needsScour is not already true, for its first touched segment
         block_starts();
@@ -804,13 +927,15 @@ struct Wave {
         // MT_OP_LOAD: MergeTree.insertSegments from SnapshotLoader.loadBody (snapshotLoader.ts:192-224),
         // no Client around it: no window asserts and no updateSeqNumbers
         const bool load = op.type == MT_OP_LOAD;
+        const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
         const int C = op.client & 0xFF;
+        s.evseq = S;
         if (load) {
             const bool ok = (C == MT_CLIENT_NONCOLLAB || (C >= 1 && C < MT_MAX_CLIENTS)) &&
                             (op.pos2 < 0 || ((op.client >> 8) >= 1 && (op.client >> 8) < MT_MAX_CLIENTS));
             if (!ok) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
-        } else if (op.type != MT_OP_NOOP) {
+        } else if (!noop) {
             if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
         } else {  // every assert of the message before any edit: the document halts before it
@@ -822,7 +947,7 @@ struct Wave {
         const uint8_t* pairs = pay + tlen;
         for (int q = 0; q < np; q++)
             if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
-        if (op.type != MT_OP_NOOP) {
+        if (!noop) {
             if (op.pos1 < 0 || (op.type != MT_OP_INSERT && !load && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
             const int L = scan(op.ref_seq, C);  // cum for the op's view (no edit yet)
             // the window asserts run after the op in the reference (completeAndLogOp, client.ts:461-464;
@@ -839,6 +964,7 @@ struct Wave {
         }
         if (s.err) return;
         if (!load && !(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
+        if (ev && s.evn > (int)evcap) fail(MT_DERR_EVENTS, S);  // halt rather than drop callbacks
     }
 
     // ---------------------------------------------------------------- generator
@@ -1024,6 +1150,8 @@ struct Wave {
             s.next_slot = n;
             s.text_top = sc.text_top;
             s.text_half = sc.text_half;
+            s.evn = g.evn ? (int32_t)g.evn[d] : 0;
+            s.evseq = sc.cur_seq;
         }
         sync();
         arena = abase + (size_t)s.text_half * textcap;
@@ -1079,6 +1207,7 @@ struct Wave {
             sc.text_top = s.text_top;
             sc.text_half = s.text_half;
             sc.n_empty = (uint32_t)nempty;
+            if (g.evn) g.evn[d] = (uint32_t)s.evn;
         }
     }
 };
@@ -1104,7 +1233,8 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     Lds<CAP>& lds = *reinterpret_cast<Lds<CAP>*>(smem);
-    Wave<CAP> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap);
+    Wave<CAP> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap, GEN || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap,
+                 g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -1158,7 +1288,8 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     Lds<CAP>& st = *reinterpret_cast<Lds<CAP>*>(ws + (size_t)w * sizeof(Lds<CAP>));
-    Wave<CAP, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap);
+    Wave<CAP, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap, g.ev ? g.ev + (size_t)d * g.evcap : nullptr,
+                       g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;

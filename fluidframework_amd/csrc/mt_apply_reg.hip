@@ -1071,7 +1071,8 @@ struct RWave {
         if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
-        if (op.type != MT_OP_NOOP) {
+        const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
+        if (!noop) {
             if (op.client == 0 || op.client > kNarrowClients) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
             for (int q = 0; q < np; q++)
@@ -1127,7 +1128,7 @@ struct RWave {
         const int32_t msn = op.msn;
         for (int ph = 0; ph < 2; ph++) {
             if (ph == 0) {
-                if (op.type == MT_OP_NOOP) continue;
+                if (noop) continue;
             } else {
                 if (op.flags & MT_F_GROUP_MORE) break;
                 // (a non-op message's asserts, all before its edits: the document halts before it)

@@ -39,6 +39,8 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
                                     hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
+                                            hipStream_t st);
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
                                          uint32_t* specs, uint32_t* counts, hipStream_t st);
@@ -95,6 +97,7 @@ struct mt_engine {
     // register-resident engine (mt_apply_reg.hip) for classes up to kRegMaxCap segments; the
     // LDS engine (mt_apply.hip) above that, or everywhere with MTGPU_ENGINE=lds
     bool use_reg = true;
+    bool reg_default = true;       // use_reg when not recording delta events (mt_events_enable)
     int n_classes = kLdsClasses;   // classes with CAP <= seg_capacity
     int first_lds = 5;             // first class not served by the register engine
     uint8_t* ws = nullptr;         // HBM workspace of the classes above 2048 segments
@@ -177,6 +180,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
         e->use_reg = !(v && strcmp(v, "lds") == 0) && e->cfg.text_capacity <= 65536;
         e->first_lds = e->use_reg ? 5 : 0;
+        e->reg_default = e->use_reg;
         const char* sv = getenv("MTGPU_SERIAL");
         e->concurrent = !(sv && strcmp(sv, "1") == 0);
     }
@@ -200,6 +204,8 @@ mt_status mt_engine_destroy(mt_engine* e) {
     hipSetDevice(e->cfg.device);
     if (e->stream) hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) hipFree(p);
+    if (e->g.ev) (void)hipFree(e->g.ev);
+    if (e->g.evn) (void)hipFree(e->g.evn);
     if (e->ws) (void)hipFree(e->ws);
     if (e->h_counts) hipHostFree(e->h_counts);
     for (auto ev : e->kev) (void)hipEventDestroy(ev);
@@ -281,6 +287,72 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
     } while (0);
     hipFree(buf);
     return st;
+}
+
+mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
+    static_assert(sizeof(mt_event) == 32, "mt_event is 32 bytes");
+    if (!e) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (e->g.ev) HIP_OK(hipFree(e->g.ev));
+    if (e->g.evn) HIP_OK(hipFree(e->g.evn));
+    e->g.ev = nullptr;
+    e->g.evn = nullptr;
+    e->g.evcap = 0;
+    // the register engine's hot loop records nothing: every class runs on the LDS engine meanwhile
+    e->use_reg = per_doc ? false : e->reg_default;
+    e->first_lds = e->use_reg ? 5 : 0;
+    if (!per_doc) return MT_OK;
+    const size_t D = e->cfg.max_docs;
+    if (hipMalloc(&e->g.ev, D * per_doc * sizeof(mt_event)) != hipSuccess ||
+        hipMalloc(&e->g.evn, D * sizeof(uint32_t)) != hipSuccess) {
+        if (e->g.ev) (void)hipFree(e->g.ev);
+        e->g.ev = nullptr;
+        e->g.evn = nullptr;
+        e->use_reg = e->reg_default;
+        e->first_lds = e->use_reg ? 5 : 0;
+        return MT_ERR_NOMEM;
+    }
+    e->g.evcap = per_doc;
+    HIP_OK(hipMemset(e->g.evn, 0, D * sizeof(uint32_t)));
+    return MT_OK;
+}
+
+mt_status mt_events_drain(mt_engine* e, mt_event* out, uint64_t cap, uint32_t* row_ptr, uint64_t* total) {
+    if (!e || !row_ptr || !total || !e->g.ev) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const uint32_t n = e->n_docs;
+    std::vector<uint32_t> cnt(n);
+    if (n) HIP_OK(hipMemcpy(cnt.data(), e->g.evn, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint32_t d = 0; d < n; d++) off[d + 1] = off[d] + std::min(cnt[d], e->g.evcap);
+    if (off[n] >= (1ull << 32)) return MT_ERR_ARG;
+    for (uint32_t d = 0; d <= n; d++) row_ptr[d] = (uint32_t)off[d];
+    *total = off[n];
+    if (!out) return MT_OK;
+    if (cap < off[n]) return MT_ERR_ARG;
+    if (off[n]) {
+        uint64_t* d_off = nullptr;
+        mt_event* d_out = nullptr;
+        if (hipMalloc(&d_off, (n + 1) * sizeof(uint64_t)) != hipSuccess) return MT_ERR_NOMEM;
+        if (hipMalloc(&d_out, off[n] * sizeof(mt_event)) != hipSuccess) {
+            (void)hipFree(d_off);
+            return MT_ERR_NOMEM;
+        }
+        mt_status st = MT_OK;
+        if (hipMemcpyAsync(d_off, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            mt_launch_events_pack(&e->g, n, d_off, d_out, e->stream) != hipSuccess ||
+            hipMemcpyAsync(out, d_out, off[n] * sizeof(mt_event), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            st = MT_ERR_HIP;
+        (void)hipFree(d_off);
+        (void)hipFree(d_out);
+        if (st) return st;
+    }
+    HIP_OK(hipMemsetAsync(e->g.evn, 0, (size_t)n * sizeof(uint32_t), e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
 }
 
 mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,

@@ -168,7 +168,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     const mt_op_rec o = ops[i];
                     if (o.type == MT_OP_LOAD) continue;  // snapshot body append: no window update
                     if (o.type > MT_OP_LOAD) break;
-                    const bool bad = o.type == MT_OP_NOOP ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
+                    const bool bad = MT_OP_IS_NOOP(o) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
                                                           : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
                     if (bad) {
                         g.sc[d].win_op = (int32_t)i;
@@ -326,6 +326,24 @@ extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, 
     hipLaunchKernelGGL(mt_fixup_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, ops, n_docs);
     return hipGetLastError();
 }
+// mt_events_drain: document d's recorded events (at most evcap) to out + off[d], one wave per document
+__global__ __launch_bounds__(64) void mt_events_pack_kernel(mt_gstate g, uint32_t n_docs, const uint64_t* __restrict__ off,
+                                                           mt_event* __restrict__ out) {
+    const uint32_t d = blockIdx.x;
+    if (d >= n_docs) return;
+    const uint32_t n = min(g.evn[d], g.evcap);
+    const mt_event* src = g.ev + (size_t)d * g.evcap;
+    mt_event* dst = out + off[d];
+    for (uint32_t i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+
+extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
+                                            hipStream_t st) {
+    if (n_docs == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_events_pack_kernel, dim3(n_docs), dim3(64), 0, st, *g, n_docs, off, out);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st) {
     hipLaunchKernelGGL(mt_checksum_kernel, dim3(n_docs), dim3(64), 0, st, *g, n_docs, out);
     return hipGetLastError();

@@ -59,5 +59,7 @@ struct mt_gstate {
     uint16_t* hslot;   // [doc][hcap]        heap segment (position between launches)
     mt_doc_scalars* sc;// [doc]
     uint8_t* text;     // [doc][2][textcap]  text arena, double-buffered for in-kernel compaction
-    uint32_t segcap, lbcap, ibcap, hcap, textcap;
+    struct mt_event* ev;  // [doc][evcap] delta / maintenance events (mt_events_enable), or null
+    uint32_t* evn;     // [doc] events recorded since the last drain (may exceed evcap: halted)
+    uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;
 };

@@ -24,7 +24,8 @@ DOC_ERRORS = {0: None,
               4: 'device capacity exceeded',
               5: 'text arena exhausted',
               6: 'client id / property key / value id out of range',
-              7: 'malformed op record'}
+              7: 'malformed op record',
+              8: 'delta-event buffer full'}
 
 
 class MtError(RuntimeError):
@@ -81,12 +82,15 @@ def lib():
         L.mt_get_snapshot.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
                                       ctypes.POINTER(u64)]
         L.mt_snapshot_extract.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u64)]
+        L.mt_events_enable.argtypes = [vp, u32]
+        L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes'):
+                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_events_enable',
+                     'mt_events_drain'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -231,6 +235,30 @@ class MergeEngine:
         buf = ctypes.create_string_buffer(128)
         _check(lib().mt_class_kernel_name(self.h, capacity, buf, 128), 'mt_class_kernel_name')
         return buf.value.decode()
+
+    # -- delta / maintenance events (mergeTreeDeltaCallback.ts; include/mtgpu.h) --------------
+    def enable_events(self, per_doc=4096):
+        """Record the callbacks of every later apply, `per_doc` records per document between drains
+        (0 stops recording).  Recording runs every document on the LDS engine."""
+        _check(lib().mt_events_enable(self.h, per_doc), 'mt_events_enable')
+        return self
+
+    def drain_event_rows(self):
+        """(rows, row_ptr): every document's mt_event records since the last drain (then cleared)."""
+        from .events import EVENT_DTYPE
+        row_ptr = np.zeros(self.n_docs + 1, dtype=np.uint32)
+        total = ctypes.c_uint64()
+        _check(lib().mt_events_drain(self.h, None, 0, _ptr(row_ptr), ctypes.byref(total)), 'mt_events_drain')
+        rows = np.zeros(max(1, total.value), dtype=EVENT_DTYPE)
+        _check(lib().mt_events_drain(self.h, _ptr(rows), total.value, _ptr(row_ptr), ctypes.byref(total)),
+               'mt_events_drain')
+        return rows[:total.value], row_ptr
+
+    def drain_events(self):
+        """Per document, its callbacks since the last drain in canonical form (events.callbacks)."""
+        from .events import callbacks
+        rows, rp = self.drain_event_rows()
+        return [callbacks(rows[rp[d]:rp[d + 1]]) for d in range(self.n_docs)]
 
     # -- readout -------------------------------------------------------------------------
     def checksums(self):

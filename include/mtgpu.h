@@ -49,6 +49,15 @@ enum mt_op_flags {
 };
 #define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload */
 #define MT_OP_NPAIRS(flags) (((flags) >> MT_F_NPAIRS_SHIFT) & 0xF)
+/* An insert whose segment spec is the empty string is dropped by Client.applyInsertOp before it
+ * touches the tree (`if (op.seg)`, client.ts:403-407: no boundary split, no completeAndLogOp
+ * asserts, no callback); only updateSeqNumbers runs.  Such a record (text insert, no props, no
+ * text bytes) is applied exactly as an MT_OP_NOOP.  An empty text WITH a props object is a real
+ * insert: the boundary split happens and blockInsert skips the zero-length segment. */
+#define MT_OP_IS_EMPTY_INSERT(o)                                                      \
+    ((o).type == MT_OP_INSERT && !((o).flags & (MT_F_PROPS | MT_F_MARKER)) &&         \
+     (o).payload_len <= 2u * MT_OP_NPAIRS((o).flags))
+#define MT_OP_IS_NOOP(o) ((o).type == MT_OP_NOOP || MT_OP_IS_EMPTY_INSERT(o))
 
 typedef struct mt_op_rec {
     int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */
@@ -92,7 +101,9 @@ enum mt_doc_err {
     MT_DERR_CAPACITY = 4,       /* segment/block/heap capacity of the device representation exceeded    */
     MT_DERR_TEXT_ARENA = 5,     /* per-document text arena exhausted                                    */
     MT_DERR_LIMITS = 6,         /* client id / property key / value id outside MT_MAX_* */
-    MT_DERR_BAD_OP = 7          /* malformed record (type, payload bounds, negative positions) */
+    MT_DERR_BAD_OP = 7,         /* malformed record (type, payload bounds, negative positions) */
+    MT_DERR_EVENTS = 8          /* delta-event buffer of the document full (mt_events_enable): the
+                                   document halts rather than drop callbacks                   */
 };
 
 typedef struct mt_cfg {
@@ -209,6 +220,48 @@ mt_status mt_get_snapshot(mt_engine* eng, uint32_t doc, uint32_t chunk_size, con
 mt_status mt_snapshot_extract(mt_engine* eng, uint32_t d0, uint32_t n, float* kernel_ms, uint64_t* n_specs);
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
+
+/* ---- delta / maintenance events -------------------------------------
+ * What Client.mergeTreeDeltaCallback and mergeTreeMaintenanceCallback receive
+ * (mergeTreeDeltaCallback.ts:15-73), fired synchronously inside applyMsg at mergeTree.ts:1981-1988
+ * (INSERT), 2705-2712 (REMOVE: the segments this op removed, not the overlapping ones),
+ * 2592-2600 (ANNOTATE, with propertyDeltas), 2231-2236 (SPLIT), 1335-1340 (APPEND), 1310-1315
+ * (UNLINK).  The engine records them per document, in firing order, one mt_event per delta
+ * segment (a callback with no delta segments -- a remove that only overlapped -- is one record
+ * flagged MT_EVF_EMPTY).  Segments are identified by position, not object identity:
+ *   leaf = ordinal of the segment among the leaves still linked at callback time (document order;
+ *          for SPLIT the second segment is not linked yet: leaf of the first + 1; -1 = not linked,
+ *          the zero-length insert of an empty text with props),
+ *   pos  = op callbacks: local-view position (characters of unremoved linked leaves before it);
+ *          maintenance callbacks: -1,
+ *   len  = segment.cachedLength at callback time (APPEND: the first segment's grown length).
+ * ANNOTATE records carry propertyDeltas as a key mask + the previous value id per key (0 =
+ * null: the key was absent).  Recording routes every document to the LDS engine. */
+enum mt_event_op {
+    MT_EV_INSERT = 0, MT_EV_REMOVE = 1, MT_EV_ANNOTATE = 2,   /* MergeTreeDeltaType (ops.ts:17-24)   */
+    MT_EV_APPEND = -1, MT_EV_SPLIT = -2, MT_EV_UNLINK = -3    /* MergeTreeMaintenanceType            */
+};
+#define MT_EVF_FIRST 1u   /* first record of a callback */
+#define MT_EVF_EMPTY 2u   /* the callback's deltaSegments is empty (no segment in this record) */
+typedef struct mt_event {   /* 32 bytes */
+    int32_t seq;            /* sequenceNumber of the message being applied                        */
+    int8_t op;              /* mt_event_op                                                        */
+    uint8_t flags;          /* MT_EVF_*                                                           */
+    uint8_t pmask;          /* ANNOTATE: keys present in propertyDeltas (bit k = key id k)        */
+    uint8_t pad;
+    int32_t leaf;
+    int32_t pos;
+    uint32_t len;
+    uint32_t pad2;
+    uint64_t pvals;         /* ANNOTATE: previous value id of key k in byte k (0 = null)          */
+} mt_event;
+/* Start recording: `per_doc` records per document between drains (0 stops recording).  A
+ * document that would exceed it halts with MT_DERR_EVENTS. */
+mt_status mt_events_enable(mt_engine* eng, uint32_t per_doc);
+/* Move every document's recorded events to the host (synchronises) and clear them: document d's
+ * records are out[row_ptr[d] .. row_ptr[d+1]) (row_ptr: n_docs + 1 entries).  With out == NULL
+ * (or cap too small: MT_ERR_ARG) only row_ptr / *total are filled and nothing is cleared. */
+mt_status mt_events_drain(mt_engine* eng, mt_event* out, uint64_t cap, uint32_t* row_ptr, uint64_t* total);
 
 /* ---- bench tooling (not part of the applyMsg boundary) -------------------------------------
  * Synthetic multi-client op streams (DESIGN.md "Synthetic workloads", after SURVEY.md §8d),

@@ -95,8 +95,50 @@ struct Doc {
     std::vector<LRU> heap{LRU{nullptr, -2}};  // L[0] = comparer min (mergeTree.ts:923-926)
     std::vector<std::unique_ptr<Node>> pool;
     int32_t err = 0, err_seq = 0;
+    // delta / maintenance callbacks (mergeTreeDeltaCallback.ts:15-73) in the engine's mt_event
+    // form (include/mtgpu.h), recorded when `rec` is set
+    bool rec = false;
+    int32_t evSeq = 0;
+    std::vector<mt_event> events;
 
     Doc() { root = newBlock(); }
+
+    // ordinal among the leaves still linked (parent set) and local-view position of `s`, walking
+    // the blocks as they stand at callback time ({-1, -1} when `s` is not linked)
+    std::pair<int, int> where(const Seg* s) const {
+        int ord = 0, pos = 0;
+        bool found = false;
+        walkWhere(root, s, ord, pos, found);
+        return found ? std::make_pair(ord, pos) : std::make_pair(-1, -1);
+    }
+    static void walkWhere(const Block* b, const Seg* s, int& ord, int& pos, bool& found) {
+        for (int i = 0; i < b->childCount && !found; i++) {
+            const Node* ch = b->children[i];
+            if (!ch->leaf) {
+                walkWhere(static_cast<const Block*>(ch), s, ord, pos, found);
+                continue;
+            }
+            if (!ch->parent) continue;
+            if (ch == s) {
+                found = true;
+                return;
+            }
+            ord++;
+            pos += localLen(static_cast<const Seg*>(ch));
+        }
+    }
+    void ev(int op, unsigned flags, int leaf, int pos, int len, uint8_t pmask = 0, uint64_t pvals = 0) {
+        mt_event e{};
+        e.seq = evSeq;
+        e.op = (int8_t)op;
+        e.flags = (uint8_t)flags;
+        e.pmask = pmask;
+        e.leaf = leaf;
+        e.pos = pos;
+        e.len = (uint32_t)len;
+        e.pvals = pvals;
+        events.push_back(e);
+    }
 
     Block* newBlock() {
         auto* b = new Block();
@@ -218,6 +260,11 @@ struct Doc {
                     } else {     // splitLeafSegment
                         if (!(pos > 0)) return nullptr;
                         newNode = splitAt(seg, pos);
+                        if (rec) {  // MergeTreeMaintenanceType.SPLIT, mergeTree.ts:2231-2236
+                            const int k = where(seg).first;
+                            ev(MT_EV_SPLIT, MT_EVF_FIRST, k, -1, seg->len());
+                            ev(MT_EV_SPLIT, 0, k + 1, -1, static_cast<Seg*>(newNode)->len());
+                        }
                         ci++;
                     }
                 }
@@ -301,6 +348,7 @@ struct Doc {
                 if (s->rseq > minSeq) {
                     hold.push_back(s);
                 } else {
+                    if (rec) ev(MT_EV_UNLINK, MT_EVF_FIRST, where(s).first, -1, s->len());  // mergeTree.ts:1310-1315
                     s->parent = nullptr;  // UNLINK
                 }
                 prev = nullptr;
@@ -308,6 +356,10 @@ struct Doc {
                 bool app = prev && canAppend(prev, s) && matchProps(prev, s) && localLen(s) > 0;
                 if (app) {
                     prev->text += s->text;  // APPEND
+                    if (rec) {  // mergeTree.ts:1335-1340
+                        ev(MT_EV_APPEND, MT_EVF_FIRST, where(prev).first, -1, prev->len());
+                        ev(MT_EV_APPEND, 0, where(s).first, -1, s->len());
+                    }
                     s->parent = nullptr;
                 } else {
                     hold.push_back(s);
@@ -459,7 +511,9 @@ struct Doc {
         // applied, in the reference's order: the document halts in the state of the messages
         // before it (the reference throws after the op's tree edits, leaving them half-done).
         if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
-        if (op.type != MT_OP_NOOP) {
+        evSeq = S;
+        const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
+        if (!noop) {
             if (op.client >= MT_MAX_CLIENTS || op.client == 0) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
             int wc = 0;
@@ -483,7 +537,7 @@ struct Doc {
         const uint8_t* pairs = pay + tlen;
         for (int q = 0; q < np; q++)
             if (pairs[2 * q] >= kMaxKeys) return fail(MT_DERR_LIMITS, S);
-        switch (op.type) {
+        switch (noop ? (uint8_t)MT_OP_NOOP : op.type) {
             case MT_OP_INSERT: {
                 if (op.pos1 < 0) return fail(MT_DERR_BAD_OP, S);
                 ensureIntervalBoundary(op.pos1, R, C);
@@ -501,6 +555,12 @@ struct Doc {
                     if (!s->parent) return fail(MT_DERR_INSERT_FAILED, S);
                     updateRoot(sp);
                     if (S > minSeq) addToLRUSet(s, S);  // saveIfLocal, mergeTree.ts:2164-2179
+                    if (rec) {  // MergeTreeDeltaType.INSERT, mergeTree.ts:1981-1988
+                        const auto w = where(s);
+                        ev(MT_EV_INSERT, MT_EVF_FIRST, w.first, w.second, s->len());
+                    }
+                } else if (rec) {
+                    ev(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // the zero-length segment is never linked
                 }
                 zamboni();
                 break;
@@ -510,6 +570,8 @@ struct Doc {
                 if (op.pos1 < 0 || op.pos2 < 0) return fail(MT_DERR_BAD_OP, S);
                 ensureIntervalBoundary(op.pos1, R, C);
                 ensureIntervalBoundary(op.pos2, R, C);
+                std::vector<Seg*> delta;  // deltaSegments of the op's callback
+                std::vector<std::pair<uint8_t, uint64_t>> pdel;
                 if (op.type == MT_OP_REMOVE) {
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
                         if (s->removed) {
@@ -518,6 +580,7 @@ struct Doc {
                             s->removed = true;
                             s->rseq = S;
                             s->rclient = C;
+                            delta.push_back(s);          // removedSegments (mergeTree.ts:2637)
                         }
                         addToLRUSet(s, S);
                     });
@@ -528,10 +591,39 @@ struct Doc {
                             s->props_defined = true;
                             std::memset(s->props, 0, sizeof(s->props));
                         }
+                        // propertyDeltas (segmentPropertiesManager.ts:60-108): a rewrite records every
+                        // key it deletes with its old value; each key of the op then records the value
+                        // before it is set -- null when absent, and for a rewrite's null-valued key the
+                        // one deleted a moment earlier (so null again)
+                        uint8_t pm = 0;
+                        uint64_t pv = 0;
+                        for (int k = 0; k < 8; k++)
+                            if (rewrite && s->props[k]) {
+                                pm |= (uint8_t)(1u << k);
+                                pv |= (uint64_t)s->props[k] << (8 * k);
+                            }
+                        for (int q = 0; q < np; q++) {
+                            const int k = pairs[2 * q];
+                            if (k >= 8) continue;
+                            const uint8_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : s->props[k];
+                            pm |= (uint8_t)(1u << k);
+                            pv = (pv & ~(0xFFull << (8 * k))) | ((uint64_t)prev << (8 * k));
+                        }
                         if (rewrite) std::memset(s->props, 0, sizeof(s->props));
                         for (int q = 0; q < np; q++) s->props[pairs[2 * q]] = pairs[2 * q + 1];
+                        delta.push_back(s);
+                        pdel.emplace_back(pm, pv);
                         addToLRUSet(s, S);
                     });
+                }
+                if (rec) {  // mergeTree.ts:2705-2712 (REMOVE), 2592-2600 (ANNOTATE)
+                    const int opk = op.type == MT_OP_REMOVE ? MT_EV_REMOVE : MT_EV_ANNOTATE;
+                    if (delta.empty()) ev(opk, MT_EVF_FIRST | MT_EVF_EMPTY, -1, -1, 0);
+                    for (size_t i = 0; i < delta.size(); i++) {
+                        const auto w = where(delta[i]);
+                        ev(opk, i == 0 ? MT_EVF_FIRST : 0, w.first, w.second, delta[i]->len(),
+                           pdel.empty() ? 0 : pdel[i].first, pdel.empty() ? 0 : pdel[i].second);
+                    }
                 }
                 zamboni();
                 break;
@@ -549,6 +641,7 @@ struct Doc {
     // no updateSeqNumbers; the segment may carry removedSeq / removedClient from its spec
     void loadInsert(const mt_op_rec& op, const uint8_t* payload) {
         const int32_t S = op.seq, R = op.ref_seq;
+        evSeq = S;
         const int c = op.client & 0xFF, rc = op.client >> 8;
         const int32_t C = c == MT_CLIENT_NONCOLLAB ? -2 : c;
         const int np = MT_OP_NPAIRS(op.flags);
@@ -839,6 +932,17 @@ int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_se
     e->docs[doc] = Doc();
     e->docs[doc].reload(segs, n_segs, text, min_seq, cur_seq);
     return 0;
+}
+
+// delta / maintenance events (mt_event form) of every document from now on
+void mto_record_events(mto_engine* e, int on) {
+    for (auto& d : e->docs) d.rec = on != 0;
+}
+// copies up to cap of document `doc`'s recorded events; returns how many it has
+uint64_t mto_events(mto_engine* e, uint32_t doc, mt_event* out, uint64_t cap) {
+    const auto& v = e->docs[doc].events;
+    if (out) std::memcpy(out, v.data(), sizeof(mt_event) * std::min<uint64_t>(cap, v.size()));
+    return v.size();
 }
 
 int mto_doc_error(mto_engine* e, uint32_t doc, int32_t* seq) {

@@ -18,6 +18,9 @@ void mto_destroy(mto_engine* e);
 int mto_apply(mto_engine* e, const mt_op_rec* ops, const uint8_t* payload, const uint32_t* row_ptr,
               uint32_t n_docs, int n_threads);
 void mto_checksums(mto_engine* e, uint64_t* out, uint32_t n_docs);
+/* delta / maintenance events (mt_event form, include/mtgpu.h) of every document from now on */
+void mto_record_events(mto_engine* e, int on);
+uint64_t mto_events(mto_engine* e, uint32_t doc, mt_event* out, uint64_t cap);
 int mto_doc_error(mto_engine* e, uint32_t doc, int32_t* seq);
 /* SnapshotLoader.loadHeader of one document (reloadFromSegments + the collab window) */
 int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_segs, const uint8_t* text,

@@ -10,6 +10,7 @@ import subprocess
 
 import numpy as np
 
+from fluidframework_amd.events import EVENT_DTYPE, callbacks
 from fluidframework_amd.oplog import OP_DTYPE, OpBatch, synth_cfg_array
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -54,6 +55,9 @@ def lib():
         L.mto_generate.argtypes = [vp, u32, u32, vp, vp, vp, vp, ctypes.c_int]
         L.mto_load.restype = ctypes.c_int
         L.mto_load.argtypes = [vp, u32, vp, u32, vp, i32, i32]
+        L.mto_record_events.argtypes = [vp, ctypes.c_int]
+        L.mto_events.restype = u64
+        L.mto_events.argtypes = [vp, u32, vp, u64]
         L.mto_seg_hash.restype = u64
         L.mto_seg_hash.argtypes = [u64, u64, i32, i32, i32, i32, u64, u64, u32]
         _lib = L
@@ -106,6 +110,20 @@ class Oracle:
             rc = lib().mto_load(self.h, int(d), _ptr(part), b - a, _ptr(text), int(min_seq[i]), int(cur_seq[i]))
             assert rc == 0
         return self
+
+    def record_events(self, on=True):
+        lib().mto_record_events(self.h, 1 if on else 0)
+        return self
+
+    def event_rows(self, doc):
+        n = lib().mto_events(self.h, doc, None, 0)
+        out = np.zeros(int(n), dtype=EVENT_DTYPE)
+        lib().mto_events(self.h, doc, _ptr(out), n)
+        return out
+
+    def events(self, doc):
+        """the document's delta / maintenance callbacks in canonical form (fluidframework_amd.events)"""
+        return callbacks(self.event_rows(doc))
 
     def checksums(self):
         out = np.zeros(self.n_docs, dtype=np.uint64)

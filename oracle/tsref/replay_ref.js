@@ -84,6 +84,61 @@ function canonical(client) {
     return { seq: w.currentSeq, msn: w.minSeq, segs, tree };
 }
 
+// Delta / maintenance callbacks of an observer (mergeTreeDeltaCallback.ts:15-73; fired at
+// mergeTree.ts:1981-1988, 2231-2236, 1310-1315, 1335-1340, 2592-2600, 2705-2712) in the canonical
+// event form (DESIGN.md "Delta events"): [seq, operation, [[leaf, pos, len, propertyDeltas], ...]]
+//   leaf = the segment's ordinal among the leaves still linked (segment.parent !== undefined) at
+//          callback time, in document order; -1 when it is not linked (a zero-length insert);
+//          a SPLIT's second segment is not linked yet: the first one's ordinal + 1
+//   pos  = op callbacks: the local-view position (sum of localNetLength of the linked leaves
+//          before it); maintenance callbacks: -1
+//   len  = segment.cachedLength at callback time
+//   propertyDeltas = ANNOTATE: {k<id>: previous value id | null} with sorted keys, else null
+function attachEvents(c, seqRef) {
+    const events = [];
+    const where = (seg) => {
+        let ord = 0, pos = 0, found = null;
+        const walk = (b) => {
+            for (let i = 0; i < b.childCount && !found; i++) {
+                const ch = b.children[i];
+                if (!ch.isLeaf()) { walk(ch); continue; }
+                if (ch.parent === undefined) continue;
+                if (ch === seg) { found = [ord, pos]; return; }
+                ord++;
+                pos += ch.removedSeq === undefined ? ch.cachedLength : 0;
+            }
+        };
+        walk(c.mergeTree.root);
+        return found || [-1, -1];
+    };
+    const pdelta = (pd) => {
+        if (!pd) return null;
+        const o = {};
+        for (const k of Object.keys(pd).sort((a, b) => parseInt(a.slice(1)) - parseInt(b.slice(1)))) {
+            o[k] = pd[k] === undefined ? null : pd[k];
+        }
+        return o;
+    };
+    c.mergeTreeDeltaCallback = (opArgs, args) => {
+        const segs = args.deltaSegments.map((d) => {
+            const [leaf, pos] = where(d.segment);
+            return [leaf, pos, d.segment.cachedLength, args.operation === 2 ? pdelta(d.propertyDeltas) : null];
+        });
+        events.push([seqRef.seq, args.operation, segs]);
+    };
+    c.mergeTreeMaintenanceCallback = (args) => {
+        const segs = [];
+        for (let i = 0; i < args.deltaSegments.length; i++) {
+            const seg = args.deltaSegments[i].segment;
+            let leaf = where(seg)[0];
+            if (args.operation === -2 && i === 1) leaf = segs[0][0] + 1;  // SPLIT: `next` not yet linked
+            segs.push([leaf, -1, seg.cachedLength, null]);
+        }
+        events.push([seqRef.seq, args.operation, segs]);
+    };
+    return events;
+}
+
 function replayDoc(log, d) {
     const c = newObserver();
     let err = null;
@@ -191,6 +246,27 @@ function main() {
         for (let d = d0; d < d1; d++) {
             const { c, err } = replayDoc(log, d);
             out.push(JSON.stringify({ doc: d, err, state: canonical(c), text: c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId()) }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
+    if (mode === "events") {
+        const d0 = process.argv[4] ? parseInt(process.argv[4], 10) : 0;
+        const d1 = Math.min(log.nDocs, process.argv[5] ? parseInt(process.argv[5], 10) : log.nDocs);
+        const out = [];
+        for (let d = d0; d < d1; d++) {
+            const c = newObserver(), seqRef = { seq: 0 };
+            const events = attachEvents(c, seqRef);
+            let err = null;
+            try {
+                for (const m of messages(log, d)) {
+                    seqRef.seq = m.sequenceNumber;
+                    c.applyMsg(m);
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            out.push(JSON.stringify({ doc: d, err, events }));
         }
         process.stdout.write(out.join("\n") + "\n");
         return;

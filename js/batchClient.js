@@ -9,7 +9,13 @@
 // insertTextRemote, removeRangeRemote, enqueueMsg, applyMessages).  Many BatchClients share one
 // BatchEngine (one MI355X); any read flushes every client's queued ops as ONE batched submit.
 // Only remote ops exist for an observer: a message carrying the client's own long id (an ack of
-// a local op) throws, as do markers, register ops and combining ops other than "rewrite".
+// a local op) throws, as do register ops and combining ops other than "rewrite".
+// Delta / maintenance callbacks (mergeTreeDeltaCallback.ts:15-73): setting a client's
+// mergeTreeDeltaCallback or mergeTreeMaintenanceCallback makes the engine record them
+// (mt_events_enable); they are delivered, in firing order, after the batch that fired them.
+// Segments are identified by position: deltaSegments[i].segment = {ordinal, position,
+// cachedLength} (ordinal among the linked leaves at callback time; position in the local view,
+// op callbacks only) -- include/mtgpu.h "delta / maintenance events".
 const path = require("path");
 
 const native = require(path.join(__dirname, "mtgpu.node"));
@@ -28,6 +34,25 @@ class BatchEngine {
         });
         this.clients = [];
         this.pending = 0;
+        this.recording = false;
+        this.eventsPerDoc = opts.eventsPerDoc || (1 << 16);
+    }
+
+    _enableEvents() {
+        if (this.recording) return;
+        this.flush();  // ops queued before the callback was set were "applied" before it
+        native.eventsEnable(this.handle, this.eventsPerDoc);
+        this.recording = true;
+    }
+
+    /** Deliver the callbacks recorded so far to each client (mt_events_drain). */
+    _dispatch() {
+        if (!this.recording) return;
+        const [rows, rpBuf] = native.eventsDrain(this.handle, this.maxDocs);
+        const rp = new Uint32Array(rpBuf.buffer, rpBuf.byteOffset, this.maxDocs + 1);
+        for (let d = 0; d < this.clients.length; d++) {
+            if (rp[d + 1] > rp[d]) this.clients[d]._deliver(rows, rp[d], rp[d + 1]);
+        }
     }
 
     createClient() {
@@ -74,13 +99,14 @@ class BatchEngine {
         if (!this.pending) return;
         const { ops, payload, rowPtr } = this._encode();
         native.submit(this.handle, ops, payload, rowPtr);
+        this._dispatch();
     }
 
     /** The same as a Promise (napi_async_work): the JS thread stays free while the GPU applies. */
     flushAsync() {
         if (!this.pending) return Promise.resolve();
         const b = this._encode();
-        return native.submitAsync(this.handle, b.ops, b.payload, b.rowPtr);
+        return native.submitAsync(this.handle, b.ops, b.payload, b.rowPtr).then(() => this._dispatch());
     }
 }
 
@@ -99,6 +125,46 @@ class BatchClient {
         this.currentSeq = 0;
         this.minSeq = 0;
         this.msgQueue = [];
+        this._delta = undefined;
+        this._maintenance = undefined;
+        this.expect = [];               // opArgs of the ops whose delta callback is still to come
+    }
+
+    get mergeTreeDeltaCallback() { return this._delta; }
+    set mergeTreeDeltaCallback(cb) { this.engine._enableEvents(); this._delta = cb; }
+    get mergeTreeMaintenanceCallback() { return this._maintenance; }
+    set mergeTreeMaintenanceCallback(cb) { this.engine._enableEvents(); this._maintenance = cb; }
+
+    _deliver(rows, lo, hi) {
+        const cbs = [];
+        for (let i = lo; i < hi; i++) {
+            const o = 32 * i;
+            const op = rows.readInt8(o + 4), flags = rows.readUInt8(o + 5);
+            if (flags & 1) cbs.push({ seq: rows.readInt32LE(o), operation: op, deltaSegments: [] });
+            if (flags & 2) continue;  // a callback without delta segments
+            const segment = { ordinal: rows.readInt32LE(o + 8), cachedLength: rows.readUInt32LE(o + 16) };
+            if (op >= 0) segment.position = rows.readInt32LE(o + 12);
+            const delta = { segment };
+            if (op === ANNOTATE) {
+                const mask = rows.readUInt8(o + 6), vals = rows.readBigUInt64LE(o + 24);
+                delta.propertyDeltas = {};
+                for (let k = 0; k < MAX_KEYS; k++) {
+                    if (!((mask >> k) & 1)) continue;
+                    const v = Number((vals >> BigInt(8 * k)) & 0xffn);
+                    delta.propertyDeltas[this.keys[k]] = v ? this.values[v] : null;
+                }
+            }
+            cbs[cbs.length - 1].deltaSegments.push(delta);
+        }
+        for (const c of cbs) {
+            if (c.operation >= 0) {
+                const opArgs = this.expect.shift();
+                if (this._delta) this._delta(opArgs, { operation: c.operation, deltaSegments: c.deltaSegments });
+            } else if (this._maintenance) {
+                // (sequenceNumber: the message being applied -- not in the reference's args)
+                this._maintenance({ operation: c.operation, deltaSegments: c.deltaSegments, sequenceNumber: c.seq });
+            }
+        }
     }
 
     startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
@@ -157,6 +223,7 @@ class BatchClient {
         if (!op) return r;
         if (op.type === INSERT) {
             if (op.register || op.relativePos1) throw new Error("BatchClient: register/relative inserts unsupported");
+            if (op.seg === "") return r;  // `if (op.seg)`: dropped before the tree (client.ts:403-407)
             let text, pairs = [];
             if (typeof op.seg === "string") text = op.seg;
             else if (op.seg && typeof op.seg === "object" && "text" in op.seg) {
@@ -205,13 +272,17 @@ class BatchClient {
             throw new Error("BatchClient: acks of local ops are not supported by the observer engine");
         }
         const op = msg.type === "op" ? msg.contents : undefined;
-        if (op && op.type === GROUP) {
-            op.ops.forEach((m, i) => this.queue.push(this._record(msg, m, client, i + 1 < op.ops.length)));
-            this.engine.pending += op.ops.length;
-        } else {
-            this.queue.push(this._record(msg, op, client, false));
-            this.engine.pending++;
-        }
+        const members = op && op.type === GROUP ? op.ops : [op];
+        members.forEach((m, i) => {
+            const r = this._record(msg, m, client, i + 1 < members.length);
+            this.queue.push(r);
+            // every applied op fires one delta callback; an empty-string insert is dropped before
+            // the tree (client.ts:403-407), a non-op message has none
+            if (this.engine.recording && r.type !== NOOP) {
+                this.expect.push({ op: m, groupOp: op.type === GROUP ? op : undefined, sequencedMessage: msg });
+            }
+        });
+        this.engine.pending += members.length;
         this.currentSeq = msg.sequenceNumber;
         this.minSeq = Math.max(this.minSeq, msg.minimumSequenceNumber);
     }

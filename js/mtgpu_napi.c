@@ -343,6 +343,61 @@ static napi_value checksums(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* eventsEnable(engine, perDoc): record delta / maintenance callbacks (mt_events_enable) */
+static napi_value events_enable(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t per = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &per));
+    engine_box* b = get_box(env, argv[0]);
+    if (!b) return throw_status(env, "mt_events_enable", MT_ERR_ARG);
+    enter(b);
+    mt_status st = mt_events_enable(b->e, per);
+    leave(b);
+    if (st) return throw_status(env, "mt_events_enable", st);
+    return NULL;
+}
+
+/* eventsDrain(engine, nDocs) -> [Buffer of 32-byte mt_event rows, Buffer of nDocs+1 u32 row pointers] */
+static napi_value events_drain(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out, rows, rp;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t n = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &n));
+    engine_box* b = get_box(env, argv[0]);
+    if (!b) return throw_status(env, "mt_events_drain", MT_ERR_ARG);
+    uint32_t nd = 0;
+    void* rpd = NULL;
+    void* data = NULL;
+    uint64_t total = 0;
+    enter(b);
+    mt_status st = mt_engine_info(b->e, &nd, NULL);
+    if (!st && nd != n) st = MT_ERR_ARG;
+    if (st) {
+        leave(b);
+        return throw_status(env, "mt_events_drain", st);
+    }
+    if (napi_create_buffer(env, (size_t)(n + 1) * 4, &rpd, &rp) != napi_ok) {
+        leave(b);
+        return NULL;
+    }
+    st = mt_events_drain(b->e, NULL, 0, (uint32_t*)rpd, &total);
+    if (!st && napi_create_buffer(env, total ? total * sizeof(mt_event) : 1, &data, &rows) != napi_ok) {
+        leave(b);
+        return NULL;
+    }
+    if (!st && total) st = mt_events_drain(b->e, (mt_event*)data, total, (uint32_t*)rpd, &total);
+    else if (!st) st = mt_events_drain(b->e, (mt_event*)data, 0, (uint32_t*)rpd, &total);
+    leave(b);
+    if (st) return throw_status(env, "mt_events_drain", st);
+    NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
+    NAPI_CALL(env, napi_set_element(env, out, 0, rows));
+    NAPI_CALL(env, napi_set_element(env, out, 1, rp));
+    return out;
+}
+
 static napi_value version(napi_env env, napi_callback_info info) {
     (void)info;
     napi_value out;
@@ -426,6 +481,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"docError", NULL, doc_error, NULL, NULL, NULL, napi_default, NULL},
         {"checksums", NULL, checksums, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, version, NULL, NULL, NULL, napi_default, NULL},
+        {"eventsEnable", NULL, events_enable, NULL, NULL, NULL, napi_default, NULL},
+        {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
         {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},
         {"deliError", NULL, deli_error, NULL, NULL, NULL, napi_default, NULL},

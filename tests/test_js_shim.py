@@ -23,7 +23,7 @@ def test_addon_loads_and_exports():
         pytest.skip('node headers absent')
     out = subprocess.run([NODE, '-e', "const b=require('./js/batchClient.js');"
                           "for (const f of ['createEngine','submit','submitAsync','getText','getState','getLength',"
-                          "'docError','checksums','version']) if (typeof b.native[f] !== 'function') throw f;"
+                          "'docError','checksums','version','eventsEnable','eventsDrain']) if (typeof b.native[f] !== 'function') throw f;"
                           "console.log(b.native.version())"], cwd=REPO, capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
     assert 'gfx950' in out.stdout
@@ -132,3 +132,25 @@ def test_deli_reuses_short_ids_after_leave():
     r = json.loads(out.stdout)
     assert r['statuses'] == {'dropped': 1, 'sent': 800}
     assert r['seq'] == 800 and r['interned'] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['scenarios', 'markers', 'errors', 'empty_inserts', 'synth_tiny', 'synth_c4'])
+def test_batchclient_delivers_reference_callbacks(name):
+    """mergeTreeDeltaCallback / mergeTreeMaintenanceCallback on BatchClient (flushes every 40
+    messages, 32 ops per launch) deliver exactly the callbacks the reference's own Client fired
+    (tests/golden/events.jsonl, make_events.py), in order, with propertyDeltas un-interned."""
+    from test_events import _err_seqs, _golden_events, _matches
+    assert _addon()
+    gold = _golden_events()[name]
+    errs = _err_seqs(name)
+    _, exp = load_golden(name)
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_golden.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          '32', 'events'], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = [json.loads(x) for x in out.stdout.strip().split('\n')]
+    for r in got:
+        d = r['doc']
+        assert _matches(gold[d], r['events'], errs.get(d)), (name, d)
+        assert (r['err'] is None) == (errs.get(d) is None), (name, d)
+        assert _to_log_ids(r['state']) == exp[d]['state'], (name, d)

@@ -31,7 +31,7 @@ def build(force=False, verbose=False, prof=False):
     os.makedirs(objdir, exist_ok=True)
     srcs = [f for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
     flags = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
-             '-Wno-unused-result'] + os.environ.get('MTGPU_EXTRA_FLAGS', '').split()
+             '-Wno-unused-result', '-Wno-unused-value'] + os.environ.get('MTGPU_EXTRA_FLAGS', '').split()
 
     def cc(f):
         obj = os.path.join(objdir, f + ('.prof.o' if prof else '.o'))

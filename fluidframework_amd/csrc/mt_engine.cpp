@@ -53,16 +53,20 @@ extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_
 namespace {
 // register engine <= 1024, LDS engine 2048, the LDS engine's HBM-workspace form above (only the
 // classes with CAP <= the engine's seg_capacity are used: mt_engine::n_classes)
-const int32_t kClasses[] = {128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384};
-constexpr int kNumClasses = 9;
-constexpr int kLdsClasses = 6;   // classes an LDS-resident kernel serves (the generator's)
+// (the register classes step by 128 slots -- K = 2, 4, 6 ... 16 registers per field -- so a
+// document pays for the slots it can reach in a launch, not for the next power of two)
+const int32_t kClasses[] = {128, 256, 384, 512, 640, 768, 896, 1024, 2048, 4096, 8192, 16384};
+constexpr int kNumClasses = 12;
+constexpr int kLdsClasses = 9;   // classes an LDS-resident kernel serves (the generator's)
+constexpr int kFirstLds = 8;     // index of the 2048 class: the first the register engine does not serve
 constexpr int kMaxSegCap = 16384;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
-const int32_t kClassParams[kNumClasses * 4] = {128,  64,   24,   128,  256,  128,  40,   192,  512,   256,  72,   320,
-                                               768,  384,  104,  448,  1024, 512,  136,  576,  2048,  1024, 264,  1088,
-                                               4096, 2048, 520,  2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256};
-// the LDS engine has no 768 instantiation: its 1024 kernel serves that class
-int lds_cap(int cap) { return cap == 768 ? 1024 : cap; }
+const int32_t kClassParams[kNumClasses * 4] = {
+    128,  64,   24,   128,  256,  128,  40,   192,  384,   192,  56,   256,  512,   256,  72,   320,
+    640,  320,  88,   384,  768,  384,  104,  448,  896,   448,  120,  512,  1024,  512,  136,  576,
+    2048, 1024, 264,  1088, 4096, 2048, 520,  2112, 8192,  4096, 1032, 4160, 16384, 8192, 2056, 8256};
+// the LDS engine is instantiated at 128 / 256 / 512 / 1024 / 2048: the next one up serves a class
+int lds_cap(int cap) { return cap <= 256 ? cap : cap <= 512 ? 512 : cap <= 1024 ? 1024 : cap; }
 }  // namespace
 
 struct mt_batch {
@@ -99,7 +103,7 @@ struct mt_engine {
     bool use_reg = true;
     bool reg_default = true;       // use_reg when not recording delta events (mt_events_enable)
     int n_classes = kLdsClasses;   // classes with CAP <= seg_capacity
-    int first_lds = 5;             // first class not served by the register engine
+    int first_lds = kFirstLds;     // first class not served by the register engine
     uint8_t* ws = nullptr;         // HBM workspace of the classes above 2048 segments
     size_t ws_bytes = 0;
     // the capacity classes of one tick touch disjoint documents: each runs on its own stream
@@ -179,7 +183,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         const char* v = getenv("MTGPU_ENGINE");
         // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
         e->use_reg = !(v && strcmp(v, "lds") == 0) && e->cfg.text_capacity <= 65536;
-        e->first_lds = e->use_reg ? 5 : 0;
+        e->first_lds = e->use_reg ? kFirstLds : 0;
         e->reg_default = e->use_reg;
         const char* sv = getenv("MTGPU_SERIAL");
         e->concurrent = !(sv && strcmp(sv, "1") == 0);
@@ -301,7 +305,7 @@ mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
     e->g.evcap = 0;
     // the register engine's hot loop records nothing: every class runs on the LDS engine meanwhile
     e->use_reg = per_doc ? false : e->reg_default;
-    e->first_lds = e->use_reg ? 5 : 0;
+    e->first_lds = e->use_reg ? kFirstLds : 0;
     if (!per_doc) return MT_OK;
     const size_t D = e->cfg.max_docs;
     if (hipMalloc(&e->g.ev, D * per_doc * sizeof(mt_event)) != hipSuccess ||
@@ -310,7 +314,7 @@ mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
         e->g.ev = nullptr;
         e->g.evn = nullptr;
         e->use_reg = e->reg_default;
-        e->first_lds = e->use_reg ? 5 : 0;
+        e->first_lds = e->use_reg ? kFirstLds : 0;
         return MT_ERR_NOMEM;
     }
     e->g.evcap = per_doc;

@@ -20,7 +20,7 @@
 //     (K predicated moves per field per lane, DPP wave_shr:1 across lanes);
 //   * cold fields (property set, text offset) stay in LDS indexed by a segment id that never
 //     changes while the segment is linked; the zamboni heap holds those ids.
-// Capacity classes K = 2, 4, 6 ... 16 (128..1024 slots in steps of 128).  Bigger documents, documents that ever
+// Capacity classes K = 2 ... 16 (128..1024 slots in steps of 64).  Bigger documents, documents that ever
 // see a client id above 32 (the register overlap set is 32 bits wide), and a launch that carries
 // snapshot body appends (MT_OP_LOAD, once in a document's life) run on mt_apply.hip's LDS engine;
 // both engines share the HBM layout of mt_state.h.
@@ -62,7 +62,7 @@ enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, 
        P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT,
        P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_NSLOT };
 #ifdef MT_PROF
-__device__ unsigned long long mt_prof_acc[192];  // [K / 2 - 1 = 0..7][24 slots]
+__device__ unsigned long long mt_prof_acc[384];  // [K - 1 = 0..15][24 slots]
 MT_DEV uint64_t prof_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -1146,10 +1146,13 @@ struct RWave {
     }
 
     // ------------------------------------------------------------ load / store
-    // K consecutive u32 of one lane (16-byte aligned when K % 4 == 0, 8-byte when K == 2)
+    // K consecutive u32 of one lane (16-byte aligned when K % 4 == 0, 8-byte when K is even)
     MT_DEV VU ld_u32(const uint32_t* p) const {
         VU v;
-        if constexpr (K % 4 == 0) {
+        if constexpr (K % 2 == 1) {
+#pragma unroll
+            for (int j = 0; j < K; j++) v[j] = p[j];
+        } else if constexpr (K % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < K / 4; c++) {
                 const U4 x = reinterpret_cast<const U4*>(p)[c];
@@ -1170,7 +1173,10 @@ struct RWave {
     }
     MT_DEV VU ld_u8(const uint8_t* p) const {  // K consecutive bytes of one lane
         VU v;
-        if constexpr (K % 4 == 0) {
+        if constexpr (K % 2 == 1) {
+#pragma unroll
+            for (int j = 0; j < K; j++) v[j] = p[j];
+        } else if constexpr (K % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < K / 4; c++) {
                 const uint32_t w = reinterpret_cast<const uint32_t*>(p)[c];
@@ -1273,7 +1279,10 @@ struct RWave {
                 for (int j = 0; j < K; j++) li[j] = i0 + j < n ? (v[j] | ((uint32_t)(i0 + j) << kLenBits)) : kEmptyLi;
             }
             __builtin_amdgcn_sched_barrier(0);
-            {
+            if constexpr (K % 2 == 1) {
+#pragma unroll
+                for (int j = 0; j < K; j++) ov[j] = (uint32_t)(g.ovl[so + i0 + j] >> 1);
+            } else {
                 const uint32_t* op = reinterpret_cast<const uint32_t*>(g.ovl + so + i0);
 #pragma unroll
                 for (int c = 0; c < K / 2; c++) {
@@ -1492,7 +1501,7 @@ MT_DEV const mt_gstate& kernarg_gstate() {
 #endif
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
-    K >= 12 ? MT_WPE12 : K == 10 ? MT_WPE10 : K == 8 ? MT_WPE8 : K == 6 ? MT_WPE6 : MT_WPE4))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+    K >= 11 ? MT_WPE12 : K >= 9 ? MT_WPE10 : K >= 7 ? MT_WPE8 : K >= 5 ? MT_WPE6 : MT_WPE4))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
@@ -1547,7 +1556,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
 #ifdef MT_PROF
     if (wv.lane == 0)
         for (int q = 0; q < P_NSLOT; q++)
-            atomicAdd(&mt_prof_acc[(K / 2 - 1) * 24 + q],
+            atomicAdd(&mt_prof_acc[(K - 1) * 24 + q],
                       (unsigned long long)wv.prof[q]);
 #endif
 }
@@ -1568,12 +1577,19 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
     }
     switch (cap_class) {
         MTR_LAUNCH(128)
+        MTR_LAUNCH(192)
         MTR_LAUNCH(256)
+        MTR_LAUNCH(320)
         MTR_LAUNCH(384)
+        MTR_LAUNCH(448)
         MTR_LAUNCH(512)
+        MTR_LAUNCH(576)
         MTR_LAUNCH(640)
+        MTR_LAUNCH(704)
         MTR_LAUNCH(768)
+        MTR_LAUNCH(832)
         MTR_LAUNCH(896)
+        MTR_LAUNCH(960)
         MTR_LAUNCH(1024)
         default:
             return hipErrorInvalidValue;
@@ -1584,10 +1600,10 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
 // diagnostic: read (and clear) the per-phase cycle totals of a -DMT_PROF build (zeros otherwise)
 extern "C" int mt_prof_read(unsigned long long* out, int n) {
 #ifdef MT_PROF
-    if (n > 192) n = 192;
+    if (n > 384) n = 384;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mtr::mt_prof_acc), n * sizeof(unsigned long long)) != hipSuccess)
         return -1;
-    unsigned long long z[192] = {0};
+    unsigned long long z[384] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(mtr::mt_prof_acc), z, sizeof z) != hipSuccess) return -1;
     return n;
 #else

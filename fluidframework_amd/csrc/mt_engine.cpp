@@ -53,20 +53,23 @@ extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_
 namespace {
 // register engine <= 1024, LDS engine 2048, the LDS engine's HBM-workspace form above (only the
 // classes with CAP <= the engine's seg_capacity are used: mt_engine::n_classes)
-// (the register classes step by 128 slots -- K = 2, 4, 6 ... 16 registers per field -- so a
-// document pays for the slots it can reach in a launch, not for the next power of two)
-const int32_t kClasses[] = {128, 256, 384, 512, 640, 768, 896, 1024, 2048, 4096, 8192, 16384};
-constexpr int kNumClasses = 12;
-constexpr int kLdsClasses = 9;   // classes an LDS-resident kernel serves (the generator's)
-constexpr int kFirstLds = 8;     // index of the 2048 class: the first the register engine does not serve
+// (the register classes step by 64 slots -- K = 2 ... 16 registers per field -- so a document pays
+// for the slots it can reach in a launch, not for the next power of two)
+const int32_t kClasses[] = {128, 192, 256, 320, 384, 448, 512, 576, 640, 704, 768, 832, 896, 960, 1024,
+                            2048, 4096, 8192, 16384};
+constexpr int kNumClasses = 19;
+constexpr int kLdsClasses = 16;  // classes an LDS-resident kernel serves (the generator's)
+constexpr int kFirstLds = 15;    // index of the 2048 class: the first the register engine does not serve
 constexpr int kMaxSegCap = 16384;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
-    128,  64,   24,   128,  256,  128,  40,   192,  384,   192,  56,   256,  512,   256,  72,   320,
-    640,  320,  88,   384,  768,  384,  104,  448,  896,   448,  120,  512,  1024,  512,  136,  576,
-    2048, 1024, 264,  1088, 4096, 2048, 520,  2112, 8192,  4096, 1032, 4160, 16384, 8192, 2056, 8256};
+    128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
+    384, 192, 56, 256, 448, 224, 64, 288, 512, 256, 72, 320, 576, 288, 80, 352,
+    640, 320, 88, 384, 704, 352, 96, 416, 768, 384, 104, 448, 832, 416, 112, 480,
+    896, 448, 120, 512, 960, 480, 128, 544, 1024, 512, 136, 576, 2048, 1024, 264, 1088,
+    4096, 2048, 520, 2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256};
 // the LDS engine is instantiated at 128 / 256 / 512 / 1024 / 2048: the next one up serves a class
-int lds_cap(int cap) { return cap <= 256 ? cap : cap <= 512 ? 512 : cap <= 1024 ? 1024 : cap; }
+int lds_cap(int cap) { return cap <= 128 ? 128 : cap <= 256 ? 256 : cap <= 512 ? 512 : cap <= 1024 ? 1024 : cap; }
 }  // namespace
 
 struct mt_batch {

@@ -198,8 +198,8 @@ mt_status mt_last_apply_stats(mt_engine* eng, float* kernel_ms, float* wall_ms, 
  * environment variable MTGPU_SERIAL=1 starts an engine with 0) or one after another on the
  * engine stream (on = 0: each class kernel has the GPU to itself, for per-kernel rooflines). */
 mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
-/* The same, per capacity class (cls = 0, 1, ... for 128 / 256 / 384 / 512 / 640 / 768 / 896 / 1024 /
- * 2048 / 4096 / 8192 / 16384 segments; MT_ERR_ARG past the last): each class is one kernel
+/* The same, per capacity class (cls = 0, 1, ... for 128, 192, 256 ... 1024 segments in steps of 64,
+ * then 2048 / 4096 / 8192 / 16384; MT_ERR_ARG past the last): each class is one kernel
  * instantiation (see mt_class_kernel_name). */
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);

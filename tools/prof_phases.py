@@ -31,13 +31,13 @@ eng = MergeEngine(a.docs, ops_per_launch=32)
 dev = eng.synthesize(seed=5, **cfg)
 L = lib()
 L.mt_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 192)()
-L.mt_prof_read(buf, 192)  # clear
+buf = (ctypes.c_ulonglong * 384)()
+L.mt_prof_read(buf, 384)  # clear
 eng.reset()
 eng.apply_staged(dev)
-L.mt_prof_read(buf, 192)
-for c, k in enumerate((2, 4, 6, 8, 10, 12, 14, 16)):
-    v = list(buf[24 * c:24 * c + len(SLOTS)])
+L.mt_prof_read(buf, 384)
+for k in range(1, 17):
+    v = list(buf[24 * (k - 1):24 * (k - 1) + len(SLOTS)])
     ops = v[SLOTS.index('ops')]
     if not ops:
         continue

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -115,6 +116,13 @@ struct mt_engine {
     bool concurrent = true;
     hipStream_t side[kNumClasses] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
+    struct {  // mt_get_snapshots: the JSON of the last sizing call
+        bool valid = false;
+        uint32_t d0 = 0, n = 0, chunk = 0, n_names = 0;
+        const char* const* names = nullptr;
+        std::string json;
+        std::vector<uint64_t> off;
+    } snap_cache;
 };
 static constexpr int32_t kRegMaxCap = 1024;
 
@@ -1002,6 +1010,57 @@ std::string snapshot_json(const HostDoc& h, const std::vector<uint32_t>& sp, uin
     return o + '}';
 }
 
+// Documents [d0, d0 + n) to the host in one pass: every field of the range in one copy each, the
+// text arenas per document, all asynchronous behind one synchronisation
+mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>& out) {
+    const mt_gstate& g = e->g;
+    std::vector<mt_doc_scalars> sc(n);
+    HIP_OK(hipMemcpyAsync(sc.data(), g.sc + d0, n * sizeof(mt_doc_scalars), hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    const size_t S = (size_t)n * g.segcap, so = (size_t)d0 * g.segcap;
+    std::vector<int32_t> seq, rseq;
+    std::vector<uint32_t> len, toff;
+    std::vector<uint64_t> ovl, props;
+    std::vector<uint8_t> client, rclient, flags, lb, ib;
+    HIP_OK(fetch(seq, g.seq, so, S, e->stream));
+    HIP_OK(fetch(rseq, g.rseq, so, S, e->stream));
+    HIP_OK(fetch(len, g.len, so, S, e->stream));
+    HIP_OK(fetch(toff, g.toff, so, S, e->stream));
+    HIP_OK(fetch(ovl, g.ovl, so, S, e->stream));
+    HIP_OK(fetch(props, g.props, so, S, e->stream));
+    HIP_OK(fetch(client, g.client, so, S, e->stream));
+    HIP_OK(fetch(rclient, g.rclient, so, S, e->stream));
+    HIP_OK(fetch(flags, g.flags, so, S, e->stream));
+    HIP_OK(fetch(lb, g.lbcnt, (size_t)d0 * g.lbcap, (size_t)n * g.lbcap, e->stream));
+    HIP_OK(fetch(ib, g.ibcnt, (size_t)d0 * (MT_MAXLEV - 1) * g.ibcap, (size_t)n * (MT_MAXLEV - 1) * g.ibcap, e->stream));
+    out.assign(n, HostDoc());
+    for (uint32_t i = 0; i < n; i++) {
+        out[i].sc = sc[i];
+        HIP_OK(fetch(out[i].text, g.text, ((size_t)(d0 + i) * 2 + sc[i].text_half) * g.textcap, sc[i].text_top, e->stream));
+    }
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < n; i++) {
+        HostDoc& h = out[i];
+        const size_t a = (size_t)i * g.segcap, m = (size_t)h.sc.nseg;
+        h.seq.assign(seq.begin() + a, seq.begin() + a + m);
+        h.rseq.assign(rseq.begin() + a, rseq.begin() + a + m);
+        h.len.assign(len.begin() + a, len.begin() + a + m);
+        h.toff.assign(toff.begin() + a, toff.begin() + a + m);
+        h.ovl.assign(ovl.begin() + a, ovl.begin() + a + m);
+        h.props.assign(props.begin() + a, props.begin() + a + m);
+        h.client.assign(client.begin() + a, client.begin() + a + m);
+        h.rclient.assign(rclient.begin() + a, rclient.begin() + a + m);
+        h.flags.assign(flags.begin() + a, flags.begin() + a + m);
+        h.levels.resize(h.sc.nlev);
+        for (int L = 0; L < h.sc.nlev; L++) {
+            const uint8_t* src = L == 0 ? lb.data() + (size_t)i * g.lbcap
+                                        : ib.data() + ((size_t)i * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap;
+            h.levels[L].assign(src, src + h.sc.nb[L]);
+        }
+    }
+    return MT_OK;
+}
+
 mt_status copy_out(const std::string& s, char* buf, uint64_t cap, uint64_t* len) {
     if (len) *len = s.size();
     if (buf && cap) {
@@ -1045,6 +1104,79 @@ mt_status mt_get_snapshot(mt_engine* e, uint32_t doc, uint32_t chunk_size, const
     if (nspec > scap) return MT_ERR_STATE;
     return copy_out(snapshot_json(h, sp, nspec, chunk_size ? chunk_size : 10000u, client_names, n_names), buf, cap,
                     len);
+}
+
+mt_status mt_get_snapshots(mt_engine* e, uint32_t d0, uint32_t n, uint32_t chunk_size, const char* const* client_names,
+                           uint32_t n_names, char* buf, uint64_t cap, uint64_t* offsets) {
+    if (!e || !offsets || d0 > e->n_docs || n > e->n_docs - d0) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    // a sizing call (buf NULL) leaves its result for the copying call with the same arguments
+    auto& c = e->snap_cache;
+    const bool hit = c.valid && c.d0 == d0 && c.n == n && c.chunk == chunk_size && c.names == client_names &&
+                     c.n_names == n_names;
+    if (!hit) {
+        c.valid = false;
+        c.json.clear();
+        c.off.assign(n + 1, 0);
+        if (n) {
+            std::vector<HostDoc> docs;
+            mt_status st = read_range(e, d0, n, docs);
+            if (st) return st;
+            // the device extraction of every document in one launch
+            const uint32_t scap = e->g.segcap;
+            uint32_t *specs = nullptr, *counts = nullptr;
+            if (hipMalloc(&specs, (size_t)n * scap * 3 * sizeof(uint32_t)) != hipSuccess) return MT_ERR_NOMEM;
+            if (hipMalloc(&counts, (size_t)n * sizeof(uint32_t)) != hipSuccess) {
+                (void)hipFree(specs);
+                return MT_ERR_NOMEM;
+            }
+            std::vector<uint32_t> hc(n), hs((size_t)n * scap * 3);
+            hipError_t r = mt_launch_snapshot(&e->g, d0, n, scap, specs, counts, e->stream);
+            if (r == hipSuccess) r = hipMemcpyAsync(hc.data(), counts, n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream);
+            if (r == hipSuccess) r = hipMemcpyAsync(hs.data(), specs, hs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream);
+            if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+            (void)hipFree(specs);
+            (void)hipFree(counts);
+            if (r != hipSuccess) return MT_ERR_HIP;
+            // the JSON of each document on the host cores, in parallel
+            std::vector<std::string> parts(n);
+            std::atomic<uint32_t> next{0};
+            std::atomic<int> bad{0};
+            const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), std::min(16u, n));
+            auto work = [&] {
+                for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+                    if (hc[i] > scap) {
+                        bad = 1;
+                        continue;
+                    }
+                    std::vector<uint32_t> sp(hs.begin() + (size_t)i * scap * 3, hs.begin() + ((size_t)i * scap + hc[i]) * 3);
+                    parts[i] = snapshot_json(docs[i], sp, hc[i], chunk_size ? chunk_size : 10000u, client_names, n_names);
+                }
+            };
+            std::vector<std::thread> th;
+            for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+            work();
+            for (auto& x : th) x.join();
+            if (bad) return MT_ERR_STATE;
+            for (uint32_t i = 0; i < n; i++) c.off[i + 1] = c.off[i] + parts[i].size();
+            c.json.reserve(c.off[n]);
+            for (auto& p : parts) c.json += p;
+        }
+        c.valid = true;
+        c.d0 = d0;
+        c.n = n;
+        c.chunk = chunk_size;
+        c.names = client_names;
+        c.n_names = n_names;
+    }
+    for (uint32_t i = 0; i <= n; i++) offsets[i] = c.off[i];
+    if (!buf) return MT_OK;
+    if (cap < c.json.size()) return MT_ERR_ARG;
+    memcpy(buf, c.json.data(), c.json.size());
+    c.valid = false;  // consumed
+    c.json.clear();
+    c.json.shrink_to_fit();
+    return MT_OK;
 }
 
 mt_status mt_snapshot_extract(mt_engine* e, uint32_t d0, uint32_t n, float* kernel_ms, uint64_t* n_specs) {

@@ -82,6 +82,8 @@ def lib():
         L.mt_get_snapshot.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
                                       ctypes.POINTER(u64)]
         L.mt_snapshot_extract.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u64)]
+        L.mt_get_snapshots.argtypes = [vp, u32, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
+                                       vp]
         L.mt_events_enable.argtypes = [vp, u32]
         L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
@@ -89,7 +91,7 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_events_enable',
+                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_events_enable',
                      'mt_events_drain'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -301,6 +303,27 @@ class MergeEngine:
         _check(L.mt_get_snapshot(self.h, doc, chunk_size, names, n, buf, ln.value + 1, ctypes.byref(ln)),
                'mt_get_snapshot')
         return json.loads(buf.raw[:ln.value].decode('latin-1'))
+
+    def snapshots_raw(self, d0=0, n=None, chunk_size=0, client_names=None):
+        """mt_get_snapshots: (bytes, offsets) of documents [d0, d0+n), their JSON written on all host cores."""
+        n = self.n_docs - d0 if n is None else n
+        names, nn = None, 0
+        if client_names is not None:
+            nn = len(client_names)
+            names = (ctypes.c_char_p * nn)(*[x.encode() for x in client_names])
+        off = np.zeros(n + 1, dtype=np.uint64)
+        L = lib()
+        _check(L.mt_get_snapshots(self.h, d0, n, chunk_size, names, nn, None, 0, _ptr(off)), 'mt_get_snapshots')
+        buf = ctypes.create_string_buffer(max(1, int(off[-1])))
+        _check(L.mt_get_snapshots(self.h, d0, n, chunk_size, names, nn, buf, int(off[-1]), _ptr(off)),
+               'mt_get_snapshots')
+        return buf.raw[:int(off[-1])], off
+
+    def snapshots(self, d0=0, n=None, chunk_size=0, client_names=None):
+        """SnapshotV1 extractSync + emit of documents [d0, d0+n) in one batched call: a list of
+        {path: parsed JSON} (the same as snapshot() per document)."""
+        raw, off = self.snapshots_raw(d0, n, chunk_size, client_names)
+        return [json.loads(raw[int(off[i]):int(off[i + 1])].decode('latin-1')) for i in range(len(off) - 1)]
 
     def snapshot_extract(self, d0=0, n=None):
         """Device extraction for documents [d0, d0+n): (kernel_ms, segment specs)."""

@@ -216,6 +216,12 @@ mt_status mt_class_kernel_name(mt_engine* eng, uint32_t capacity, char* buf, uin
  * interned by the host; JSON key order is key-id order, the reference's is insertion order). */
 mt_status mt_get_snapshot(mt_engine* eng, uint32_t doc, uint32_t chunk_size, const char* const* client_names,
                           uint32_t n_names, char* buf, uint64_t cap, uint64_t* len);
+/* The same for documents [d0, d0+n) at once (a summary of many documents): one extraction launch,
+ * one copy per state array, the JSON written on all host cores.  Document d0+i's object is
+ * buf[offsets[i] .. offsets[i+1]) (offsets: n+1 entries, no separators, no NUL).  Call once with
+ * buf = NULL for the sizes (the result is kept), then with a buffer of offsets[n] bytes. */
+mt_status mt_get_snapshots(mt_engine* eng, uint32_t d0, uint32_t n, uint32_t chunk_size, const char* const* client_names,
+                           uint32_t n_names, char* buf, uint64_t cap, uint64_t* offsets);
 /* Run the device extraction for documents [d0, d0+n) (all docs of a summary in one launch);
  * reports the kernel time and the number of segment specs produced (bench tooling). */
 mt_status mt_snapshot_extract(mt_engine* eng, uint32_t d0, uint32_t n, float* kernel_ms, uint64_t* n_specs);

@@ -96,8 +96,11 @@ def test_snapshot_matches_reference(name, chunk):
     eng = MergeEngine(batch.n_docs, ops_per_launch=32)
     eng.apply(batch)
     names = ['observer'] + ['c%d' % i for i in range(1, 64)]
-    for d, w in enumerate(load_snapshots(name, chunk)):
+    want = load_snapshots(name, chunk)
+    for d, w in enumerate(want):
         assert eng.snapshot(d, chunk or 0, names) == w['snapshot'], (name, d)
+    # the batched, multithreaded form (mt_get_snapshots) of every document at once
+    assert eng.snapshots(0, batch.n_docs, chunk or 0, names) == [w['snapshot'] for w in want], name
 
 
 def test_snapshot_matches_restatement_on_fuzz(oracle_lib):
@@ -115,3 +118,7 @@ def test_snapshot_matches_restatement_on_fuzz(oracle_lib):
         st = o.state(d)
         for chunk in (0, 97):
             assert eng.snapshot(d, chunk, names) == snapshot.emit(st, chunk or snapshot.DEFAULT_CHUNK), d
+    for chunk in (0, 97):
+        got = eng.snapshots(5, 40, chunk, names)
+        for i, d in enumerate(range(5, 45)):
+            assert got[i] == snapshot.emit(o.state(d), chunk or snapshot.DEFAULT_CHUNK), (chunk, d)

@@ -1493,15 +1493,22 @@ MT_DEV const mt_gstate& kernarg_gstate() {
 #ifndef MT_WPE4
 #define MT_WPE4 4
 #endif
+#ifndef MT_WPE7
+#define MT_WPE7 MT_WPE8
+#endif
 #ifndef MT_WPE6
 #define MT_WPE6 MT_WPE8
+#endif
+#ifndef MT_WPE5
+#define MT_WPE5 MT_WPE6
 #endif
 #ifndef MT_WPE10
 #define MT_WPE10 MT_WPE12
 #endif
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
-    K >= 11 ? MT_WPE12 : K >= 9 ? MT_WPE10 : K >= 7 ? MT_WPE8 : K >= 5 ? MT_WPE6 : MT_WPE4))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+    K >= 11 ? MT_WPE12 : K >= 9 ? MT_WPE10 : K == 8 ? MT_WPE8 : K == 7 ? MT_WPE7 : K == 6 ? MT_WPE6 : K == 5 ? MT_WPE5
+                                                                                                 : MT_WPE4))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,

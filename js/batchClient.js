@@ -308,7 +308,7 @@ class BatchClient {
         this.engine.flush();
         const st = JSON.parse(native.getState(this.engine.handle, this.doc));
         for (const s of st.segs) {
-            s[2] = this.longIds[s[2]];
+            s[2] = s[2] < 0 ? s[2] : this.longIds[s[2]];  // (-2: NonCollabClient, a segment loaded below the MSN)
             if (s[4] !== -1) s[4] = this.longIds[s[4]];
             s[5] = s[5].map((x) => this.longIds[x]);
             if (s[6]) {

@@ -343,6 +343,35 @@ static napi_value checksums(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* docsLoad(engine, docIdsU32, segRowPtrU32, segs (32-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
+ * SnapshotLoader.loadHeader for a batch of documents (mt_docs_load) */
+static napi_value docs_load(napi_env env, napi_callback_info info) {
+    size_t argc = 7;
+    napi_value argv[7];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 7 ? get_box(env, argv[0]) : NULL;
+    size_t nid = 0, nrow = 0, nseg = 0, ntext = 0, nmin = 0, ncur = 0;
+    const void* ids = b ? buffer_data(env, argv[1], &nid) : NULL;
+    const void* row = b ? buffer_data(env, argv[2], &nrow) : NULL;
+    const void* segs = b ? buffer_data(env, argv[3], &nseg) : NULL;
+    const void* text = b ? buffer_data(env, argv[4], &ntext) : NULL;
+    const void* mn = b ? buffer_data(env, argv[5], &nmin) : NULL;
+    const void* cs = b ? buffer_data(env, argv[6], &ncur) : NULL;
+    const size_t n = nid / 4;
+    if (!b || nid % 4 || nrow != 4 * (n + 1) || nmin != 4 * n || ncur != 4 * n || nseg % sizeof(mt_load_seg) ||
+        (n && ((const uint32_t*)row)[n] - ((const uint32_t*)row)[0] != nseg / sizeof(mt_load_seg))) {
+        napi_throw_type_error(env, NULL, "docsLoad(engine, docIds, segRowPtr, segs, text, minSeq, curSeq)");
+        return NULL;
+    }
+    enter(b);
+    mt_status st = mt_docs_load(b->e, (uint32_t)n, (const uint32_t*)ids, (const uint32_t*)row,
+                                (const mt_load_seg*)segs, (const uint8_t*)text, ntext, (const int32_t*)mn,
+                                (const int32_t*)cs);
+    leave(b);
+    if (st) return throw_status(env, "mt_docs_load", st);
+    return NULL;
+}
+
 /* eventsEnable(engine, perDoc): record delta / maintenance callbacks (mt_events_enable) */
 static napi_value events_enable(napi_env env, napi_callback_info info) {
     size_t argc = 2;
@@ -482,6 +511,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"checksums", NULL, checksums, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, version, NULL, NULL, NULL, napi_default, NULL},
         {"eventsEnable", NULL, events_enable, NULL, NULL, NULL, napi_default, NULL},
+        {"docsLoad", NULL, docs_load, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
         {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},

@@ -154,3 +154,55 @@ def test_batchclient_delivers_reference_callbacks(name):
         assert _matches(gold[d], r['events'], errs.get(d)), (name, d)
         assert (r['err'] is None) == (errs.get(d) is None), (name, d)
         assert _to_log_ids(r['state']) == exp[d]['state'], (name, d)
+
+
+def _js_state_to_log(state):
+    """BatchClient.getState (long client ids "c<k>", "observer"; -2 = NonCollabClient) in the golden
+    logs' id space; property names and values as they are."""
+    def cid(x):
+        return x if isinstance(x, int) else (0 if x == 'observer' else int(x[1:]))
+    segs = [[t, sq, cid(c), rs, cid(rc) if rc != -1 else -1, sorted(cid(o) for o in ov), p]
+            for t, sq, c, rs, rc, ov, p in state['segs']]
+    return dict(state, segs=segs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['scenarios', 'synth_c3', 'synth_c4', 'markers', 'synth_markers'])
+def test_batchclient_loads_reference_snapshots(name):
+    """js/snapshotLoader.js (SnapshotLoader over mt_docs_load + MT_OP_LOAD appends): the snapshot
+    the reference emitted after messages [0, k), loaded into BatchClients, then messages [k, n):
+    the reference's state after the same (tests/golden/load_<set>.jsonl)."""
+    from test_snapshot_load import err_code, load_set
+    assert _addon()
+    rows = load_set(name)
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_load.js'), 'sets',
+                          os.path.join(GOLDEN, f'load_{name}.jsonl'), os.path.join(GOLDEN, name + '.mtlog'), '32'],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    for r in rows:
+        g = got[r['doc']]
+        assert (g['err'] is None) == (err_code(r['err']) == 0), (name, r['doc'], g['err'], r['err'])
+        if r['state'] is not None:
+            assert _js_state_to_log(g['state']) == r['state'], (name, r['doc'])
+
+
+@pytest.mark.gpu
+def test_batchclient_loads_reference_snapshot_files():
+    """The reference's own snapshot test files (v1 / legacy / legacy with catch-up ops, header-only
+    and header + body, annotated) through BatchClient: the loaded state, then the spec's edits."""
+    from test_snapshot_load import REF_DIR, err_code
+    assert _addon()
+    with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
+        cases = {c['file']: c for c in (json.loads(x) for x in f if x.strip())}
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_load.js'), 'files',
+                          os.path.join(REF_DIR, 'expected.jsonl'), REF_DIR], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.strip().split('\n')]
+    assert len(lines) >= 6
+    for g in lines:
+        c = cases[g['file']]
+        assert _js_state_to_log(g['loaded']) == c['loaded'], g['file']
+        assert (g['err'] is None) == (err_code(c['err']) == 0), g['file']
+        assert _js_state_to_log(g['state']) == c['state'], g['file']

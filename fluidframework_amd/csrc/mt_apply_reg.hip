@@ -60,7 +60,7 @@ MT_DEV int wave_total(int v) { return wave_last(wave_incl_scan(v)); }
 // ---- optional per-phase cycle accounting (diagnostic build: -DMT_PROF; never in the product)
 enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, P_OPS, P_ZPOP, P_REPACK,
        P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT,
-       P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_NSLOT };
+       P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_B_SRCH, P_B_LEAF, P_NSLOT };
 #ifdef MT_PROF
 __device__ unsigned long long mt_prof_acc[384];  // [K - 1 = 0..15][24 slots]
 MT_DEV uint64_t prof_now() {
@@ -448,14 +448,23 @@ struct RWave {
     MT_DEV bool insert_at(int k, int a, int en, Elem e, int32_t sq) {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
         const bool front = k == a;  // new first child: it takes over the block's marks
+        PROF_BEGIN(ti0);
         shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
         if (front) {
             set_bs(k + 1, false);
             set_sc(k + 1, MT_SC_UNDEF);
         }
+        PROF_END(prof, P_B_INS, ti0);
         nlive += 1;
-        if (live_in(a, en + 1) >= kMaxNodes) return split_leaf(a, en + 1, sq);
-        return true;
+        PROF_BEGIN(ti1);
+        const bool over = live_in(a, en + 1) >= kMaxNodes;
+        PROF_END(prof, P_B_LEAF, ti1);
+        if (!over) return true;
+        PROF_BEGIN(ti2);
+        PROF_CNT(P_N_COMPACT, 1);
+        const bool r = split_leaf(a, en + 1, sq);
+        PROF_END(prof, P_COMPACT, ti2);
+        return r;
     }
     MT_DEV int alloc_id(int32_t sq) {
         if (next_id >= CAP) {
@@ -524,6 +533,7 @@ struct RWave {
     // visible to the op's view that strictly contains pos, cut it (left part in place, cum kept
     // valid for the view) and return its right part r, to be inserted at slot k1 of leaf block b.
     MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& ba, int& be) {
+        PROF_BEGIN(ts0);
         int cs = cs0();
         int hitj = -1;
 #pragma unroll
@@ -532,6 +542,7 @@ struct RWave {
             cs = cum[j];
         }
         const uint64_t m = wave_ballot(hitj >= 0);
+        PROF_END(prof, P_B_SRCH, ts0);
         if (!m) return false;
         PROF_CNT(P_N_SPLIT, 1);
         PROF_BEGIN(tb0);

@@ -179,3 +179,33 @@ def test_engine_events_large_document(oracle_lib):
     assert eng.error(0) == (0, 0)
     assert eng.drain_events()[0] == o.events(0)
     assert eng.checksums()[0] == o.checksums()[0]
+
+
+@pytest.mark.gpu
+def test_engine_events_switch_on_and_off(oracle_lib):
+    """Recording can start after the register engine has applied part of the log and stop again:
+    the first third unrecorded (register engine), the second recorded (LDS engine), the last
+    unrecorded; the recorded callbacks are the oracle's for exactly the middle third, and the final
+    state is the oracle's."""
+    from fluidframework_amd.oplog import OpBatch
+    full = oracle_lib.generate(64, seed=91, n_clients=16, ops_per_doc=480, max_lag=32, n_keys=3, n_values=5,
+                               p_insert=0.5, p_remove=0.3, p_overlap=0.5, p_null=0.1, p_insert_props=0.2)
+    parts = []
+    for lo, hi in ((0, 160), (160, 320), (320, 480)):
+        idx = np.concatenate([np.arange(int(full.row_ptr[d]) + lo, int(full.row_ptr[d]) + hi)
+                              for d in range(full.n_docs)])
+        parts.append(OpBatch(full.ops[idx].copy(), full.payload,
+                             np.arange(0, full.n_docs * (hi - lo) + 1, hi - lo, dtype=np.uint32)))
+    o = oracle_lib.Oracle(full.n_docs).record_events().apply(full)
+    eng = _engine(full.n_docs, 32)
+    eng.apply(parts[0])
+    eng.enable_events(1 << 14)
+    eng.apply(parts[1])
+    got = eng.drain_events()
+    eng.enable_events(0)
+    eng.apply(parts[2])
+    for d in range(full.n_docs):
+        a = int(full.ops[int(full.row_ptr[d]) + 160]['seq'])
+        b = int(full.ops[int(full.row_ptr[d]) + 320]['seq'])
+        assert got[d] == [e for e in o.events(d) if a <= e[0] < b], d
+    assert np.array_equal(eng.checksums(), o.checksums())

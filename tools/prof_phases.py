@@ -16,7 +16,7 @@ from fluidframework_amd.oplog import CONFIGS  # noqa: E402
 
 SLOTS = ['load', 'scan', 'boundary', 'insert', 'range', 'zamboni', 'scour', 'store', 'ops', 'zpop', 'repack',
          'b_get', 'b_blk', 'b_txt', 'b_ins', 'n_scour', 'n_unlink', 'n_append', 'n_split', 'compact',
-         'n_compact', 'n_appbytes']
+         'n_compact', 'n_appbytes', 'b_srch', 'b_leaf']
 
 ap = argparse.ArgumentParser()
 ap.add_argument('--config', default='C3')

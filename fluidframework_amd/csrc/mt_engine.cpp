@@ -40,6 +40,8 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
                                     hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q, uint32_t n, mt_tile_result* out,
+                                      hipStream_t st);
 extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
                                             hipStream_t st);
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
@@ -302,6 +304,26 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
     } while (0);
     hipFree(buf);
     return st;
+}
+
+mt_status mt_find_tiles(mt_engine* e, const mt_tile_query* q, uint32_t n, mt_tile_result* out) {
+    static_assert(sizeof(mt_tile_query) == 48, "mt_tile_query is 48 bytes");
+    if (!e || (n && (!q || !out))) return MT_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if (q[i].doc >= e->n_docs) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    void* buf = nullptr;
+    const size_t qb = (size_t)n * sizeof(mt_tile_query), rb = (size_t)n * sizeof(mt_tile_result);
+    if (hipMalloc(&buf, qb + rb) != hipSuccess) return MT_ERR_NOMEM;
+    auto* dq = static_cast<mt_tile_query*>(buf);
+    auto* dr = reinterpret_cast<mt_tile_result*>(static_cast<uint8_t*>(buf) + qb);
+    hipError_t r = hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = mt_launch_tiles(&e->g, dq, n, dr, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(out, dr, rb, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    return r == hipSuccess ? MT_OK : MT_ERR_HIP;
 }
 
 mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {

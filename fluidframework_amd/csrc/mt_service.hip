@@ -326,6 +326,108 @@ extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, 
     hipLaunchKernelGGL(mt_fixup_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, ops, n_docs);
     return hipGetLastError();
 }
+// mt_find_tiles: Client.findTile for a batch of queries, one wave per query, over the document's
+// compact HBM state in the local view (include/mtgpu.h; mergeTree.ts:1763-1870, 996-1035)
+__global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile_query* __restrict__ q, uint32_t nq,
+                                                      mt_tile_result* __restrict__ out) {
+    const uint32_t w = blockIdx.x;
+    if (w >= nq) return;
+    const int lane = lane_id();
+    const mt_tile_query qq = q[w];
+    const uint32_t d = qq.doc;
+    const mt_doc_scalars sc = g.sc[d];
+    const int n = sc.nseg;
+    const size_t so = (size_t)d * g.segcap;
+    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    const int pos = qq.pos;
+    auto labeled = [&](int i) -> bool {  // refHasTileLabel (mergeTree.ts:581-597)
+        if (qq.key >= MT_MAX_KEYS || !(g.flags[so + i] & MT_SF_MARKER) || !(text[g.toff[so + i]] & 1u)) return false;
+        const uint32_t v = (uint32_t)(g.props[so + i] >> (8 * qq.key)) & 0xFFu;
+        return v != 0 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
+    };
+    auto local_len = [&](int i) -> int { return (g.flags[so + i] & MT_SF_REMOVED) ? 0 : (int)g.len[so + i]; };
+    int res = -1, rpos = -1;
+    if (qq.preceding) {
+        // search: the last live tile at a position <= pos (shifted children's rightmostTiles, then
+        // the leaf holding pos)
+        int carry = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const int ll = i < n ? local_len(i) : 0;
+            const int incl = wave_incl_scan(ll);
+            const int start = carry + incl - ll;
+            const bool cand = i < n && ll > 0 && start <= pos && labeled(i);
+            const uint64_t m = wave_ballot(cand);
+            if (m) {
+                const int l = 63 - __builtin_clzll(m);
+                res = base + l;
+                rpos = __builtin_amdgcn_readlane(start, l);
+            }
+            if (__builtin_amdgcn_readfirstlane(start) > pos) break;
+            carry += wave_last(incl);
+        }
+    } else {
+        int total = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            total += wave_sum(i < n ? local_len(i) : 0);
+        }
+        if (pos <= total && n > 0) {
+            // the leaf backwardSearch stops on: the last segment starting at or before pos
+            int carry = 0, is = -1, istart = 0, base = 0;
+            for (; base < n; base += 64) {
+                const int i = base + lane;
+                const int ll = i < n ? local_len(i) : 0;
+                const int incl = wave_incl_scan(ll);
+                const int start = carry + incl - ll;
+                const uint64_t m = wave_ballot(i < n && start <= pos);
+                if (m) {
+                    const int l = 63 - __builtin_clzll(m);
+                    is = base + l;
+                    istart = __builtin_amdgcn_readlane(start, l);
+                }
+                if (m != ~0ull) break;
+                carry += wave_last(incl);
+            }
+            // ... unless a trailing empty leaf block comes after it at that same position
+            const bool trailing_empty = is == n - 1 && pos == total && sc.nb[0] > 0 &&
+                                        g.lbcnt[(size_t)d * g.lbcap + sc.nb[0] - 1] == 0;
+            if (!trailing_empty) {
+                if (labeled(is)) {  // recordTileStart: removed or not
+                    res = is;
+                    rpos = istart;
+                } else {
+                    // the first live tile after it (shifted children's leftmostTiles)
+                    int c2 = istart + local_len(is);
+                    for (int b2 = is + 1; b2 < n && res < 0; b2 += 64) {
+                        const int i = b2 + lane;
+                        const int ll = i < n ? local_len(i) : 0;
+                        const int incl = wave_incl_scan(ll);
+                        const uint64_t m = wave_ballot(i < n && ll > 0 && labeled(i));
+                        if (m) {
+                            const int l = __builtin_ctzll(m);
+                            res = b2 + l;
+                            rpos = c2 + __builtin_amdgcn_readlane(incl - ll, l);
+                        }
+                        c2 += wave_last(incl);
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        out[w].pos = res >= 0 ? rpos : -1;
+        out[w].ordinal = res;
+    }
+}
+
+extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q, uint32_t n, mt_tile_result* out,
+                                      hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_tiles_kernel, dim3(n), dim3(64), 0, st, *g, q, n, out);
+    return hipGetLastError();
+}
+
 // mt_events_drain: document d's recorded events (at most evcap) to out + off[d], one wave per document
 __global__ __launch_bounds__(64) void mt_events_pack_kernel(mt_gstate g, uint32_t n_docs, const uint64_t* __restrict__ off,
                                                            mt_event* __restrict__ out) {

@@ -28,6 +28,13 @@ DOC_ERRORS = {0: None,
               8: 'delta-event buffer full'}
 
 
+# mt_tile_query / mt_tile_result (include/mtgpu.h "findTile")
+TILE_QUERY_DTYPE = np.dtype([('doc', '<u4'), ('pos', '<i4'), ('key', 'u1'), ('preceding', 'u1'), ('pad0', 'u1'),
+                             ('pad1', 'u1'), ('vmask', '<u4', (8,)), ('pad2', '<u4')])
+TILE_RESULT_DTYPE = np.dtype([('pos', '<i4'), ('ordinal', '<i4')])
+assert TILE_QUERY_DTYPE.itemsize == 48
+
+
 class MtError(RuntimeError):
     pass
 
@@ -84,6 +91,7 @@ def lib():
         L.mt_snapshot_extract.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u64)]
         L.mt_get_snapshots.argtypes = [vp, u32, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
                                        vp]
+        L.mt_find_tiles.argtypes = [vp, vp, u32, vp]
         L.mt_events_enable.argtypes = [vp, u32]
         L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
@@ -91,7 +99,7 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_set_concurrent_classes', 'mt_events_enable',
+                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_set_concurrent_classes', 'mt_events_enable',
                      'mt_events_drain'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -237,6 +245,14 @@ class MergeEngine:
         buf = ctypes.create_string_buffer(128)
         _check(lib().mt_class_kernel_name(self.h, capacity, buf, 128), 'mt_class_kernel_name')
         return buf.value.decode()
+
+    # -- findTile (include/mtgpu.h) --------------------------------------------------------
+    def find_tiles(self, queries):
+        """Client.findTile for a batch of TILE_QUERY_DTYPE rows: TILE_RESULT_DTYPE rows (pos -1: none)."""
+        q = np.ascontiguousarray(queries, dtype=TILE_QUERY_DTYPE)
+        out = np.zeros(len(q), dtype=TILE_RESULT_DTYPE)
+        _check(lib().mt_find_tiles(self.h, _ptr(q), len(q), _ptr(out)), 'mt_find_tiles')
+        return out
 
     # -- delta / maintenance events (mergeTreeDeltaCallback.ts; include/mtgpu.h) --------------
     def enable_events(self, per_doc=4096):

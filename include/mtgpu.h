@@ -228,6 +228,33 @@ mt_status mt_snapshot_extract(mt_engine* eng, uint32_t d0, uint32_t n, float* ke
 /* Segment count of every document (after sync). */
 mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 
+/* ---- findTile (tiles) ------------------------------------------------
+ * Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> MergeTree.findTile,
+ * mergeTree.ts:1763-1789) for a batch of queries, in the document's local view: preceding = 1
+ * (search, :1793-1829): the last live tile at a position <= pos; preceding = 0 (backwardSearch,
+ * :1831-1870): none past the length; else the leaf the search stops on (the last segment starting
+ * at or before pos -- removed or not -- unless a trailing empty leaf block comes after it) if that
+ * is a tile, otherwise the first live tile after it.  A tile is a Marker whose refType has Tile
+ * (ops.ts:8) and whose "referenceTileLabels" property (key id `key` of the document) holds the
+ * label; the host passes the label as the set of value ids whose label arrays contain it.
+ * The reference answers through HierMergeBlock caches that annotateRange does not refresh
+ * (mergeTree.ts:2584): after an annotate that changes a tile's labels it can report the old labels
+ * until the block is next updated; the engine answers from the current labels. */
+typedef struct mt_tile_query {  /* 48 bytes */
+    uint32_t doc;
+    int32_t pos;                /* startPos */
+    uint8_t key;                /* key id of "referenceTileLabels" in this document (>= 8: no tiles) */
+    uint8_t preceding;
+    uint8_t pad[2];
+    uint32_t vmask[8];          /* bit v: value id v's label array holds the label */
+    uint32_t pad2;
+} mt_tile_query;
+typedef struct mt_tile_result {
+    int32_t pos;                /* the tile's local position (getPosition), -1: none */
+    int32_t ordinal;            /* its index among the document's segments, -1: none */
+} mt_tile_result;
+mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_tile_result* out);
+
 /* ---- delta / maintenance events -------------------------------------
  * What Client.mergeTreeDeltaCallback and mergeTreeMaintenanceCallback receive
  * (mergeTreeDeltaCallback.ts:15-73), fired synchronously inside applyMsg at mergeTree.ts:1981-1988

@@ -25,6 +25,14 @@ const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const MAX_CLIENTS = 64, MAX_KEYS = 8, MAX_VALUES = 255;
 const REC = 32;
 
+function canonicalJson(v) {
+    if (Array.isArray(v)) return "[" + v.map(canonicalJson).join(",") + "]";
+    if (v !== null && typeof v === "object") {
+        return "{" + Object.keys(v).sort().map((k) => JSON.stringify(k) + ":" + canonicalJson(v[k])).join(",") + "}";
+    }
+    return JSON.stringify(v);
+}
+
 class BatchEngine {
     constructor(opts = {}) {
         this.maxDocs = opts.maxDocs || 1;
@@ -200,10 +208,12 @@ class BatchClient {
             const v = props[k];
             let vid = 0;
             if (v !== null) {
-                if (typeof v === "object" || typeof v === "undefined" || (typeof v === "number" && isNaN(v))) {
-                    throw new Error("BatchClient: property values must be JSON primitives");
+                if (typeof v === "undefined" || typeof v === "function" || (typeof v === "number" && isNaN(v))) {
+                    throw new Error("BatchClient: property values must be JSON values");
                 }
-                const key = JSON.stringify(v);
+                // objects and arrays (e.g. referenceTileLabels) are interned by content with sorted
+                // keys: matchProperties compares them structurally (properties.ts:62-93)
+                const key = canonicalJson(v);
                 vid = this.valueIds.get(key);
                 if (vid === undefined) {
                     vid = this.values.length;
@@ -298,6 +308,32 @@ class BatchClient {
     }
 
     getText() { this.engine.flush(); this._checkError(); return native.getText(this.engine.handle, this.doc); }
+
+    /**
+     * Client.findTile (client.ts:1073-1076): the tile holding `tileLabel` in its
+     * "referenceTileLabels" property nearest to startPos -- at or before it (preceding), else at or
+     * after it -- as {tile: {ordinal}, pos}, or undefined (include/mtgpu.h "findTile").
+     */
+    findTile(startPos, tileLabel, preceding = true) {
+        this.engine.flush();
+        this._checkError();
+        const q = Buffer.alloc(48);
+        q.writeUInt32LE(this.doc, 0);
+        q.writeInt32LE(startPos, 4);
+        const kid = this.keyIds.get("referenceTileLabels");
+        q.writeUInt8(kid === undefined ? 0xff : kid, 8);
+        q.writeUInt8(preceding ? 1 : 0, 9);
+        for (let v = 1; v < this.values.length; v++) {
+            const labels = this.values[v];
+            if (Array.isArray(labels) && labels.includes(tileLabel)) {
+                const o = 12 + 4 * (v >> 5);
+                q.writeUInt32LE((q.readUInt32LE(o) | (1 << (v & 31))) >>> 0, o);
+            }
+        }
+        const r = native.findTiles(this.engine.handle, q);
+        const pos = r.readInt32LE(0);
+        return pos < 0 ? undefined : { tile: { ordinal: r.readInt32LE(4) }, pos };
+    }
     getLength() { this.engine.flush(); this._checkError(); return native.getLength(this.engine.handle, this.doc); }
     getCurrentSeq() { return this.currentSeq; }
     getClientId() { return 0; }

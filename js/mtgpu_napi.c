@@ -343,6 +343,28 @@ static napi_value checksums(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* findTiles(engine, queries (48-byte mt_tile_query rows)) -> Buffer of 8-byte mt_tile_result rows */
+static napi_value find_tiles(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 2 ? get_box(env, argv[0]) : NULL;
+    size_t nq = 0;
+    const void* q = b ? buffer_data(env, argv[1], &nq) : NULL;
+    if (!b || nq % sizeof(mt_tile_query)) {
+        napi_throw_type_error(env, NULL, "findTiles(engine, queries)");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(nq / sizeof(mt_tile_query));
+    void* data = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(mt_tile_result) : 1, &data, &out));
+    enter(b);
+    mt_status st = mt_find_tiles(b->e, (const mt_tile_query*)q, n, (mt_tile_result*)data);
+    leave(b);
+    if (st) return throw_status(env, "mt_find_tiles", st);
+    return out;
+}
+
 /* docsLoad(engine, docIdsU32, segRowPtrU32, segs (32-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
  * SnapshotLoader.loadHeader for a batch of documents (mt_docs_load) */
 static napi_value docs_load(napi_env env, napi_callback_info info) {
@@ -512,6 +534,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"version", NULL, version, NULL, NULL, NULL, napi_default, NULL},
         {"eventsEnable", NULL, events_enable, NULL, NULL, NULL, napi_default, NULL},
         {"docsLoad", NULL, docs_load, NULL, NULL, NULL, napi_default, NULL},
+        {"findTiles", NULL, find_tiles, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
         {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},

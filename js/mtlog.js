@@ -27,31 +27,40 @@ function readOp(log, i) {
     };
 }
 
-function propsOf(log, r) {
+// Tile-label logs (opts.tileKey = k): key k is the reserved "referenceTileLabels" property
+// (mergeTree.ts:575) and its value id v the label array ["L<i>" for every bit i of v]
+function tileLabels(v) {
+    const out = [];
+    for (let i = 0; i < 8; i++) if ((v >> i) & 1) out.push("L" + i);
+    return out;
+}
+
+function propsOf(log, r, opts) {
     const np = (r.flags >> 3) & 15;
     const start = log.payOff + r.poff + r.plen - 2 * np;
     const props = {};
     for (let q = 0; q < np; q++) {
         const k = log.buf.readUInt8(start + 2 * q), v = log.buf.readUInt8(start + 2 * q + 1);
-        props["k" + k] = v === 0 ? null : v;
+        if (opts && opts.tileKey === k) props.referenceTileLabels = v === 0 ? null : tileLabels(v);
+        else props["k" + k] = v === 0 ? null : v;
     }
     return props;
 }
 
-function toOp(log, r) {
+function toOp(log, r, opts) {
     const np = (r.flags >> 3) & 15;
     if (r.type === 0 && (r.flags & 128)) {
         const seg = { marker: { refType: log.buf.readUInt8(log.payOff + r.poff) } };
-        if (r.flags & 2) seg.props = propsOf(log, r);
+        if (r.flags & 2) seg.props = propsOf(log, r, opts);
         return { type: 0, pos1: r.pos1, seg };
     }
     if (r.type === 0) {
         const text = log.buf.toString("latin1", log.payOff + r.poff, log.payOff + r.poff + r.plen - 2 * np);
-        return { type: 0, pos1: r.pos1, seg: (r.flags & 2) ? { text, props: propsOf(log, r) } : text };
+        return { type: 0, pos1: r.pos1, seg: (r.flags & 2) ? { text, props: propsOf(log, r, opts) } : text };
     }
     if (r.type === 1) return { type: 1, pos1: r.pos1, pos2: r.pos2 };
     if (r.type === 2) {
-        const op = { type: 2, pos1: r.pos1, pos2: r.pos2, props: propsOf(log, r) };
+        const op = { type: 2, pos1: r.pos1, pos2: r.pos2, props: propsOf(log, r, opts) };
         if (r.flags & 1) op.combiningOp = { name: "rewrite" };
         return op;
     }
@@ -67,11 +76,11 @@ function msgOf(r, op) {
 }
 
 /** The messages of document d, GROUP members folded into one message (client.ts:782-790). */
-function* messages(log, d) {
+function* messages(log, d, opts) {
     let group = null;
     for (let i = log.rowPtr[d]; i < log.rowPtr[d + 1]; i++) {
         const r = readOp(log, i);
-        const op = toOp(log, r);
+        const op = toOp(log, r, opts);
         if (group || (r.flags & 4)) {
             if (!group) group = { r, ops: [] };
             if (op) group.ops.push(op);
@@ -85,4 +94,4 @@ function* messages(log, d) {
     }
 }
 
-module.exports = { loadLog, messages };
+module.exports = { loadLog, messages, tileLabels };

@@ -708,6 +708,82 @@ struct Doc {
         return t;
     }
     int length(int32_t R, int32_t C) const { return nodeLen(root, R, C); }
+
+    // ------------------------------------------------------------------- findTile
+    // Client.findTile -> MergeTree.findTile (client.ts:1073-1076, mergeTree.ts:1763-1789) for the
+    // own client: search / backwardSearch (:1797-1870) in the local view, leaf action
+    // recordTileStart and shift action tileShift (:996-1035), whose block case reads the
+    // HierMergeBlock's rightmostTiles / leftmostTiles (the right- / leftmost live tile of the
+    // block, addNodeReferences :263-318).  A tile: a Marker whose refType has Tile (ops.ts:8) and
+    // whose "referenceTileLabels" (property `key`) value id is in `vmask` (refHasTileLabel :588).
+    struct TileQ {
+        int key;
+        const uint8_t* vmask;  // 256 bits
+        bool has(const Seg* s) const {
+            if (!s->marker || !(s->text.size() && ((uint8_t)s->text[0] & 1u))) return false;
+            const int v = s->props[key];
+            return v != 0 && ((vmask[v >> 3] >> (v & 7)) & 1);
+        }
+    };
+    static const Seg* edgeTile(const Node* n, const TileQ& q, bool rightmost) {
+        if (n->leaf) {
+            const Seg* s = static_cast<const Seg*>(n);
+            return localLen(s) > 0 && q.has(s) ? s : nullptr;
+        }
+        const Block* b = static_cast<const Block*>(n);
+        for (int i = 0; i < b->childCount; i++) {
+            const Seg* t = edgeTile(b->children[rightmost ? b->childCount - 1 - i : i], q, rightmost);
+            if (t) return t;
+        }
+        return nullptr;
+    }
+    void searchTile(const Block* b, int pos, const TileQ& q, const Seg*& tile) const {
+        for (int i = 0; i < b->childCount; i++) {
+            const Node* ch = b->children[i];
+            const int len = localNodeLen(ch);
+            if (pos < len) {
+                if (!ch->leaf) return searchTile(static_cast<const Block*>(ch), pos, q, tile);
+                if (q.has(static_cast<const Seg*>(ch))) tile = static_cast<const Seg*>(ch);  // recordTileStart
+                return;
+            }
+            if (const Seg* t = edgeTile(ch, q, true)) tile = t;  // tileShift
+            pos -= len;
+        }
+    }
+    void backwardSearchTile(const Block* b, int pos, int segEnd, const TileQ& q, const Seg*& tile) const {
+        for (int i = b->childCount - 1; i >= 0; i--) {
+            const Node* ch = b->children[i];
+            const int len = localNodeLen(ch);
+            const int segpos = segEnd - len;
+            if (pos >= segpos) {
+                if (!ch->leaf) return backwardSearchTile(static_cast<const Block*>(ch), pos, segEnd, q, tile);
+                if (q.has(static_cast<const Seg*>(ch))) tile = static_cast<const Seg*>(ch);  // (removed or not)
+                return;
+            }
+            if (const Seg* t = edgeTile(ch, q, false)) tile = t;
+            segEnd = segpos;
+        }
+    }
+    // the tile's local position (getPosition), or -1 when there is none
+    int findTile(int pos, int key, const uint8_t* vmask, bool preceding) const {
+        const TileQ q{key, vmask};
+        const Seg* tile = nullptr;
+        if (preceding) {
+            searchTile(root, pos, q, tile);
+        } else {
+            const int len = localNodeLen(root);
+            if (pos > len) return -1;
+            backwardSearchTile(root, pos, len, q, tile);
+        }
+        if (!tile) return -1;
+        int at = 0;
+        bool found = false;
+        walkSegs(root, [&](const Seg* s) {
+            if (s == tile) found = true;
+            if (!found) at += localLen(s);
+        });
+        return at;
+    }
 };
 
 // ------------------------------------------------------------------ checksum
@@ -932,6 +1008,11 @@ int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_se
     e->docs[doc] = Doc();
     e->docs[doc].reload(segs, n_segs, text, min_seq, cur_seq);
     return 0;
+}
+
+// Client.findTile of document `doc` (tile labels: property `key`, value ids in the 256-bit vmask)
+int32_t mto_find_tile(mto_engine* e, uint32_t doc, int32_t pos, uint32_t key, const uint8_t* vmask, int preceding) {
+    return e->docs[doc].findTile(pos, (int)key, vmask, preceding != 0);
 }
 
 // delta / maintenance events (mt_event form) of every document from now on

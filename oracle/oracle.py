@@ -56,6 +56,8 @@ def lib():
         L.mto_load.restype = ctypes.c_int
         L.mto_load.argtypes = [vp, u32, vp, u32, vp, i32, i32]
         L.mto_record_events.argtypes = [vp, ctypes.c_int]
+        L.mto_find_tile.restype = i32
+        L.mto_find_tile.argtypes = [vp, u32, i32, u32, vp, ctypes.c_int]
         L.mto_events.restype = u64
         L.mto_events.argtypes = [vp, u32, vp, u64]
         L.mto_seg_hash.restype = u64
@@ -124,6 +126,12 @@ class Oracle:
     def events(self, doc):
         """the document's delta / maintenance callbacks in canonical form (fluidframework_amd.events)"""
         return callbacks(self.event_rows(doc))
+
+    def find_tile(self, doc, pos, key, vmask, preceding=True):
+        """Client.findTile: the tile's position or None (vmask: 32-byte bitmask of label value ids)"""
+        m = np.ascontiguousarray(vmask, dtype=np.uint8)
+        r = lib().mto_find_tile(self.h, doc, pos, key, _ptr(m), 1 if preceding else 0)
+        return None if r < 0 else r
 
     def checksums(self):
         out = np.zeros(self.n_docs, dtype=np.uint64)

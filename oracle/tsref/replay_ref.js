@@ -271,6 +271,37 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "tiles") {
+        // findTile (client.ts:1073-1076, mergeTree.ts:1763-1789) on each document after its whole
+        // log, key <tileKey> carrying the tile labels (mtlog.js tileLabels); queries: every label
+        // L0..L3, both directions, at a spread of positions around and past the length
+        const tileKey = parseInt(process.argv[4] || "7", 10);
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const c = newObserver();
+            let err = null;
+            try {
+                for (const m of messages(log, d, { tileKey })) c.applyMsg(m);
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            const len = c.getLength();
+            const ps = Array.from(new Set([0, 1, 2, len >> 3, len >> 2, len >> 1, (3 * len) >> 2, len - 2, len - 1, len,
+                len + 1].filter((p) => p >= 0))).sort((a, b) => a - b);
+            const answers = [];
+            for (const p of ps) {
+                for (let l = 0; l < 4; l++) {
+                    for (const preceding of [true, false]) {
+                        const t = c.findTile(p, "L" + l, preceding);
+                        answers.push([p, l, preceding ? 1 : 0, t ? t.pos : null]);
+                    }
+                }
+            }
+            out.push(JSON.stringify({ doc: d, err, len, answers }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "errstate") {
         const out = [];
         for (let d = 0; d < log.nDocs; d++) {

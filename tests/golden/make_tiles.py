@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/tiles.expected.jsonl FROM THE REFERENCE ITSELF (build container only).
+
+Client.findTile(startPos, tileLabel, preceding) (client.ts:1073-1076 -> mergeTree.ts:1763-1789:
+search / backwardSearch with the HierMergeBlock rightmostTiles / leftmostTiles caches) asked of the
+reference's own observer Client after each document's log.  Tile labels ride on property key 0:
+value id v is the label array ["L<i>" for each bit i of v] under "referenceTileLabels"
+(mergeTree.ts:575; js/mtlog.js tileLabels).
+  * tiles_scenarios: the findTile cases of client.spec.ts:28-210 restated as remote inserts
+    (label "EOP" -> "L0"), plus removed / re-annotated tiles;
+  * tiles_synth: marker-heavy synthetic logs (refTypes Tile / NestBegin / NestEnd, labels set at
+    insert, tiles removed and zambonied; no annotates, see synthetic()).
+One JSON line per (log, document): {log, doc, err, len, answers: [[pos, label, preceding, tile pos |
+null], ...]}.
+"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from fluidframework_amd.oplog import REF_NEST_BEGIN, REF_TILE  # noqa: E402
+from make_golden import A, I, M, N, R, build_log  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+TILE_KEY = 0
+
+
+def scenarios():
+    docs = []
+    L0 = {TILE_KEY: 1}
+    # client.spec.ts:29-52: tile at 0, then "abc" at 0 -> tile at 3
+    docs.append([M(1, 0, 0, 1, 0, REF_TILE, L0), I(2, 1, 0, 1, 0, 'abc')])
+    # :54-75: "abc d", tile at 0
+    docs.append([I(1, 0, 0, 1, 0, 'abc d'), M(2, 1, 0, 1, 0, REF_TILE, L0)])
+    # :77-149: tile, "abc d" at 0, tile at 0, "ef" at 7, tile at 8
+    docs.append([M(1, 0, 0, 1, 0, REF_TILE, L0), I(2, 1, 0, 1, 0, 'abc d'), M(3, 2, 0, 1, 0, REF_TILE, L0),
+                 I(4, 3, 0, 1, 7, 'ef'), M(5, 4, 0, 1, 8, REF_TILE, L0)])
+    # :151-177: a single tile
+    docs.append([M(1, 0, 0, 1, 0, REF_TILE, L0)])
+    # :179-203: tile then "abc" before it; index past the end
+    docs.append([M(1, 0, 0, 1, 0, REF_TILE, L0), I(2, 1, 0, 1, 0, 'abc')])
+    # :205-: text without any tile
+    docs.append([I(1, 0, 0, 1, 0, 'abc')])
+    # removed tiles (a removed tile is only found as the leaf a backward search stops on), a
+    # NestBegin marker with labels (not a Tile), labels rewritten by annotate, an empty document
+    docs.append([I(1, 0, 0, 1, 0, 'hello world'), M(2, 1, 0, 2, 5, REF_TILE, {TILE_KEY: 3}),
+                 M(3, 2, 0, 1, 8, REF_NEST_BEGIN, {TILE_KEY: 1}), M(4, 3, 0, 2, 12, REF_TILE, {TILE_KEY: 2}),
+                 R(5, 4, 0, 1, 5, 6), A(6, 5, 0, 2, 0, 13, {TILE_KEY: 4}), M(7, 6, 0, 3, 13, REF_TILE, L0),
+                 R(8, 7, 0, 2, 13, 14)])
+    docs.append([I(1, 0, 0, 1, 0, 'ab'), R(2, 1, 0, 1, 0, 2)])
+    # many tiles through block splits, then zamboni (msn advance)
+    d, s = [], 0
+    for k in range(24):
+        s += 1
+        d.append(M(s, s - 1, 0, 1 + k % 3, k, REF_TILE, {TILE_KEY: 1 + k % 7}) if k % 2 == 0
+                 else I(s, s - 1, 0, 1 + k % 3, k, 'p%d' % k))
+    s += 1
+    d.append(R(s, s - 1, 0, 2, 10, 20))
+    for _ in range(4):
+        s += 1
+        d.append(N(s, s - 1))
+    docs.append(d)
+    return build_log(docs)
+
+
+def synthetic():
+    # inserts and removes only: an annotate that changes a tile's labels leaves the reference's
+    # HierMergeBlock tile caches stale (annotateRange refreshes no block, mergeTree.ts:2584), which
+    # the engine does not reproduce (DESIGN.md "findTile")
+    return oracle.generate(16, seed=404, n_clients=10, ops_per_doc=500, max_lag=24, n_keys=2, n_values=15,
+                           p_insert=0.6, p_remove=0.4, p_overlap=0.4, p_insert_props=0.6, p_marker=0.4)
+
+
+def main():
+    subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
+    oracle.build()
+    replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
+    out = []
+    for name, batch in (('tiles_scenarios', scenarios()), ('tiles_synth', synthetic())):
+        path = os.path.join(HERE, name + '.mtlog')
+        batch.save(path)
+        res = subprocess.run(['node', replay, 'tiles', path, str(TILE_KEY)], check=True, capture_output=True,
+                             text=True)
+        for line in res.stdout.strip().split('\n'):
+            r = json.loads(line)
+            out.append(json.dumps(dict(log=name, **r), separators=(',', ':')))
+        print(name, batch.n_docs, 'docs')
+    with open(os.path.join(HERE, 'tiles.expected.jsonl'), 'w') as f:
+        f.write('\n'.join(out) + '\n')
+
+
+if __name__ == '__main__':
+    main()

@@ -206,3 +206,19 @@ def test_batchclient_loads_reference_snapshot_files():
         assert _js_state_to_log(g['loaded']) == c['loaded'], g['file']
         assert (g['err'] is None) == (err_code(c['err']) == 0), g['file']
         assert _js_state_to_log(g['state']) == c['state'], g['file']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth'])
+def test_batchclient_find_tile_matches_reference(name):
+    """BatchClient.findTile (mt_find_tiles via the addon; label arrays interned by content) gives
+    the reference Client.findTile answers of tests/golden/tiles.expected.jsonl."""
+    from test_tiles import load_tiles
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_tiles.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          os.path.join(GOLDEN, 'tiles.expected.jsonl'), name, '0'], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r['answers'] for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    for r in load_tiles()[name]:
+        assert got[r['doc']] == r['answers'], (name, r['doc'])

@@ -40,6 +40,8 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                                     uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
                                     hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
+extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* q, uint32_t n, uint32_t cap,
+                                       mt_stack_item* items, uint32_t* depth, hipStream_t st);
 extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q, uint32_t n, mt_tile_result* out,
                                       hipStream_t st);
 extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
@@ -321,6 +323,30 @@ mt_status mt_find_tiles(mt_engine* e, const mt_tile_query* q, uint32_t n, mt_til
     hipError_t r = hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, e->stream);
     if (r == hipSuccess) r = mt_launch_tiles(&e->g, dq, n, dr, e->stream);
     if (r == hipSuccess) r = hipMemcpyAsync(out, dr, rb, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    return r == hipSuccess ? MT_OK : MT_ERR_HIP;
+}
+
+mt_status mt_range_stacks(mt_engine* e, const mt_tile_query* q, uint32_t n, uint32_t cap, mt_stack_item* items,
+                          uint32_t* depth) {
+    static_assert(sizeof(mt_stack_item) == 12, "mt_stack_item is 12 bytes");
+    if (!e || (n && (!q || !depth || (cap && !items)))) return MT_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if (q[i].doc >= e->n_docs) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    void* buf = nullptr;
+    const size_t qb = (size_t)n * sizeof(mt_tile_query), ib = (size_t)n * cap * sizeof(mt_stack_item),
+                 db = (size_t)n * sizeof(uint32_t);
+    if (hipMalloc(&buf, qb + ib + db) != hipSuccess) return MT_ERR_NOMEM;
+    auto* dq = static_cast<mt_tile_query*>(buf);
+    auto* di = reinterpret_cast<mt_stack_item*>(static_cast<uint8_t*>(buf) + qb);
+    auto* dd = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + qb + ib);
+    hipError_t r = hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = mt_launch_stacks(&e->g, dq, n, cap, di, dd, e->stream);
+    if (r == hipSuccess && ib) r = hipMemcpyAsync(items, di, ib, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(depth, dd, db, hipMemcpyDeviceToHost, e->stream);
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
     (void)hipFree(buf);
     return r == hipSuccess ? MT_OK : MT_ERR_HIP;

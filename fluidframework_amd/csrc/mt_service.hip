@@ -428,6 +428,68 @@ extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q
     return hipGetLastError();
 }
 
+// mt_range_stacks: Client.getStackContext for a batch of (document, position, label) queries, one wave
+// per query (include/mtgpu.h; mergeTree.ts:1750-1760, 953-994, 246-261).  The stack is always its
+// unmatched ends followed by its unmatched begins (an end is pushed only when the top is not a
+// begin), so the fold needs only the two lengths: ends `a`, depth `t`; the top is a begin iff t > a.
+__global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_tile_query* __restrict__ q, uint32_t nq,
+                                                       uint32_t cap, mt_stack_item* __restrict__ items,
+                                                       uint32_t* __restrict__ depth) {
+    const uint32_t w = blockIdx.x;
+    if (w >= nq) return;
+    const int lane = lane_id();
+    const mt_tile_query qq = q[w];
+    const uint32_t d = qq.doc;
+    const mt_doc_scalars sc = g.sc[d];
+    const int n = sc.nseg;
+    const size_t so = (size_t)d * g.segcap;
+    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    const int pos = qq.pos;
+    mt_stack_item* out = items + (size_t)w * cap;
+    int a = 0, t = 0, carry = 0;
+    bool touched = false;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const int ll = (i < n && !(g.flags[so + i] & MT_SF_REMOVED)) ? (int)g.len[so + i] : 0;
+        const int incl = wave_incl_scan(ll);
+        const int start = carry + incl - ll;
+        uint32_t rt = 0;
+        bool cand = false;
+        if (i < n && ll > 0 && start <= pos && qq.key < MT_MAX_KEYS && (g.flags[so + i] & MT_SF_MARKER)) {
+            rt = text[g.toff[so + i]];
+            const uint32_t v = (uint32_t)(g.props[so + i] >> (8 * qq.key)) & 0xFFu;
+            cand = (rt & 6u) && v != 0 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
+        }
+        uint64_t m = wave_ballot(cand);
+        touched |= m != 0;
+        while (m) {  // applyRangeReference for each, in document order
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t r = __builtin_amdgcn_readlane(rt, l);
+            int slot = -1;
+            if (r & 2u) {
+                slot = t++;
+            } else if (t > a) {
+                t--;
+            } else {
+                slot = t++;
+                a = t;
+            }
+            if (slot >= 0 && slot < (int)cap && lane == l) out[slot] = mt_stack_item{start, i, r};
+        }
+        if (__builtin_amdgcn_readfirstlane(start) > pos) break;
+        carry += wave_last(incl);
+    }
+    if (lane == 0) depth[w] = (uint32_t)t | (touched ? MT_STACK_TOUCHED : 0u);
+}
+
+extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* q, uint32_t n, uint32_t cap,
+                                       mt_stack_item* items, uint32_t* depth, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_stacks_kernel, dim3(n), dim3(64), 0, st, *g, q, n, cap, items, depth);
+    return hipGetLastError();
+}
+
 // mt_events_drain: document d's recorded events (at most evcap) to out + off[d], one wave per document
 __global__ __launch_bounds__(64) void mt_events_pack_kernel(mt_gstate g, uint32_t n_docs, const uint64_t* __restrict__ off,
                                                            mt_event* __restrict__ out) {

@@ -33,6 +33,8 @@ TILE_QUERY_DTYPE = np.dtype([('doc', '<u4'), ('pos', '<i4'), ('key', 'u1'), ('pr
                              ('pad1', 'u1'), ('vmask', '<u4', (8,)), ('pad2', '<u4')])
 TILE_RESULT_DTYPE = np.dtype([('pos', '<i4'), ('ordinal', '<i4')])
 assert TILE_QUERY_DTYPE.itemsize == 48
+# mt_stack_item (include/mtgpu.h "range stacks")
+STACK_ITEM_DTYPE = np.dtype([('pos', '<i4'), ('ordinal', '<i4'), ('ref_type', '<u4')])
 
 
 class MtError(RuntimeError):
@@ -92,6 +94,7 @@ def lib():
         L.mt_get_snapshots.argtypes = [vp, u32, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
                                        vp]
         L.mt_find_tiles.argtypes = [vp, vp, u32, vp]
+        L.mt_range_stacks.argtypes = [vp, vp, u32, u32, vp, vp]
         L.mt_events_enable.argtypes = [vp, u32]
         L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
@@ -99,8 +102,8 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_set_concurrent_classes', 'mt_events_enable',
-                     'mt_events_drain'):
+                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_range_stacks', 'mt_set_concurrent_classes',
+                     'mt_events_enable', 'mt_events_drain'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -253,6 +256,19 @@ class MergeEngine:
         out = np.zeros(len(q), dtype=TILE_RESULT_DTYPE)
         _check(lib().mt_find_tiles(self.h, _ptr(q), len(q), _ptr(out)), 'mt_find_tiles')
         return out
+
+    def range_stacks(self, queries, cap=64):
+        """Client.getStackContext for a batch of TILE_QUERY_DTYPE rows (key: the range-labels key id,
+        vmask: the label's value ids; preceding ignored): one list of STACK_ITEM_DTYPE rows per
+        query, bottom to top.  A stack deeper than `cap` is asked again with room for it."""
+        q = np.ascontiguousarray(queries, dtype=TILE_QUERY_DTYPE)
+        items = np.zeros((len(q), cap), dtype=STACK_ITEM_DTYPE)
+        depth = np.zeros(len(q), dtype=np.uint32)
+        _check(lib().mt_range_stacks(self.h, _ptr(q), len(q), cap, _ptr(items), _ptr(depth)), 'mt_range_stacks')
+        depth &= 0x7FFFFFFF  # MT_STACK_DEPTH
+        if len(q) and int(depth.max()) > cap:
+            return self.range_stacks(q, int(depth.max()))
+        return [items[i, :int(depth[i])] for i in range(len(q))]
 
     # -- delta / maintenance events (mergeTreeDeltaCallback.ts; include/mtgpu.h) --------------
     def enable_events(self, per_doc=4096):

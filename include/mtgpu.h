@@ -255,6 +255,29 @@ typedef struct mt_tile_result {
 } mt_tile_result;
 mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_tile_result* out);
 
+/* ---- range stacks -----------------------------------------------------
+ * Client.getStackContext(startPos, [rangeLabel]) (client.ts:946-948 -> MergeTree.getStackContext,
+ * mergeTree.ts:1750-1760) for a batch of (document, position, label) queries in the local view: the
+ * live range markers (refType NestBegin | NestEnd, ops.ts:8) whose "referenceRangeLabels" property
+ * (key id `q.key`) holds the label, at positions <= pos (the shifted ones and the leaf holding pos),
+ * folded in document order by applyRangeReference (mergeTree.ts:246-261: NestBegin pushes; an end
+ * pops a NestBegin top and is pushed otherwise).  The stack is therefore its unmatched ends followed
+ * by its unmatched begins.  Query i's stack, bottom to top, goes to items[i*cap ...] (at most cap
+ * entries) and its full depth to depth[i] & MT_STACK_DEPTH; MT_STACK_TOUCHED is set when any such
+ * marker was folded (the reference's RangeStackMap then holds the label, possibly with an empty
+ * stack; otherwise the label is absent).  q.preceding is ignored.  Like findTile, the reference
+ * folds HierMergeBlock rangeStacks caches that annotateRange does not refresh (mergeTree.ts:2584);
+ * the engine answers from the current labels. */
+#define MT_STACK_DEPTH 0x7FFFFFFFu
+#define MT_STACK_TOUCHED 0x80000000u
+typedef struct mt_stack_item {  /* 12 bytes */
+    int32_t pos;                /* the marker's local position (getPosition) */
+    int32_t ordinal;            /* its index among the document's segments */
+    uint32_t ref_type;          /* its refType */
+} mt_stack_item;
+mt_status mt_range_stacks(mt_engine* eng, const mt_tile_query* q, uint32_t n, uint32_t cap, mt_stack_item* items,
+                          uint32_t* depth);
+
 /* ---- delta / maintenance events -------------------------------------
  * What Client.mergeTreeDeltaCallback and mergeTreeMaintenanceCallback receive
  * (mergeTreeDeltaCallback.ts:15-73), fired synchronously inside applyMsg at mergeTree.ts:1981-1988

@@ -318,22 +318,61 @@ class BatchClient {
         this.engine.flush();
         this._checkError();
         const q = Buffer.alloc(48);
-        q.writeUInt32LE(this.doc, 0);
-        q.writeInt32LE(startPos, 4);
-        const kid = this.keyIds.get("referenceTileLabels");
-        q.writeUInt8(kid === undefined ? 0xff : kid, 8);
-        q.writeUInt8(preceding ? 1 : 0, 9);
-        for (let v = 1; v < this.values.length; v++) {
-            const labels = this.values[v];
-            if (Array.isArray(labels) && labels.includes(tileLabel)) {
-                const o = 12 + 4 * (v >> 5);
-                q.writeUInt32LE((q.readUInt32LE(o) | (1 << (v & 31))) >>> 0, o);
-            }
-        }
+        this._labelQuery(q, 0, "referenceTileLabels", startPos, tileLabel, preceding);
         const r = native.findTiles(this.engine.handle, q);
         const pos = r.readInt32LE(0);
         return pos < 0 ? undefined : { tile: { ordinal: r.readInt32LE(4) }, pos };
     }
+    // one 48-byte mt_tile_query: `label` as the set of value ids whose label arrays (property `key`) hold it
+    _labelQuery(q, off, key, pos, label, preceding) {
+        q.writeUInt32LE(this.doc, off);
+        q.writeInt32LE(pos, off + 4);
+        const kid = this.keyIds.get(key);
+        q.writeUInt8(kid === undefined ? 0xff : kid, off + 8);
+        q.writeUInt8(preceding ? 1 : 0, off + 9);
+        for (let v = 1; v < this.values.length; v++) {
+            const labels = this.values[v];
+            if (Array.isArray(labels) && labels.includes(label)) {
+                const o = off + 12 + 4 * (v >> 5);
+                q.writeUInt32LE((q.readUInt32LE(o) | (1 << (v & 31))) >>> 0, o);
+            }
+        }
+    }
+
+    /**
+     * Client.getStackContext (client.ts:946-948): for each of `rangeLabels` that a live NestBegin /
+     * NestEnd marker at or before startPos carries in "referenceRangeLabels", the stack
+     * applyRangeReference folds them into, as {items: [{ordinal, pos, refType}, ...]} bottom to top
+     * (include/mtgpu.h "range stacks").
+     */
+    getStackContext(startPos, rangeLabels) {
+        this.engine.flush();
+        this._checkError();
+        const n = rangeLabels.length;
+        const q = Buffer.alloc(48 * n);
+        rangeLabels.forEach((l, i) => this._labelQuery(q, 48 * i, "referenceRangeLabels", startPos, l, false));
+        let cap = 16;
+        let [items, depth] = native.rangeStacks(this.engine.handle, q, cap);
+        let deepest = 0;
+        for (let i = 0; i < n; i++) deepest = Math.max(deepest, depth.readUInt32LE(4 * i) & 0x7fffffff);
+        if (deepest > cap) {
+            cap = deepest;
+            [items, depth] = native.rangeStacks(this.engine.handle, q, cap);
+        }
+        const stacks = {};
+        rangeLabels.forEach((l, i) => {
+            const w = depth.readUInt32LE(4 * i);
+            if (!(w & 0x80000000)) return;  // no marker of the label: absent, as in the reference's map
+            const st = [];
+            for (let k = 0; k < (w & 0x7fffffff); k++) {
+                const o = 12 * (i * cap + k);
+                st.push({ pos: items.readInt32LE(o), ordinal: items.readInt32LE(o + 4), refType: items.readUInt32LE(o + 8) });
+            }
+            stacks[l] = { items: st };
+        });
+        return stacks;
+    }
+
     getLength() { this.engine.flush(); this._checkError(); return native.getLength(this.engine.handle, this.doc); }
     getCurrentSeq() { return this.currentSeq; }
     getClientId() { return 0; }

@@ -365,6 +365,34 @@ static napi_value find_tiles(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* rangeStacks(engine, queries (48-byte mt_tile_query rows), cap) -> [Buffer of n*cap 12-byte mt_stack_item
+ * rows, Buffer of n uint32 depth words (MT_STACK_TOUCHED | depth)] */
+static napi_value range_stacks(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out, ib, db;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 3 ? get_box(env, argv[0]) : NULL;
+    size_t nq = 0;
+    const void* q = b ? buffer_data(env, argv[1], &nq) : NULL;
+    uint32_t cap = 0;
+    if (!b || nq % sizeof(mt_tile_query) || napi_get_value_uint32(env, argv[2], &cap) != napi_ok) {
+        napi_throw_type_error(env, NULL, "rangeStacks(engine, queries, cap)");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(nq / sizeof(mt_tile_query));
+    void *items = NULL, *depth = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, (size_t)n * cap ? (size_t)n * cap * sizeof(mt_stack_item) : 1, &items, &ib));
+    NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(uint32_t) : 1, &depth, &db));
+    enter(b);
+    mt_status st = mt_range_stacks(b->e, (const mt_tile_query*)q, n, cap, (mt_stack_item*)items, (uint32_t*)depth);
+    leave(b);
+    if (st) return throw_status(env, "mt_range_stacks", st);
+    NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
+    NAPI_CALL(env, napi_set_element(env, out, 0, ib));
+    NAPI_CALL(env, napi_set_element(env, out, 1, db));
+    return out;
+}
+
 /* docsLoad(engine, docIdsU32, segRowPtrU32, segs (32-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
  * SnapshotLoader.loadHeader for a batch of documents (mt_docs_load) */
 static napi_value docs_load(napi_env env, napi_callback_info info) {
@@ -535,6 +563,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"eventsEnable", NULL, events_enable, NULL, NULL, NULL, napi_default, NULL},
         {"docsLoad", NULL, docs_load, NULL, NULL, NULL, napi_default, NULL},
         {"findTiles", NULL, find_tiles, NULL, NULL, NULL, napi_default, NULL},
+        {"rangeStacks", NULL, range_stacks, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
         {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},

@@ -28,7 +28,8 @@ function readOp(log, i) {
 }
 
 // Tile-label logs (opts.tileKey = k): key k is the reserved "referenceTileLabels" property
-// (mergeTree.ts:575) and its value id v the label array ["L<i>" for every bit i of v]
+// (mergeTree.ts:575) and its value id v the label array ["L<i>" for every bit i of v]; the same
+// for opts.rangeKey and "referenceRangeLabels" (mergeTree.ts:576)
 function tileLabels(v) {
     const out = [];
     for (let i = 0; i < 8; i++) if ((v >> i) & 1) out.push("L" + i);
@@ -42,6 +43,7 @@ function propsOf(log, r, opts) {
     for (let q = 0; q < np; q++) {
         const k = log.buf.readUInt8(start + 2 * q), v = log.buf.readUInt8(start + 2 * q + 1);
         if (opts && opts.tileKey === k) props.referenceTileLabels = v === 0 ? null : tileLabels(v);
+        else if (opts && opts.rangeKey === k) props.referenceRangeLabels = v === 0 ? null : tileLabels(v);
         else props["k" + k] = v === 0 ? null : v;
     }
     return props;

@@ -784,6 +784,69 @@ struct Doc {
         });
         return at;
     }
+
+    // ------------------------------------------------------------------- getStackContext
+    // Client.getStackContext -> MergeTree.getStackContext (client.ts:946-948, mergeTree.ts:1750-1760)
+    // for one range label: search (:1797-1829) with leaf action recordRangeLeaf and shift action
+    // rangeShift (:965-994) -- a shifted leaf applies itself when live, a shifted block applies its
+    // HierMergeBlock rangeStacks (addNodeReferences :263-318, built from its live markers) through
+    // applyStackDelta; applyRangeReference (:246-261): NestBegin pushes, an end pops a NestBegin
+    // top and is pushed otherwise.  A range marker: refType NestBegin | NestEnd (ops.ts:8) whose
+    // "referenceRangeLabels" (property `key`) value id is in `vmask` (hasRangeLabel).
+    static void applyRange(std::vector<const Seg*>& st, const Seg* m) {
+        const uint8_t rt = (uint8_t)m->text[0];
+        if (rt & 2u) st.push_back(m);
+        else if (!st.empty() && ((uint8_t)st.back()->text[0] & 2u)) st.pop_back();
+        else st.push_back(m);
+    }
+    static bool rangeMarker(const Seg* s, const TileQ& q) {
+        if (!s->marker || !s->text.size() || !((uint8_t)s->text[0] & 6u)) return false;
+        const int v = s->props[q.key];
+        return v != 0 && ((q.vmask[v >> 3] >> (v & 7)) & 1);
+    }
+    // a block's rangeStacks entry for the label, recomputed from its children
+    static std::vector<const Seg*> blockStack(const Node* n, const TileQ& q) {
+        std::vector<const Seg*> st;
+        if (n->leaf) {
+            const Seg* s = static_cast<const Seg*>(n);
+            if (localLen(s) > 0 && rangeMarker(s, q)) applyRange(st, s);
+            return st;
+        }
+        const Block* b = static_cast<const Block*>(n);
+        for (int i = 0; i < b->childCount; i++)
+            for (const Seg* m : blockStack(b->children[i], q)) applyRange(st, m);  // applyStackDelta
+        return st;
+    }
+    void searchRange(const Block* b, int pos, const TileQ& q, std::vector<const Seg*>& st) const {
+        for (int i = 0; i < b->childCount; i++) {
+            const Node* ch = b->children[i];
+            const int len = localNodeLen(ch);
+            if (pos < len) {
+                if (!ch->leaf) return searchRange(static_cast<const Block*>(ch), pos, q, st);
+                if (rangeMarker(static_cast<const Seg*>(ch), q)) applyRange(st, static_cast<const Seg*>(ch));
+                return;  // recordRangeLeaf
+            }
+            for (const Seg* m : blockStack(ch, q)) applyRange(st, m);  // rangeShift
+            pos -= len;
+        }
+    }
+    // the label's stack bottom to top as (local position, refType)
+    std::vector<std::pair<int, int>> stackContext(int pos, int key, const uint8_t* vmask) const {
+        const TileQ q{key, vmask};
+        std::vector<const Seg*> st;
+        searchRange(root, pos, q, st);
+        std::vector<std::pair<int, int>> out;
+        for (const Seg* m : st) {
+            int at = 0;
+            bool found = false;
+            walkSegs(root, [&](const Seg* s) {
+                if (s == m) found = true;
+                if (!found) at += localLen(s);
+            });
+            out.emplace_back(at, (int)(uint8_t)m->text[0]);
+        }
+        return out;
+    }
 };
 
 // ------------------------------------------------------------------ checksum
@@ -1013,6 +1076,18 @@ int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_se
 // Client.findTile of document `doc` (tile labels: property `key`, value ids in the 256-bit vmask)
 int32_t mto_find_tile(mto_engine* e, uint32_t doc, int32_t pos, uint32_t key, const uint8_t* vmask, int preceding) {
     return e->docs[doc].findTile(pos, (int)key, vmask, preceding != 0);
+}
+
+// Client.getStackContext of document `doc` for one range label (property `key`, value ids in vmask):
+// writes up to cap (position, refType) pairs bottom to top into out; returns the stack depth
+uint32_t mto_stack_context(mto_engine* e, uint32_t doc, int32_t pos, uint32_t key, const uint8_t* vmask, int32_t* out,
+                           uint32_t cap) {
+    const auto st = e->docs[doc].stackContext(pos, (int)key, vmask);
+    for (uint32_t i = 0; i < st.size() && i < cap; i++) {
+        out[2 * i] = st[i].first;
+        out[2 * i + 1] = st[i].second;
+    }
+    return (uint32_t)st.size();
 }
 
 // delta / maintenance events (mt_event form) of every document from now on

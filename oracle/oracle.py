@@ -58,6 +58,8 @@ def lib():
         L.mto_record_events.argtypes = [vp, ctypes.c_int]
         L.mto_find_tile.restype = i32
         L.mto_find_tile.argtypes = [vp, u32, i32, u32, vp, ctypes.c_int]
+        L.mto_stack_context.restype = u32
+        L.mto_stack_context.argtypes = [vp, u32, i32, u32, vp, vp, u32]
         L.mto_events.restype = u64
         L.mto_events.argtypes = [vp, u32, vp, u64]
         L.mto_seg_hash.restype = u64
@@ -132,6 +134,16 @@ class Oracle:
         m = np.ascontiguousarray(vmask, dtype=np.uint8)
         r = lib().mto_find_tile(self.h, doc, pos, key, _ptr(m), 1 if preceding else 0)
         return None if r < 0 else r
+
+    def stack_context(self, doc, pos, key, vmask):
+        """Client.getStackContext for one range label: [[marker position, refType], ...] bottom to top"""
+        m = np.ascontiguousarray(vmask, dtype=np.uint8)
+        out = np.zeros(2 * 64, dtype=np.int32)
+        n = lib().mto_stack_context(self.h, doc, pos, key, _ptr(m), _ptr(out), 64)
+        if n > 64:
+            out = np.zeros(2 * n, dtype=np.int32)
+            lib().mto_stack_context(self.h, doc, pos, key, _ptr(m), _ptr(out), n)
+        return [[int(out[2 * i]), int(out[2 * i + 1])] for i in range(n)]
 
     def checksums(self):
         out = np.zeros(self.n_docs, dtype=np.uint64)

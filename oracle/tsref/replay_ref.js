@@ -302,6 +302,37 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "stacks") {
+        // getStackContext (client.ts:946-948, mergeTree.ts:1750-1760): the NestBegin / NestEnd stack of
+        // each label L0..L3 at a spread of positions, range labels on key <rangeKey>; each stack as
+        // [[marker position, refType], ...] bottom to top ([] when the label has none)
+        const rangeKey = parseInt(process.argv[4] || "1", 10);
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const c = newObserver();
+            let err = null;
+            try {
+                for (const m of messages(log, d, { rangeKey })) c.applyMsg(m);
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            const len = c.getLength();
+            const ps = Array.from(new Set([0, 1, 2, len >> 3, len >> 2, len >> 1, (3 * len) >> 2, len - 2, len - 1, len,
+                len + 1].filter((p) => p >= 0))).sort((a, b) => a - b);
+            const answers = [];
+            for (const p of ps) {
+                for (let l = 0; l < 4; l++) {
+                    const stacks = c.getStackContext(p, ["L" + l]);
+                    const st = stacks["L" + l];
+                    const items = st ? st.items.map((m) => [c.mergeTree.getPosition(m, 0, c.getClientId()), m.refType]) : [];
+                    answers.push([p, l, items]);
+                }
+            }
+            out.push(JSON.stringify({ doc: d, err, len, answers }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "errstate") {
         const out = [];
         for (let d = 0; d < log.nDocs; d++) {

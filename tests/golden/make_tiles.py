@@ -11,7 +11,9 @@ value id v is the label array ["L<i>" for each bit i of v] under "referenceTileL
   * tiles_synth: marker-heavy synthetic logs (refTypes Tile / NestBegin / NestEnd, labels set at
     insert, tiles removed and zambonied; no annotates, see synthetic()).
 One JSON line per (log, document): {log, doc, err, len, answers: [[pos, label, preceding, tile pos |
-null], ...]}.
+null], ...]}.  stacks.expected.jsonl: Client.getStackContext(pos, [label]) (client.ts:946-948,
+mergeTree.ts:1750-1760) on the same logs with range labels on key 1 ("referenceRangeLabels"):
+[[pos, label, [[marker position, refType], ...]], ...].
 """
 import json
 import os
@@ -23,11 +25,12 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 sys.path.insert(0, HERE)
 
-from fluidframework_amd.oplog import REF_NEST_BEGIN, REF_TILE  # noqa: E402
+from fluidframework_amd.oplog import REF_NEST_BEGIN, REF_NEST_END, REF_TILE  # noqa: E402
 from make_golden import A, I, M, N, R, build_log  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 TILE_KEY = 0
+RANGE_KEY = 1
 
 
 def scenarios():
@@ -65,6 +68,13 @@ def scenarios():
         s += 1
         d.append(N(s, s - 1))
     docs.append(d)
+    # range stacks (key 1 = "referenceRangeLabels"): nested NestBegin / NestEnd pairs with mixed
+    # labels, an unmatched end, a removed begin
+    R1 = RANGE_KEY
+    docs.append([I(1, 0, 0, 1, 0, 'abcdefghij'), M(2, 1, 0, 1, 1, REF_NEST_BEGIN, {R1: 1}),
+                 M(3, 2, 0, 1, 3, REF_NEST_BEGIN, {R1: 3}), M(4, 3, 0, 2, 6, REF_NEST_END, {R1: 2}),
+                 M(5, 4, 0, 1, 8, REF_NEST_END, {R1: 1}), M(6, 5, 0, 2, 10, REF_NEST_END, {R1: 1}),
+                 M(7, 6, 0, 3, 12, REF_NEST_BEGIN, {R1: 6}), R(8, 7, 0, 1, 3, 4), M(9, 8, 0, 2, 14, REF_TILE, {R1: 1})])
     return build_log(docs)
 
 
@@ -91,6 +101,16 @@ def main():
             out.append(json.dumps(dict(log=name, **r), separators=(',', ':')))
         print(name, batch.n_docs, 'docs')
     with open(os.path.join(HERE, 'tiles.expected.jsonl'), 'w') as f:
+        f.write('\n'.join(out) + '\n')
+    # getStackContext on the same logs, range labels on key 1
+    out = []
+    for name in ('tiles_scenarios', 'tiles_synth'):
+        res = subprocess.run(['node', replay, 'stacks', os.path.join(HERE, name + '.mtlog'), str(RANGE_KEY)],
+                             check=True, capture_output=True, text=True)
+        for line in res.stdout.strip().split('\n'):
+            r = json.loads(line)
+            out.append(json.dumps(dict(log=name, **r), separators=(',', ':')))
+    with open(os.path.join(HERE, 'stacks.expected.jsonl'), 'w') as f:
         f.write('\n'.join(out) + '\n')
 
 

@@ -23,7 +23,7 @@ def test_addon_loads_and_exports():
         pytest.skip('node headers absent')
     out = subprocess.run([NODE, '-e', "const b=require('./js/batchClient.js');"
                           "for (const f of ['createEngine','submit','submitAsync','getText','getState','getLength',"
-                          "'docError','checksums','version','eventsEnable','eventsDrain']) if (typeof b.native[f] !== 'function') throw f;"
+                          "'docError','checksums','version','eventsEnable','eventsDrain','findTiles','rangeStacks','docsLoad']) if (typeof b.native[f] !== 'function') throw f;"
                           "console.log(b.native.version())"], cwd=REPO, capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
     assert 'gfx950' in out.stdout
@@ -221,4 +221,20 @@ def test_batchclient_find_tile_matches_reference(name):
     assert out.returncode == 0, out.stderr[-2000:]
     got = {r['doc']: r['answers'] for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
     for r in load_tiles()[name]:
+        assert got[r['doc']] == r['answers'], (name, r['doc'])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth'])
+def test_batchclient_stack_context_matches_reference(name):
+    """BatchClient.getStackContext (mt_range_stacks via the addon) gives the reference
+    Client.getStackContext stacks of tests/golden/stacks.expected.jsonl."""
+    from test_stacks import load_stacks
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_stacks.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          os.path.join(GOLDEN, 'stacks.expected.jsonl'), name, '1'], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r['answers'] for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    for r in load_stacks()[name]:
         assert got[r['doc']] == r['answers'], (name, r['doc'])

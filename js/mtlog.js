@@ -77,7 +77,8 @@ function msgOf(r, op) {
     };
 }
 
-/** The messages of document d, GROUP members folded into one message (client.ts:782-790). */
+/** The messages of document d, GROUP members folded into one message (client.ts:782-790); a record
+ * with seq -1 is a local edit of the document's editing client: {local: true, client, op, index}. */
 function* messages(log, d, opts) {
     let group = null;
     for (let i = log.rowPtr[d]; i < log.rowPtr[d + 1]; i++) {
@@ -90,6 +91,10 @@ function* messages(log, d, opts) {
             const g = group;
             group = null;
             yield msgOf(g.r, { type: 3, ops: g.ops });
+            continue;
+        }
+        if (r.seq === -1) {  // an edit of the document's local client (seq UnassignedSequenceNumber)
+            yield { local: true, client: r.client, op, index: i - log.rowPtr[d] };
             continue;
         }
         yield msgOf(r, op);

@@ -37,6 +37,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <list>
 #include <memory>
 #include <random>
 #include <string>
@@ -52,8 +53,14 @@ constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;         // zamboniSegmentsMaxCount, mergeTree.ts:1061
 constexpr int kMaxKeys = 32;
+constexpr int32_t kUnassigned = -1;    // UnassignedSequenceNumber, constants.ts
 
 struct Block;
+struct Seg;
+// SegmentGroup (mergeTree.ts:195-202): the segments one local edit touched, acked together
+struct Group {
+    std::vector<Seg*> segs;
+};
 
 struct Node {
     bool leaf;
@@ -71,6 +78,11 @@ struct Seg : Node {
     bool props_defined = false;
     uint8_t props[kMaxKeys] = {0};    // value id per key (0 = absent)
     bool marker = false;              // a Marker (mergeTree.ts:630-798): text = its one refType byte
+    // an editing client's pending state: segmentGroups (FIFO, mergeTree.ts:441) and the
+    // SegmentPropertiesManager counts (segmentPropertiesManager.ts:11-12)
+    std::vector<Group*> groups;
+    uint8_t pend[kMaxKeys] = {0};
+    int pendRewrite = 0;
     Seg() : Node(true) {}
     int len() const { return (int)text.size(); }
 };
@@ -100,6 +112,10 @@ struct Doc {
     bool rec = false;
     int32_t evSeq = 0;
     std::vector<mt_event> events;
+    // the editing client (collabWindow.clientId): the client of the document's first local edit
+    // (a record with seq -1); its sequenced messages are acks.  -100: an observer
+    int32_t own = -100;
+    std::list<Group> pending;          // MergeTree.pendingSegments (mergeTree.ts:1093)
 
     Doc() { root = newBlock(); }
 
@@ -154,9 +170,10 @@ struct Doc {
     // ---------------------------------------------------------------- visibility
     // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697)
     static int segLen(const Seg* s, int32_t R, int32_t C) {
-        if (s->client == C || s->seq <= R) {
+        if (s->client == C || (s->seq != kUnassigned && s->seq <= R)) {
             if (s->removed) {
-                if (s->rclient == C || (C >= 0 && ((s->overlap >> C) & 1)) || s->rseq <= R) return 0;
+                if (s->rclient == C || (C >= 0 && ((s->overlap >> C) & 1)) || (s->rseq != kUnassigned && s->rseq <= R))
+                    return 0;
             }
             return s->len();
         }
@@ -178,16 +195,45 @@ struct Doc {
         for (int i = 0; i < b->childCount; i++) t += localNodeLen(b->children[i]);
         return t;
     }
+    // nodeLength (mergeTree.ts:1659-1699): the editing client's own view is the local one
+    int viewLen(const Node* n, int32_t R, int32_t C) const { return C == own ? localNodeLen(n) : nodeLen(n, R, C); }
 
-    // breakTie, mergeTree.ts:2248-2277 (clientId is never the observer's own)
-    static bool breakTie(int pos, const Node* n, int32_t R) {
+    // breakTie, mergeTree.ts:2248-2277
+    bool breakTie(int pos, const Node* n, int32_t R, int32_t C) const {
         if (!n->leaf) return true;
         if (pos == 0) {
             const Seg* s = static_cast<const Seg*>(n);
-            if (s->removed && s->rseq <= R) return false;
-            return true;  // seq !== UnassignedSequenceNumber for every acked segment
+            if (s->removed && s->rseq <= R && s->rseq != kUnassigned) return false;
+            if (C == own) return true;             // a local change sees everything
+            return s->seq != kUnassigned;          // newer segments come before older ones
         }
         return false;
+    }
+    // blockInsert's continuePredicate (mergeTree.ts:2143-2160): rightExcursion from block b
+    // (:2313-2343) reaches the first leaf after it that the local view shows, and the insert
+    // continues past b when that leaf is a pending local insert
+    bool continueLocal(const Block* b) const {
+        const Node* node = b;
+        for (const Block* parent = b->parent; parent; node = parent, parent = parent->parent) {
+            bool after = false;
+            for (int i = 0; i < parent->childCount; i++) {
+                const Node* ch = parent->children[i];
+                if (!after) {
+                    after = ch == node;
+                    continue;
+                }
+                if (ch->leaf) return static_cast<const Seg*>(ch)->seq == kUnassigned;  // leafAction, any length
+                if (const Seg* f = firstLocal(ch)) return f->seq == kUnassigned;      // nodeMap, local view
+            }
+        }
+        return false;
+    }
+    static const Seg* firstLocal(const Node* n) {
+        if (n->leaf) return localLen(static_cast<const Seg*>(n)) > 0 ? static_cast<const Seg*>(n) : nullptr;
+        const Block* b = static_cast<const Block*>(n);
+        for (int i = 0; i < b->childCount; i++)
+            if (const Seg* f = firstLocal(b->children[i])) return f;
+        return nullptr;
     }
 
     static void assign(Block* b, Node* child, int i) {
@@ -234,20 +280,33 @@ struct Doc {
         r->client = s->client;
         r->overlap = s->overlap;
         r->marker = s->marker;
+        // segmentGroups.copyTo and the property manager's pending counts (mergeTree.ts:555-560,
+        // segmentPropertiesManager.ts:113-127)
+        r->groups = s->groups;
+        for (Group* g : r->groups) g->segs.push_back(r);
+        std::memcpy(r->pend, s->pend, sizeof(r->pend));
+        r->pendRewrite = s->pendRewrite;
         return r;
     }
 
     // insertingWalk, mergeTree.ts:2345-2474.  insertMode=false: ensureIntervalBoundary walk.
     // Returns the block produced by a split (or nullptr).  `ok` is cleared if an insert fell through.
-    Block* insertingWalk(Block* b, int pos, int32_t R, int32_t C, Seg* cand) {
+    // `sequenced`: the insert has a sequence number (the continuePredicate applies).  Returns the
+    // unfinished node (unfinished()) when the walk should go on past b.
+    static Block* unfinished() { return reinterpret_cast<Block*>(uintptr_t(1)); }
+    Block* insertingWalk(Block* b, int pos, int32_t R, int32_t C, Seg* cand, bool sequenced = true) {
         int ci;
         Node* newNode = nullptr;
         for (ci = 0; ci < b->childCount; ci++) {
             Node* child = b->children[ci];
-            int len = nodeLen(child, R, C);
-            if (pos < len || (pos == len && breakTie(pos, child, R))) {
+            int len = viewLen(child, R, C);
+            if (pos < len || (pos == len && breakTie(pos, child, R, C))) {
                 if (!child->leaf) {
-                    Block* sp = insertingWalk(static_cast<Block*>(child), pos, R, C, cand);
+                    Block* sp = insertingWalk(static_cast<Block*>(child), pos, R, C, cand, sequenced);
+                    if (sp == unfinished()) {  // act as if the child were shifted
+                        pos -= len;
+                        continue;
+                    }
                     if (!sp) return nullptr;
                     newNode = sp;
                     ci++;
@@ -273,7 +332,10 @@ struct Doc {
                 pos -= len;
             }
         }
-        if (!newNode && pos == 0 && cand) newNode = cand;  // leaf(undefined): append to this block
+        if (!newNode && pos == 0 && cand) {
+            if (sequenced && !pending.empty() && continueLocal(b)) return unfinished();
+            newNode = cand;  // leaf(undefined): append to this block
+        }
         if (!newNode) return nullptr;
         for (int i = b->childCount; i > ci; i--) {
             b->children[i] = b->children[i - 1];
@@ -344,7 +406,10 @@ struct Doc {
                 continue;
             }
             Seg* s = static_cast<Seg*>(child);
-            if (s->removed) {
+            if (!s->groups.empty()) {  // pending local edits: held (mergeTree.ts:1295, 1356-1358)
+                hold.push_back(s);
+                prev = nullptr;
+            } else if (s->removed) {
                 if (s->rseq > minSeq) {
                     hold.push_back(s);
                 } else {
@@ -433,7 +498,7 @@ struct Doc {
     bool nodeMap(Block* node, int32_t R, int32_t C, int start, int end, F&& leaf) {
         for (int ci = 0; ci < node->childCount; ci++) {
             Node* child = node->children[ci];
-            int len = nodeLen(child, R, C);
+            int len = viewLen(child, R, C);
             if (end > 0 && len > 0 && start < len) {
                 if (!child->leaf) {
                     nodeMap(static_cast<Block*>(child), R, C, start, end, leaf);
@@ -502,9 +567,157 @@ struct Doc {
         currentSeq = cur_seq;
     }
 
+    // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111), collaborating, no
+    // combining op but "rewrite": a local change (seq -1) counts its keys pending; a remote one
+    // leaves keys with pending local changes alone and is dropped whole while a local rewrite is
+    // pending.  propertyDeltas in (pm, pv) for keys < 8.  Returns false when dropped.
+    static bool addProps(Seg* s, const uint8_t* pairs, int np, bool rewrite, bool local, uint8_t& pm, uint64_t& pv) {
+        if (!s->props_defined) {
+            s->props_defined = true;
+            std::memset(s->props, 0, sizeof(s->props));
+            std::memset(s->pend, 0, sizeof(s->pend));
+            s->pendRewrite = 0;
+        }
+        if (s->pendRewrite > 0 && !local) return false;
+        auto modify = [&](int k) { return local || s->pend[k] == 0; };
+        auto delta = [&](int k, uint8_t prev) {
+            if (k >= 8) return;
+            pm |= (uint8_t)(1u << k);
+            pv = (pv & ~(0xFFull << (8 * k))) | ((uint64_t)prev << (8 * k));
+        };
+        if (rewrite) {
+            if (local) s->pendRewrite++;
+            for (int k = 0; k < kMaxKeys; k++) {
+                bool keep = false;  // newProps[key] truthy
+                for (int q = 0; q < np; q++) keep = keep || (pairs[2 * q] == k && pairs[2 * q + 1] != 0);
+                if (s->props[k] && !keep && modify(k)) {
+                    delta(k, s->props[k]);
+                    s->props[k] = 0;
+                }
+            }
+        }
+        for (int q = 0; q < np; q++) {
+            const int k = pairs[2 * q];
+            if (local) {
+                s->pend[k]++;
+            } else if (!modify(k)) {
+                continue;
+            }
+            delta(k, s->props[k]);
+            s->props[k] = pairs[2 * q + 1];
+        }
+        return true;
+    }
+
+    // addToPendingList (mergeTree.ts:1922-1929): one group per local edit
+    void join(Group*& g, Seg* s) {
+        if (!g) {
+            pending.emplace_back();
+            g = &pending.back();
+        }
+        g->segs.push_back(s);
+        s->groups.push_back(g);
+    }
+
+    // A local edit of the editing client (client.ts:163-214 -> applyInsertOp / applyRemoveRangeOp /
+    // applyAnnotateRangeOp with refSeq = currentSeq, seq = UnassignedSequenceNumber): insertSegments
+    // / markRangeRemoved / annotateRange in the local view, the touched segments joining a new
+    // pending group; no zamboni, no window asserts, no seq update (mergeTree.ts:1968-1998,
+    // 2607-2719, 2565-2605)
+    void applyLocal(const mt_op_rec& op, const uint8_t* payload) {
+        if (own == -100) own = op.client;
+        if (op.client != own || op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, kUnassigned);
+        if (op.type > MT_OP_ANNOTATE) return fail(MT_DERR_BAD_OP, kUnassigned);
+        const int32_t R = currentSeq, C = own, S = kUnassigned;
+        const int np = MT_OP_NPAIRS(op.flags);
+        if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+        const uint8_t* pay = payload + op.payload_off;
+        const int tlen = (int)op.payload_len - 2 * np;
+        const uint8_t* pairs = pay + tlen;
+        for (int q = 0; q < np; q++)
+            if (pairs[2 * q] >= kMaxKeys) return fail(MT_DERR_LIMITS, S);
+        Group* g = nullptr;
+        if (op.type == MT_OP_INSERT) {
+            if (tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
+            ensureIntervalBoundary(op.pos1, R, C);
+            Seg* x = newSeg();
+            x->text.assign(reinterpret_cast<const char*>(pay), tlen);
+            if (op.flags & MT_F_PROPS) {
+                x->props_defined = true;
+                for (int q = 0; q < np; q++) x->props[pairs[2 * q]] = pairs[2 * q + 1];
+            }
+            x->seq = S;
+            x->client = C;
+            x->marker = (op.flags & MT_F_MARKER) != 0;
+            Block* sp = insertingWalk(root, op.pos1, R, C, x, false);
+            if (!x->parent) return fail(MT_DERR_INSERT_FAILED, S);
+            updateRoot(sp);
+            join(g, x);  // saveIfLocal
+            return;
+        }
+        ensureIntervalBoundary(op.pos1, R, C);
+        ensureIntervalBoundary(op.pos2, R, C);
+        if (op.type == MT_OP_REMOVE) {
+            nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* x) {
+                if (x->removed) {
+                    if (x->rseq == kUnassigned) {
+                        x->rclient = C;
+                        x->rseq = S;
+                    } else {
+                        x->overlap |= 1ull << C;
+                    }
+                } else {
+                    x->removed = true;
+                    x->rseq = S;
+                    x->rclient = C;
+                }
+                if (x->removed && x->rseq == kUnassigned) join(g, x);
+            });
+        } else {
+            const bool rewrite = op.flags & MT_F_REWRITE;
+            nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* x) {
+                uint8_t pm = 0;
+                uint64_t pv = 0;
+                addProps(x, pairs, np, rewrite, true, pm, pv);
+                join(g, x);
+            });
+        }
+    }
+
+    // ackPendingSegment (client.ts:588-625 -> mergeTree.ts:1893-1920, BaseSegment.ack :487-522):
+    // the editing client's own sequenced message settles its oldest pending group
+    void applyAck(const mt_op_rec& op, const uint8_t* payload, bool last_member) {
+        const int32_t S = op.seq;
+        evSeq = S;
+        if (!pending.empty()) {
+            Group& g = pending.front();
+            const int np = MT_OP_NPAIRS(op.flags);
+            const uint8_t* pairs = payload + op.payload_off + (op.payload_len - 2 * np);
+            for (Seg* x : g.segs) {
+                if (x->groups.empty() || x->groups.front() != &g) return fail(MT_DERR_BAD_OP, S);
+                x->groups.erase(x->groups.begin());
+                if (op.type == MT_OP_INSERT) {
+                    x->seq = S;
+                } else if (op.type == MT_OP_REMOVE) {
+                    if (x->rseq == kUnassigned) x->rseq = S;  // else a remote removal overwrote it
+                } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
+                    if (op.flags & MT_F_REWRITE) x->pendRewrite--;
+                    for (int q = 0; q < np; q++)
+                        if (x->pend[pairs[2 * q]] > 0) x->pend[pairs[2 * q]]--;
+                }
+                addToLRUSet(x, S);
+            }
+            pending.pop_front();
+        }
+        zamboni();
+        if (last_member) updateSeqNumbers(op.msn, S);
+    }
+
     void applyOp(const mt_op_rec& op, const uint8_t* payload, bool last_member) {
         if (err) return;
         if (op.type == MT_OP_LOAD) return loadInsert(op, payload);
+        if (op.seq == kUnassigned) return applyLocal(op, payload);
+        if ((int32_t)op.client == own && op.type <= MT_OP_ANNOTATE) return applyAck(op, payload, last_member);
         const int32_t S = op.seq, R = op.ref_seq, C = op.client;
         const int np = MT_OP_NPAIRS(op.flags);
         // Every assert the reference raises for this message is checked BEFORE anything is
@@ -523,7 +736,7 @@ struct Doc {
             if (wc) {
                 // those asserts run after the op: a failing insert throws first (mergeTree.ts:2210)
                 const int tl = (int)op.payload_len - 2 * np;
-                if (op.type == MT_OP_INSERT && tl > 0 && op.pos1 > nodeLen(root, op.ref_seq, op.client))
+                if (op.type == MT_OP_INSERT && tl > 0 && op.pos1 > viewLen(root, op.ref_seq, op.client))
                     wc = MT_DERR_INSERT_FAILED;
                 return fail(wc, S);
             }
@@ -575,7 +788,12 @@ struct Doc {
                 if (op.type == MT_OP_REMOVE) {
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
                         if (s->removed) {
-                            s->overlap |= 1ull << C;     // addOverlappingClient
+                            if (s->rseq == kUnassigned) {  // a pending local removal: the remote one replaces it
+                                s->rclient = C;
+                                s->rseq = S;
+                            } else {
+                                s->overlap |= 1ull << C;     // addOverlappingClient
+                            }
                         } else {
                             s->removed = true;
                             s->rseq = S;
@@ -587,30 +805,9 @@ struct Doc {
                 } else {
                     const bool rewrite = op.flags & MT_F_REWRITE;
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
-                        if (!s->props_defined) {
-                            s->props_defined = true;
-                            std::memset(s->props, 0, sizeof(s->props));
-                        }
-                        // propertyDeltas (segmentPropertiesManager.ts:60-108): a rewrite records every
-                        // key it deletes with its old value; each key of the op then records the value
-                        // before it is set -- null when absent, and for a rewrite's null-valued key the
-                        // one deleted a moment earlier (so null again)
                         uint8_t pm = 0;
                         uint64_t pv = 0;
-                        for (int k = 0; k < 8; k++)
-                            if (rewrite && s->props[k]) {
-                                pm |= (uint8_t)(1u << k);
-                                pv |= (uint64_t)s->props[k] << (8 * k);
-                            }
-                        for (int q = 0; q < np; q++) {
-                            const int k = pairs[2 * q];
-                            if (k >= 8) continue;
-                            const uint8_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : s->props[k];
-                            pm |= (uint8_t)(1u << k);
-                            pv = (pv & ~(0xFFull << (8 * k))) | ((uint64_t)prev << (8 * k));
-                        }
-                        if (rewrite) std::memset(s->props, 0, sizeof(s->props));
-                        for (int q = 0; q < np; q++) s->props[pairs[2 * q]] = pairs[2 * q + 1];
+                        addProps(s, pairs, np, rewrite, false, pm, pv);
                         delta.push_back(s);
                         pdel.emplace_back(pm, pv);
                         addToLRUSet(s, S);

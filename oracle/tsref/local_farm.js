@@ -1,0 +1,139 @@
+"use strict";
+// A multi-client farm over the REFERENCE merge-tree Clients (type-stripped into oracle/_tsref) that
+// writes op logs seen from one editing client: the client under test ("c1") makes local edits
+// (insertSegmentLocal / removeRangeLocal / annotateRangeLocal, client.ts:163-214) while the other
+// clients edit concurrently; a toy sequencer orders every client's messages (msn = the least
+// seq any client may still reference: its currentSeq or an in-flight op's refSeq) and each client receives the sequenced stream at its own pace, so
+// c1's own messages come back as acks (client.ts:588-625, 804-806) interleaved with remote ops.
+// The pattern of client.conflictFarm.spec.ts / mergeTreeOperationRunner.ts; with `partial` c1 also
+// lags behind the stream.  A run whose clients end with different text is dropped (the reference
+// itself diverges on some lagging-client runs; such logs are not used as fixtures).
+// TEST INFRASTRUCTURE ONLY (this container).
+//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial]] -> JSON {docs: [[record, ...], ...]}
+//   record = [seq, ref, msn, client, type, pos1, pos2, text, props {key id: value id | null} | null,
+//             flags]; c1's local edits have seq = -1 (UnassignedSequenceNumber), ref = msn = 0
+const path = require("path");
+const ROOT = path.join(__dirname, "..", "_tsref", "merge-tree", "src");
+const { Client } = require(path.join(ROOT, "client.js"));
+const { TextSegment } = require(path.join(ROOT, "textSegment.js"));
+const { Marker } = require(path.join(ROOT, "mergeTree.js"));
+
+function specToSegment(spec) { return TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec); }
+const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+
+function rng(seed) {  // xorshift32
+    let s = seed >>> 0 || 1;
+    return () => {
+        s ^= s << 13; s >>>= 0; s ^= s >>> 17; s ^= s << 5; s >>>= 0;
+        return s / 4294967296;
+    };
+}
+
+const F_REWRITE = 1;
+function record(seq, ref, msn, client, op) {
+    const props = (p) => {
+        if (!p) return null;
+        const o = {};
+        for (const k of Object.keys(p)) o[parseInt(k.slice(1), 10)] = p[k] === null || p[k] === undefined ? null : p[k];
+        return o;
+    };
+    if (op.type === 0) {
+        const seg = op.seg;
+        const text = typeof seg === "string" ? seg : seg.text;
+        return [seq, ref, msn, client, 0, op.pos1, 0, text, typeof seg === "string" ? null : props(seg.props), 0];
+    }
+    if (op.type === 1) return [seq, ref, msn, client, 1, op.pos1, op.pos2, null, null, 0];
+    return [seq, ref, msn, client, 2, op.pos1, op.pos2, null, props(op.props),
+        op.combiningOp && op.combiningOp.name === "rewrite" ? F_REWRITE : 0];
+}
+
+function farm(seed, nOps, nClients, partial) {
+    const r = rng(seed);
+    const ri = (n) => Math.floor(r() * n);
+    const clients = [];
+    for (let i = 1; i <= nClients; i++) {
+        const c = new Client(specToSegment, logger);
+        c.startOrUpdateCollaboration("c" + i);
+        clients.push(c);
+    }
+    const queue = [];      // submitted, not yet sequenced: {client, ref, op}
+    const seqd = [];       // sequenced messages
+    const cursor = clients.map(() => 0);
+    const log = [];        // c1's view
+    let seq = 0, made = 0;
+    const deliver = (i) => {
+        const m = seqd[cursor[i]++];
+        clients[i].applyMsg(m);
+        if (i === 0) log.push(record(m.sequenceNumber, m.referenceSequenceNumber, m.minimumSequenceNumber,
+            parseInt(m.clientId.slice(1), 10), m.contents));
+    };
+    const localOp = (i) => {
+        const c = clients[i];
+        const len = c.getLength();
+        const pick = r();
+        let op;
+        if (len === 0 || pick < 0.45) {
+            const n = 1 + ri(4);
+            let text = "";
+            for (let q = 0; q < n; q++) text += String.fromCharCode(97 + ri(26));
+            let props;
+            if (r() < 0.25) { props = {}; props["k" + ri(3)] = 1 + ri(4); }
+            const seg = new TextSegment(text);
+            if (props) seg.addProperties(props);
+            op = c.insertSegmentLocal(ri(len + 1), seg);
+        } else {
+            const a = ri(len), b = a + 1 + ri(Math.min(6, len - a));
+            if (pick < 0.75) {
+                op = c.removeRangeLocal(a, b);
+            } else {
+                const props = {};
+                const nk = 1 + ri(2);
+                for (let q = 0; q < nk; q++) props["k" + ri(3)] = r() < 0.15 ? null : 1 + ri(4);
+                op = c.annotateRangeLocal(a, b, props, r() < 0.1 ? { name: "rewrite" } : undefined);
+            }
+        }
+        if (!op) throw new Error("local op rejected");
+        queue.push({ client: i + 1, ref: c.getCurrentSeq(), op });
+        if (i === 0) log.push(record(-1, 0, 0, 1, op));
+        made++;
+    };
+    const sequenceAll = () => {
+        while (queue.length) {
+            const q = queue.shift();
+            seq++;
+            // no client may still reference a seq below the msn: its in-flight ops included
+            const msn = Math.min(q.ref, ...clients.map((c) => c.getCurrentSeq()), ...queue.map((o) => o.ref));
+            seqd.push({ clientId: "c" + q.client, clientSequenceNumber: 1, contents: q.op, metadata: undefined,
+                minimumSequenceNumber: msn, origin: undefined, referenceSequenceNumber: q.ref, sequenceNumber: seq,
+                timestamp: 0, term: 1, traces: [], type: "op" });
+        }
+    };
+    // rounds (mergeTreeOperationRunner.ts): clients edit, the round's ops are sequenced, and every
+    // client catches up -- c1 only to a random point when `partial`, so its next edits interleave
+    // with the rest of the stream
+    while (made < nOps) {
+        for (let i = 0; i < nClients; i++) {
+            const k = r() < 0.6 ? 1 + ri(3) : 0;
+            for (let q = 0; q < k; q++) localOp(i);
+        }
+        sequenceAll();
+        for (let i = 1; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
+        const upto = partial ? cursor[0] + ri(seqd.length - cursor[0] + 1) : seqd.length;
+        while (cursor[0] < upto) deliver(0);
+    }
+    while (cursor[0] < seqd.length) deliver(0);
+    const txt = (c) => c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId());
+    const t0 = txt(clients[0]);
+    for (const c of clients) if (txt(c) !== t0) return null;  // the clients diverged: drop the run
+    return log;
+}
+
+const [nDocs, seed, nOps, nClients, partial] = process.argv.slice(2).map((x) => parseInt(x, 10));
+const docs = [];
+let dropped = 0;
+for (let d = 0, k = 0; d < nDocs; k++) {
+    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1);
+    if (log) { docs.push(log); d++; } else dropped++;
+}
+process.stderr.write(`local_farm: ${nDocs} documents, ${dropped} runs dropped (clients diverged)\n`);
+process.stdout.write(JSON.stringify({ docs }) + "\n");

@@ -302,6 +302,48 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "local") {
+        // an editing client (client.ts:163-214, 588-625): the document's records with seq -1 are its
+        // local edits (insertSegmentLocal / removeRangeLocal / annotateRangeLocal), the rest the
+        // sequenced stream it receives -- its own messages among them, acked.  States after
+        // record counts k of a spread of checkpoints and at the end: [[k, state], ...]
+        const nck = parseInt(process.argv[4] || "6", 10);
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const n = log.rowPtr[d + 1] - log.rowPtr[d];
+            const items = [...messages(log, d)];
+            const own = items.find((x) => x.local);
+            const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+            const c = new Client(specToSegment, logger);
+            c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+            const cks = new Set();
+            for (let q = 1; q < nck; q++) cks.add(Math.floor((q * n) / nck));
+            const states = [];
+            let err = null, k = 0;
+            try {
+                for (const it of items) {
+                    if (it.local) {
+                        const op = it.op;
+                        let ok;
+                        if (op.type === 0) ok = c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                        else if (op.type === 1) ok = c.removeRangeLocal(op.pos1, op.pos2);
+                        else ok = c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+                        if (!ok) throw new Error("local edit rejected");
+                    } else {
+                        c.applyMsg(it);
+                    }
+                    k++;
+                    if (cks.has(k)) states.push([k, canonical(c)]);
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            states.push([k, canonical(c)]);
+            out.push(JSON.stringify({ doc: d, err, states }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "stacks") {
         // getStackContext (client.ts:946-948, mergeTree.ts:1750-1760): the NestBegin / NestEnd stack of
         // each label L0..L3 at a spread of positions, range labels on key <rangeKey>; each stack as

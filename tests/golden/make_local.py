@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Regenerate the editing-client fixtures FROM THE REFERENCE ITSELF (build container only).
+
+SURVEY.md §8(f) rank 4, local (pending) edits and acks: oracle/tsref/local_farm.js runs reference
+Clients c1..c4 editing one document concurrently (insertSegmentLocal / removeRangeLocal /
+annotateRangeLocal, client.ts:163-214) behind a toy sequencer and writes the log as c1 sees it --
+its own edits as records with seq -1, then the sequenced stream, its own messages coming back as
+acks (client.ts:588-625, 804-806; mergeTree.ts:1893-1929; BaseSegment.ack :487-522).
+oracle/tsref/replay_ref.js `local` replays each log on a fresh reference Client "c1" and reports
+its canonical state at checkpoints (pending segments: seq -1; a pending removal: rseq -1 with its
+rclient) and at the end:
+  * local_rounds: every client catches up at the end of each round (mergeTreeOperationRunner.ts);
+  * local_lag: c1 catches up to a random point only, so its edits interleave with remote ops it
+    has not seen yet.
+local.expected.jsonl: one JSON line per (log, document): {log, doc, err, states: [[k, state], ...]}
+with k the number of the document's records applied.
+"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from make_golden import build_log  # noqa: E402
+
+LOGS = (('local_rounds', 24, 11, 300, 0), ('local_lag', 24, 12, 300, 1))
+
+
+def main():
+    subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
+    farm = os.path.join(REPO, 'oracle/tsref/local_farm.js')
+    replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
+    out = []
+    for name, n_docs, seed, n_ops, partial in LOGS:
+        res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial)], check=True,
+                             capture_output=True, text=True)
+        docs = []
+        for recs in json.loads(res.stdout)['docs']:
+            docs.append([(s, r, m, c, t, p1, p2, text, None if props is None else {int(k): v for k, v in props.items()},
+                          flags) for (s, r, m, c, t, p1, p2, text, props, flags) in recs])
+        path = os.path.join(HERE, name + '.mtlog')
+        build_log(docs).save(path)
+        res = subprocess.run(['node', replay, 'local', path, '6'], check=True, capture_output=True, text=True)
+        for line in res.stdout.strip().split('\n'):
+            out.append(json.dumps(dict(log=name, **json.loads(line)), separators=(',', ':')))
+        print(name, len(docs), 'docs', sum(len(d) for d in docs), 'records')
+    with open(os.path.join(HERE, 'local.expected.jsonl'), 'w') as f:
+        f.write('\n'.join(out) + '\n')
+
+
+if __name__ == '__main__':
+    main()

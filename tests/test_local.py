@@ -61,3 +61,17 @@ def test_oracle_editing_client_matches_reference(oracle_lib, name):
             o = oracle_lib.Oracle(1).apply(prefix(batch, r['doc'], k))
             assert o.error(0) == (0, 0), (name, r['doc'], k)
             assert o.state(0) == want, (name, r['doc'], k)
+
+
+@pytest.mark.gpu
+def test_engine_rejects_local_edits_loudly():
+    """The device engines do not apply local edits yet: every document of a local-edit log halts
+    with an error at its first local record instead of diverging silently."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, 'local_lag.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    eng.apply(batch)
+    for d in range(batch.n_docs):
+        code, seq = eng.error(d)
+        assert code != 0 and seq == -1, (d, code, seq)

@@ -26,7 +26,7 @@ namespace mt {
 constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
 
-template <int CAP>
+template <int CAP, bool LOC = false>
 struct Lds {
     static constexpr int LB = CAP / 2;      // leaf blocks
     static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
@@ -56,15 +56,21 @@ struct Lds {
     int32_t gcref[64];      // generator: latest refSeq per client (deli clientSeqManager)
     int32_t gstall;         // generator: client 1 holds its refSeq until this seq
     uint32_t gpay;          // generator: payload bytes used in this document's region
+    // an editing client's document (LOC, mt_loc): per slot the pending group mask, the pending
+    // property counts (MT_PK_*) and the creation stamp
+    mt_loc lc;
+    uint64_t gm[LOC ? CAP : 1];
+    uint64_t pk[LOC ? CAP : 1];
+    uint32_t ct[LOC ? CAP : 1];
 };
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
 // SURVEY.md §8 a9 "unbounded B-tree"): the same structure lives in a per-wave workspace in HBM
 // (mt_launch_apply_big); lanes exchange it through the vector L1 / L2, so a pass boundary also
 // waits for the wave's outstanding stores (workgroup scope = the wave's CU).
-template <int CAP, bool G = false>
+template <int CAP, bool G = false, bool LOC = false>
 struct Wave {
-    using L = Lds<CAP>;
+    using L = Lds<CAP, LOC>;
     MT_DEV static void sync() {
         if (G) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -199,6 +205,19 @@ struct Wave {
     // -------------------------------------------------------------- visibility
     // nodeLength leaf branch for a remote client (mergeTree.ts:1667-1697)
     MT_DEV int vis(int slot, int32_t R, int C) const {
+        if constexpr (LOC) {
+            // the editing client sees its local view (nodeLength :1660-1665, localNetLength
+            // :1161-1172); others never see a pending insert (seq -1) and see through a pending
+            // removal (removedSeq -1) (:1675-1686)
+            if (C == s.lc.own) return (s.flags[slot] & MT_SF_REMOVED) ? 0 : (int)s.len[slot];
+            const bool seen = (s.client[slot] == C) || (s.seq[slot] != -1 && s.seq[slot] <= R);
+            if (!seen) return 0;
+            if ((s.flags[slot] & MT_SF_REMOVED) &&
+                (s.rclient[slot] == C || (C < 64 && ((s.ovl[slot] >> C) & 1ull)) ||
+                 (s.rseq[slot] != -1 && s.rseq[slot] <= R)))
+                return 0;
+            return (int)s.len[slot];
+        }
         const bool seen = (s.client[slot] == C) || (s.seq[slot] <= R);
         if (!seen) return 0;
         if (s.flags[slot] & MT_SF_REMOVED) {
@@ -252,7 +271,7 @@ struct Wave {
 
     // ----------------------------------------------------------------- blocks
     MT_DEV uint8_t* lvl(int L) { return L == 0 ? s.lbcnt : s.ibcnt[L - 1]; }
-    MT_DEV int lvlcap(int L) const { return L == 0 ? Lds<CAP>::LB : Lds<CAP>::IB; }
+    MT_DEV int lvlcap(int Lv) const { return Lv == 0 ? L::LB : L::IB; }
 
     // bst[b] = first position of leaf block b (bst[nb0] = n)
     MT_DEV void block_starts() {
@@ -477,6 +496,12 @@ struct Wave {
             s.len[t] = s.len[sl] - (uint32_t)off;
             s.toff[t] = s.toff[sl] + (uint32_t)off;
             s.len[sl] = (uint32_t)off;
+            if constexpr (LOC) {  // segmentGroups.copyTo + the property manager's counts (mergeTree.ts:555-560)
+                s.gm[t] = s.gm[sl];
+                s.pk[t] = s.pk[sl];
+                s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
+                s.ct[t] = s.lc.stamp;
+            }
             const uint8_t last = arena[s.toff[sl] + (uint32_t)off - 1];
             s.flags[sl] = (uint8_t)((s.flags[sl] & ~MT_SF_NL) | (last == '\n' ? MT_SF_NL : 0));
         }
@@ -493,7 +518,7 @@ struct Wave {
     // ------------------------------------------------------------------- heap
     // Heap<LRUSegment> (collections.ts:213-265), comparer maxSeq (mergeTree.ts:923-926)
     MT_DEV bool heap_push(int32_t key, int sl, int32_t seq) {
-        if (s.heap_n + 1 >= Lds<CAP>::H) return fail(MT_DERR_CAPACITY, seq), false;
+        if (s.heap_n + 1 >= L::H) return fail(MT_DERR_CAPACITY, seq), false;
         if (lane == 0) {
             int k = s.heap_n + 1;
             s.hseq[k] = key;
@@ -570,7 +595,12 @@ struct Wave {
         for (int q = 0; q < cnt; q++) {
             const int sl = s.order[st + q];
             const uint8_t f = s.flags[sl];
-            if (f & MT_SF_REMOVED) {
+            bool pending = false;
+            if constexpr (LOC) pending = s.gm[sl] != 0;  // segmentGroups not empty: held (mergeTree.ts:1295)
+            if (pending) {
+                keep[kept++] = (uint16_t)sl;
+                prev = -1;
+            } else if (f & MT_SF_REMOVED) {
                 if (s.rseq[sl] > minSeq) {
                     keep[kept++] = (uint16_t)sl;
                 } else {
@@ -772,17 +802,47 @@ struct Wave {
                 }
             }
             if (b < 0) return fail(MT_DERR_INSERT_FAILED, S);
-            const int st = s.bst[b], c = s.lbcnt[b];
-            // leaf placement: first child with pos < len, or pos == len == 0 and breakTie
-            bool hit = false;
-            if (lane < c) {
-                const int k = st + lane;
-                const int ce = s.cum[k], cs = cstart(k);
-                const int sl = s.order[k];
-                const bool rm_before = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] <= R;
-                hit = ce > pos || (ce == pos && cs == pos && !rm_before);
+            int st = s.bst[b], c = s.lbcnt[b];
+            uint64_t m;
+            for (;;) {
+                // leaf placement: first child with pos < len, or pos == len == 0 and breakTie
+                bool hit = false;
+                if (lane < c) {
+                    const int k = st + lane;
+                    const int ce = s.cum[k], cs = cstart(k);
+                    const int sl = s.order[k];
+                    bool rm_before = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] <= R;
+                    bool tie = true;
+                    if constexpr (LOC) {  // breakTie (mergeTree.ts:2248-2277) with pending segments
+                        rm_before = rm_before && s.rseq[sl] != -1;
+                        tie = C == s.lc.own || s.seq[sl] != -1;
+                    }
+                    hit = ce > pos || (ce == pos && cs == pos && !rm_before && tie);
+                }
+                m = wave_ballot(hit);
+                if constexpr (LOC) {
+                    // blockInsert's continuePredicate (mergeTree.ts:2143-2160, 2431-2436): a sequenced
+                    // insert that runs off block b goes on into the next block when the first leaf
+                    // after b in the local view is a pending local insert
+                    if (!m && S != -1 && b + 1 < nb) {
+                        const int e0 = st + c, n = s.n;
+                        int f = -1;
+                        for (int base = e0; base < n && f < 0; base += 64) {
+                            const int k = base + lane;
+                            const bool lv = k < n && !(s.flags[s.order[k]] & MT_SF_REMOVED) && s.len[s.order[k]] > 0;
+                            const uint64_t lm = wave_ballot(lv);
+                            if (lm) f = base + first_lane(lm);
+                        }
+                        if (f >= 0 && s.seq[s.order[f]] == -1) {
+                            b = b + 1;
+                            st = s.bst[b];
+                            c = s.lbcnt[b];
+                            continue;
+                        }
+                    }
+                }
+                break;
             }
-            const uint64_t m = wave_ballot(hit);
             // not found: append at the end of block b (pos_rem == 0 there, mergeTree.ts:2431-2444)
             const int k = m ? st + first_lane(m) : st + c;
             const int t = alloc_slot(S);
@@ -822,6 +882,16 @@ struct Wave {
                 }
                 s.flags[t] = f;
                 s.props[t] = p;
+                if constexpr (LOC) {  // a local insert is its edit's one pending segment (saveIfLocal)
+                    s.gm[t] = S == -1 ? (1ull << (s.lc.ghi & 63u)) : 0ull;
+                    s.pk[t] = 0;
+                    s.lc.stamp = s.lc.stamp + 1;
+                    s.ct[t] = s.lc.stamp;
+                    if (S == -1) {
+                        s.lc.gt[s.lc.ghi & 63u] = s.ct[t];
+                        s.lc.ghi = s.lc.ghi + 1;
+                    }
+                }
             }
             s.text_top = top + (uint32_t)tlen;
             sync();
@@ -837,7 +907,7 @@ struct Wave {
         } else if (op.type != MT_OP_LOAD) {
             emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
         }
-        zamboni();
+        if (S != -1) zamboni();  // (a local edit runs no zamboni, mergeTree.ts:1994-1997)
     }
 
     MT_DEV void op_range(const mt_op_rec& op, const uint8_t* pairs, int np) {
@@ -850,6 +920,18 @@ struct Wave {
         const int n = s.n;
         const uint64_t cbit = 1ull << C;
         const bool rewrite = op.flags & MT_F_REWRITE;
+        const bool local = S == -1;
+        uint64_t gbit = 0;
+        if constexpr (LOC) {
+            if (local) {  // this edit's pending group (addToPendingList, mergeTree.ts:1922-1929)
+                gbit = 1ull << (s.lc.ghi & 63u);
+                sync();
+                if (lane == 0) s.lc.gt[s.lc.ghi & 63u] = s.lc.stamp + 1;  // every member existed before it
+                sync();
+                s.lc.ghi = s.lc.ghi + 1;
+                sync();
+            }
+        }
         if (!is_remove) emit_range(false, S, C, start, end, pairs, np, rewrite);
         for (int base = 0; base < n; base += 64) {
             const int i = base + lane;
@@ -857,8 +939,18 @@ struct Wave {
                 const int ce = s.cum[i], cs = cstart(i);
                 if (ce > cs && cs < end && ce > start) {
                     const int sl = s.order[i];
-                    if (is_remove) {
-                        if (s.flags[sl] & MT_SF_REMOVED) {
+                    if constexpr (LOC) {
+                        if (local) s.gm[sl] |= gbit;
+                    }
+                    if (LOC && !is_remove) {
+                        annotate_loc(sl, pairs, np, rewrite, local);
+                    } else if (is_remove) {
+                        bool pend_rm = false;
+                        if constexpr (LOC) pend_rm = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] == -1;
+                        if (pend_rm) {  // a pending local removal: this one replaces it (mergeTree.ts:2621-2627)
+                            s.rseq[sl] = S;
+                            s.rclient[sl] = (uint8_t)C;
+                        } else if (s.flags[sl] & MT_SF_REMOVED) {
                             s.ovl[sl] |= cbit;  // addOverlappingClient (first remover wins)
                         } else {
                             s.flags[sl] |= MT_SF_REMOVED;
@@ -875,6 +967,7 @@ struct Wave {
             }
         }
         sync();
+        if (local) return;  // pending segments join no LRU set and a local edit runs no zamboni
         if (is_remove) emit_range(true, S, C, start, end, pairs, np, rewrite);
         // addToLRUSet for touched segments in document order: one heap push per leaf block
         // whose needsScour is not already true, for its first touched segment
@@ -905,6 +998,124 @@ struct Wave {
         zamboni();
     }
 
+    // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) for an editing
+    // client's document: a local change counts its keys pending (and a rewrite), a remote one skips
+    // keys with pending local changes and is dropped whole while a local rewrite is pending
+    MT_DEV void annotate_loc(int sl, const uint8_t* pairs, int np, bool rewrite, bool local) {
+        if constexpr (LOC) {
+            uint64_t p = (s.flags[sl] & MT_SF_PDEF) ? s.props[sl] : 0;
+            uint64_t pk = (s.flags[sl] & MT_SF_PDEF) ? s.pk[sl] : 0;
+            s.flags[sl] |= MT_SF_PDEF;
+            if (!local && MT_PK_RW(pk) > 0) {
+                s.props[sl] = p;
+                s.pk[sl] = pk;
+                return;
+            }
+            if (rewrite) {
+                if (local) pk += 1ull << 56;
+                for (int k = 0; k < 8; k++) {
+                    bool keep = false;  // newProps[key] truthy
+                    for (int q = 0; q < np; q++) keep = keep || (pairs[2 * q] == k && pairs[2 * q + 1] != 0);
+                    if (((p >> (8 * k)) & 0xFFu) && !keep && (local || MT_PK_KEY(pk, k) == 0)) p &= ~(0xFFull << (8 * k));
+                }
+            }
+            for (int q = 0; q < np; q++) {
+                const int k = pairs[2 * q];
+                if (local) {
+                    if (MT_PK_KEY(pk, k) < 127) pk += 1ull << (7 * k);
+                } else if (MT_PK_KEY(pk, k) > 0) {
+                    continue;
+                }
+                p = (p & ~(0xFFull << (8 * k))) | ((uint64_t)pairs[2 * q + 1] << (8 * k));
+            }
+            s.props[sl] = p;
+            s.pk[sl] = pk;
+        }
+    }
+
+    // ackPendingSegment (client.ts:588-625 -> mergeTree.ts:1893-1920, BaseSegment.ack :487-522): the
+    // editing client's own sequenced message settles its oldest pending edit.  Its group's list
+    // order (which the heap pushes follow) is rebuilt: the members that existed when the edit was
+    // made (stamp < gt) in document order, then the parts split off later, by stamp.
+    MT_DEV void ack_one(int k, int32_t S, uint64_t bit, uint8_t type, const uint8_t* pairs, int np, bool rewrite) {
+        if constexpr (LOC) {
+            const int sl = s.order[k];
+            sync();
+            if (lane == 0) {
+                s.gm[sl] &= ~bit;
+                if (type == MT_OP_INSERT) {
+                    s.seq[sl] = S;
+                } else if (type == MT_OP_REMOVE) {
+                    if (s.rseq[sl] == -1) s.rseq[sl] = S;  // else a remote removal overwrote it
+                } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
+                    uint64_t pk = s.pk[sl];
+                    if (rewrite && MT_PK_RW(pk) > 0) pk -= 1ull << 56;
+                    for (int q = 0; q < np; q++)
+                        if (MT_PK_KEY(pk, pairs[2 * q]) > 0) pk -= 1ull << (7 * pairs[2 * q]);
+                    s.pk[sl] = pk;
+                }
+            }
+            sync();
+            add_lru(block_of_pos(k), sl, S);
+        }
+    }
+    MT_DEV void op_ack(const mt_op_rec& op, const uint8_t* pairs, int np) {
+        if constexpr (LOC) {
+            const int32_t S = op.seq;
+            if (s.lc.glo < s.lc.ghi) {
+                const uint32_t Lo = s.lc.glo;
+                const uint64_t bit = 1ull << (Lo & 63u);
+                const uint32_t gt = s.lc.gt[Lo & 63u];
+                const bool rewrite = op.flags & MT_F_REWRITE;
+                block_starts();
+                const int n = s.n;
+                for (int base = 0; base < n; base += 64) {  // the original members, in document order
+                    const int i = base + lane;
+                    bool mem = false;
+                    if (i < n) {
+                        const int sl = s.order[i];
+                        mem = (s.gm[sl] & bit) && s.ct[sl] < gt;
+                    }
+                    uint64_t m = wave_ballot(mem);
+                    while (m) {
+                        const int fl = first_lane(m);
+                        m &= m - 1;
+                        ack_one(base + fl, S, bit, op.type, pairs, np, rewrite);
+                        if (s.err) return;
+                    }
+                }
+                for (;;) {  // the parts split off later, by creation stamp
+                    uint32_t best = 0xFFFFFFFFu;
+                    for (int base = 0; base < n; base += 64) {
+                        const int i = base + lane;
+                        uint32_t v = 0xFFFFFFFFu;
+                        if (i < n) {
+                            const int sl = s.order[i];
+                            if (s.gm[sl] & bit) v = s.ct[sl];
+                        }
+                        uint32_t mv = v;
+                        for (int o = 32; o; o >>= 1) mv = min(mv, (uint32_t)__shfl_xor((int)mv, o, 64));
+                        best = min(best, mv);
+                    }
+                    if (best == 0xFFFFFFFFu) break;
+                    int k = -1;
+                    for (int base = 0; base < n && k < 0; base += 64) {
+                        const int i = base + lane;
+                        const uint64_t hm = wave_ballot(i < n && (s.gm[s.order[i]] & bit) && s.ct[s.order[i]] == best);
+                        if (hm) k = base + first_lane(hm);
+                    }
+                    if (k < 0) break;
+                    ack_one(k, S, bit, op.type, pairs, np, rewrite);
+                    if (s.err) return;
+                }
+                sync();
+                s.lc.glo = Lo + 1;
+                sync();
+            }
+            zamboni();
+        }
+    }
+
     // Client.updateSeqNumbers + MergeTree.setMinSeq (client.ts:821-828, mergeTree.ts:1718-1736)
     MT_DEV void update_seq(int32_t msn, int32_t seq) {
         if (!(s.cur_seq <= seq)) return fail(MT_DERR_SEQ_ORDER, seq);
@@ -920,9 +1131,56 @@ struct Wave {
         }
     }
 
+    // A local edit of the editing client (client.ts:163-214 -> applyInsertOp / applyRemoveRangeOp /
+    // applyAnnotateRangeOp): refSeq = currentSeq, seq = UnassignedSequenceNumber, the local view; no
+    // window asserts, no seq update.  The first one names the document's editing client.
+    MT_DEV void apply_local(const mt_op_rec& op, const uint8_t* payload) {
+        const int np = MT_OP_NPAIRS(op.flags);
+        const int C = op.client;
+        if (s.lc.own < 0) {
+            sync();
+            s.lc.own = C;
+            sync();
+        }
+        if (C != s.lc.own || C == 0 || C >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, -1);
+        if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, -1);
+        if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, -1);
+        const uint8_t* pay = payload + op.payload_off;
+        const int tlen = (int)op.payload_len - 2 * np;
+        const uint8_t* pairs = pay + tlen;
+        for (int q = 0; q < np; q++)
+            if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, -1);
+        mt_op_rec o = op;
+        o.ref_seq = s.cur_seq;
+        const int L = scan(o.ref_seq, C);
+        if (op.type == MT_OP_INSERT) {
+            if (tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
+            if (o.pos1 < 0 || o.pos1 > L) return fail(MT_DERR_INSERT_FAILED, -1);
+            op_insert(o, pay, tlen, pairs, np);
+        } else {
+            if (o.pos1 < 0 || o.pos2 > L || o.pos1 >= o.pos2) return fail(MT_DERR_BAD_OP, -1);  // getValidOpRange
+            op_range(o, pairs, np);
+        }
+    }
+    MT_DEV void apply_ack(const mt_op_rec& op, const uint8_t* payload) {
+        const int np = MT_OP_NPAIRS(op.flags);
+        const int32_t S = op.seq;
+        if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                                  // client.ts:824
+        if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);           // :826
+        if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+        op_ack(op, payload + op.payload_off + (op.payload_len - 2 * np), np);
+        if (s.err) return;
+        if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
+    }
+
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
         const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
+        if constexpr (LOC) {
+            if (op.type <= MT_OP_ANNOTATE && S == -1) return apply_local(op, payload);
+            if (s.lc.own >= 0 && (int)op.client == s.lc.own && op.type <= MT_OP_ANNOTATE && !MT_OP_IS_NOOP(op))
+                return apply_ack(op, payload);
+        }
         if (op.type > MT_OP_LOAD) return fail(MT_DERR_BAD_OP, S);
         // MT_OP_LOAD: MergeTree.insertSegments from SnapshotLoader.loadBody (snapshotLoader.ts:192-224),
         // no Client around it: no window asserts and no updateSeqNumbers
@@ -1153,6 +1411,24 @@ struct Wave {
             s.evn = g.evn ? (int32_t)g.evn[d] : 0;
             s.evseq = sc.cur_seq;
         }
+        if constexpr (LOC) {
+            if (lane == 0) {
+                s.lc.own = g.loc[d].own;
+                s.lc.glo = g.loc[d].glo;
+                s.lc.ghi = g.loc[d].ghi;
+                s.lc.stamp = g.loc[d].stamp;
+            }
+            s.lc.gt[lane] = g.loc[d].gt[lane];
+            sync();
+            // (a document that has not edited yet has never stored these arrays)
+            const bool has = s.lc.own >= 0;
+            const size_t lo2 = (size_t)d * MT_LOC_CAP;
+            for (int i = lane; i < n; i += 64) {
+                s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
+                s.pk[i] = has ? g.pk[lo2 + i] : 0ull;
+                s.ct[i] = has ? g.ct[lo2 + i] : 0u;
+            }
+        }
         sync();
         arena = abase + (size_t)s.text_half * textcap;
     }
@@ -1209,6 +1485,24 @@ struct Wave {
             sc.n_empty = (uint32_t)nempty;
             if (g.evn) g.evn[d] = (uint32_t)s.evn;
         }
+        if constexpr (LOC) {
+            if (s.lc.own >= 0) {
+                const size_t lo2 = (size_t)d * MT_LOC_CAP;
+                for (int i = lane; i < min(nn, MT_LOC_CAP); i += 64) {
+                    const int sl = s.order[i];
+                    g.gm[lo2 + i] = s.gm[sl];
+                    g.pk[lo2 + i] = s.pk[sl];
+                    g.ct[lo2 + i] = s.ct[sl];
+                }
+                if (lane == 0) {
+                    g.loc[d].own = s.lc.own;
+                    g.loc[d].glo = s.lc.glo;
+                    g.loc[d].ghi = s.lc.ghi;
+                    g.loc[d].stamp = s.lc.stamp;
+                }
+                g.loc[d].gt[lane] = s.lc.gt[lane];
+            }
+        }
     }
 };
 
@@ -1222,7 +1516,7 @@ struct GenArgs {
     const uint32_t* gids; // or the global id of every local document (a hash-routed shard)
 };
 
-template <int CAP, bool GEN>
+template <int CAP, bool GEN, bool LOC = false>
 __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
                                                    uint8_t* __restrict__ payload,
                                                    const uint32_t* __restrict__ row_ptr,
@@ -1232,13 +1526,28 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
-    Lds<CAP>& lds = *reinterpret_cast<Lds<CAP>*>(smem);
-    Wave<CAP> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap, GEN || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap,
-                 g.evcap);
+    Lds<CAP, LOC>& lds = *reinterpret_cast<Lds<CAP, LOC>*>(smem);
+    // (an editing client's document records no delta events)
+    Wave<CAP, false, LOC> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap,
+                             GEN || LOC || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap, g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
+    if (LOC) {  // the editing form has one capacity: a document that could outgrow it halts
+        const mt_doc_scalars& sc = g.sc[d];
+        const int nops = (int)(b - a);
+        int ib_need = 0;
+        for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
+        if (!(sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= CAP && sc.nb[0] + 2 * nops + 1 <= Lds<CAP, LOC>::LB &&
+              ib_need + nops + 1 <= Lds<CAP, LOC>::IB && sc.heap_n + 4 * nops + 16 <= Lds<CAP, LOC>::H)) {
+            if (threadIdx.x == 0 && !sc.err) {
+                g.sc[d].err = MT_DERR_CAPACITY;
+                g.sc[d].err_seq = ops[a].seq;
+            }
+            return;
+        }
+    }
     wv.load(g, d);
     if (GEN) {
         lds.gcref[wv.lane] = gen.cref[(size_t)d * 64 + wv.lane];
@@ -1371,6 +1680,18 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
             return hipErrorInvalidValue;
     }
 #undef MT_LAUNCH_BIG
+}
+
+// documents with an editing client (mt_bin_kernel's last bucket): the LDS engine's editing form
+extern "C" hipError_t mt_launch_apply_loc(const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+                                          const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
+                                          uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    mt::GenArgs ga{};
+    hipLaunchKernelGGL((mt::apply_kernel<MT_LOC_CAP, false, true>), dim3(n_docs), dim3(64),
+                       sizeof(mt::Lds<MT_LOC_CAP, true>), stream, *g, const_cast<mt_op_rec*>(ops),
+                       const_cast<uint8_t*>(payload), row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);
+    return hipGetLastError();
 }
 
 extern "C" size_t mt_lds_bytes(int cap_class) {

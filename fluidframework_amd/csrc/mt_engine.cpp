@@ -27,6 +27,9 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
+extern "C" hipError_t mt_launch_apply_loc(const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+                                          const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
+                                          uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
@@ -183,12 +186,16 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.ibcnt, D * (MT_MAXLEV - 1) * g.ibcap)) || (st = dalloc(e, &g.hseq, D * g.hcap)) ||
         (st = dalloc(e, &g.hslot, D * g.hcap)) || (st = dalloc(e, &g.sc, D)) ||
         (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
-        (st = dalloc(e, &e->d_counts, kNumClasses)) || (st = dalloc(e, &e->d_acc, kNumClasses)) || (st = dalloc(e, &e->d_ids, D * kNumClasses))) {
+        (st = dalloc(e, &g.gm, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pk, D * MT_LOC_CAP)) ||
+        (st = dalloc(e, &g.ct, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
+        // (+1: the editing documents' bucket after the capacity classes)
+        (st = dalloc(e, &e->d_counts, kNumClasses + 1)) || (st = dalloc(e, &e->d_acc, kNumClasses + 1)) ||
+        (st = dalloc(e, &e->d_ids, D * (kNumClasses + 1)))) {
         mt_engine_destroy(e);
         return st;
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&e->h_counts, kNumClasses * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_counts, (kNumClasses + 1) * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_ERR_HIP;
@@ -492,15 +499,15 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     e->last_launches = 0;
     uint32_t nk = 0;
-    HIP_OK(hipMemsetAsync(e->d_acc, 0, kNumClasses * sizeof(unsigned long long), e->stream));
+    HIP_OK(hipMemsetAsync(e->d_acc, 0, (kNumClasses + 1) * sizeof(unsigned long long), e->stream));
     e->kev_cls.clear();
     HIP_OK(hipEventRecord(e->ev0, e->stream));
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
-        HIP_OK(hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream));
+        HIP_OK(hipMemsetAsync(e->d_counts, 0, (kNumClasses + 1) * sizeof(uint32_t), e->stream));
         HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, e->n_classes, e->first_lds,
                              e->d_counts, e->d_ids, b->ops, e->d_acc, e->stream));
-        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, (kNumClasses + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
         // the classes above 2048 segments keep each document's structure in an HBM workspace
@@ -520,7 +527,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         }
         if (e->concurrent) HIP_OK(hipEventRecord(e->fork_ev, e->stream));
         bool joined[kNumClasses] = {};
-        for (int c = 0; c < kNumClasses; c++) {
+        for (int c = 0; c < e->n_classes; c++) {  // (h_counts[n_classes]: the editing bucket, below)
             const uint32_t cnt = e->h_counts[c];
             if (!cnt) continue;
             hipStream_t st = e->stream;
@@ -553,6 +560,10 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(hipEventRecord(e->join_ev[c], e->side[c]));
             HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
+        // documents with an editing client (local edits + acks): the LDS engine's editing form
+        if (const uint32_t cnt = e->h_counts[e->n_classes])
+            HIP_OK(mt_launch_apply_loc(&e->g, b->ops, b->payload, b->row_ptr, e->d_ids + (size_t)e->n_classes * b->n_docs,
+                                       cnt, lo, per, e->stream));
     }
     HIP_OK(mt_launch_fixup(&e->g, b->ops, b->n_docs, e->stream));  // error precedence, see mt_service.hip
     HIP_OK(hipEventRecord(e->ev1, e->stream));
@@ -623,7 +634,7 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
     if (r == hipSuccess) r = hipMemsetAsync(pay_used, 0, (size_t)n * sizeof(uint32_t), e->stream);
     const uint32_t tick = 64;
     for (uint32_t lo = 0; r == hipSuccess && lo < per; lo += tick) {
-        r = hipMemsetAsync(e->d_counts, 0, kNumClasses * sizeof(uint32_t), e->stream);
+        r = hipMemsetAsync(e->d_counts, 0, (kNumClasses + 1) * sizeof(uint32_t), e->stream);
         if (r == hipSuccess)
             r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, std::min(e->n_classes, kLdsClasses), 0,
                               e->d_counts, e->d_ids, nullptr, nullptr, e->stream);
@@ -631,7 +642,7 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
             r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                e->stream);
         if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
-        for (int c = 0; r == hipSuccess && c < kNumClasses; c++) {
+        for (int c = 0; r == hipSuccess && c < std::min(e->n_classes, kLdsClasses); c++) {
             if (!e->h_counts[c]) continue;
             r = mt_launch_gen(lds_cap(kClasses[c]), &e->g, cfg, doc_id_base, gids, cref, stall, pay_used, payload_per_doc, b->ops,
                               b->payload, b->row_ptr, e->d_ids + (size_t)c * n, e->h_counts[c], lo, tick, e->stream);

@@ -20,6 +20,8 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     sc.n_empty = 1;  // the root leaf block starts empty
     sc.win_op = -1;
     g.sc[d] = sc;
+    g.loc[d].own = -1;  // an observer until its first local edit
+    g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = 0;
     g.lbcnt[(size_t)d * g.lbcap] = 0;
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
 }
@@ -136,6 +138,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
         sc.cur_seq = cur_seq[w];
         sc.min_seq = min_seq[w];
         g.sc[d] = sc;
+        g.loc[d].own = -1;
+        g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = 0;
     }
 }
 
@@ -159,17 +163,25 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         const mt_doc_scalars sc = g.sc[d];
         if (a < b && !sc.err) {
             const int nops = (int)(b - a);
+            int32_t own = g.loc[d].own;
             if (ops && sc.win_op < 0) {
                 // replay the collab window over this launch's ops (client.ts:461-464, 821-828;
                 // mergeTree.ts:1718-1722) to find the first op the apply will halt on for a window
-                // assert; mt_fixup_kernel decides after the apply whether "insert failed" outranks it
+                // assert; mt_fixup_kernel decides after the apply whether "insert failed" outranks it.
+                // An editing client's local edits (seq -1) touch no window; its acks assert only in
+                // updateSeqNumbers (client.ts:804-806, 821-828)
                 int32_t cur = sc.cur_seq, mn = sc.min_seq;
                 for (uint32_t i = a; i < b; i++) {
                     const mt_op_rec o = ops[i];
                     if (o.type == MT_OP_LOAD) continue;  // snapshot body append: no window update
                     if (o.type > MT_OP_LOAD) break;
-                    const bool bad = MT_OP_IS_NOOP(o) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
-                                                          : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
+                    if (o.seq == -1) {
+                        if (own < 0) own = o.client;
+                        continue;
+                    }
+                    const bool ack = (int32_t)o.client == own;
+                    const bool bad = (MT_OP_IS_NOOP(o) || ack) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
+                                                              : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
                     if (bad) {
                         g.sc[d].win_op = (int32_t)i;
                         break;
@@ -199,6 +211,9 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
             c = n_classes - 1;
+            bool editing = own >= 0;
+            if (ops)
+                for (uint32_t i = a; i < b && !editing; i++) editing = ops[i].seq == -1 && ops[i].type != MT_OP_LOAD;
             // (wide documents and snapshot appends start at the first class the LDS engine serves)
             for (int k = (wide || lds_only) ? first_lds : 0; k < n_classes; k++) {
                 const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
@@ -209,6 +224,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     break;
                 }
             }
+            if (editing) c = n_classes;  // the editing documents' bucket (mt_launch_apply_loc)
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
                 // accounting"): persistent state in + out, op records, payload
@@ -223,7 +239,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    for (int k = 0; k < n_classes; k++) {
+    for (int k = 0; k <= n_classes; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;
         const int leader = first_lane(m);

@@ -41,6 +41,22 @@ struct mt_doc_scalars {      // 80 bytes
                              // replay of the window), -1 if none: mt_fixup_kernel's input
 };
 
+// An editing client's document (client.ts:163-214, 588-625): its local
+// edits are pending until their acks.  Pending edit ordinals [glo, ghi) (at most 64 at once) index
+// the per-segment group masks (bit = ordinal % 64); gt[] holds the creation stamp counter at each
+// edit, so an ack can rebuild its group's list order.
+struct mt_loc {
+    int32_t own;             // the editing client's short id; -1: an observer
+    uint32_t glo, ghi;
+    uint32_t stamp;          // creation stamps handed out (segments created while editing)
+    uint32_t gt[64];
+};
+#define MT_LOC_CAP 1024      // an editing document runs on the LDS engine at this capacity
+// pending property counts per segment (SegmentPropertiesManager, segmentPropertiesManager.ts:11-12):
+// 7 bits per key id 0..7 at bit 7k, the pending rewrite count in bits 56..63
+#define MT_PK_KEY(pk, k) ((uint32_t)((pk) >> (7 * (k))) & 0x7Fu)
+#define MT_PK_RW(pk) ((uint32_t)((pk) >> 56))
+
 // Device pointers + capacities (one allocation per array, [n_docs][capacity]).
 struct mt_gstate {
     int32_t* seq;      // [doc][segcap]
@@ -61,5 +77,9 @@ struct mt_gstate {
     uint8_t* text;     // [doc][2][textcap]  text arena, double-buffered for in-kernel compaction
     struct mt_event* ev;  // [doc][evcap] delta / maintenance events (mt_events_enable), or null
     uint32_t* evn;     // [doc] events recorded since the last drain (may exceed evcap: halted)
+    uint64_t* gm;      // [doc][segcap] editing documents: pending group mask per segment
+    uint64_t* pk;      // [doc][segcap] pending property counts (MT_PK_*)
+    uint32_t* ct;      // [doc][segcap] creation stamp
+    mt_loc* loc;       // [doc]
     uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;
 };

@@ -63,15 +63,34 @@ def test_oracle_editing_client_matches_reference(oracle_lib, name):
             assert o.state(0) == want, (name, r['doc'], k)
 
 
+def checkpoint_batch(batch, rows, q):
+    """every document's first k records, k = its q-th checkpoint (rows: the fixture's records)"""
+    from fluidframework_amd.oplog import OpBatch
+    idx, rp = [], [0]
+    for r in rows:
+        a = int(batch.row_ptr[r['doc']])
+        k = r['states'][q][0]
+        idx.append(np.arange(a, a + k))
+        rp.append(rp[-1] + k)
+    return OpBatch(batch.ops[np.concatenate(idx)].copy(), batch.payload, np.array(rp, dtype=np.uint32))
+
+
 @pytest.mark.gpu
-def test_engine_rejects_local_edits_loudly():
-    """The device engines do not apply local edits yet: every document of a local-edit log halts
-    with an error at its first local record instead of diverging silently."""
+@pytest.mark.parametrize('b', [1, 7, 32])
+@pytest.mark.parametrize('name', LOGS)
+def test_engine_editing_client_matches_reference(name, b):
+    """The device's editing form (mt_apply.hip, LOC): every checkpoint state -- pending inserts,
+    removals and property changes included -- and the final state equal the reference's, at several
+    launch sizes (so acks and local edits straddle launches)."""
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import OpBatch
-    batch = OpBatch.load(os.path.join(GOLDEN, 'local_lag.mtlog'))
-    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
-    eng.apply(batch)
-    for d in range(batch.n_docs):
-        code, seq = eng.error(d)
-        assert code != 0 and seq == -1, (d, code, seq)
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    rows = load_local()[name]
+    for q in range(len(rows[0]['states'])):
+        cb = checkpoint_batch(batch, rows, q)
+        eng = MergeEngine(cb.n_docs, ops_per_launch=b)
+        eng.apply(cb)
+        for i, r in enumerate(rows):
+            assert eng.error(i) == (0, 0), (name, r['doc'], q, eng.error(i))
+            assert eng.state(i) == r['states'][q][1], (name, r['doc'], q, b)
+        eng.close()

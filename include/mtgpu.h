@@ -58,6 +58,18 @@ enum mt_op_flags {
     ((o).type == MT_OP_INSERT && !((o).flags & (MT_F_PROPS | MT_F_MARKER)) &&         \
      (o).payload_len <= 2u * MT_OP_NPAIRS((o).flags))
 #define MT_OP_IS_NOOP(o) ((o).type == MT_OP_NOOP || MT_OP_IS_EMPTY_INSERT(o))
+/* An editing client.  A record with seq = MT_SEQ_LOCAL is a local edit of the
+ * document's editing client (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+ * client.ts:163-214): INSERT / REMOVE / ANNOTATE at positions of its local view, applied at once
+ * with refSeq = its currentSeq (ref_seq and msn are ignored), no window asserts, no seq update.
+ * The first such record names the document's editing client (its `client`); from then on that
+ * client's sequenced records are its acks (client.ts:804-806 -> ackPendingSegment,
+ * mergeTree.ts:1893-1920): each settles the oldest pending edit and then updates the window.
+ * Remote ops see the pending segments as the reference does (nodeLength, breakTie,
+ * blockInsert's continuePredicate, pending property keys).  Such a document runs on the LDS
+ * engine's editing form (capacity MT_LOC_CAP = 1024 segments, at most 64 pending edits; beyond:
+ * MT_DERR_CAPACITY) and records no delta events. */
+#define MT_SEQ_LOCAL (-1)
 
 typedef struct mt_op_rec {
     int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */

@@ -10,8 +10,8 @@ continuePredicate :2143-2160).
 Pinned by the reference itself: tests/golden/local.expected.jsonl holds the canonical states
 (checkpoints with pending segments, and the end) of reference Clients replaying the local_* logs
 (tests/golden/make_local.py: a farm of reference clients, logged as client c1 sees it; records
-with seq -1 are c1's local edits).  The CPU oracle restates the editing client; the device engines
-do not implement it yet."""
+with seq -1 are c1's local edits).  The CPU oracle restates the editing client; on the device the
+LDS engine's editing form applies it (mt_apply.hip LOC, include/mtgpu.h MT_SEQ_LOCAL)."""
 import json
 import os
 

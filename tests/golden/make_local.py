@@ -11,7 +11,8 @@ its canonical state at checkpoints (pending segments: seq -1; a pending removal:
 rclient) and at the end:
   * local_rounds: every client catches up at the end of each round (mergeTreeOperationRunner.ts);
   * local_lag: c1 catches up to a random point only, so its edits interleave with remote ops it
-    has not seen yet.
+    has not seen yet;
+  * local_big: longer lagging runs (zamboni, block splits and packs around pending segments).
 local.expected.jsonl: one JSON line per (log, document): {log, doc, err, states: [[k, state], ...]}
 with k the number of the document's records applied.
 """
@@ -27,7 +28,8 @@ sys.path.insert(0, HERE)
 
 from make_golden import build_log  # noqa: E402
 
-LOGS = (('local_rounds', 24, 11, 300, 0), ('local_lag', 24, 12, 300, 1))
+LOGS = (('local_rounds', 24, 11, 300, 0, 6), ('local_lag', 24, 12, 300, 1, 6),
+        ('local_big', 16, 13, 1500, 1, 2))  # (name, docs, seed, edits over all clients, lag, checkpoints)
 
 
 def main():
@@ -35,7 +37,7 @@ def main():
     farm = os.path.join(REPO, 'oracle/tsref/local_farm.js')
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
     out = []
-    for name, n_docs, seed, n_ops, partial in LOGS:
+    for name, n_docs, seed, n_ops, partial, nck in LOGS:
         res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial)], check=True,
                              capture_output=True, text=True)
         docs = []
@@ -44,7 +46,7 @@ def main():
                           flags) for (s, r, m, c, t, p1, p2, text, props, flags) in recs])
         path = os.path.join(HERE, name + '.mtlog')
         build_log(docs).save(path)
-        res = subprocess.run(['node', replay, 'local', path, '6'], check=True, capture_output=True, text=True)
+        res = subprocess.run(['node', replay, 'local', path, str(nck)], check=True, capture_output=True, text=True)
         for line in res.stdout.strip().split('\n'):
             out.append(json.dumps(dict(log=name, **json.loads(line)), separators=(',', ':')))
         print(name, len(docs), 'docs', sum(len(d) for d in docs), 'records')

@@ -1142,7 +1142,8 @@ struct Wave {
             s.lc.own = C;
             sync();
         }
-        if (C != s.lc.own || C == 0 || C >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, -1);
+        // (the editing client may be short id 0, the reference's own id, client.ts:1057-1062)
+        if (C != s.lc.own || C >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, -1);
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, -1);
         if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, -1);
         const uint8_t* pay = payload + op.payload_off;

@@ -8,8 +8,9 @@
 // plus the TestClient helpers of src/test/testClient.ts:102-234 (getText, makeOpMessage,
 // insertTextRemote, removeRangeRemote, enqueueMsg, applyMessages).  Many BatchClients share one
 // BatchEngine (one MI355X); any read flushes every client's queued ops as ONE batched submit.
-// Only remote ops exist for an observer: a message carrying the client's own long id (an ack of
-// a local op) throws, as do register ops and combining ops other than "rewrite".
+// An editing client's local edits (insertTextLocal / insertMarkerLocal / removeRangeLocal /
+// annotateRangeLocal) apply on the device in its local view and its own sequenced messages ack
+// them; register ops and combining ops other than "rewrite" throw.
 // Delta / maintenance callbacks (mergeTreeDeltaCallback.ts:15-73): setting a client's
 // mergeTreeDeltaCallback or mergeTreeMaintenanceCallback makes the engine record them
 // (mt_events_enable); they are delivered, in firing order, after the batch that fired them.
@@ -275,11 +276,44 @@ class BatchClient {
         return r;
     }
 
-    /** Client.applyMsg (client.ts:797-819): queued, applied in the next device batch. */
+    // ---- an editing client (client.ts:163-214): local edits are queued as MT_SEQ_LOCAL records of
+    // the client's own short id (0) and applied on the device in the local view; the client's own
+    // sequenced messages, passed to applyMsg, are their acks (include/mtgpu.h)
+    _local(op) {
+        if (this.longClientId === undefined) throw new Error("BatchClient: startOrUpdateCollaboration first");
+        if (this.engine.recording) throw new Error("BatchClient: delta callbacks are not recorded for an editing client");
+        const msg = { sequenceNumber: -1, referenceSequenceNumber: this.currentSeq, minimumSequenceNumber: 0 };
+        const r = this._record(msg, op, this._shortId(this.longClientId), false);
+        if (r.type === NOOP) return undefined;  // insertSegmentLocal: nothing for an empty segment
+        this.queue.push(r);
+        this.engine.pending += 1;
+        return op;
+    }
+    /** TestClient.insertTextLocal (testClient.ts:133-143) -> insertSegmentLocal: the insert op. */
+    insertTextLocal(pos, text, props) {
+        return this._local({ type: INSERT, pos1: pos, seg: props ? { text, props } : text });
+    }
+    /** TestClient.insertMarkerLocal (testClient.ts:178-188). */
+    insertMarkerLocal(pos, refType, props) {
+        const seg = { marker: { refType } };
+        if (props) seg.props = props;
+        return this._local({ type: INSERT, pos1: pos, seg });
+    }
+    /** Client.removeRangeLocal (client.ts:188-195). */
+    removeRangeLocal(start, end) { return this._local({ type: REMOVE, pos1: start, pos2: end }); }
+    /** Client.annotateRangeLocal (client.ts:163-179). */
+    annotateRangeLocal(start, end, props, combiningOp) {
+        const op = { type: ANNOTATE, pos1: start, pos2: end, props };
+        if (combiningOp) op.combiningOp = combiningOp;
+        return this._local(op);
+    }
+
+    /** Client.applyMsg (client.ts:797-819): queued, applied in the next device batch.  A message of
+     * this client's own long id acks its oldest pending local edit (client.ts:804-806). */
     applyMsg(msg) {
         const client = this._shortId(msg.clientId);
-        if (msg.type === "op" && msg.clientId === this.longClientId) {
-            throw new Error("BatchClient: acks of local ops are not supported by the observer engine");
+        if (msg.type === "op" && msg.clientId === this.longClientId && this.engine.recording) {
+            throw new Error("BatchClient: delta callbacks are not recorded for an editing client");
         }
         const op = msg.type === "op" ? msg.contents : undefined;
         const members = op && op.type === GROUP ? op.ops : [op];

@@ -626,7 +626,7 @@ struct Doc {
     // 2607-2719, 2565-2605)
     void applyLocal(const mt_op_rec& op, const uint8_t* payload) {
         if (own == -100) own = op.client;
-        if (op.client != own || op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, kUnassigned);
+        if (op.client != own || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, kUnassigned);
         if (op.type > MT_OP_ANNOTATE) return fail(MT_DERR_BAD_OP, kUnassigned);
         const int32_t R = currentSeq, C = own, S = kUnassigned;
         const int np = MT_OP_NPAIRS(op.flags);

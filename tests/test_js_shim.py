@@ -238,3 +238,21 @@ def test_batchclient_stack_context_matches_reference(name):
     got = {r['doc']: r['answers'] for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
     for r in load_stacks()[name]:
         assert got[r['doc']] == r['answers'], (name, r['doc'])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['local_rounds', 'local_lag', 'local_big'])
+def test_batchclient_editing_client_matches_reference(name):
+    """BatchClient as an editing client (insertTextLocal / removeRangeLocal / annotateRangeLocal,
+    its own sequenced messages as acks through applyMsg) ends every local_* document in the
+    reference client's final state (tests/golden/local.expected.jsonl)."""
+    from test_local import load_local
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog')],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    for r in load_local()[name]:
+        g = got[r['doc']]
+        assert g['err'] is None, (name, r['doc'], g['err'])
+        assert _js_state_to_log(g['state']) == r['states'][-1][1], (name, r['doc'])

@@ -24,7 +24,8 @@ for (let d = 0; d < log.nDocs; d++) {
         let r;
         if (op.type === 0) {
             r = typeof op.seg === "string" ? c.insertTextLocal(op.pos1, op.seg)
-                : c.insertTextLocal(op.pos1, op.seg.text, op.seg.props);
+                : op.seg.marker ? c.insertMarkerLocal(op.pos1, op.seg.marker.refType, op.seg.props)
+                    : c.insertTextLocal(op.pos1, op.seg.text, op.seg.props);
         } else if (op.type === 1) {
             r = c.removeRangeLocal(op.pos1, op.pos2);
         } else {

@@ -9,7 +9,7 @@
 // lags behind the stream.  A run whose clients end with different text is dropped (the reference
 // itself diverges on some lagging-client runs; such logs are not used as fixtures).
 // TEST INFRASTRUCTURE ONLY (this container).
-//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial]] -> JSON {docs: [[record, ...], ...]}
+//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial [markers]]] -> JSON {docs: [[record, ...], ...]}
 //   record = [seq, ref, msn, client, type, pos1, pos2, text, props {key id: value id | null} | null,
 //             flags]; c1's local edits have seq = -1 (UnassignedSequenceNumber), ref = msn = 0
 const path = require("path");
@@ -29,7 +29,7 @@ function rng(seed) {  // xorshift32
     };
 }
 
-const F_REWRITE = 1;
+const F_REWRITE = 1, F_MARKER = 128;
 function record(seq, ref, msn, client, op) {
     const props = (p) => {
         if (!p) return null;
@@ -39,6 +39,10 @@ function record(seq, ref, msn, client, op) {
     };
     if (op.type === 0) {
         const seg = op.seg;
+        if (seg.marker) {  // IJSONMarkerSegment: the record's one text byte is its refType
+            return [seq, ref, msn, client, 0, op.pos1, 0, String.fromCharCode(seg.marker.refType), props(seg.props),
+                F_MARKER];
+        }
         const text = typeof seg === "string" ? seg : seg.text;
         return [seq, ref, msn, client, 0, op.pos1, 0, text, typeof seg === "string" ? null : props(seg.props), 0];
     }
@@ -47,7 +51,7 @@ function record(seq, ref, msn, client, op) {
         op.combiningOp && op.combiningOp.name === "rewrite" ? F_REWRITE : 0];
 }
 
-function farm(seed, nOps, nClients, partial) {
+function farm(seed, nOps, nClients, partial, markers) {
     const r = rng(seed);
     const ri = (n) => Math.floor(r() * n);
     const clients = [];
@@ -78,7 +82,7 @@ function farm(seed, nOps, nClients, partial) {
             for (let q = 0; q < n; q++) text += String.fromCharCode(97 + ri(26));
             let props;
             if (r() < 0.25) { props = {}; props["k" + ri(3)] = 1 + ri(4); }
-            const seg = new TextSegment(text);
+            const seg = markers && r() < 0.15 ? new Marker([1, 2, 4][ri(3)]) : new TextSegment(text);
             if (props) seg.addProperties(props);
             op = c.insertSegmentLocal(ri(len + 1), seg);
         } else {
@@ -128,11 +132,11 @@ function farm(seed, nOps, nClients, partial) {
     return log;
 }
 
-const [nDocs, seed, nOps, nClients, partial] = process.argv.slice(2).map((x) => parseInt(x, 10));
+const [nDocs, seed, nOps, nClients, partial, markers] = process.argv.slice(2).map((x) => parseInt(x, 10));
 const docs = [];
 let dropped = 0;
 for (let d = 0, k = 0; d < nDocs; k++) {
-    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1);
+    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1);
     if (log) { docs.push(log); d++; } else dropped++;
 }
 process.stderr.write(`local_farm: ${nDocs} documents, ${dropped} runs dropped (clients diverged)\n`);

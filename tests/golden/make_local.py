@@ -12,7 +12,8 @@ rclient) and at the end:
   * local_rounds: every client catches up at the end of each round (mergeTreeOperationRunner.ts);
   * local_lag: c1 catches up to a random point only, so its edits interleave with remote ops it
     has not seen yet;
-  * local_big: longer lagging runs (zamboni, block splits and packs around pending segments).
+  * local_big: longer lagging runs (zamboni, block splits and packs around pending segments);
+  * local_markers: lagging runs whose inserts are Tile / NestBegin / NestEnd markers 15 % of the time.
 local.expected.jsonl: one JSON line per (log, document): {log, doc, err, states: [[k, state], ...]}
 with k the number of the document's records applied.
 """
@@ -28,8 +29,9 @@ sys.path.insert(0, HERE)
 
 from make_golden import build_log  # noqa: E402
 
-LOGS = (('local_rounds', 24, 11, 300, 0, 6), ('local_lag', 24, 12, 300, 1, 6),
-        ('local_big', 16, 13, 1500, 1, 2))  # (name, docs, seed, edits over all clients, lag, checkpoints)
+LOGS = (('local_rounds', 24, 11, 300, 0, 6, 0), ('local_lag', 24, 12, 300, 1, 6, 0),
+        ('local_big', 16, 13, 1500, 1, 2, 0), ('local_markers', 16, 14, 600, 1, 4, 1))
+# (name, docs, seed, edits over all clients, lag, checkpoints, markers among the inserts)
 
 
 def main():
@@ -37,8 +39,8 @@ def main():
     farm = os.path.join(REPO, 'oracle/tsref/local_farm.js')
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
     out = []
-    for name, n_docs, seed, n_ops, partial, nck in LOGS:
-        res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial)], check=True,
+    for name, n_docs, seed, n_ops, partial, nck, markers in LOGS:
+        res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial), str(markers)], check=True,
                              capture_output=True, text=True)
         docs = []
         for recs in json.loads(res.stdout)['docs']:

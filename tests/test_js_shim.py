@@ -241,7 +241,7 @@ def test_batchclient_stack_context_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['local_rounds', 'local_lag', 'local_big'])
+@pytest.mark.parametrize('name', ['local_rounds', 'local_lag', 'local_big', 'local_markers'])
 def test_batchclient_editing_client_matches_reference(name):
     """BatchClient as an editing client (insertTextLocal / removeRangeLocal / annotateRangeLocal,
     its own sequenced messages as acks through applyMsg) ends every local_* document in the

@@ -20,7 +20,7 @@ import pytest
 
 from conftest import GOLDEN
 
-LOGS = ['local_rounds', 'local_lag', 'local_big']
+LOGS = ['local_rounds', 'local_lag', 'local_big', 'local_markers']
 
 
 def load_local():

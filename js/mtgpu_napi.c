@@ -381,7 +381,8 @@ static napi_value range_stacks(napi_env env, napi_callback_info info) {
     }
     const uint32_t n = (uint32_t)(nq / sizeof(mt_tile_query));
     void *items = NULL, *depth = NULL;
-    NAPI_CALL(env, napi_create_buffer(env, (size_t)n * cap ? (size_t)n * cap * sizeof(mt_stack_item) : 1, &items, &ib));
+    const size_t ni = (size_t)n * cap;
+    NAPI_CALL(env, napi_create_buffer(env, ni != 0 ? ni * sizeof(mt_stack_item) : 1, &items, &ib));
     NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(uint32_t) : 1, &depth, &db));
     enter(b);
     mt_status st = mt_range_stacks(b->e, (const mt_tile_query*)q, n, cap, (mt_stack_item*)items, (uint32_t*)depth);

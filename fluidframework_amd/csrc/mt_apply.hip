@@ -1178,6 +1178,7 @@ struct Wave {
         const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
         if constexpr (LOC) {
+            if (S == MT_SEQ_REGEN) return fail(MT_DERR_BAD_OP, S);  // reconnect: the oracle only (include/mtgpu.h)
             if (op.type <= MT_OP_ANNOTATE && S == -1) return apply_local(op, payload);
             if (s.lc.own >= 0 && (int)op.client == s.lc.own && op.type <= MT_OP_ANNOTATE && !MT_OP_IS_NOOP(op))
                 return apply_ack(op, payload);

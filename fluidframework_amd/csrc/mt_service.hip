@@ -179,6 +179,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                         if (own < 0) own = o.client;
                         continue;
                     }
+                    if (o.seq == MT_SEQ_REGEN) break;  // the apply halts there (MT_DERR_BAD_OP)
                     const bool ack = (int32_t)o.client == own;
                     const bool bad = (MT_OP_IS_NOOP(o) || ack) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
                                                               : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));

@@ -70,6 +70,11 @@ enum mt_op_flags {
  * engine's editing form (capacity MT_LOC_CAP = 1024 segments, at most 64 pending edits; beyond:
  * MT_DERR_CAPACITY) and records no delta events. */
 #define MT_SEQ_LOCAL (-1)
+/* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =
+ * MT_SEQ_REGEN from the editing client holds a pending op to regenerate.  Restated and pinned by
+ * the CPU oracle (tests/test_local.py); the device does not regenerate yet and halts the document
+ * there with MT_DERR_BAD_OP. */
+#define MT_SEQ_REGEN (-2)
 
 typedef struct mt_op_rec {
     int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */

@@ -90,14 +90,22 @@ function* messages(log, d, opts) {
             if (r.flags & 4) continue;
             const g = group;
             group = null;
-            yield msgOf(g.r, { type: 3, ops: g.ops });
+            const m = msgOf(g.r, { type: 3, ops: g.ops });
+            Object.defineProperty(m, "end", { value: i + 1 - log.rowPtr[d] });  // records consumed so far
+            yield m;
             continue;
         }
         if (r.seq === -1) {  // an edit of the document's local client (seq UnassignedSequenceNumber)
-            yield { local: true, client: r.client, op, index: i - log.rowPtr[d] };
+            yield { local: true, client: r.client, op, index: i - log.rowPtr[d], end: i + 1 - log.rowPtr[d] };
             continue;
         }
-        yield msgOf(r, op);
+        if (r.seq === -2) {  // reconnect: the local client regenerates this pending op (regeneratePendingOp)
+            yield { regen: true, client: r.client, op, index: i - log.rowPtr[d], end: i + 1 - log.rowPtr[d] };
+            continue;
+        }
+        const m = msgOf(r, op);
+        Object.defineProperty(m, "end", { value: i + 1 - log.rowPtr[d] });
+        yield m;
     }
 }
 

@@ -60,6 +60,7 @@ struct Seg;
 // SegmentGroup (mergeTree.ts:195-202): the segments one local edit touched, acked together
 struct Group {
     std::vector<Seg*> segs;
+    int32_t localSeq = 0;
 };
 
 struct Node {
@@ -83,6 +84,7 @@ struct Seg : Node {
     std::vector<Group*> groups;
     uint8_t pend[kMaxKeys] = {0};
     int pendRewrite = 0;
+    int32_t lseq = 0, lrseq = 0;      // localSeq / localRemovedSeq (0: undefined; mergeTree.ts:91-92)
     Seg() : Node(true) {}
     int len() const { return (int)text.size(); }
 };
@@ -95,6 +97,8 @@ struct Block : Node {
     int8_t needsScour = kUndef;
     Block() : Node(false) {}
 };
+
+void json_escape(std::string& o, const std::string& s);
 
 struct LRU {
     Seg* seg;
@@ -116,6 +120,9 @@ struct Doc {
     // (a record with seq -1); its sequenced messages are acks.  -100: an observer
     int32_t own = -100;
     std::list<Group> pending;          // MergeTree.pendingSegments (mergeTree.ts:1093)
+    int32_t localSeq = 0;              // collabWindow.localSeq (mergeTree.ts:831)
+    uint32_t nrec = 0;                 // records of this document applied so far
+    std::string regenJson;             // the ops regeneratePendingOp produced: [[record, [op, ...]], ...]
 
     Doc() { root = newBlock(); }
 
@@ -286,6 +293,8 @@ struct Doc {
         for (Group* g : r->groups) g->segs.push_back(r);
         std::memcpy(r->pend, s->pend, sizeof(r->pend));
         r->pendRewrite = s->pendRewrite;
+        r->lseq = s->lseq;
+        r->lrseq = s->lrseq;
         return r;
     }
 
@@ -637,8 +646,9 @@ struct Doc {
         for (int q = 0; q < np; q++)
             if (pairs[2 * q] >= kMaxKeys) return fail(MT_DERR_LIMITS, S);
         Group* g = nullptr;
+        if (op.type == MT_OP_INSERT && tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
+        const int32_t L = ++localSeq;
         if (op.type == MT_OP_INSERT) {
-            if (tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
             ensureIntervalBoundary(op.pos1, R, C);
             Seg* x = newSeg();
             x->text.assign(reinterpret_cast<const char*>(pay), tlen);
@@ -649,10 +659,12 @@ struct Doc {
             x->seq = S;
             x->client = C;
             x->marker = (op.flags & MT_F_MARKER) != 0;
+            x->lseq = L;
             Block* sp = insertingWalk(root, op.pos1, R, C, x, false);
             if (!x->parent) return fail(MT_DERR_INSERT_FAILED, S);
             updateRoot(sp);
             join(g, x);  // saveIfLocal
+            g->localSeq = L;
             return;
         }
         ensureIntervalBoundary(op.pos1, R, C);
@@ -663,6 +675,7 @@ struct Doc {
                     if (x->rseq == kUnassigned) {
                         x->rclient = C;
                         x->rseq = S;
+                        x->lrseq = 0;
                     } else {
                         x->overlap |= 1ull << C;
                     }
@@ -670,6 +683,7 @@ struct Doc {
                     x->removed = true;
                     x->rseq = S;
                     x->rclient = C;
+                    x->lrseq = L;
                 }
                 if (x->removed && x->rseq == kUnassigned) join(g, x);
             });
@@ -682,6 +696,83 @@ struct Doc {
                 join(g, x);
             });
         }
+        if (g) g->localSeq = L;
+    }
+
+    // Client.regeneratePendingOp -> resetPendingDeltaToOps (client.ts:708-766, 855-893) for the
+    // oldest pending edit, whose op is `op`: its segments in document order, each at its
+    // findReconnectionPostition (:674-706, the view as of the edit's localSeq), become one new op
+    // each (a removal only while still locally removed), each with a new pending group of the same
+    // localSeq at the queue's tail.  The new ops go to regenJson.
+    void applyRegen(const mt_op_rec& op, const uint8_t* payload) {
+        if (pending.empty()) return fail(MT_DERR_BAD_OP, -2);
+        Group* g = &pending.front();
+        std::vector<std::pair<int, Seg*>> mem;
+        int ord = 0;
+        walkSegs(root, [&](const Seg* s) {
+            for (Seg* x : g->segs)
+                if (x == s) mem.emplace_back(ord, x);
+            ord++;
+        });
+        std::sort(mem.begin(), mem.end(), [](const std::pair<int, Seg*>& a, const std::pair<int, Seg*>& b) {
+            return a.first < b.first;
+        });
+        const int np = MT_OP_NPAIRS(op.flags);
+        const uint8_t* pairs = payload + op.payload_off + (op.payload_len - 2 * np);
+        std::string ops;
+        for (auto& m : mem) {
+            Seg* x = m.second;
+            if (x->groups.empty() || x->groups.front() != g) return fail(MT_DERR_BAD_OP, -2);
+            x->groups.erase(x->groups.begin());
+            const int32_t L = g->localSeq;
+            int pos = 0;
+            bool found = false;
+            walkSegs(root, [&](const Seg* s) {
+                if (s == x) found = true;
+                if (found) return;
+                if ((s->lseq == 0 || s->lseq <= L) && (!s->removed || (s->lrseq != 0 && s->lrseq > L))) pos += s->len();
+            });
+            std::string one;
+            auto propsJson = [](const uint8_t* kv, int n, bool nulls) {
+                std::string o = "{";
+                for (int q = 0; q < n; q++) {
+                    if (!nulls && kv[2 * q + 1] == 0) continue;
+                    if (o.size() > 1) o += ',';
+                    o += "\"" + std::to_string(kv[2 * q]) + "\":" + (kv[2 * q + 1] ? std::to_string(kv[2 * q + 1]) : "null");
+                }
+                return o + "}";
+            };
+            if (op.type == MT_OP_ANNOTATE) {
+                one = "[2," + std::to_string(pos) + "," + std::to_string(pos + x->len()) + ",null," +
+                      propsJson(pairs, np, true) + "," + ((op.flags & MT_F_REWRITE) ? "1" : "0") + "]";
+            } else if (op.type == MT_OP_INSERT) {
+                std::string t;
+                json_escape(t, x->text);
+                std::string p = "null";
+                if (x->props_defined) {
+                    std::vector<uint8_t> kv;
+                    for (int k = 0; k < kMaxKeys; k++)
+                        if (x->props[k]) kv.push_back((uint8_t)k), kv.push_back(x->props[k]);
+                    p = propsJson(kv.data(), (int)kv.size() / 2, false);
+                }
+                one = "[0," + std::to_string(pos) + ",0," + t + "," + p + "," + (x->marker ? "128" : "0") + "]";
+            } else if (op.type == MT_OP_REMOVE) {
+                if (x->lrseq != 0) one = "[1," + std::to_string(pos) + "," + std::to_string(pos + x->len()) + ",null,null,0]";
+            } else {
+                return fail(MT_DERR_BAD_OP, -2);
+            }
+            if (one.empty()) continue;
+            if (!ops.empty()) ops += ',';
+            ops += one;
+            pending.emplace_back();
+            Group& ng = pending.back();
+            ng.localSeq = g->localSeq;
+            ng.segs.push_back(x);
+            x->groups.push_back(&ng);
+        }
+        pending.pop_front();
+        if (!regenJson.empty()) regenJson += ',';
+        regenJson += "[" + std::to_string(nrec) + ",[" + ops + "]]";
     }
 
     // ackPendingSegment (client.ts:588-625 -> mergeTree.ts:1893-1920, BaseSegment.ack :487-522):
@@ -698,7 +789,9 @@ struct Doc {
                 x->groups.erase(x->groups.begin());
                 if (op.type == MT_OP_INSERT) {
                     x->seq = S;
+                    x->lseq = 0;
                 } else if (op.type == MT_OP_REMOVE) {
+                    x->lrseq = 0;
                     if (x->rseq == kUnassigned) x->rseq = S;  // else a remote removal overwrote it
                 } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
                     if (op.flags & MT_F_REWRITE) x->pendRewrite--;
@@ -715,8 +808,13 @@ struct Doc {
 
     void applyOp(const mt_op_rec& op, const uint8_t* payload, bool last_member) {
         if (err) return;
+        struct Count {  // the document's record index, for regenJson
+            uint32_t& n;
+            ~Count() { n++; }
+        } count{nrec};
         if (op.type == MT_OP_LOAD) return loadInsert(op, payload);
         if (op.seq == kUnassigned) return applyLocal(op, payload);
+        if (op.seq == -2) return applyRegen(op, payload);
         if ((int32_t)op.client == own && op.type <= MT_OP_ANNOTATE) return applyAck(op, payload, last_member);
         const int32_t S = op.seq, R = op.ref_seq, C = op.client;
         const int np = MT_OP_NPAIRS(op.flags);
@@ -791,6 +889,7 @@ struct Doc {
                             if (s->rseq == kUnassigned) {  // a pending local removal: the remote one replaces it
                                 s->rclient = C;
                                 s->rseq = S;
+                                s->lrseq = 0;
                             } else {
                                 s->overlap |= 1ull << C;     // addOverlappingClient
                             }
@@ -1285,6 +1384,14 @@ uint32_t mto_stack_context(mto_engine* e, uint32_t doc, int32_t pos, uint32_t ke
         out[2 * i + 1] = st[i].second;
     }
     return (uint32_t)st.size();
+}
+
+// the ops regeneratePendingOp produced for document `doc` (records with seq -2) as JSON
+// [[record index, [[type, pos1, pos2, text | null, props | null, flags], ...]], ...]
+uint64_t mto_doc_regen_json(mto_engine* e, uint32_t doc, char* buf, uint64_t cap) {
+    const std::string j = "[" + e->docs[doc].regenJson + "]";
+    if (buf && cap) std::memcpy(buf, j.data(), std::min<uint64_t>(cap, j.size()));
+    return j.size();
 }
 
 // delta / maintenance events (mt_event form) of every document from now on

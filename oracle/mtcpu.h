@@ -21,6 +21,7 @@ void mto_checksums(mto_engine* e, uint64_t* out, uint32_t n_docs);
 /* Client.findTile of one document: the tile's local position or -1 (labels = property `key`,
  * value ids in the 256-bit vmask) */
 int32_t mto_find_tile(mto_engine* e, uint32_t doc, int32_t pos, uint32_t key, const uint8_t* vmask, int preceding);
+uint64_t mto_doc_regen_json(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
 uint32_t mto_stack_context(mto_engine* e, uint32_t doc, int32_t pos, uint32_t key, const uint8_t* vmask, int32_t* out,
                            uint32_t cap);
 /* delta / maintenance events (mt_event form, include/mtgpu.h) of every document from now on */

@@ -58,6 +58,8 @@ def lib():
         L.mto_record_events.argtypes = [vp, ctypes.c_int]
         L.mto_find_tile.restype = i32
         L.mto_find_tile.argtypes = [vp, u32, i32, u32, vp, ctypes.c_int]
+        L.mto_doc_regen_json.restype = u64
+        L.mto_doc_regen_json.argtypes = [vp, u32, ctypes.c_char_p, u64]
         L.mto_stack_context.restype = u32
         L.mto_stack_context.argtypes = [vp, u32, i32, u32, vp, vp, u32]
         L.mto_events.restype = u64
@@ -134,6 +136,14 @@ class Oracle:
         m = np.ascontiguousarray(vmask, dtype=np.uint8)
         r = lib().mto_find_tile(self.h, doc, pos, key, _ptr(m), 1 if preceding else 0)
         return None if r < 0 else r
+
+    def regen(self, doc):
+        """the ops Client.regeneratePendingOp produced at the document's seq -2 records:
+        [[record index, [[type, pos1, pos2, text, props, flags], ...]], ...]"""
+        n = lib().mto_doc_regen_json(self.h, doc, None, 0)
+        buf = ctypes.create_string_buffer(int(n))
+        lib().mto_doc_regen_json(self.h, doc, buf, n)
+        return json.loads(buf.raw[:n].decode('latin-1'))
 
     def stack_context(self, doc, pos, key, vmask):
         """Client.getStackContext for one range label: [[marker position, refType], ...] bottom to top"""

@@ -9,7 +9,7 @@
 // lags behind the stream.  A run whose clients end with different text is dropped (the reference
 // itself diverges on some lagging-client runs; such logs are not used as fixtures).
 // TEST INFRASTRUCTURE ONLY (this container).
-//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial [markers]]] -> JSON {docs: [[record, ...], ...]}
+//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial [markers [reconnect]]]] -> JSON {docs: [[record, ...], ...]}
 //   record = [seq, ref, msn, client, type, pos1, pos2, text, props {key id: value id | null} | null,
 //             flags]; c1's local edits have seq = -1 (UnassignedSequenceNumber), ref = msn = 0
 const path = require("path");
@@ -30,6 +30,18 @@ function rng(seed) {  // xorshift32
 }
 
 const F_REWRITE = 1, F_MARKER = 128;
+// one record per op; a GROUP op as its members (all but the last flagged "more"), an empty GROUP
+// as a no-op record
+const F_GROUP_MORE = 4;
+function records(seq, ref, msn, client, op) {
+    if (op.type !== 3) return [record(seq, ref, msn, client, op)];
+    if (!op.ops.length) return [[seq, ref, msn, client, 3, 0, 0, null, null, 0]];
+    return op.ops.map((m, i) => {
+        const r = record(seq, ref, msn, client, m);
+        if (i + 1 < op.ops.length) r[9] |= F_GROUP_MORE;
+        return r;
+    });
+}
 function record(seq, ref, msn, client, op) {
     const props = (p) => {
         if (!p) return null;
@@ -51,7 +63,7 @@ function record(seq, ref, msn, client, op) {
         op.combiningOp && op.combiningOp.name === "rewrite" ? F_REWRITE : 0];
 }
 
-function farm(seed, nOps, nClients, partial, markers) {
+function farm(seed, nOps, nClients, partial, markers, reconnect) {
     const r = rng(seed);
     const ri = (n) => Math.floor(r() * n);
     const clients = [];
@@ -64,11 +76,12 @@ function farm(seed, nOps, nClients, partial, markers) {
     const seqd = [];       // sequenced messages
     const cursor = clients.map(() => 0);
     const log = [];        // c1's view
+    const regen = [];      // [index of the seq -2 record, regenerated ops]
     let seq = 0, made = 0;
     const deliver = (i) => {
         const m = seqd[cursor[i]++];
         clients[i].applyMsg(m);
-        if (i === 0) log.push(record(m.sequenceNumber, m.referenceSequenceNumber, m.minimumSequenceNumber,
+        if (i === 0) log.push(...records(m.sequenceNumber, m.referenceSequenceNumber, m.minimumSequenceNumber,
             parseInt(m.clientId.slice(1), 10), m.contents));
     };
     const localOp = (i) => {
@@ -97,7 +110,8 @@ function farm(seed, nOps, nClients, partial, markers) {
             }
         }
         if (!op) throw new Error("local op rejected");
-        queue.push({ client: i + 1, ref: c.getCurrentSeq(), op });
+        // (the pending group of the edit: what regeneratePendingOp is handed on reconnect)
+        queue.push({ client: i + 1, ref: c.getCurrentSeq(), op, sg: c.peekPendingSegmentGroups() });
         if (i === 0) log.push(record(-1, 0, 0, 1, op));
         made++;
     };
@@ -120,23 +134,43 @@ function farm(seed, nOps, nClients, partial, markers) {
             const k = r() < 0.6 ? 1 + ri(3) : 0;
             for (let q = 0; q < k; q++) localOp(i);
         }
+        // reconnect (client.reconnectFarm.spec.ts): c1's messages of this round are never sequenced;
+        // c1 catches up with everything else, then regenerates each lost op (regeneratePendingOp,
+        // client.ts:855-893) and submits the new one.  In c1's log: one record with seq -2 per lost
+        // op (the op being reset), and the regenerated ops in `regen`
+        let lost = [];
+        if (reconnect && r() < 0.5) {
+            lost = queue.filter((q) => q.client === 1);
+            for (let q = queue.length - 1; q >= 0; q--) if (queue[q].client === 1) queue.splice(q, 1);
+        }
         sequenceAll();
         for (let i = 1; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
         const upto = partial ? cursor[0] + ri(seqd.length - cursor[0] + 1) : seqd.length;
         while (cursor[0] < upto) deliver(0);
+        for (const q of lost) {
+            const c = clients[0];
+            log.push(...records(-2, 0, 0, 1, q.op));
+            const op = c.regeneratePendingOp(q.op, q.sg);
+            regen.push([log.length - 1, (op.type === 3 ? op.ops : [op]).map((m) => record(0, 0, 0, 1, m).slice(4))]);
+            queue.push({ client: 1, ref: c.getCurrentSeq(), op, sg: undefined });
+        }
+        if (lost.length) {  // the regenerated ops are sequenced and reach everyone in the same round
+            sequenceAll();
+            for (let i = 0; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
+        }
     }
     while (cursor[0] < seqd.length) deliver(0);
     const txt = (c) => c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId());
     const t0 = txt(clients[0]);
     for (const c of clients) if (txt(c) !== t0) return null;  // the clients diverged: drop the run
-    return log;
+    return reconnect ? { log, regen } : log;
 }
 
-const [nDocs, seed, nOps, nClients, partial, markers] = process.argv.slice(2).map((x) => parseInt(x, 10));
+const [nDocs, seed, nOps, nClients, partial, markers, reconnect] = process.argv.slice(2).map((x) => parseInt(x, 10));
 const docs = [];
 let dropped = 0;
 for (let d = 0, k = 0; d < nDocs; k++) {
-    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1);
+    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1, reconnect === 1);
     if (log) { docs.push(log); d++; } else dropped++;
 }
 process.stderr.write(`local_farm: ${nDocs} documents, ${dropped} runs dropped (clients diverged)\n`);

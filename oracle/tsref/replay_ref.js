@@ -38,6 +38,24 @@ const { loadLog, messages } = require(path.join(__dirname, "..", "..", "js", "mt
 // the segment factory a SharedString uses (sequence/src/sharedString.ts segmentFromSpec): text or marker
 function specToSegment(spec) { return TextSegment.fromJSONObject(spec) || Marker.fromJSONObject(spec); }
 
+// a merge-tree op as an op-record tuple [type, pos1, pos2, text | null, {key id: value id | null} | null,
+// flags] (F_REWRITE 1, F_MARKER 128; local_farm.js writes the same form)
+function opTuple(op) {
+    const props = (p) => {
+        if (!p) return null;
+        const o = {};
+        for (const k of Object.keys(p)) o[parseInt(k.slice(1), 10)] = p[k] === undefined ? null : p[k];
+        return o;
+    };
+    if (op.type === 0) {
+        const seg = op.seg;
+        if (seg.marker) return [0, op.pos1, 0, String.fromCharCode(seg.marker.refType), props(seg.props), 128];
+        return [0, op.pos1, 0, typeof seg === "string" ? seg : seg.text, typeof seg === "string" ? null : props(seg.props), 0];
+    }
+    if (op.type === 1) return [1, op.pos1, op.pos2, null, null, 0];
+    return [2, op.pos1, op.pos2, null, props(op.props), op.combiningOp && op.combiningOp.name === "rewrite" ? 1 : 0];
+}
+
 function newObserver() {
     const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
     const c = new Client(specToSegment, logger);
@@ -319,10 +337,14 @@ function main() {
             const cks = new Set();
             for (let q = 1; q < nck; q++) cks.add(Math.floor((q * n) / nck));
             const states = [];
+            const regen = [];
             let err = null, k = 0;
             try {
                 for (const it of items) {
-                    if (it.local) {
+                    if (it.regen) {  // regeneratePendingOp of the oldest pending edit (client.ts:855-893)
+                        const op2 = c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+                        regen.push([it.index, (op2.type === 3 ? op2.ops : [op2]).map(opTuple)]);
+                    } else if (it.local) {
                         const op = it.op;
                         let ok;
                         if (op.type === 0) ok = c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
@@ -332,14 +354,14 @@ function main() {
                     } else {
                         c.applyMsg(it);
                     }
-                    k++;
+                    k = it.end;  // records consumed (a GROUP message is several)
                     if (cks.has(k)) states.push([k, canonical(c)]);
                 }
             } catch (e) {
                 err = String(e.message || e);
             }
             states.push([k, canonical(c)]);
-            out.push(JSON.stringify({ doc: d, err, states }));
+            out.push(JSON.stringify(regen.length ? { doc: d, err, states, regen } : { doc: d, err, states }));
         }
         process.stdout.write(out.join("\n") + "\n");
         return;

@@ -13,7 +13,10 @@ rclient) and at the end:
   * local_lag: c1 catches up to a random point only, so its edits interleave with remote ops it
     has not seen yet;
   * local_big: longer lagging runs (zamboni, block splits and packs around pending segments);
-  * local_markers: lagging runs whose inserts are Tile / NestBegin / NestEnd markers 15 % of the time.
+  * local_markers: lagging runs whose inserts are Tile / NestBegin / NestEnd markers 15 % of the time;
+  * local_reconnect: c1 loses the messages of a round now and then and regenerates them
+    (regeneratePendingOp, client.ts:855-893; the client.reconnectFarm.spec.ts pattern): a record
+    with seq -2 holds the op being reset, `regen` the ops the reference regenerated from it.
 local.expected.jsonl: one JSON line per (log, document): {log, doc, err, states: [[k, state], ...]}
 with k the number of the document's records applied.
 """
@@ -30,8 +33,9 @@ sys.path.insert(0, HERE)
 from make_golden import build_log  # noqa: E402
 
 LOGS = (('local_rounds', 24, 11, 300, 0, 6, 0), ('local_lag', 24, 12, 300, 1, 6, 0),
-        ('local_big', 16, 13, 1500, 1, 2, 0), ('local_markers', 16, 14, 600, 1, 4, 1))
-# (name, docs, seed, edits over all clients, lag, checkpoints, markers among the inserts)
+        ('local_big', 16, 13, 1500, 1, 2, 0), ('local_markers', 16, 14, 600, 1, 4, 1),
+        ('local_reconnect', 24, 15, 400, 0, 4, 1, 1))
+# (name, docs, seed, edits over all clients, lag, checkpoints, markers among the inserts[, reconnects])
 
 
 def main():
@@ -39,18 +43,25 @@ def main():
     farm = os.path.join(REPO, 'oracle/tsref/local_farm.js')
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
     out = []
-    for name, n_docs, seed, n_ops, partial, nck, markers in LOGS:
-        res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial), str(markers)], check=True,
-                             capture_output=True, text=True)
-        docs = []
+    for name, n_docs, seed, n_ops, partial, nck, markers, *rc in LOGS:
+        reconnect = rc[0] if rc else 0
+        res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), '4', str(partial), str(markers),
+                              str(reconnect)], check=True, capture_output=True, text=True)
+        docs, farm_regen = [], []
         for recs in json.loads(res.stdout)['docs']:
+            if reconnect:
+                farm_regen.append(recs['regen'])
+                recs = recs['log']
             docs.append([(s, r, m, c, t, p1, p2, text, None if props is None else {int(k): v for k, v in props.items()},
                           flags) for (s, r, m, c, t, p1, p2, text, props, flags) in recs])
         path = os.path.join(HERE, name + '.mtlog')
         build_log(docs).save(path)
         res = subprocess.run(['node', replay, 'local', path, str(nck)], check=True, capture_output=True, text=True)
         for line in res.stdout.strip().split('\n'):
-            out.append(json.dumps(dict(log=name, **json.loads(line)), separators=(',', ':')))
+            r = json.loads(line)
+            if reconnect:  # the replay regenerated what the farm's client did
+                assert r['regen'] == farm_regen[r['doc']], (name, r['doc'])
+            out.append(json.dumps(dict(log=name, **r), separators=(',', ':')))
         print(name, len(docs), 'docs', sum(len(d) for d in docs), 'records')
     with open(os.path.join(HERE, 'local.expected.jsonl'), 'w') as f:
         f.write('\n'.join(out) + '\n')

@@ -21,6 +21,7 @@ import pytest
 from conftest import GOLDEN
 
 LOGS = ['local_rounds', 'local_lag', 'local_big', 'local_markers']
+RECONNECT = 'local_reconnect'
 
 
 def load_local():
@@ -63,6 +64,26 @@ def test_oracle_editing_client_matches_reference(oracle_lib, name):
             assert o.state(0) == want, (name, r['doc'], k)
 
 
+def test_oracle_reconnect_matches_reference(oracle_lib):
+    """Client.regeneratePendingOp (client.ts:708-766, 855-893) on reconnect: the ops the oracle
+    regenerates at every seq -2 record equal the reference's, and every checkpoint state (pending
+    groups re-queued, the regenerated ops acked) too."""
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, RECONNECT + '.mtlog'))
+    rows = load_local()[RECONNECT]
+    assert sum(len(r['regen']) for r in rows) > 1000
+    assert any(len(ops) > 1 for r in rows for _, ops in r['regen'])  # regenerated GROUP ops
+    o = oracle_lib.Oracle(batch.n_docs).apply(batch)
+    for r in rows:
+        d = r['doc']
+        assert o.error(d) == (0, 0), (d, o.error(d))
+        assert o.regen(d) == r['regen'], d
+        assert o.state(d) == r['states'][-1][1], d
+        for k, want in r['states'][:-1]:
+            p = oracle_lib.Oracle(1).apply(prefix(batch, d, k))
+            assert p.state(0) == want, (d, k)
+
+
 def checkpoint_batch(batch, rows, q):
     """every document's first k records, k = its q-th checkpoint (rows: the fixture's records)"""
     from fluidframework_amd.oplog import OpBatch
@@ -94,3 +115,16 @@ def test_engine_editing_client_matches_reference(name, b):
             assert eng.error(i) == (0, 0), (name, r['doc'], q, eng.error(i))
             assert eng.state(i) == r['states'][q][1], (name, r['doc'], q, b)
         eng.close()
+
+
+@pytest.mark.gpu
+def test_engine_halts_loudly_at_reconnect():
+    """The device does not regenerate pending ops yet: each document halts with MT_DERR_BAD_OP at its
+    first seq -2 record instead of diverging."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, RECONNECT + '.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    eng.apply(batch)
+    for d in range(batch.n_docs):
+        assert eng.error(d) == (7, -2), (d, eng.error(d))

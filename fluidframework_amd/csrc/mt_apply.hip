@@ -62,6 +62,7 @@ struct Lds {
     uint64_t gm[LOC ? CAP : 1];
     uint64_t pk[LOC ? CAP : 1];
     uint32_t ct[LOC ? CAP : 1];
+    uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
 };
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
@@ -87,6 +88,9 @@ struct Wave {
     const uint32_t textcap;
     mt_event* const ev;     // the document's delta-event records (null: not recording)
     const uint32_t evcap;
+    uint32_t rix = 0;       // index of the record being applied within its document
+    mt_op_rec* rg = nullptr;  // (LOC) the document's regenerated-op buffer and its payload
+    uint8_t* rgp = nullptr;
 
     MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc, mt_event* e = nullptr, uint32_t ec = 0)
         : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc), ev(e), evcap(ec) {}
@@ -499,6 +503,7 @@ struct Wave {
             if constexpr (LOC) {  // segmentGroups.copyTo + the property manager's counts (mergeTree.ts:555-560)
                 s.gm[t] = s.gm[sl];
                 s.pk[t] = s.pk[sl];
+                s.lsq[t] = s.lsq[sl];
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
                 s.ct[t] = s.lc.stamp;
             }
@@ -885,10 +890,12 @@ struct Wave {
                 if constexpr (LOC) {  // a local insert is its edit's one pending segment (saveIfLocal)
                     s.gm[t] = S == -1 ? (1ull << (s.lc.ghi & 63u)) : 0ull;
                     s.pk[t] = 0;
+                    s.lsq[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
                     s.lc.stamp = s.lc.stamp + 1;
                     s.ct[t] = s.lc.stamp;
                     if (S == -1) {
                         s.lc.gt[s.lc.ghi & 63u] = s.ct[t];
+                        s.lc.gls[s.lc.ghi & 63u] = s.lc.lseq;
                         s.lc.ghi = s.lc.ghi + 1;
                     }
                 }
@@ -926,7 +933,10 @@ struct Wave {
             if (local) {  // this edit's pending group (addToPendingList, mergeTree.ts:1922-1929)
                 gbit = 1ull << (s.lc.ghi & 63u);
                 sync();
-                if (lane == 0) s.lc.gt[s.lc.ghi & 63u] = s.lc.stamp + 1;  // every member existed before it
+                if (lane == 0) {
+                    s.lc.gt[s.lc.ghi & 63u] = s.lc.stamp + 1;  // every member existed before it
+                    s.lc.gls[s.lc.ghi & 63u] = s.lc.lseq;
+                }
                 sync();
                 s.lc.ghi = s.lc.ghi + 1;
                 sync();
@@ -950,12 +960,16 @@ struct Wave {
                         if (pend_rm) {  // a pending local removal: this one replaces it (mergeTree.ts:2621-2627)
                             s.rseq[sl] = S;
                             s.rclient[sl] = (uint8_t)C;
+                            if constexpr (LOC) s.lsq[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
                         } else if (s.flags[sl] & MT_SF_REMOVED) {
                             s.ovl[sl] |= cbit;  // addOverlappingClient (first remover wins)
                         } else {
                             s.flags[sl] |= MT_SF_REMOVED;
                             s.rseq[sl] = S;
                             s.rclient[sl] = (uint8_t)C;
+                            if constexpr (LOC) {  // localRemovedSeq (mergeTree.ts:2637)
+                                s.lsq[sl] = (s.lsq[sl] & 0xFFFFFFFFull) | ((uint64_t)(local ? s.lc.lseq : 0u) << 32);
+                            }
                         }
                     } else {  // SegmentPropertiesManager.addProperties (remote, no combining op)
                         uint64_t p = (s.flags[sl] & MT_SF_PDEF) ? s.props[sl] : 0;
@@ -1045,7 +1059,9 @@ struct Wave {
                 s.gm[sl] &= ~bit;
                 if (type == MT_OP_INSERT) {
                     s.seq[sl] = S;
+                    s.lsq[sl] &= ~0xFFFFFFFFull;
                 } else if (type == MT_OP_REMOVE) {
+                    s.lsq[sl] &= 0xFFFFFFFFull;
                     if (s.rseq[sl] == -1) s.rseq[sl] = S;  // else a remote removal overwrote it
                 } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
                     uint64_t pk = s.pk[sl];
@@ -1116,6 +1132,122 @@ struct Wave {
         }
     }
 
+    // Client.regeneratePendingOp -> resetPendingDeltaToOps (client.ts:708-766, 855-893) for the
+    // oldest pending edit, whose op is `op`: its segments in document order, each at its
+    // findReconnectionPostition (:674-706: the segments before it inserted and not removed as of the
+    // edit's localSeq), become one new op each (a removal only while still locally removed), each
+    // with a new pending group of the same localSeq at the queue's tail.  The new ops go to the
+    // document's regenerated-op buffer after a header record (type MT_OP_NOOP) carrying rix.
+    MT_DEV void op_regen(const mt_op_rec& op, const uint8_t* payload) {
+        if constexpr (LOC) {
+            const int32_t S = MT_SEQ_REGEN;
+            if (s.lc.own < 0 || (int)op.client != s.lc.own || op.type > MT_OP_ANNOTATE) return fail(MT_DERR_BAD_OP, S);
+            if (s.lc.glo == s.lc.ghi) return fail(MT_DERR_BAD_OP, S);
+            const int np = MT_OP_NPAIRS(op.flags);
+            const uint8_t* opairs = payload + op.payload_off + (op.payload_len - 2 * np);
+            const uint32_t Lo = s.lc.glo;
+            const uint64_t bit = 1ull << (Lo & 63u);
+            const uint32_t Ls = s.lc.gls[Lo & 63u];
+            auto emit_rec = [&](const mt_op_rec& r) -> bool {
+                if (s.lc.rgn >= MT_RG_RECS || s.lc.rgpn + r.payload_len > MT_RG_BYTES) return fail(MT_DERR_CAPACITY, S), false;
+                if (lane == 0) rg[s.lc.rgn] = r;
+                sync();
+                s.lc.rgn = s.lc.rgn + 1;
+                s.lc.rgpn = s.lc.rgpn + r.payload_len;
+                sync();
+                return true;
+            };
+            mt_op_rec h{};
+            h.seq = (int32_t)rix;
+            h.type = MT_OP_NOOP;
+            if (!emit_rec(h)) return;
+            const int n = s.n;
+            for (int base = 0; base < n; base += 64) {
+                const int i = base + lane;
+                const bool mem = i < n && (s.gm[s.order[i]] & bit);
+                uint64_t m = wave_ballot(mem);
+                while (m) {
+                    const int k = base + first_lane(m);
+                    m &= m - 1;
+                    const int sl = s.order[k];
+                    int pos = 0;  // findReconnectionPostition
+                    for (int b2 = 0; b2 < k; b2 += 64) {
+                        const int j = b2 + lane;
+                        int v = 0;
+                        if (j < k) {
+                            const int sj = s.order[j];
+                            const uint32_t lo = (uint32_t)s.lsq[sj], hi = (uint32_t)(s.lsq[sj] >> 32);
+                            if ((lo == 0 || lo <= Ls) && (!(s.flags[sj] & MT_SF_REMOVED) || (hi != 0 && hi > Ls))) v = (int)s.len[sj];
+                        }
+                        pos += wave_sum(v);
+                    }
+                    sync();
+                    if (lane == 0) s.gm[sl] &= ~bit;
+                    sync();
+                    const uint32_t len = s.len[sl];
+                    mt_op_rec r{};
+                    r.seq = (int32_t)rix;
+                    r.type = op.type;
+                    r.client = (uint16_t)s.lc.own;
+                    r.pos1 = pos;
+                    r.pos2 = op.type == MT_OP_INSERT ? 0 : pos + (int32_t)len;
+                    r.payload_off = s.lc.rgpn;
+                    bool keep = true;
+                    uint8_t kv[16];
+                    int nkv = 0;
+                    if (op.type == MT_OP_INSERT) {  // the segment's spec: its text (or refType) and props
+                        const uint8_t f = s.flags[sl];
+                        r.flags = (f & MT_SF_MARKER) ? MT_F_MARKER : 0;
+                        if (f & MT_SF_PDEF) {
+                            r.flags |= MT_F_PROPS;
+                            for (int q = 0; q < 8; q++) {
+                                const uint8_t v = (uint8_t)(s.props[sl] >> (8 * q));
+                                if (v) {
+                                    kv[2 * nkv] = (uint8_t)q;
+                                    kv[2 * nkv + 1] = v;
+                                    nkv++;
+                                }
+                            }
+                        }
+                        r.payload_len = len + 2u * (uint32_t)nkv;
+                    } else if (op.type == MT_OP_REMOVE) {
+                        keep = (s.lsq[sl] >> 32) != 0;  // still locally removed
+                        r.payload_len = 0;
+                    } else {
+                        r.flags = op.flags & MT_F_REWRITE;
+                        nkv = np < 8 ? np : 8;
+                        for (int q = 0; q < 2 * nkv; q++) kv[q] = opairs[q];
+                        r.payload_len = 2u * (uint32_t)nkv;
+                    }
+                    if (!keep) continue;
+                    r.flags |= (uint8_t)(nkv << MT_F_NPAIRS_SHIFT);
+                    if (s.lc.rgpn + r.payload_len > MT_RG_BYTES) return fail(MT_DERR_CAPACITY, S);
+                    if (op.type == MT_OP_INSERT) {
+                        for (uint32_t t = lane; t < len; t += 64) rgp[s.lc.rgpn + t] = arena[s.toff[sl] + t];
+                    }
+                    if (lane == 0)
+                        for (int q = 0; q < 2 * nkv; q++) rgp[s.lc.rgpn + (op.type == MT_OP_INSERT ? len : 0) + q] = kv[q];
+                    if (!emit_rec(r)) return;
+                    // its own pending group, same localSeq, at the queue's tail
+                    if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, S);
+                    sync();
+                    if (lane == 0) {
+                        const uint32_t N = s.lc.ghi;
+                        s.gm[sl] |= 1ull << (N & 63u);
+                        s.lc.gls[N & 63u] = Ls;
+                        s.lc.gt[N & 63u] = s.ct[sl];
+                    }
+                    sync();
+                    s.lc.ghi = s.lc.ghi + 1;
+                    sync();
+                }
+            }
+            sync();
+            s.lc.glo = Lo + 1;
+            sync();
+        }
+    }
+
     // Client.updateSeqNumbers + MergeTree.setMinSeq (client.ts:821-828, mergeTree.ts:1718-1736)
     MT_DEV void update_seq(int32_t msn, int32_t seq) {
         if (!(s.cur_seq <= seq)) return fail(MT_DERR_SEQ_ORDER, seq);
@@ -1154,8 +1286,11 @@ struct Wave {
         mt_op_rec o = op;
         o.ref_seq = s.cur_seq;
         const int L = scan(o.ref_seq, C);
+        if (op.type == MT_OP_INSERT && tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
+        sync();
+        s.lc.lseq = s.lc.lseq + 1;  // ++collabWindow.localSeq (mergeTree.ts:1976, 2571, 2613)
+        sync();
         if (op.type == MT_OP_INSERT) {
-            if (tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
             if (o.pos1 < 0 || o.pos1 > L) return fail(MT_DERR_INSERT_FAILED, -1);
             op_insert(o, pay, tlen, pairs, np);
         } else {
@@ -1178,7 +1313,7 @@ struct Wave {
         const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
         if constexpr (LOC) {
-            if (S == MT_SEQ_REGEN) return fail(MT_DERR_BAD_OP, S);  // reconnect: the oracle only (include/mtgpu.h)
+            if (S == MT_SEQ_REGEN) return op_regen(op, payload);
             if (op.type <= MT_OP_ANNOTATE && S == -1) return apply_local(op, payload);
             if (s.lc.own >= 0 && (int)op.client == s.lc.own && op.type <= MT_OP_ANNOTATE && !MT_OP_IS_NOOP(op))
                 return apply_ack(op, payload);
@@ -1419,8 +1554,12 @@ struct Wave {
                 s.lc.glo = g.loc[d].glo;
                 s.lc.ghi = g.loc[d].ghi;
                 s.lc.stamp = g.loc[d].stamp;
+                s.lc.lseq = g.loc[d].lseq;
+                s.lc.rgn = g.loc[d].rgn;
+                s.lc.rgpn = g.loc[d].rgpn;
             }
             s.lc.gt[lane] = g.loc[d].gt[lane];
+            s.lc.gls[lane] = g.loc[d].gls[lane];
             sync();
             // (a document that has not edited yet has never stored these arrays)
             const bool has = s.lc.own >= 0;
@@ -1429,6 +1568,7 @@ struct Wave {
                 s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
                 s.pk[i] = has ? g.pk[lo2 + i] : 0ull;
                 s.ct[i] = has ? g.ct[lo2 + i] : 0u;
+                s.lsq[i] = has ? g.lsq[lo2 + i] : 0ull;
             }
         }
         sync();
@@ -1495,14 +1635,19 @@ struct Wave {
                     g.gm[lo2 + i] = s.gm[sl];
                     g.pk[lo2 + i] = s.pk[sl];
                     g.ct[lo2 + i] = s.ct[sl];
+                    g.lsq[lo2 + i] = s.lsq[sl];
                 }
                 if (lane == 0) {
                     g.loc[d].own = s.lc.own;
                     g.loc[d].glo = s.lc.glo;
                     g.loc[d].ghi = s.lc.ghi;
                     g.loc[d].stamp = s.lc.stamp;
+                    g.loc[d].lseq = s.lc.lseq;
+                    g.loc[d].rgn = s.lc.rgn;
+                    g.loc[d].rgpn = s.lc.rgpn;
                 }
                 g.loc[d].gt[lane] = s.lc.gt[lane];
+                g.loc[d].gls[lane] = s.lc.gls[lane];
             }
         }
     }
@@ -1551,6 +1696,10 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
         }
     }
     wv.load(g, d);
+    if (LOC) {
+        wv.rg = g.rg + (size_t)d * MT_RG_RECS;
+        wv.rgp = g.rgp + (size_t)d * MT_RG_BYTES;
+    }
     if (GEN) {
         lds.gcref[wv.lane] = gen.cref[(size_t)d * 64 + wv.lane];
         if (wv.lane == 0) {
@@ -1580,6 +1729,7 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
         for (uint32_t i = a; i < b; i++) {
             if (lds.err) break;
             const mt_op_rec op = ops[i];
+            wv.rix = i - r0;
             wv.apply(op, payload);
         }
     }

@@ -188,6 +188,8 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
         (st = dalloc(e, &g.gm, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pk, D * MT_LOC_CAP)) ||
         (st = dalloc(e, &g.ct, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
+        (st = dalloc(e, &g.lsq, D * MT_LOC_CAP)) || (st = dalloc(e, &g.rg, D * MT_RG_RECS)) ||
+        (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) ||
         // (+1: the editing documents' bucket after the capacity classes)
         (st = dalloc(e, &e->d_counts, kNumClasses + 1)) || (st = dalloc(e, &e->d_acc, kNumClasses + 1)) ||
         (st = dalloc(e, &e->d_ids, D * (kNumClasses + 1)))) {
@@ -333,6 +335,24 @@ mt_status mt_find_tiles(mt_engine* e, const mt_tile_query* q, uint32_t n, mt_til
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
     (void)hipFree(buf);
     return r == hipSuccess ? MT_OK : MT_ERR_HIP;
+}
+
+mt_status mt_regen_drain(mt_engine* e, uint32_t doc, mt_op_rec* recs, uint32_t cap, uint8_t* payload, uint32_t pcap,
+                         uint32_t* n, uint32_t* pn) {
+    if (!e || doc >= e->n_docs || !n || !pn) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    uint32_t cnt[2] = {0, 0};  // mt_loc::rgn, rgpn (adjacent)
+    HIP_OK(hipMemcpy(cnt, &e->g.loc[doc].rgn, sizeof cnt, hipMemcpyDeviceToHost));
+    *n = cnt[0];
+    *pn = cnt[1];
+    if (recs && cap)
+        HIP_OK(hipMemcpy(recs, e->g.rg + (size_t)doc * MT_RG_RECS, std::min(cap, cnt[0]) * sizeof(mt_op_rec),
+                         hipMemcpyDeviceToHost));
+    if (payload && pcap)
+        HIP_OK(hipMemcpy(payload, e->g.rgp + (size_t)doc * MT_RG_BYTES, std::min(pcap, cnt[1]), hipMemcpyDeviceToHost));
+    if (recs) HIP_OK(hipMemset(&e->g.loc[doc].rgn, 0, sizeof cnt));
+    return MT_OK;
 }
 
 mt_status mt_range_stacks(mt_engine* e, const mt_tile_query* q, uint32_t n, uint32_t cap, mt_stack_item* items,

@@ -21,7 +21,7 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     sc.win_op = -1;
     g.sc[d] = sc;
     g.loc[d].own = -1;  // an observer until its first local edit
-    g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = 0;
+    g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = g.loc[d].lseq = g.loc[d].rgn = g.loc[d].rgpn = 0;
     g.lbcnt[(size_t)d * g.lbcap] = 0;
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
 }
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
         sc.min_seq = min_seq[w];
         g.sc[d] = sc;
         g.loc[d].own = -1;
-        g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = 0;
+        g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = g.loc[d].lseq = g.loc[d].rgn = g.loc[d].rgpn = 0;
     }
 }
 
@@ -179,7 +179,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                         if (own < 0) own = o.client;
                         continue;
                     }
-                    if (o.seq == MT_SEQ_REGEN) break;  // the apply halts there (MT_DERR_BAD_OP)
+                    if (o.seq == MT_SEQ_REGEN) continue;  // reconnect: no window update
                     const bool ack = (int32_t)o.client == own;
                     const bool bad = (MT_OP_IS_NOOP(o) || ack) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
                                                               : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));

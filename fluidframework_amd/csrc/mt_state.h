@@ -50,7 +50,12 @@ struct mt_loc {
     uint32_t glo, ghi;
     uint32_t stamp;          // creation stamps handed out (segments created while editing)
     uint32_t gt[64];
+    uint32_t lseq;           // collabWindow.localSeq (mergeTree.ts:831)
+    uint32_t gls[64];        // each pending group's localSeq
+    uint32_t rgn, rgpn;      // regenerated op records / payload bytes not drained yet
 };
+#define MT_RG_RECS 256       // regenerated op records per document between drains
+#define MT_RG_BYTES 4096     // and their payload bytes
 #define MT_LOC_CAP 1024      // an editing document runs on the LDS engine at this capacity
 // pending property counts per segment (SegmentPropertiesManager, segmentPropertiesManager.ts:11-12):
 // 7 bits per key id 0..7 at bit 7k, the pending rewrite count in bits 56..63
@@ -80,6 +85,9 @@ struct mt_gstate {
     uint64_t* gm;      // [doc][segcap] editing documents: pending group mask per segment
     uint64_t* pk;      // [doc][segcap] pending property counts (MT_PK_*)
     uint32_t* ct;      // [doc][segcap] creation stamp
+    uint64_t* lsq;     // [doc][segcap] localSeq (low 32 bits) / localRemovedSeq (high), 0: undefined
     mt_loc* loc;       // [doc]
+    struct mt_op_rec* rg;  // [doc][MT_RG_RECS] regenerated ops (seq = the resetting record's index)
+    uint8_t* rgp;      // [doc][MT_RG_BYTES] their payload
     uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;
 };

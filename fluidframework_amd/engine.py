@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-from .oplog import OpBatch
+from .oplog import OP_DTYPE, OpBatch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('MTGPU_LIB') or os.path.join(HERE, 'libmtgpu.so')
@@ -95,6 +95,7 @@ def lib():
                                        vp]
         L.mt_find_tiles.argtypes = [vp, vp, u32, vp]
         L.mt_range_stacks.argtypes = [vp, vp, u32, u32, vp, vp]
+        L.mt_regen_drain.argtypes = [vp, u32, vp, u32, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.mt_events_enable.argtypes = [vp, u32]
         L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
         L.mt_version.restype = ctypes.c_char_p
@@ -102,7 +103,7 @@ def lib():
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
-                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_range_stacks', 'mt_set_concurrent_classes',
+                     'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_range_stacks', 'mt_regen_drain', 'mt_set_concurrent_classes',
                      'mt_events_enable', 'mt_events_drain'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -255,6 +256,37 @@ class MergeEngine:
         q = np.ascontiguousarray(queries, dtype=TILE_QUERY_DTYPE)
         out = np.zeros(len(q), dtype=TILE_RESULT_DTYPE)
         _check(lib().mt_find_tiles(self.h, _ptr(q), len(q), _ptr(out)), 'mt_find_tiles')
+        return out
+
+    def regen_drain(self, doc):
+        """The ops the document regenerated at its MT_SEQ_REGEN records (Client.regeneratePendingOp)
+        since the last drain: [[record index, [[type, pos1, pos2, text | None, props | None,
+        flags], ...]], ...] (flags: 128 marker, 1 rewrite; props keyed by key id as strings)."""
+        n, pn = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _check(lib().mt_regen_drain(self.h, doc, None, 0, None, 0, ctypes.byref(n), ctypes.byref(pn)), 'mt_regen_drain')
+        recs = np.zeros(n.value, dtype=OP_DTYPE)
+        pay = np.zeros(max(1, pn.value), dtype=np.uint8)
+        _check(lib().mt_regen_drain(self.h, doc, _ptr(recs), n.value, _ptr(pay), pn.value, ctypes.byref(n),
+                                    ctypes.byref(pn)), 'mt_regen_drain')
+        out = []
+        for r in recs:
+            t = int(r['type'])
+            if t == 3:  # header: the resetting record's index
+                out.append([int(r['seq']), []])
+                continue
+            fl = int(r['flags'])
+            npairs = (fl >> 3) & 15
+            off, ln = int(r['payload_off']), int(r['payload_len'])
+            body = bytes(pay[off:off + ln])
+            pairs = body[ln - 2 * npairs:]
+            if t == 0:
+                props = {str(pairs[2 * q]): int(pairs[2 * q + 1]) for q in range(npairs)} if fl & 2 else None
+                out[-1][1].append([0, int(r['pos1']), 0, body[:ln - 2 * npairs].decode('latin-1'), props, fl & 128])
+            elif t == 1:
+                out[-1][1].append([1, int(r['pos1']), int(r['pos2']), None, None, 0])
+            else:
+                props = {str(pairs[2 * q]): (int(pairs[2 * q + 1]) or None) for q in range(npairs)}
+                out[-1][1].append([2, int(r['pos1']), int(r['pos2']), None, props, fl & 1])
         return out
 
     def range_stacks(self, queries, cap=64):

@@ -71,9 +71,10 @@ enum mt_op_flags {
  * MT_DERR_CAPACITY) and records no delta events. */
 #define MT_SEQ_LOCAL (-1)
 /* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =
- * MT_SEQ_REGEN from the editing client holds a pending op to regenerate.  Restated and pinned by
- * the CPU oracle (tests/test_local.py); the device does not regenerate yet and halts the document
- * there with MT_DERR_BAD_OP. */
+ * MT_SEQ_REGEN from the editing client holds the pending op to regenerate (the oldest one): its
+ * segments, in document order, each at its findReconnectionPostition as of the edit's localSeq,
+ * become new ops (a removal only while the segment is still locally removed), each with a new
+ * pending group at the queue's tail.  The new ops are read with mt_regen_drain. */
 #define MT_SEQ_REGEN (-2)
 
 typedef struct mt_op_rec {
@@ -271,6 +272,16 @@ typedef struct mt_tile_result {
     int32_t ordinal;            /* its index among the document's segments, -1: none */
 } mt_tile_result;
 mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_tile_result* out);
+
+/* The ops document `doc` regenerated at its MT_SEQ_REGEN records since the last drain (at most 256
+ * records / 4 KiB of payload between drains, else MT_DERR_CAPACITY): per regenerated op one
+ * MT_OP_NOOP header record whose seq is the index of the resetting record within the document's
+ * records, then the new ops (mt_op_rec, payload offsets into `payload`: an insert carries its text
+ * or refType byte and its props, F_PROPS when its properties are defined; an annotate the reset
+ * op's props).  *n / *pn: records / payload bytes available; with recs != NULL the buffer is
+ * drained. */
+mt_status mt_regen_drain(mt_engine* eng, uint32_t doc, mt_op_rec* recs, uint32_t cap, uint8_t* payload, uint32_t pcap,
+                         uint32_t* n, uint32_t* pn);
 
 /* ---- range stacks -----------------------------------------------------
  * Client.getStackContext(startPos, [rangeLabel]) (client.ts:946-948 -> MergeTree.getStackContext,

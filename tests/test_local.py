@@ -118,13 +118,27 @@ def test_engine_editing_client_matches_reference(name, b):
 
 
 @pytest.mark.gpu
-def test_engine_halts_loudly_at_reconnect():
-    """The device does not regenerate pending ops yet: each document halts with MT_DERR_BAD_OP at its
-    first seq -2 record instead of diverging."""
+@pytest.mark.parametrize('b', [1, 16])
+def test_engine_reconnect_matches_reference(b):
+    """Reconnect on the device (MT_SEQ_REGEN records -> mt_regen_drain): the ops regenerated at every
+    seq -2 record and the states at every checkpoint equal the reference's."""
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import OpBatch
     batch = OpBatch.load(os.path.join(GOLDEN, RECONNECT + '.mtlog'))
-    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    rows = load_local()[RECONNECT]
+    eng = MergeEngine(batch.n_docs, ops_per_launch=b)
     eng.apply(batch)
-    for d in range(batch.n_docs):
-        assert eng.error(d) == (7, -2), (d, eng.error(d))
+    for r in rows:
+        d = r['doc']
+        assert eng.error(d) == (0, 0), (d, eng.error(d))
+        assert eng.regen_drain(d) == r['regen'], d
+        assert eng.state(d) == r['states'][-1][1], d
+    eng.close()
+    for q in range(max(len(r['states']) for r in rows) - 1):
+        sub = [r for r in rows if q < len(r['states']) - 1]  # (a checkpoint inside a GROUP ack is skipped)
+        cb = checkpoint_batch(batch, sub, q)
+        eng = MergeEngine(cb.n_docs, ops_per_launch=b)
+        eng.apply(cb)
+        for i, r in enumerate(sub):
+            assert eng.state(i) == r['states'][q][1], (r['doc'], q)
+        eng.close()

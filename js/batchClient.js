@@ -299,6 +299,53 @@ class BatchClient {
         if (props) seg.props = props;
         return this._local({ type: INSERT, pos1: pos, seg });
     }
+    /**
+     * Client.regeneratePendingOp (client.ts:855-893) on reconnect, for the oldest pending edit, whose
+     * op is `resetOp` (the segment group is implied: the head of the pending queue): the new op to
+     * resubmit -- one op per segment, a GROUP op when there are several (or none).
+     */
+    regeneratePendingOp(resetOp) {
+        const members = resetOp.type === GROUP ? resetOp.ops : [resetOp];
+        for (const m of members) {
+            const msg = { sequenceNumber: -2, referenceSequenceNumber: this.currentSeq, minimumSequenceNumber: 0 };
+            const r = this._record(msg, m, this._shortId(this.longClientId), false);
+            if (r.type === NOOP) throw new Error("BatchClient: nothing to regenerate");
+            this.queue.push(r);
+            this.engine.pending += 1;
+        }
+        this.engine.flush();
+        this._checkError();
+        const [recs, pay] = native.regenDrain(this.engine.handle, this.doc);
+        const ops = [];
+        for (let o = 0; o + REC <= recs.length && recs.length >= REC; o += REC) {
+            const type = recs.readUInt8(o + 14), flags = recs.readUInt8(o + 15);
+            if (type === NOOP) continue;  // one header per regenerated op
+            const pos1 = recs.readInt32LE(o + 16), pos2 = recs.readInt32LE(o + 20);
+            const off = recs.readUInt32LE(o + 24), len = recs.readUInt32LE(o + 28);
+            const np = (flags >> 3) & 15;
+            const props = {};
+            for (let q = 0; q < np; q++) {
+                const k = pay.readUInt8(off + len - 2 * np + 2 * q), v = pay.readUInt8(off + len - 2 * np + 2 * q + 1);
+                props[this.keys[k]] = v ? this.values[v] : null;
+            }
+            if (type === INSERT) {
+                const text = pay.toString("latin1", off, off + len - 2 * np);
+                let seg;
+                if (flags & F_MARKER) seg = { marker: { refType: text.charCodeAt(0) } };
+                else seg = (flags & F_PROPS) ? { text } : text;
+                if (flags & F_PROPS) seg.props = props;
+                ops.push({ type: INSERT, pos1, seg });
+            } else if (type === REMOVE) {
+                ops.push({ type: REMOVE, pos1, pos2 });
+            } else {
+                const op = { type: ANNOTATE, pos1, pos2, props };
+                if (flags & F_REWRITE) op.combiningOp = { name: "rewrite" };
+                ops.push(op);
+            }
+        }
+        return ops.length === 1 ? ops[0] : { type: GROUP, ops };
+    }
+
     /** Client.removeRangeLocal (client.ts:188-195). */
     removeRangeLocal(start, end) { return this._local({ type: REMOVE, pos1: start, pos2: end }); }
     /** Client.annotateRangeLocal (client.ts:163-179). */

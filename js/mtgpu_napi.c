@@ -394,6 +394,32 @@ static napi_value range_stacks(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* regenDrain(engine, doc) -> [Buffer of 32-byte mt_op_rec rows, Buffer of their payload] (mt_regen_drain) */
+static napi_value regen_drain(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out, rb, pb;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 2 ? get_box(env, argv[0]) : NULL;
+    uint32_t doc = 0;
+    if (!b || napi_get_value_uint32(env, argv[1], &doc) != napi_ok) {
+        napi_throw_type_error(env, NULL, "regenDrain(engine, doc)");
+        return NULL;
+    }
+    uint32_t n = 0, pn = 0;
+    enter(b);
+    mt_status st = mt_regen_drain(b->e, doc, NULL, 0, NULL, 0, &n, &pn);
+    void *recs = NULL, *pay = NULL;
+    if (!st && napi_create_buffer(env, n ? n * sizeof(mt_op_rec) : 1, &recs, &rb) == napi_ok &&
+        napi_create_buffer(env, pn ? pn : 1, &pay, &pb) == napi_ok)
+        st = mt_regen_drain(b->e, doc, (mt_op_rec*)recs, n, (uint8_t*)pay, pn, &n, &pn);
+    leave(b);
+    if (st) return throw_status(env, "mt_regen_drain", st);
+    NAPI_CALL(env, napi_create_array_with_length(env, 2, &out));
+    NAPI_CALL(env, napi_set_element(env, out, 0, rb));
+    NAPI_CALL(env, napi_set_element(env, out, 1, pb));
+    return out;
+}
+
 /* docsLoad(engine, docIdsU32, segRowPtrU32, segs (32-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
  * SnapshotLoader.loadHeader for a batch of documents (mt_docs_load) */
 static napi_value docs_load(napi_env env, napi_callback_info info) {
@@ -565,6 +591,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"docsLoad", NULL, docs_load, NULL, NULL, NULL, napi_default, NULL},
         {"findTiles", NULL, find_tiles, NULL, NULL, NULL, napi_default, NULL},
         {"rangeStacks", NULL, range_stacks, NULL, NULL, NULL, napi_default, NULL},
+        {"regenDrain", NULL, regen_drain, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},
         {"deliTicket", NULL, deli_ticket, NULL, NULL, NULL, napi_default, NULL},

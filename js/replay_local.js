@@ -7,6 +7,23 @@
 const { BatchEngine } = require("./batchClient.js");
 const { loadLog, messages } = require("./mtlog.js");
 
+// an op as [type, pos1, pos2, text | null, {key id: value | null} | null, flags] (replay_ref.js opTuple)
+function tuple(op) {
+    const props = (p) => {
+        if (!p) return null;
+        const o = {};
+        for (const k of Object.keys(p)) o[parseInt(k.slice(1), 10)] = p[k];
+        return o;
+    };
+    if (op.type === 0) {
+        const seg = op.seg;
+        if (seg.marker) return [0, op.pos1, 0, String.fromCharCode(seg.marker.refType), props(seg.props), 128];
+        return [0, op.pos1, 0, typeof seg === "string" ? seg : seg.text, typeof seg === "string" ? null : props(seg.props), 0];
+    }
+    if (op.type === 1) return [1, op.pos1, op.pos2, null, null, 0];
+    return [2, op.pos1, op.pos2, null, props(op.props), op.combiningOp && op.combiningOp.name === "rewrite" ? 1 : 0];
+}
+
 const log = loadLog(process.argv[2]);
 const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16 });
 const clients = [];
@@ -15,7 +32,13 @@ for (let d = 0; d < log.nDocs; d++) {
     const own = items.find((x) => x.local);
     const c = eng.createClient();
     c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+    const regen = [];
     for (const it of items) {
+        if (it.regen) {  // reconnect: the op to resubmit, as record tuples
+            const op = c.regeneratePendingOp(it.op);
+            regen.push([it.index, (op.type === 3 ? op.ops : [op]).map(tuple)]);
+            continue;
+        }
         if (!it.local) {
             c.applyMsg(it);
             continue;
@@ -33,11 +56,12 @@ for (let d = 0; d < log.nDocs; d++) {
         }
         if (!r) throw new Error("local edit rejected");
     }
+    c.regen = regen;
     clients.push(c);
 }
 const out = clients.map((c, d) => {
     let err = null, state = null;
     try { state = c.getState(); } catch (e) { err = String(e.message || e); }
-    return JSON.stringify({ doc: d, err, state });
+    return JSON.stringify(c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state });
 });
 process.stdout.write(out.join("\n") + "\n");

@@ -23,7 +23,7 @@ def test_addon_loads_and_exports():
         pytest.skip('node headers absent')
     out = subprocess.run([NODE, '-e', "const b=require('./js/batchClient.js');"
                           "for (const f of ['createEngine','submit','submitAsync','getText','getState','getLength',"
-                          "'docError','checksums','version','eventsEnable','eventsDrain','findTiles','rangeStacks','docsLoad']) if (typeof b.native[f] !== 'function') throw f;"
+                          "'docError','checksums','version','eventsEnable','eventsDrain','findTiles','rangeStacks','docsLoad','regenDrain']) if (typeof b.native[f] !== 'function') throw f;"
                           "console.log(b.native.version())"], cwd=REPO, capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
     assert 'gfx950' in out.stdout
@@ -241,11 +241,12 @@ def test_batchclient_stack_context_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['local_rounds', 'local_lag', 'local_big', 'local_markers'])
+@pytest.mark.parametrize('name', ['local_rounds', 'local_lag', 'local_big', 'local_markers', 'local_reconnect'])
 def test_batchclient_editing_client_matches_reference(name):
     """BatchClient as an editing client (insertTextLocal / removeRangeLocal / annotateRangeLocal,
-    its own sequenced messages as acks through applyMsg) ends every local_* document in the
-    reference client's final state (tests/golden/local.expected.jsonl)."""
+    its own sequenced messages as acks through applyMsg, regeneratePendingOp on reconnect) ends
+    every local_* document in the reference client's final state and regenerates the reference's
+    ops (tests/golden/local.expected.jsonl)."""
     from test_local import load_local
     assert _addon()
     out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog')],
@@ -256,3 +257,4 @@ def test_batchclient_editing_client_matches_reference(name):
         g = got[r['doc']]
         assert g['err'] is None, (name, r['doc'], g['err'])
         assert _js_state_to_log(g['state']) == r['states'][-1][1], (name, r['doc'])
+        assert g.get('regen', []) == r.get('regen', []), (name, r['doc'])  # regeneratePendingOp

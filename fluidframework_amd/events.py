@@ -20,7 +20,7 @@ assert EVENT_DTYPE.itemsize == 32
 
 EV_INSERT, EV_REMOVE, EV_ANNOTATE = 0, 1, 2
 EV_APPEND, EV_SPLIT, EV_UNLINK = -1, -2, -3
-EVF_FIRST, EVF_EMPTY = 1, 2
+EVF_FIRST, EVF_EMPTY, EVF_NOPD = 1, 2, 4
 OP_NAMES = {EV_INSERT: 'INSERT', EV_REMOVE: 'REMOVE', EV_ANNOTATE: 'ANNOTATE', EV_APPEND: 'APPEND',
             EV_SPLIT: 'SPLIT', EV_UNLINK: 'UNLINK'}
 
@@ -47,6 +47,6 @@ def callbacks(rows):
             raise ValueError('event stream does not start with a callback')
         if flags & EVF_EMPTY:
             continue
-        pd = property_deltas(int(r['pmask']), int(r['pvals'])) if op == EV_ANNOTATE else None
+        pd = property_deltas(int(r['pmask']), int(r['pvals'])) if op == EV_ANNOTATE and not flags & EVF_NOPD else None
         out[-1][2].append([int(r['leaf']), int(r['pos']), int(r['len']), pd])
     return out

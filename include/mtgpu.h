@@ -327,6 +327,8 @@ enum mt_event_op {
     MT_EV_APPEND = -1, MT_EV_SPLIT = -2, MT_EV_UNLINK = -3    /* MergeTreeMaintenanceType            */
 };
 #define MT_EVF_FIRST 1u   /* first record of a callback */
+#define MT_EVF_NOPD 4u  /* ANNOTATE delta segment whose propertyDeltas is undefined (a remote annotate
+                         dropped while the editing client's rewrite is pending) */
 #define MT_EVF_EMPTY 2u   /* the callback's deltaSegments is empty (no segment in this record) */
 typedef struct mt_event {   /* 32 bytes */
     int32_t seq;            /* sequenceNumber of the message being applied                        */

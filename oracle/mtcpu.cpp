@@ -618,6 +618,19 @@ struct Doc {
         return true;
     }
 
+    // the REMOVE / ANNOTATE callback (mergeTree.ts:2705-2712, 2592-2600): its delta segments in order
+    void emitRange(int opk, const std::vector<Seg*>& delta, const std::vector<std::pair<uint8_t, uint64_t>>& pdel,
+                   const std::vector<bool>& nopd) {
+        if (delta.empty()) ev(opk, MT_EVF_FIRST | MT_EVF_EMPTY, -1, -1, 0);
+        for (size_t i = 0; i < delta.size(); i++) {
+            const auto w = where(delta[i]);
+            unsigned f = i == 0 ? MT_EVF_FIRST : 0;
+            if (i < nopd.size() && nopd[i]) f |= MT_EVF_NOPD;
+            ev(opk, f, w.first, w.second, delta[i]->len(), pdel.empty() ? 0 : pdel[i].first,
+               pdel.empty() ? 0 : pdel[i].second);
+        }
+    }
+
     // addToPendingList (mergeTree.ts:1922-1929): one group per local edit
     void join(Group*& g, Seg* s) {
         if (!g) {
@@ -638,6 +651,7 @@ struct Doc {
         if (op.client != own || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, kUnassigned);
         if (op.type > MT_OP_ANNOTATE) return fail(MT_DERR_BAD_OP, kUnassigned);
         const int32_t R = currentSeq, C = own, S = kUnassigned;
+        evSeq = S;
         const int np = MT_OP_NPAIRS(op.flags);
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
         const uint8_t* pay = payload + op.payload_off;
@@ -665,12 +679,19 @@ struct Doc {
             updateRoot(sp);
             join(g, x);  // saveIfLocal
             g->localSeq = L;
+            if (rec) {  // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988)
+                const auto w = where(x);
+                ev(MT_EV_INSERT, MT_EVF_FIRST, w.first, w.second, x->len());
+            }
             return;
         }
         ensureIntervalBoundary(op.pos1, R, C);
         ensureIntervalBoundary(op.pos2, R, C);
+        std::vector<Seg*> delta;
+        std::vector<std::pair<uint8_t, uint64_t>> pdel;
         if (op.type == MT_OP_REMOVE) {
             nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* x) {
+                if (!x->removed) delta.push_back(x);  // removedSegments
                 if (x->removed) {
                     if (x->rseq == kUnassigned) {
                         x->rclient = C;
@@ -693,10 +714,13 @@ struct Doc {
                 uint8_t pm = 0;
                 uint64_t pv = 0;
                 addProps(x, pairs, np, rewrite, true, pm, pv);
+                delta.push_back(x);
+                pdel.emplace_back(pm, pv);
                 join(g, x);
             });
         }
         if (g) g->localSeq = L;
+        if (rec) emitRange(op.type == MT_OP_REMOVE ? MT_EV_REMOVE : MT_EV_ANNOTATE, delta, pdel, {});
     }
 
     // Client.regeneratePendingOp -> resetPendingDeltaToOps (client.ts:708-766, 855-893) for the
@@ -883,6 +907,7 @@ struct Doc {
                 ensureIntervalBoundary(op.pos2, R, C);
                 std::vector<Seg*> delta;  // deltaSegments of the op's callback
                 std::vector<std::pair<uint8_t, uint64_t>> pdel;
+                std::vector<bool> nopd;
                 if (op.type == MT_OP_REMOVE) {
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
                         if (s->removed) {
@@ -906,21 +931,15 @@ struct Doc {
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
                         uint8_t pm = 0;
                         uint64_t pv = 0;
-                        addProps(s, pairs, np, rewrite, false, pm, pv);
+                        // (dropped while a local rewrite is pending: propertyDeltas undefined)
+                        const bool kept = addProps(s, pairs, np, rewrite, false, pm, pv);
                         delta.push_back(s);
-                        pdel.emplace_back(pm, pv);
+                        pdel.emplace_back(kept ? pm : (uint8_t)0, kept ? pv : 0);
+                        nopd.push_back(!kept);
                         addToLRUSet(s, S);
                     });
                 }
-                if (rec) {  // mergeTree.ts:2705-2712 (REMOVE), 2592-2600 (ANNOTATE)
-                    const int opk = op.type == MT_OP_REMOVE ? MT_EV_REMOVE : MT_EV_ANNOTATE;
-                    if (delta.empty()) ev(opk, MT_EVF_FIRST | MT_EVF_EMPTY, -1, -1, 0);
-                    for (size_t i = 0; i < delta.size(); i++) {
-                        const auto w = where(delta[i]);
-                        ev(opk, i == 0 ? MT_EVF_FIRST : 0, w.first, w.second, delta[i]->len(),
-                           pdel.empty() ? 0 : pdel[i].first, pdel.empty() ? 0 : pdel[i].second);
-                    }
-                }
+                if (rec) emitRange(op.type == MT_OP_REMOVE ? MT_EV_REMOVE : MT_EV_ANNOTATE, delta, pdel, nopd);
                 zamboni();
                 break;
             }

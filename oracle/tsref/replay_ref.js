@@ -366,6 +366,43 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "localevents") {
+        // the delta / maintenance callbacks an editing client fires (local edits: seq -1; its
+        // acks and remote ops: the message's seq), canonical form as in "events"
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const items = [...messages(log, d)];
+            const own = items.find((x) => x.local);
+            const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+            const c = new Client(specToSegment, logger);
+            c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+            const seqRef = { seq: 0 };
+            const events = attachEvents(c, seqRef);
+            let err = null;
+            try {
+                for (const it of items) {
+                    if (it.regen) {
+                        seqRef.seq = -2;
+                        c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+                    } else if (it.local) {
+                        seqRef.seq = -1;
+                        const op = it.op;
+                        if (op.type === 0) c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                        else if (op.type === 1) c.removeRangeLocal(op.pos1, op.pos2);
+                        else c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+                    } else {
+                        seqRef.seq = it.sequenceNumber;
+                        c.applyMsg(it);
+                    }
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            out.push(JSON.stringify({ doc: d, err, events }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "stacks") {
         // getStackContext (client.ts:946-948, mergeTree.ts:1750-1760): the NestBegin / NestEnd stack of
         // each label L0..L3 at a spread of positions, range labels on key <rangeKey>; each stack as

@@ -65,6 +65,24 @@ def main():
         print(name, len(docs), 'docs', sum(len(d) for d in docs), 'records')
     with open(os.path.join(HERE, 'local.expected.jsonl'), 'w') as f:
         f.write('\n'.join(out) + '\n')
+    # the callbacks the reference's editing client fired (local_events.jsonl): in full for the first
+    # documents of each log, as count + SHA-256 of the canonical list for the others
+    import hashlib
+    ev_out = []
+    for name, *_ in LOGS:
+        res = subprocess.run(['node', replay, 'localevents', os.path.join(HERE, name + '.mtlog')], check=True,
+                             capture_output=True, text=True)
+        for line in res.stdout.strip().split('\n'):
+            r = json.loads(line)
+            assert r['err'] is None, (name, r['doc'], r['err'])
+            ev = r['events']
+            rec = dict(log=name, doc=r['doc'], n=len(ev),
+                       sha256=hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest())
+            if r['doc'] < 2:
+                rec['events'] = ev
+            ev_out.append(json.dumps(rec, separators=(',', ':')))
+    with open(os.path.join(HERE, 'local_events.jsonl'), 'w') as f:
+        f.write('\n'.join(ev_out) + '\n')
 
 
 if __name__ == '__main__':

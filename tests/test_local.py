@@ -64,6 +64,27 @@ def test_oracle_editing_client_matches_reference(oracle_lib, name):
             assert o.state(0) == want, (name, r['doc'], k)
 
 
+@pytest.mark.parametrize('name', LOGS + [RECONNECT])
+def test_oracle_editing_client_events_match_reference(oracle_lib, name):
+    """The delta / maintenance callbacks of an editing client (mergeTreeDeltaCallback.ts): its local
+    edits fire INSERT / REMOVE / ANNOTATE with seq -1, remote annotates over pending keys record only
+    the keys they change (none, propertyDeltas undefined, while a local rewrite is pending); pinned
+    by the reference's own callbacks (tests/golden/local_events.jsonl)."""
+    import hashlib
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    o = oracle_lib.Oracle(batch.n_docs).record_events().apply(batch)
+    with open(os.path.join(GOLDEN, 'local_events.jsonl')) as f:
+        gold = [json.loads(x) for x in f if json.loads(x)['log'] == name]
+    assert sum(g['n'] for g in gold) > 1000
+    for g in gold:
+        ev = o.events(g['doc'])
+        if 'events' in g:
+            assert ev == g['events'], (name, g['doc'])
+        assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+            g['sha256'], (name, g['doc'])
+
+
 def test_oracle_reconnect_matches_reference(oracle_lib):
     """Client.regeneratePendingOp (client.ts:708-766, 855-893) on reconnect: the ops the oracle
     regenerates at every seq -2 record equal the reference's, and every checkpoint state (pending

@@ -144,12 +144,14 @@ struct Wave {
             bool hit = false;
             int ll = 0;
             uint32_t ln = 0;
-            uint8_t pm = 0;
+            uint8_t pm = 0, xf = 0;
             uint64_t pv = 0;
             if (i < n) {
                 const int sl = s.order[i];
                 const uint8_t f = s.flags[sl];
                 ln = s.len[sl];
+                uint64_t pk = 0;  // (LOC, a remote annotate: keys with pending local changes are skipped)
+                if constexpr (LOC) pk = (S != -1 && (f & MT_SF_PDEF)) ? s.pk[sl] : 0ull;
                 ll = (f & MT_SF_REMOVED) ? 0 : (int)ln;
                 const int ce = s.cum[i], cs = cstart(i);
                 hit = ce > cs && cs < end && ce > start;
@@ -161,16 +163,25 @@ struct Wave {
                     // records the value before it is set (null when absent, and null for a rewrite's
                     // null-valued key, deleted a moment earlier)
                     const uint64_t old = (f & MT_SF_PDEF) ? s.props[sl] : 0;
-                    if (rewrite) {
-                        for (int k = 0; k < 8; k++)
-                            if ((old >> (8 * k)) & 0xFF) pm |= (uint8_t)(1u << k);
-                        pv = old;
-                    }
-                    for (int q = 0; q < np; q++) {
-                        const int k = pairs[2 * q];
-                        const uint64_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : ((old >> (8 * k)) & 0xFF);
-                        pm |= (uint8_t)(1u << k);
-                        pv = (pv & ~(0xFFull << (8 * k))) | (prev << (8 * k));
+                    if (MT_PK_RW(pk) > 0) {
+                        xf = MT_EVF_NOPD;  // dropped while a local rewrite is pending: propertyDeltas undefined
+                    } else {
+                        if (rewrite) {
+                            for (int k = 0; k < 8; k++)
+                                if (((old >> (8 * k)) & 0xFF) && MT_PK_KEY(pk, k) == 0) {
+                                    bool keep = false;  // a key the rewrite sets again keeps its value here
+                                    for (int q = 0; q < np; q++) keep = keep || (pairs[2 * q] == k && pairs[2 * q + 1] != 0);
+                                    if (!keep) pm |= (uint8_t)(1u << k);
+                                }
+                            pv = old;
+                        }
+                        for (int q = 0; q < np; q++) {
+                            const int k = pairs[2 * q];
+                            if (MT_PK_KEY(pk, k) > 0) continue;
+                            const uint64_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : ((old >> (8 * k)) & 0xFF);
+                            pm |= (uint8_t)(1u << k);
+                            pv = (pv & ~(0xFFull << (8 * k))) | (prev << (8 * k));
+                        }
                     }
                 }
             }
@@ -181,7 +192,7 @@ struct Wave {
                 mt_event e{};
                 e.seq = s.evseq;
                 e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
-                e.flags = (uint8_t)(idx == 0 ? MT_EVF_FIRST : 0);
+                e.flags = (uint8_t)((idx == 0 ? MT_EVF_FIRST : 0) | xf);
                 e.pmask = pm;
                 e.leaf = i;
                 e.pos = lpos + incl - ll;
@@ -981,8 +992,8 @@ struct Wave {
             }
         }
         sync();
-        if (local) return;  // pending segments join no LRU set and a local edit runs no zamboni
         if (is_remove) emit_range(true, S, C, start, end, pairs, np, rewrite);
+        if (local) return;  // pending segments join no LRU set and a local edit runs no zamboni
         // addToLRUSet for touched segments in document order: one heap push per leaf block
         // whose needsScour is not already true, for its first touched segment
         block_starts();
@@ -1285,6 +1296,7 @@ struct Wave {
             if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, -1);
         mt_op_rec o = op;
         o.ref_seq = s.cur_seq;
+        s.evseq = -1;  // (a local edit's callbacks: seq -1)
         const int L = scan(o.ref_seq, C);
         if (op.type == MT_OP_INSERT && tlen <= 0) return;  // insertSegmentLocal: nothing for an empty segment
         sync();
@@ -1297,16 +1309,19 @@ struct Wave {
             if (o.pos1 < 0 || o.pos2 > L || o.pos1 >= o.pos2) return fail(MT_DERR_BAD_OP, -1);  // getValidOpRange
             op_range(o, pairs, np);
         }
+        if (ev && s.evn > (int)evcap) fail(MT_DERR_EVENTS, -1);
     }
     MT_DEV void apply_ack(const mt_op_rec& op, const uint8_t* payload) {
         const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
+        s.evseq = S;
         if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                                  // client.ts:824
         if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);           // :826
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
         op_ack(op, payload + op.payload_off + (op.payload_len - 2 * np), np);
         if (s.err) return;
         if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
+        if (ev && s.evn > (int)evcap) fail(MT_DERR_EVENTS, S);
     }
 
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
@@ -1674,9 +1689,8 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     Lds<CAP, LOC>& lds = *reinterpret_cast<Lds<CAP, LOC>*>(smem);
-    // (an editing client's document records no delta events)
     Wave<CAP, false, LOC> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap,
-                             GEN || LOC || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap, g.evcap);
+                             GEN || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap, g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;

@@ -163,3 +163,28 @@ def test_engine_reconnect_matches_reference(b):
         for i, r in enumerate(sub):
             assert eng.state(i) == r['states'][q][1], (r['doc'], q)
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', LOGS + [RECONNECT])
+def test_engine_editing_client_events_match_reference(name):
+    """The device's editing form records the editing client's callbacks (mt_events_enable): equal to
+    the reference's (tests/golden/local_events.jsonl)."""
+    import hashlib
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16).enable_events(1 << 15)
+    eng.apply(batch)
+    got = eng.drain_events()
+    with open(os.path.join(GOLDEN, 'local_events.jsonl')) as f:
+        gold = [json.loads(x) for x in f if json.loads(x)['log'] == name]
+    for g in gold:
+        d = g['doc']
+        assert eng.error(d) == (0, 0), (name, d, eng.error(d))
+        ev = got[d]
+        if 'events' in g:
+            assert ev == g['events'], (name, d)
+        assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+            g['sha256'], (name, d)
+    eng.close()

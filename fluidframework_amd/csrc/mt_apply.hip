@@ -156,7 +156,7 @@ struct Wave {
                 const int ce = s.cum[i], cs = cstart(i);
                 hit = ce > cs && cs < end && ce > start;
                 if (is_remove) {
-                    hit = hit && (f & MT_SF_REMOVED) && s.rseq[sl] == S && s.rclient[sl] == C;
+                    hit = hit && (f & MT_SF_REMOVED) && !(f & MT_SF_OVW) && s.rseq[sl] == S && s.rclient[sl] == C;
                 } else if (hit) {
                     // SegmentPropertiesManager.addProperties' deltas (segmentPropertiesManager.ts:60-108):
                     // a rewrite records each key it deletes with its old value; every key of the op
@@ -971,6 +971,7 @@ struct Wave {
                         if (pend_rm) {  // a pending local removal: this one replaces it (mergeTree.ts:2621-2627)
                             s.rseq[sl] = S;
                             s.rclient[sl] = (uint8_t)C;
+                            s.flags[sl] |= MT_SF_OVW;  // (not among this op's removedSegments)
                             if constexpr (LOC) s.lsq[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
                         } else if (s.flags[sl] & MT_SF_REMOVED) {
                             s.ovl[sl] |= cbit;  // addOverlappingClient (first remover wins)
@@ -993,6 +994,12 @@ struct Wave {
         }
         sync();
         if (is_remove) emit_range(true, S, C, start, end, pairs, np, rewrite);
+        if constexpr (LOC) {
+            if (is_remove) {
+                for (int i = lane; i < n; i += 64) s.flags[s.order[i]] &= (uint8_t)~MT_SF_OVW;
+                sync();
+            }
+        }
         if (local) return;  // pending segments join no LRU set and a local edit runs no zamboni
         // addToLRUSet for touched segments in document order: one heap push per leaf block
         // whose needsScour is not already true, for its first touched segment

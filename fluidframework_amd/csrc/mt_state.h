@@ -20,6 +20,7 @@
 #define MT_SF_NL 4u          // text ends with "\n" (TextSegment.canAppend, textSegment.ts:63-68)
 #define MT_SF_HASNL 8u       // text contains a "\n" somewhere (a split of a segment without one needs no text read)
 #define MT_SF_MARKER 16u     // a Marker (length 1; its one arena byte is its ReferenceType)
+#define MT_SF_OVW 128u       // (within one op only) a pending local removal this remote removal took over
 
 // needsScour tri-state (mergeTree.ts:63, 1279, 1438, 1445)
 #define MT_SC_UNDEF 0

@@ -68,7 +68,7 @@ enum mt_op_flags {
  * Remote ops see the pending segments as the reference does (nodeLength, breakTie,
  * blockInsert's continuePredicate, pending property keys).  Such a document runs on the LDS
  * engine's editing form (capacity MT_LOC_CAP = 1024 segments, at most 64 pending edits; beyond:
- * MT_DERR_CAPACITY) and records no delta events. */
+ * MT_DERR_CAPACITY); its delta events include the local edits' callbacks (seq -1). */
 #define MT_SEQ_LOCAL (-1)
 /* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =
  * MT_SEQ_REGEN from the editing client holds the pending op to regenerate (the oldest one): its

@@ -154,7 +154,7 @@ class BatchClient {
             const segment = { ordinal: rows.readInt32LE(o + 8), cachedLength: rows.readUInt32LE(o + 16) };
             if (op >= 0) segment.position = rows.readInt32LE(o + 12);
             const delta = { segment };
-            if (op === ANNOTATE) {
+            if (op === ANNOTATE && !(flags & 4)) {  // (MT_EVF_NOPD: propertyDeltas undefined)
                 const mask = rows.readUInt8(o + 6), vals = rows.readBigUInt64LE(o + 24);
                 delta.propertyDeltas = {};
                 for (let k = 0; k < MAX_KEYS; k++) {
@@ -281,11 +281,11 @@ class BatchClient {
     // sequenced messages, passed to applyMsg, are their acks (include/mtgpu.h)
     _local(op) {
         if (this.longClientId === undefined) throw new Error("BatchClient: startOrUpdateCollaboration first");
-        if (this.engine.recording) throw new Error("BatchClient: delta callbacks are not recorded for an editing client");
         const msg = { sequenceNumber: -1, referenceSequenceNumber: this.currentSeq, minimumSequenceNumber: 0 };
         const r = this._record(msg, op, this._shortId(this.longClientId), false);
         if (r.type === NOOP) return undefined;  // insertSegmentLocal: nothing for an empty segment
         this.queue.push(r);
+        if (this.engine.recording) this.expect.push({ op });  // a local edit's callback: no sequencedMessage
         this.engine.pending += 1;
         return op;
     }
@@ -359,9 +359,7 @@ class BatchClient {
      * this client's own long id acks its oldest pending local edit (client.ts:804-806). */
     applyMsg(msg) {
         const client = this._shortId(msg.clientId);
-        if (msg.type === "op" && msg.clientId === this.longClientId && this.engine.recording) {
-            throw new Error("BatchClient: delta callbacks are not recorded for an editing client");
-        }
+        const ack = msg.type === "op" && msg.clientId === this.longClientId;  // fires no delta callback
         const op = msg.type === "op" ? msg.contents : undefined;
         const members = op && op.type === GROUP ? op.ops : [op];
         members.forEach((m, i) => {
@@ -369,7 +367,7 @@ class BatchClient {
             this.queue.push(r);
             // every applied op fires one delta callback; an empty-string insert is dropped before
             // the tree (client.ts:403-407), a non-op message has none
-            if (this.engine.recording && r.type !== NOOP) {
+            if (this.engine.recording && r.type !== NOOP && !ack) {
                 this.expect.push({ op: m, groupOp: op.type === GROUP ? op : undefined, sequencedMessage: msg });
             }
         });

@@ -25,7 +25,13 @@ function tuple(op) {
 }
 
 const log = loadLog(process.argv[2]);
+const withEvents = process.argv[3] === "events";
 const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16 });
+const sortKeys = (pd) => {
+    const o = {};
+    for (const k of Object.keys(pd).sort((a, b) => parseInt(a.slice(1), 10) - parseInt(b.slice(1), 10))) o[k] = pd[k];
+    return o;
+};
 const clients = [];
 for (let d = 0; d < log.nDocs; d++) {
     const items = [...messages(log, d)];
@@ -33,6 +39,16 @@ for (let d = 0; d < log.nDocs; d++) {
     const c = eng.createClient();
     c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
     const regen = [];
+    c.events = [];
+    if (withEvents) {  // the canonical event form of fluidframework_amd/events.py; a local edit's seq is -1
+        const seg = (x, pd) => [x.segment.ordinal, x.segment.position === undefined ? -1 : x.segment.position,
+            x.segment.cachedLength, pd];
+        c.mergeTreeDeltaCallback = (opArgs, args) => c.events.push([
+            opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, args.operation,
+            args.deltaSegments.map((x) => seg(x, args.operation === 2 && x.propertyDeltas ? sortKeys(x.propertyDeltas) : null))]);
+        c.mergeTreeMaintenanceCallback = (args) => c.events.push([args.sequenceNumber, args.operation,
+            args.deltaSegments.map((x) => seg(x, null))]);
+    }
     for (const it of items) {
         if (it.regen) {  // reconnect: the op to resubmit, as record tuples
             const op = c.regeneratePendingOp(it.op);
@@ -62,6 +78,8 @@ for (let d = 0; d < log.nDocs; d++) {
 const out = clients.map((c, d) => {
     let err = null, state = null;
     try { state = c.getState(); } catch (e) { err = String(e.message || e); }
-    return JSON.stringify(c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state });
+    const line = c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state };
+    if (withEvents) line.events = c.events;
+    return JSON.stringify(line);
 });
 process.stdout.write(out.join("\n") + "\n");

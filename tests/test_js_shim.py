@@ -258,3 +258,25 @@ def test_batchclient_editing_client_matches_reference(name):
         assert g['err'] is None, (name, r['doc'], g['err'])
         assert _js_state_to_log(g['state']) == r['states'][-1][1], (name, r['doc'])
         assert g.get('regen', []) == r.get('regen', []), (name, r['doc'])  # regeneratePendingOp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['local_lag', 'local_reconnect'])
+def test_batchclient_editing_client_callbacks_match_reference(name):
+    """mergeTreeDeltaCallback / mergeTreeMaintenanceCallback on an editing BatchClient: its local
+    edits' callbacks (no sequencedMessage), remote ops' and zamboni's, in order -- the reference's
+    (tests/golden/local_events.jsonl)."""
+    import hashlib
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          'events'], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    with open(os.path.join(GOLDEN, 'local_events.jsonl')) as f:
+        gold = [json.loads(x) for x in f if json.loads(x)['log'] == name]
+    for g in gold:
+        ev = got[g['doc']]['events']
+        if 'events' in g:
+            assert ev == g['events'], (name, g['doc'])
+        assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+            g['sha256'], (name, g['doc'])

@@ -9,8 +9,9 @@
 // insertTextRemote, removeRangeRemote, enqueueMsg, applyMessages).  Many BatchClients share one
 // BatchEngine (one MI355X); any read flushes every client's queued ops as ONE batched submit.
 // An editing client's local edits (insertTextLocal / insertMarkerLocal / removeRangeLocal /
-// annotateRangeLocal) apply on the device in its local view and its own sequenced messages ack
-// them; register ops and combining ops other than "rewrite" throw.
+// annotateRangeLocal) apply on the device in its local view, its own sequenced messages ack them,
+// and regeneratePendingOp serves a reconnect; register ops and combining ops other than "rewrite"
+// throw.
 // Delta / maintenance callbacks (mergeTreeDeltaCallback.ts:15-73): setting a client's
 // mergeTreeDeltaCallback or mergeTreeMaintenanceCallback makes the engine record them
 // (mt_events_enable); they are delivered, in firing order, after the batch that fired them.

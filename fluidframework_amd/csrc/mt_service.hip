@@ -573,7 +573,7 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
             pr = g.props[so + i];
             const bool rm = fl & MT_SF_REMOVED;
             const int32_t s = g.seq[so + i];
-            if (rm && g.rseq[so + i] <= msn) cls = 0;
+            if (s == -1 || (rm && g.rseq[so + i] <= msn)) cls = 0;  // pending insert / removal (snapshotV1.ts:184)
             else if (s <= msn && !rm) cls = 1;
             else cls = 2;
         }

@@ -40,8 +40,10 @@ def extract(state, name=client_name):
         lens.append(1 if isinstance(p[0], dict) else len(p[0]))
 
     for text, seq, c, rseq, rc, _ov, props in state['segs']:
-        removed = rseq != -1
-        if removed and rseq <= msn:                  # removed at or below the MSN: elided
+        removed = rseq != -1 or rc != -1             # (a pending local removal: rseq -1 by the editing client)
+        if seq == -1:                                # a pending local insert: elided (snapshotV1.ts:184)
+            continue
+        if removed and rseq <= msn:                  # removed at or below the MSN (or pending): elided
             continue
         if seq <= msn and not removed:               # below the MSN: coalesce
             mk = isinstance(text, dict) or (prev is not None and isinstance(prev[0], dict))

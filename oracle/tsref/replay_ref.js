@@ -158,10 +158,30 @@ function attachEvents(c, seqRef) {
 }
 
 function replayDoc(log, d) {
-    const c = newObserver();
+    const items = [...messages(log, d)];
+    const own = items.find((x) => x.local);
+    let c;
+    if (own) {  // an editing client's log (seq -1 local edits, seq -2 reconnects; "local" mode)
+        const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+        c = new Client(specToSegment, logger);
+        c.startOrUpdateCollaboration("c" + own.client);
+    } else {
+        c = newObserver();
+    }
     let err = null;
     try {
-        for (const m of messages(log, d)) c.applyMsg(m);
+        for (const it of items) {
+            if (it.regen) {
+                c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+            } else if (it.local) {
+                const op = it.op;
+                if (op.type === 0) c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                else if (op.type === 1) c.removeRangeLocal(op.pos1, op.pos2);
+                else c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+            } else {
+                c.applyMsg(it);
+            }
+        }
     } catch (e) {
         err = String(e.message || e);
     }

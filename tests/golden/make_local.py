@@ -83,6 +83,23 @@ def main():
             ev_out.append(json.dumps(rec, separators=(',', ':')))
     with open(os.path.join(HERE, 'local_events.jsonl'), 'w') as f:
         f.write('\n'.join(ev_out) + '\n')
+    # SnapshotV1 of editing clients with pending edits (snapshotV1.ts:176-241 elides pending
+    # inserts and removals): local_lag cut at its second checkpoint, snapshots by the reference
+    from fluidframework_amd.oplog import OpBatch
+    import numpy as np
+    src = OpBatch.load(os.path.join(HERE, 'local_lag.mtlog'))
+    rows = [json.loads(x) for x in out if json.loads(x)['log'] == 'local_lag']
+    idx, rp = [], [0]
+    for r in rows:
+        a, k = int(src.row_ptr[r['doc']]), r['states'][1][0]
+        idx.append(np.arange(a, a + k))
+        rp.append(rp[-1] + k)
+    mid = OpBatch(src.ops[np.concatenate(idx)].copy(), src.payload, np.array(rp, dtype=np.uint32))
+    mid.save(os.path.join(HERE, 'local_mid.mtlog'))
+    res = subprocess.run(['node', replay, 'snapshot', os.path.join(HERE, 'local_mid.mtlog')], check=True,
+                         capture_output=True, text=True)
+    with open(os.path.join(HERE, 'local_mid.snapshot.jsonl'), 'w') as f:
+        f.write(res.stdout)
 
 
 if __name__ == '__main__':

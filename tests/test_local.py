@@ -188,3 +188,34 @@ def test_engine_editing_client_events_match_reference(name):
         assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
             g['sha256'], (name, d)
     eng.close()
+
+
+def test_oracle_snapshot_of_editing_client_matches_reference(oracle_lib):
+    """SnapshotV1 of editing clients with pending edits (snapshotV1.ts:176-241: pending inserts and
+    pending removals are elided): the restatement on the oracle's state == the reference's tree
+    (tests/golden/local_mid.snapshot.jsonl: local_lag cut where edits are pending)."""
+    from fluidframework_amd.oplog import OpBatch
+    from oracle import snapshot
+    from test_snapshot import load_snapshots
+    batch = OpBatch.load(os.path.join(GOLDEN, 'local_mid.mtlog'))
+    o = oracle_lib.Oracle(batch.n_docs).apply(batch)
+    want = load_snapshots('local_mid')
+    pending = 0
+    for w in want:
+        st = o.state(w['doc'])
+        pending += sum(1 for s in st['segs'] if s[1] == -1 or (s[3] == -1 and s[4] != -1))
+        assert snapshot.emit(st, snapshot.DEFAULT_CHUNK) == w['snapshot'], w['doc']
+    assert pending > 10
+
+
+@pytest.mark.gpu
+def test_engine_snapshot_of_editing_client_matches_reference():
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    from test_snapshot import load_snapshots
+    batch = OpBatch.load(os.path.join(GOLDEN, 'local_mid.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.apply(batch)
+    names = ['observer'] + ['c%d' % i for i in range(1, 64)]
+    for w in load_snapshots('local_mid'):
+        assert eng.snapshot(w['doc'], 0, names) == w['snapshot'], w['doc']

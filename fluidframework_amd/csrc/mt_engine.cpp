@@ -1036,7 +1036,8 @@ std::string snapshot_json(const HostDoc& h, const std::vector<uint32_t>& sp, uin
         const bool meta = sp[3 * k + 1] & 1u;
         std::string text;
         for (int i = pos; i < pos + cnt; i++) {
-            if ((h.flags[i] & MT_SF_REMOVED) && h.rseq[i] <= h.sc.min_seq) continue;  // elided inside the run
+            // elided inside the run: removed at or below the MSN, or a pending local insert / removal
+            if (h.seq[i] == -1 || ((h.flags[i] & MT_SF_REMOVED) && h.rseq[i] <= h.sc.min_seq)) continue;
             text.append((const char*)h.text.data() + h.toff[i], h.len[i]);
         }
         lens[k] = sp[3 * k + 2];

@@ -79,7 +79,8 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--seed', type=int, default=20261015)
     p.add_argument('--comm', choices=['auto', 'rccl', 'gloo'], default='auto',
-                   help='rank exchange: RCCL over xGMI (default), or gloo (ranks sharing one GPU, tests)')
+                   help='rank exchange: RCCL over xGMI (default for N > 1; "rccl" also at N = 1, a one-rank '
+                        'communicator), or gloo (ranks sharing one GPU, tests)')
     p.add_argument('--devices', default='', help='device of each local rank, e.g. "0,0" (default: rank i -> GPU i)')
     p.add_argument('--no-h2d', action='store_true', help='skip the extra step whose op log is uploaded from '
                                                          'host memory inside the timed region (value_with_h2d)')
@@ -120,7 +121,7 @@ def main():
     from fluidframework_amd.oplog import CONFIGS, DELI_CONFIGS
     from fluidframework_amd import shard
 
-    if world == 1:
+    if world == 1 and args.comm != 'rccl':
         comm = shard.LocalComm()
     elif args.comm == 'gloo':
         import torch.distributed as tdist
@@ -228,7 +229,7 @@ def main():
 
     value_h2d = None
     if not args.no_h2d and deli is None:
-        value_h2d = h2d_step(eng, dev, n_ops, barrier, comm)
+        value_h2d = h2d_step(eng, dev, n_total * ops_per_doc, barrier, comm)
 
     # final per-document checksum gather to rank 0 (RCCL ncclGather from HBM; the only collective)
     parts = comm.gather_checksums(eng, max_docs)
@@ -309,10 +310,11 @@ def main():
     comm.close()
 
 
-def h2d_step(eng, dev, n_ops, barrier, comm):
+def h2d_step(eng, dev, job_ops, barrier, comm):
     """One step whose op log starts in page-locked host memory ("from the first
     H2D of the op batch"): mt_batch_upload (record validation + H2D over PCIe) and the apply,
-    timed together.  Returns ops/s over all ranks and the upload's share."""
+    timed together.  Returns the job's ops (every rank's documents) per second and the upload's
+    share."""
     from fluidframework_amd.engine import DeviceBatch
     from fluidframework_amd.hipmem import PinnedArray
     from fluidframework_amd.oplog import OpBatch
@@ -335,7 +337,7 @@ def h2d_step(eng, dev, n_ops, barrier, comm):
     staged.free()
     for p in pins:
         p.free()
-    return {'value': round(n_ops * comm.world / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3),
+    return {'value': round(job_ops / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3),
             'step_s': round(el, 3), 'bytes_uploaded': int(len(pinned.ops) * 32 + len(pinned.payload)),
             'note': 'op log from page-locked host memory: validation + H2D + apply in the timed region'}
 

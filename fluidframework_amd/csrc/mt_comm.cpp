@@ -121,36 +121,55 @@ mt_status mt_comm_barrier(mt_comm* c) {
     return MT_OK;
 }
 
+// A rank that cannot take part (no device memory for its row) aborts the communicator, so the
+// other ranks' ncclGather returns an error instead of blocking forever; a rank whose checksums
+// fail still takes part with a poisoned row (count = ~0), which rank 0 reports as MT_ERR_COMM.
+static mt_status comm_abort(mt_comm* c, mt_status st) {
+    fprintf(stderr, "libmtgpu: rank %d cannot join the checksum gather: aborting the communicator\n", c->rank);
+    if (c->nc) (void)ncclCommAbort(c->nc);
+    c->nc = nullptr;
+    return st;
+}
+
 mt_status mt_comm_gather_checksums(mt_comm* c, mt_engine* eng, uint32_t max_docs_per_rank, uint64_t* out,
                                    uint32_t* counts) {
-    if (!c || !eng) return MT_ERR_ARG;
+    if (!c || !eng || !c->nc) return MT_ERR_ARG;
     if (c->rank == 0 && (!out || !counts)) return MT_ERR_ARG;
     uint32_t n_docs = 0;
     mt_status st = mt_engine_info(eng, &n_docs, nullptr);
     if (st) return st;
-    if (n_docs > max_docs_per_rank) return MT_ERR_ARG;
+    if (n_docs > max_docs_per_rank) return MT_ERR_ARG;  // (every rank is given the same bound)
     CM_HIP(hipSetDevice(c->device));
     // [0] = this rank's document count, [1 .. max] = its checksums (zero padded): one gather
     const size_t row = (size_t)max_docs_per_rank + 1;
     uint64_t *d_send = nullptr, *d_recv = nullptr;
-    CM_HIP(hipMalloc(&d_send, row * sizeof(uint64_t)));
+    if (hipMalloc(&d_send, row * sizeof(uint64_t)) != hipSuccess) return comm_abort(c, MT_ERR_NOMEM);
     if (c->rank == 0 && hipMalloc(&d_recv, row * c->n_ranks * sizeof(uint64_t)) != hipSuccess) {
         (void)hipFree(d_send);
-        return MT_ERR_NOMEM;
+        return comm_abort(c, MT_ERR_NOMEM);
     }
-    const uint64_t cnt = n_docs;
+    uint64_t cnt = n_docs;
     bool ok = hipMemsetAsync(d_send, 0, row * sizeof(uint64_t), c->stream) == hipSuccess &&
-              hipMemcpyAsync(d_send, &cnt, sizeof cnt, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
               hipStreamSynchronize(c->stream) == hipSuccess;
     if (ok && n_docs) ok = mt_checksums_device(eng, d_send + 1, n_docs) == MT_OK;
-    ncclResult_t r = ncclSuccess;
-    if (ok) r = ncclGather(d_send, d_recv, row, ncclUint64, 0, c->nc, c->stream);
-    ok = ok && r == ncclSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    const bool local_ok = ok;
+    if (!local_ok) cnt = ~0ull;  // poisoned row: this rank's checksums are not valid
+    ok = hipMemcpyAsync(d_send, &cnt, sizeof cnt, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+    if (!ok) {
+        (void)hipFree(d_send);
+        if (d_recv) (void)hipFree(d_recv);
+        return comm_abort(c, MT_ERR_HIP);
+    }
+    const ncclResult_t r = ncclGather(d_send, d_recv, row, ncclUint64, 0, c->nc, c->stream);
+    ok = r == ncclSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    bool poisoned = false;
     if (ok && c->rank == 0) {
         uint64_t* h = new uint64_t[row * c->n_ranks];
         ok = hipMemcpy(h, d_recv, row * c->n_ranks * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess;
         for (int q = 0; ok && q < c->n_ranks; q++) {
-            counts[q] = (uint32_t)h[(size_t)q * row];
+            poisoned = poisoned || h[(size_t)q * row] > max_docs_per_rank;
+            counts[q] = poisoned ? 0u : (uint32_t)h[(size_t)q * row];
             memcpy(out + (size_t)q * max_docs_per_rank, h + (size_t)q * row + 1, max_docs_per_rank * sizeof(uint64_t));
         }
         delete[] h;
@@ -159,6 +178,11 @@ mt_status mt_comm_gather_checksums(mt_comm* c, mt_engine* eng, uint32_t max_docs
     if (d_recv) (void)hipFree(d_recv);
     if (r != ncclSuccess) {
         fprintf(stderr, "libmtgpu: ncclGather failed: %s\n", ncclGetErrorString(r));
+        return MT_ERR_COMM;
+    }
+    if (!local_ok) return MT_ERR_HIP;
+    if (poisoned) {
+        fprintf(stderr, "libmtgpu: a rank's checksums failed: the gather is incomplete\n");
         return MT_ERR_COMM;
     }
     return ok ? MT_OK : MT_ERR_HIP;

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
             const uint32_t opi = (uint32_t)stage[lane].w;
             if (ops && opi && opi <= n_ops) {
                 mt_op_rec* o = ops + (opi - 1u);
-                o->seq = t.w == MT_TK_SENT ? t.x : -1;
+                o->seq = t.w == MT_TK_SENT ? t.x : MT_SEQ_NACK;  // never MT_SEQ_LOCAL
                 o->msn = t.y;
                 o->ref_seq = t.z;
             }

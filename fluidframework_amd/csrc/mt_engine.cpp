@@ -123,8 +123,10 @@ struct mt_engine {
     bool concurrent = true;
     hipStream_t side[kNumClasses] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
+    uint64_t gen = 0;  // bumped by every call that can change document state (snap_cache's key)
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
+        uint64_t gen = 0;
         uint32_t d0 = 0, n = 0, chunk = 0, n_names = 0;
         const char* const* names = nullptr;
         std::string json;
@@ -263,6 +265,7 @@ mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
     if (!e || n_docs > e->cfg.max_docs) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     e->n_docs = n_docs;
+    e->gen++;
     HIP_OK(mt_launch_init(&e->g, n_docs, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return MT_OK;
@@ -287,6 +290,7 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
         if (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS) return MT_ERR_ARG;
     }
     HIP_OK(hipSetDevice(e->cfg.device));
+    e->gen++;
     // one staging allocation: ids, rebased row pointers, windows, segments, text
     std::vector<uint32_t> rp(n + 1);
     for (uint32_t i = 0; i <= n; i++) rp[i] = seg_row_ptr[i] - seg_row_ptr[0];
@@ -346,12 +350,13 @@ mt_status mt_regen_drain(mt_engine* e, uint32_t doc, mt_op_rec* recs, uint32_t c
     HIP_OK(hipMemcpy(cnt, &e->g.loc[doc].rgn, sizeof cnt, hipMemcpyDeviceToHost));
     *n = cnt[0];
     *pn = cnt[1];
-    if (recs && cap)
-        HIP_OK(hipMemcpy(recs, e->g.rg + (size_t)doc * MT_RG_RECS, std::min(cap, cnt[0]) * sizeof(mt_op_rec),
-                         hipMemcpyDeviceToHost));
-    if (payload && pcap)
-        HIP_OK(hipMemcpy(payload, e->g.rgp + (size_t)doc * MT_RG_BYTES, std::min(pcap, cnt[1]), hipMemcpyDeviceToHost));
-    if (recs) HIP_OK(hipMemset(&e->g.loc[doc].rgn, 0, sizeof cnt));
+    if (!recs) return MT_OK;  // sizes only
+    // a drain takes everything or nothing: buffers too small leave the records in place
+    if (cap < cnt[0] || (cnt[1] && (!payload || pcap < cnt[1]))) return MT_ERR_ARG;
+    if (cnt[0])
+        HIP_OK(hipMemcpy(recs, e->g.rg + (size_t)doc * MT_RG_RECS, cnt[0] * sizeof(mt_op_rec), hipMemcpyDeviceToHost));
+    if (cnt[1]) HIP_OK(hipMemcpy(payload, e->g.rgp + (size_t)doc * MT_RG_BYTES, cnt[1], hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(&e->g.loc[doc].rgn, 0, sizeof cnt));
     return MT_OK;
 }
 
@@ -515,6 +520,7 @@ mt_status mt_batch_free(mt_engine* e, mt_batch* b) {
 mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     if (!e || !b || b->n_docs != e->n_docs) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
+    e->gen++;
     const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     e->last_launches = 0;
@@ -619,6 +625,7 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
         cfg->n_values > MT_MAX_VALUES)
         return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
+    e->gen++;
     const uint32_t n = e->n_docs, per = cfg->ops_per_doc;
     const uint64_t n_ops = (uint64_t)n * per;
     if (n_ops >= (1ull << 32) || (uint64_t)n * payload_per_doc >= (1ull << 32)) return MT_ERR_ARG;
@@ -1192,7 +1199,7 @@ mt_status mt_get_snapshots(mt_engine* e, uint32_t d0, uint32_t n, uint32_t chunk
     HIP_OK(hipSetDevice(e->cfg.device));
     // a sizing call (buf NULL) leaves its result for the copying call with the same arguments
     auto& c = e->snap_cache;
-    const bool hit = c.valid && c.d0 == d0 && c.n == n && c.chunk == chunk_size && c.names == client_names &&
+    const bool hit = c.valid && c.gen == e->gen && c.d0 == d0 && c.n == n && c.chunk == chunk_size && c.names == client_names &&
                      c.n_names == n_names;
     if (!hit) {
         c.valid = false;
@@ -1243,6 +1250,7 @@ mt_status mt_get_snapshots(mt_engine* e, uint32_t d0, uint32_t n, uint32_t chunk
             for (auto& p : parts) c.json += p;
         }
         c.valid = true;
+        c.gen = e->gen;
         c.d0 = d0;
         c.n = n;
         c.chunk = chunk_size;

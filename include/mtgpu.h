@@ -76,6 +76,11 @@ enum mt_op_flags {
  * become new ops (a removal only while the segment is still locally removed), each with a new
  * pending group at the queue's tail.  The new ops are read with mt_regen_drain. */
 #define MT_SEQ_REGEN (-2)
+/* An op record whose message deli did not send (nacked, dropped, deferred or never sent; the fused
+ * hand-off of mt_deli_ticket_device stamps it).  Any seq below MT_SEQ_REGEN is such a record: it is
+ * never a local edit, and the apply engine halts the document on it with MT_DERR_SEQ_ORDER
+ * ("Incoming remote op sequence# <= local collabWindow's currentSequence#", client.ts:461-462). */
+#define MT_SEQ_NACK (-3)
 
 typedef struct mt_op_rec {
     int32_t seq;          /* sequenceNumber                     (protocol.ts:132-172)           */
@@ -279,7 +284,7 @@ mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_t
  * records, then the new ops (mt_op_rec, payload offsets into `payload`: an insert carries its text
  * or refType byte and its props, F_PROPS when its properties are defined; an annotate the reset
  * op's props).  *n / *pn: records / payload bytes available; with recs != NULL the buffer is
- * drained. */
+ * drained -- all of it: with cap < *n or pcap < *pn nothing is copied or cleared (MT_ERR_ARG). */
 mt_status mt_regen_drain(mt_engine* eng, uint32_t doc, mt_op_rec* recs, uint32_t cap, uint8_t* payload, uint32_t pcap,
                          uint32_t* n, uint32_t* pn);
 
@@ -503,8 +508,8 @@ mt_status mt_deli_ticket(mt_deli* dl, const mt_raw_msg* msgs, uint64_t n_msgs, c
                          uint32_t n_docs, mt_ticket* out);
 /* The same on device-resident buffers (HBM), asynchronous on the deli's stream.  d_ops (optional)
  * fuses the hand-off to the apply engine: a message with op_index = k + 1 carries op record k, and
- * that record gets the seq / msn / ref_seq of its ticket (seq = -1 when the message was not sent,
- * which the apply engine rejects as MT_DERR_SEQ_ORDER); op_index past n_ops links nothing. */
+ * that record gets the seq / msn / ref_seq of its ticket (seq = MT_SEQ_NACK when the message was not
+ * sent, which the apply engine rejects as MT_DERR_SEQ_ORDER); op_index past n_ops links nothing. */
 mt_status mt_deli_ticket_device(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row_ptr, uint32_t n_docs,
                                 mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops);
 /* Bench tooling: construct documents [0, n_docs) all from the same checkpoint (device fill). */

@@ -176,3 +176,55 @@ def test_c5_joins_through_deli_then_apply(oracle_lib):
     eng.apply_staged(dev)
     assert np.array_equal(eng.checksums(), o.checksums())
     assert all(eng.error(d) == (0, 0) for d in range(0, n, 97))
+
+
+def test_unsent_messages_halt_the_document(oracle_lib):
+    """a message deli does not send (here a csn gap and a refSeq below the msn, both
+    nacked, lambda.ts:269-275, 319-335) stamps MT_SEQ_NACK into its op record, never the local-edit
+    seq -1: the apply engine halts that document with MT_DERR_SEQ_ORDER at that record instead of
+    applying the nacked op as a pending local edit; the other documents replay unchanged."""
+    from fluidframework_amd.deli import RAW_DTYPE, TICKET_DTYPE, batch_device_ptrs
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.hipmem import DeviceBuffer
+    from fluidframework_amd.oplog import CONFIGS, OpBatch
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 256
+    n = 64
+    eng = MergeEngine(n, ops_per_launch=32)
+    dev = eng.synthesize(seed=11, **cfg)
+    host = dev.to_host()
+    d_ops, _, d_row = batch_device_ptrs(dev)
+    msgs = DeviceBuffer(dev.n_ops * RAW_DTYPE.itemsize)
+    tick = DeviceBuffer(dev.n_ops * TICKET_DTYPE.itemsize)
+    dl = _seq(n)
+    dl.restore_all(seq=0, clients={c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)})
+    dl.raw_from_ops(d_ops, d_row, n, msgs.ptr)
+    dl.sync()
+    raw = msgs.download(RAW_DTYPE)
+    rp = host.row_ptr.astype(np.int64)
+    raw['csn'][rp[0] + 100] += 5                      # doc 0: a gap in the sender's csn
+    j = rp[1] + 150                                   # doc 1: a refSeq below the msn
+    assert host.ops['msn'][j - 1] > 0
+    raw['ref_seq'][j] = int(host.ops['msn'][j - 1]) - 1
+    msgs.upload(raw)
+    dl2 = _seq(n)
+    dl2.restore_all(seq=0, clients={c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)})
+    dl2.ticket_device(msgs.ptr, d_row, n, tick.ptr, d_ops, dev.n_ops)
+    dl2.sync()
+    docs = [od.DeliDoc(seq=0, clients={c: (0, 0, False) for c in range(1, cfg['n_clients'] + 1)}) for _ in range(n)]
+    want, _ = od.ticket_batch(raw, host.row_ptr, docs)
+    got = _tickets(tick.download(TICKET_DTYPE))
+    assert np.array_equal(got, want)
+    assert want[rp[0] + 100, 3] != od.SENT and want[j, 3] != od.SENT
+    stamped = host.ops.copy()
+    sent = want[:, 3] == od.SENT
+    stamped['seq'] = np.where(sent, want[:, 0], -3)   # MT_SEQ_NACK
+    stamped['msn'], stamped['ref_seq'] = want[:, 1], want[:, 2]
+    assert np.array_equal(dev.to_host().ops, stamped)
+    eng.reset()
+    eng.apply_staged(dev)
+    o = oracle_lib.Oracle(n).apply(OpBatch(stamped, host.payload, host.row_ptr), threads=8)
+    assert eng.error(0) == (1, -3) and eng.error(1) == (1, -3)
+    assert all(eng.error(d) == o.error(d) for d in range(n))
+    assert np.array_equal(eng.checksums(), o.checksums())

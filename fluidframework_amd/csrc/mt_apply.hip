@@ -16,7 +16,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mtgpu.h"
+#include "mt_checksum.h"
 #include "mt_state.h"
 #include "mt_synth.h"
 #include "mt_wave.h"
@@ -26,7 +29,20 @@ namespace mt {
 constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
 
-template <int CAP, bool LOC = false>
+// An op's property pairs in its payload: narrow (key u8, value u8) or wide (MT_OP_WIDE: key u8,
+// value u16 LE); value 0 = null = delete
+struct Pairs {
+    const uint8_t* p;
+    int np;
+    bool wide;
+    MT_DEV int key(int q) const { return p[wide ? 3 * q : 2 * q]; }
+    MT_DEV uint32_t val(int q) const { return wide ? (uint32_t)p[3 * q + 1] | ((uint32_t)p[3 * q + 2] << 8) : p[2 * q + 1]; }
+    MT_DEV int key_limit() const { return wide ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS; }
+};
+
+// W: a wide document (include/mtgpu.h "limits"): per slot also the overlap ids >= 64 (ovx) and the
+// property words ph / pxl / pxh (u16 value ids, keys 8..15); UTF-16 text
+template <int CAP, bool LOC = false, bool W = false>
 struct Lds {
     static constexpr int LB = CAP / 2;      // leaf blocks
     static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
@@ -63,15 +79,21 @@ struct Lds {
     uint64_t pk[LOC ? CAP : 1];
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
+    uint64_t ovx[W ? CAP : 1];
+    uint64_t ph[W ? CAP : 1];
+    uint64_t pxl[W ? CAP : 1];
+    uint64_t pxh[W ? CAP : 1];
+    uint32_t wide;                // the document's mt_doc_scalars.wide bits
 };
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
 // SURVEY.md §8 a9 "unbounded B-tree"): the same structure lives in a per-wave workspace in HBM
 // (mt_launch_apply_big); lanes exchange it through the vector L1 / L2, so a pass boundary also
 // waits for the wave's outstanding stores (workgroup scope = the wave's CU).
-template <int CAP, bool G = false, bool LOC = false>
+template <int CAP, bool G = false, bool LOC = false, bool W = false>
 struct Wave {
-    using L = Lds<CAP, LOC>;
+    using L = Lds<CAP, LOC, W>;
+    using TC = typename std::conditional<W, uint16_t, uint8_t>::type;  // a text code unit in the arena
     MT_DEV static void sync() {
         if (G) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -83,22 +105,103 @@ struct Wave {
     }
     L& s;
     const int lane;
-    uint8_t* const abase;   // document's double-buffered arena: [2][textcap]
-    uint8_t* arena;         // current half
-    const uint32_t textcap;
+    TC* const abase;        // document's double-buffered arena: [2][textcap]
+    TC* arena;              // current half
+    const uint32_t textcap; // code units per half
     mt_event* const ev;     // the document's delta-event records (null: not recording)
     const uint32_t evcap;
     uint32_t rix = 0;       // index of the record being applied within its document
     mt_op_rec* rg = nullptr;  // (LOC) the document's regenerated-op buffer and its payload
     uint8_t* rgp = nullptr;
 
-    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc, mt_event* e = nullptr, uint32_t ec = 0)
-        : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc), ev(e), evcap(ec) {}
+    MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc_bytes, mt_event* e = nullptr, uint32_t ec = 0)
+        : s(lds), lane(lane_id()), abase(reinterpret_cast<TC*>(a)), arena(reinterpret_cast<TC*>(a)),
+          textcap(tc_bytes / (uint32_t)sizeof(TC)), ev(e), evcap(ec) {}
+
+    // ------------------------------------------------------------ wide state
+    // removedClientOverlap holds client C (ids < 64: the bitmask; a wide document's others: ovx)
+    MT_DEV bool ovl_has(int slot, int C) const {
+        if (C < 64) return C >= 0 && ((s.ovl[slot] >> C) & 1ull);
+        if constexpr (W) return mt_ovx_has(s.ovx[slot], (uint32_t)C);
+        return false;
+    }
+    // addOverlappingClient (mergeTree.ts:2544-2552); false: a wide segment's ovx list is full
+    MT_DEV bool ovl_add(int slot, int C) {
+        if (C < 64) {
+            s.ovl[slot] |= 1ull << C;
+            return true;
+        }
+        if constexpr (W) {
+            const uint64_t x = s.ovx[slot];
+            if (mt_ovx_has(x, (uint32_t)C)) return true;
+            if (x >> 56) return false;
+            uint64_t out = 0;  // insert C into the ascending byte list
+            int j = 0;
+            bool done = false;
+            for (int b = 0; b < 8; b++) {
+                const uint32_t v = (uint32_t)(x >> (8 * b)) & 0xFFu;
+                if (!v) break;
+                if (!done && (uint32_t)C < v) {
+                    out |= (uint64_t)C << (8 * j++);
+                    done = true;
+                }
+                out |= (uint64_t)v << (8 * j++);
+            }
+            if (!done) out |= (uint64_t)C << (8 * j);
+            s.ovx[slot] = out;
+            return true;
+        }
+        return false;
+    }
+    // value id of key k of a slot (0 = absent)
+    MT_DEV uint32_t pval(int sl, int k) const {
+        const int sh = 8 * (k & 7);
+        if constexpr (W) {
+            const uint64_t lo = k < 8 ? s.props[sl] : s.pxl[sl], hi = k < 8 ? s.ph[sl] : s.pxh[sl];
+            return (uint32_t)((lo >> sh) & 0xFFu) | ((uint32_t)((hi >> sh) & 0xFFu) << 8);
+        }
+        return k < 8 ? (uint32_t)((s.props[sl] >> sh) & 0xFFu) : 0u;
+    }
+    MT_DEV void pset(int sl, int k, uint32_t v) {
+        const int sh = 8 * (k & 7);
+        const uint64_t m = ~(0xFFull << sh);
+        if (k < 8) s.props[sl] = (s.props[sl] & m) | ((uint64_t)(v & 0xFFu) << sh);
+        if constexpr (W) {
+            if (k < 8) {
+                s.ph[sl] = (s.ph[sl] & m) | ((uint64_t)(v >> 8) << sh);
+            } else {
+                s.pxl[sl] = (s.pxl[sl] & m) | ((uint64_t)(v & 0xFFu) << sh);
+                s.pxh[sl] = (s.pxh[sl] & m) | ((uint64_t)(v >> 8) << sh);
+            }
+        }
+    }
+    MT_DEV void pclear(int sl) {
+        s.props[sl] = 0;
+        if constexpr (W) s.ph[sl] = s.pxl[sl] = s.pxh[sl] = 0;
+    }
+    MT_DEV void pcopy(int dst, int src) {
+        s.props[dst] = s.props[src];
+        if constexpr (W) {
+            s.ph[dst] = s.ph[src];
+            s.pxl[dst] = s.pxl[src];
+            s.pxh[dst] = s.pxh[src];
+        }
+    }
+    MT_DEV bool peq(int a, int b) const {
+        if (s.props[a] != s.props[b]) return false;
+        if constexpr (W) return s.ph[a] == s.ph[b] && s.pxl[a] == s.pxl[b] && s.pxh[a] == s.pxh[b];
+        return true;
+    }
+    // the op's (key, value) pairs onto a slot's props (properties.ts:95-116)
+    MT_DEV void papply(int sl, const Pairs& pr) {
+        for (int q = 0; q < pr.np; q++) pset(sl, pr.key(q), pr.val(q));
+    }
+    static constexpr int kKeys = W ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS;
 
     // ------------------------------------------------------------ delta events
     // One callback record (mt_event, include/mtgpu.h), written by lane 0 in firing order: the
     // reference's mergeTreeDeltaCallback / mergeTreeMaintenanceCallback (mergeTreeDeltaCallback.ts).
-    MT_DEV void emit(int op, unsigned flags, int leaf, int pos, uint32_t len, uint8_t pmask = 0, uint64_t pvals = 0) {
+    MT_DEV void emit(int op, unsigned flags, int leaf, int pos, uint32_t len) {
         if (!ev) return;
         const int n = s.evn;
         if (lane == 0 && n < (int)evcap) {
@@ -106,11 +209,9 @@ struct Wave {
             e.seq = s.evseq;
             e.op = (int8_t)op;
             e.flags = (uint8_t)flags;
-            e.pmask = pmask;
             e.leaf = leaf;
             e.pos = pos;
             e.len = len;
-            e.pvals = pvals;
             ev[n] = e;
         }
         sync();
@@ -133,8 +234,7 @@ struct Wave {
     // document order, lane-parallel.  REMOVE runs after the edits (segments this op removed: rseq
     // == S by C; their local position with the removal applied), ANNOTATE before them (the
     // propertyDeltas need the previous values; annotate does not move the local view).
-    MT_DEV void emit_range(bool is_remove, int32_t S, int C, int start, int end, const uint8_t* pairs, int np,
-                           bool rewrite) {
+    MT_DEV void emit_range(bool is_remove, int32_t S, int C, int start, int end, const Pairs& pr, bool rewrite) {
         if (!ev) return;
         const int n = s.n, e0 = s.evn;
         int cnt = 0, lpos = 0;
@@ -144,10 +244,12 @@ struct Wave {
             bool hit = false;
             int ll = 0;
             uint32_t ln = 0;
-            uint8_t pm = 0, xf = 0;
-            uint64_t pv = 0;
+            uint32_t pm = 0;
+            uint8_t xf = 0;
+            uint16_t pv[16] = {0};
+            int sl = 0;
             if (i < n) {
-                const int sl = s.order[i];
+                sl = s.order[i];
                 const uint8_t f = s.flags[sl];
                 ln = s.len[sl];
                 uint64_t pk = 0;  // (LOC, a remote annotate: keys with pending local changes are skipped)
@@ -162,25 +264,27 @@ struct Wave {
                     // a rewrite records each key it deletes with its old value; every key of the op
                     // records the value before it is set (null when absent, and null for a rewrite's
                     // null-valued key, deleted a moment earlier)
-                    const uint64_t old = (f & MT_SF_PDEF) ? s.props[sl] : 0;
+                    const bool pdef = (f & MT_SF_PDEF) != 0;
                     if (MT_PK_RW(pk) > 0) {
                         xf = MT_EVF_NOPD;  // dropped while a local rewrite is pending: propertyDeltas undefined
                     } else {
                         if (rewrite) {
-                            for (int k = 0; k < 8; k++)
-                                if (((old >> (8 * k)) & 0xFF) && MT_PK_KEY(pk, k) == 0) {
+                            for (int k = 0; k < kKeys; k++) {
+                                const uint32_t old = pdef ? pval(sl, k) : 0u;
+                                if (old && (k >= 8 || MT_PK_KEY(pk, k) == 0)) {
                                     bool keep = false;  // a key the rewrite sets again keeps its value here
-                                    for (int q = 0; q < np; q++) keep = keep || (pairs[2 * q] == k && pairs[2 * q + 1] != 0);
-                                    if (!keep) pm |= (uint8_t)(1u << k);
+                                    for (int q = 0; q < pr.np; q++) keep = keep || (pr.key(q) == k && pr.val(q) != 0);
+                                    if (!keep) pm |= 1u << k;
                                 }
-                            pv = old;
+                                pv[k] = (uint16_t)old;
+                            }
                         }
-                        for (int q = 0; q < np; q++) {
-                            const int k = pairs[2 * q];
-                            if (MT_PK_KEY(pk, k) > 0) continue;
-                            const uint64_t prev = (rewrite && pairs[2 * q + 1] == 0) ? 0 : ((old >> (8 * k)) & 0xFF);
-                            pm |= (uint8_t)(1u << k);
-                            pv = (pv & ~(0xFFull << (8 * k))) | (prev << (8 * k));
+                        for (int q = 0; q < pr.np; q++) {
+                            const int k = pr.key(q);
+                            if (k < 8 && MT_PK_KEY(pk, k) > 0) continue;
+                            const uint32_t prev = (rewrite && pr.val(q) == 0) ? 0u : (pdef ? pval(sl, k) : 0u);
+                            pm |= 1u << k;
+                            pv[k] = (uint16_t)prev;
                         }
                     }
                 }
@@ -193,11 +297,11 @@ struct Wave {
                 e.seq = s.evseq;
                 e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
                 e.flags = (uint8_t)((idx == 0 ? MT_EVF_FIRST : 0) | xf);
-                e.pmask = pm;
+                e.pmask = (uint16_t)pm;
                 e.leaf = i;
                 e.pos = lpos + incl - ll;
                 e.len = ln;
-                e.pvals = pv;
+                for (int k = 0; k < 16; k++) e.pvals[k] = (pm >> k) & 1u ? pv[k] : (uint16_t)0;
                 ev[e0 + idx] = e;
             }
             cnt += __popcll(m);
@@ -228,8 +332,7 @@ struct Wave {
             const bool seen = (s.client[slot] == C) || (s.seq[slot] != -1 && s.seq[slot] <= R);
             if (!seen) return 0;
             if ((s.flags[slot] & MT_SF_REMOVED) &&
-                (s.rclient[slot] == C || (C < 64 && ((s.ovl[slot] >> C) & 1ull)) ||
-                 (s.rseq[slot] != -1 && s.rseq[slot] <= R)))
+                (s.rclient[slot] == C || ovl_has(slot, C) || (s.rseq[slot] != -1 && s.rseq[slot] <= R)))
                 return 0;
             return (int)s.len[slot];
         }
@@ -237,7 +340,7 @@ struct Wave {
         if (!seen) return 0;
         if (s.flags[slot] & MT_SF_REMOVED) {
             // (C = NonCollabClient for a snapshot body append: no overlap bit, MT_OP_LOAD)
-            if (s.rclient[slot] == C || (C < 64 && ((s.ovl[slot] >> C) & 1ull)) || s.rseq[slot] <= R) return 0;
+            if (s.rclient[slot] == C || ovl_has(slot, C) || s.rseq[slot] <= R) return 0;
         }
         return (int)s.len[slot];
     }
@@ -435,7 +538,7 @@ struct Wave {
     MT_DEV void arena_copy(uint32_t dst, uint32_t src, uint32_t n) {
         for (uint32_t base = 0; base < n; base += 64) {
             const uint32_t i = base + lane;
-            uint8_t v = 0;
+            TC v = 0;
             if (i < n) v = arena[src + i];
             __threadfence_block();
             if (i < n) arena[dst + i] = v;
@@ -447,7 +550,7 @@ struct Wave {
     // (TextSegment text has no identity; only its content is state).  Afterwards adjacent
     // segments are adjacent in the arena, so later appends are free.
     MT_DEV void compact_text() {
-        uint8_t* dst = abase + (size_t)(s.text_half ^ 1u) * textcap;
+        TC* dst = abase + (size_t)(s.text_half ^ 1u) * textcap;
         const int n = s.n;
         uint32_t carry = 0;
         for (int base = 0; base < n; base += 64) {
@@ -457,7 +560,7 @@ struct Wave {
             const int incl = wave_incl_scan(l);
             const uint32_t at = carry + (uint32_t)(incl - l);
             if (i < n) {
-                const uint8_t* src = arena + s.toff[sl];
+                const TC* src = arena + s.toff[sl];
                 for (int q = 0; q < l; q++) dst[at + q] = src[q];
             }
             sync();
@@ -506,7 +609,8 @@ struct Wave {
             s.rseq[t] = s.rseq[sl];
             s.rclient[t] = s.rclient[sl];
             s.ovl[t] = s.ovl[sl];
-            s.props[t] = s.props[sl];
+            if constexpr (W) s.ovx[t] = s.ovx[sl];
+            pcopy(t, sl);
             s.flags[t] = s.flags[sl];
             s.len[t] = s.len[sl] - (uint32_t)off;
             s.toff[t] = s.toff[sl] + (uint32_t)off;
@@ -518,7 +622,7 @@ struct Wave {
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
                 s.ct[t] = s.lc.stamp;
             }
-            const uint8_t last = arena[s.toff[sl] + (uint32_t)off - 1];
+            const TC last = arena[s.toff[sl] + (uint32_t)off - 1];
             s.flags[sl] = (uint8_t)((s.flags[sl] & ~MT_SF_NL) | (last == '\n' ? MT_SF_NL : 0));
         }
         const int old_end = s.cum[k];
@@ -595,8 +699,8 @@ struct Wave {
     }
 
     // ---------------------------------------------------------------- zamboni
-    static MT_DEV bool props_match(uint8_t fa, uint64_t pa, uint8_t fb, uint64_t pb) {
-        return ((fa ^ fb) & MT_SF_PDEF) == 0 && pa == pb;  // matchProperties, properties.ts:62-93
+    MT_DEV bool props_match(int a, int b) const {  // matchProperties, properties.ts:62-93
+        return ((s.flags[a] ^ s.flags[b]) & MT_SF_PDEF) == 0 && peq(a, b);
     }
 
     // scourNode on leaf block b (mergeTree.ts:1289-1365).  Unlinks removed segments at or
@@ -632,7 +736,7 @@ struct Wave {
                     // appended to: Marker.canAppend, TextSegment.is, mergeTree.ts:793; textSegment.ts:63-68)
                     app = !((s.flags[prev] | f) & MT_SF_MARKER) && !(s.flags[prev] & MT_SF_NL) &&
                           (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
-                          props_match(s.flags[prev], s.props[prev], f, s.props[sl]) && ql > 0;
+                          props_match(prev, sl) && ql > 0;
                 }
                 if (app) {
                     append_text(prev, sl);
@@ -784,17 +888,7 @@ struct Wave {
     }
 
     // -------------------------------------------------------------------- ops
-    // props: apply (key, value) pairs; value 0 = null = delete (properties.ts:95-116)
-    static MT_DEV uint64_t apply_pairs(uint64_t p, const uint8_t* pairs, int np) {
-        for (int q = 0; q < np; q++) {
-            const int k = pairs[2 * q];
-            const uint64_t v = pairs[2 * q + 1];
-            p = (p & ~(0xFFull << (8 * k))) | (v << (8 * k));
-        }
-        return p;
-    }
-
-    MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const uint8_t* pairs, int np) {
+    MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const Pairs& pr) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client & 0xFF, pos = op.pos1;  // (MT_OP_LOAD: removedClient in the high byte)
         if (!boundary(pos, R, C, S)) return;  // cum: apply() scanned for (R, C)
@@ -866,12 +960,16 @@ struct Wave {
             if (!arena_reserve((uint32_t)tlen, S)) return;
             const uint32_t top = s.text_top;
             bool hasnl = false;
+            const bool wop = (op.type & MT_OP_WIDE) != 0;  // the payload text is UTF-16 code units
+            auto unit = [&](int i) -> uint32_t {
+                return wop ? (uint32_t)pay[2 * i] | ((uint32_t)pay[2 * i + 1] << 8) : (uint32_t)pay[i];
+            };
             for (int base = 0; base < tlen; base += 64) {
                 const int i = base + lane;
-                uint8_t c = 0;
+                uint32_t c = 0;
                 if (i < tlen) {
-                    c = pay[i];
-                    arena[top + i] = c;
+                    c = unit(i);
+                    arena[top + i] = (TC)c;
                 }
                 hasnl = hasnl || wave_ballot(i < tlen && c == '\n') != 0;
             }
@@ -879,25 +977,25 @@ struct Wave {
             if (lane == 0) {
                 // a snapshot body segment may arrive removed (SnapshotLoader.specToSegment,
                 // snapshotLoader.ts:101-106): MT_OP_LOAD carries removedSeq in pos2
-                const bool lrm = op.type == MT_OP_LOAD && op.pos2 >= 0;
+                const bool lrm = MT_OP_TYPE(op) == MT_OP_LOAD && op.pos2 >= 0;
                 s.seq[t] = S;
                 s.client[t] = (uint8_t)C;
                 s.rseq[t] = lrm ? op.pos2 : 0;
                 s.rclient[t] = lrm ? (uint8_t)(op.client >> 8) : 0;
                 s.ovl[t] = 0;
+                if constexpr (W) s.ovx[t] = 0;
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
                 // a Marker (MT_F_MARKER): length 1, its arena byte is its ReferenceType
                 uint8_t f = (op.flags & MT_F_MARKER) ? MT_SF_MARKER
-                                                     : ((pay[tlen - 1] == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0));
+                                                     : ((unit(tlen - 1) == '\n' ? MT_SF_NL : 0) | (hasnl ? MT_SF_HASNL : 0));
                 f |= lrm ? MT_SF_REMOVED : 0;
-                uint64_t p = 0;
+                pclear(t);
                 if (op.flags & MT_F_PROPS) {  // TextSegment.make -> addProperties
                     f |= MT_SF_PDEF;
-                    p = apply_pairs(0, pairs, np);
+                    papply(t, pr);
                 }
                 s.flags[t] = f;
-                s.props[t] = p;
                 if constexpr (LOC) {  // a local insert is its edit's one pending segment (saveIfLocal)
                     s.gm[t] = S == -1 ? (1ull << (s.lc.ghi & 63u)) : 0ull;
                     s.pk[t] = 0;
@@ -921,22 +1019,21 @@ struct Wave {
                 if (!add_lru(bb, t, S)) return;
             }
             // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988); a snapshot body append has no opArgs
-            if (ev && op.type != MT_OP_LOAD) emit(MT_EV_INSERT, MT_EVF_FIRST, k, local_prefix(k), (uint32_t)tlen);
-        } else if (op.type != MT_OP_LOAD) {
+            if (ev && MT_OP_TYPE(op) != MT_OP_LOAD) emit(MT_EV_INSERT, MT_EVF_FIRST, k, local_prefix(k), (uint32_t)tlen);
+        } else if (MT_OP_TYPE(op) != MT_OP_LOAD) {
             emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
         }
         if (S != -1) zamboni();  // (a local edit runs no zamboni, mergeTree.ts:1994-1997)
     }
 
-    MT_DEV void op_range(const mt_op_rec& op, const uint8_t* pairs, int np) {
+    MT_DEV void op_range(const mt_op_rec& op, const Pairs& pr) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, start = op.pos1, end = op.pos2;
-        const bool is_remove = op.type == MT_OP_REMOVE;
+        const bool is_remove = MT_OP_TYPE(op) == MT_OP_REMOVE;
         if (!boundary(start, R, C, S)) return;  // cum: apply() scanned for (R, C)
         if (!boundary(end, R, C, S)) return;
         // markRangeRemoved / annotateRange leaf actions over mapRange (mergeTree.ts:2903-2965)
         const int n = s.n;
-        const uint64_t cbit = 1ull << C;
         const bool rewrite = op.flags & MT_F_REWRITE;
         const bool local = S == -1;
         uint64_t gbit = 0;
@@ -953,7 +1050,8 @@ struct Wave {
                 sync();
             }
         }
-        if (!is_remove) emit_range(false, S, C, start, end, pairs, np, rewrite);
+        if (!is_remove) emit_range(false, S, C, start, end, pr, rewrite);
+        bool over = false;  // (a wide segment's overlap list full)
         for (int base = 0; base < n; base += 64) {
             const int i = base + lane;
             if (i < n) {
@@ -964,7 +1062,7 @@ struct Wave {
                         if (local) s.gm[sl] |= gbit;
                     }
                     if (LOC && !is_remove) {
-                        annotate_loc(sl, pairs, np, rewrite, local);
+                        annotate_loc(sl, pr.p, pr.np, rewrite, local);
                     } else if (is_remove) {
                         bool pend_rm = false;
                         if constexpr (LOC) pend_rm = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] == -1;
@@ -974,7 +1072,7 @@ struct Wave {
                             s.flags[sl] |= MT_SF_OVW;  // (not among this op's removedSegments)
                             if constexpr (LOC) s.lsq[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
                         } else if (s.flags[sl] & MT_SF_REMOVED) {
-                            s.ovl[sl] |= cbit;  // addOverlappingClient (first remover wins)
+                            over = !ovl_add(sl, C) || over;  // addOverlappingClient (first remover wins)
                         } else {
                             s.flags[sl] |= MT_SF_REMOVED;
                             s.rseq[sl] = S;
@@ -984,16 +1082,16 @@ struct Wave {
                             }
                         }
                     } else {  // SegmentPropertiesManager.addProperties (remote, no combining op)
-                        uint64_t p = (s.flags[sl] & MT_SF_PDEF) ? s.props[sl] : 0;
-                        if (rewrite) p = 0;
-                        s.props[sl] = apply_pairs(p, pairs, np);
+                        if (rewrite || !(s.flags[sl] & MT_SF_PDEF)) pclear(sl);
+                        papply(sl, pr);
                         s.flags[sl] |= MT_SF_PDEF;
                     }
                 }
             }
         }
+        if (wave_ballot(over)) return fail(MT_DERR_LIMITS, S);
         sync();
-        if (is_remove) emit_range(true, S, C, start, end, pairs, np, rewrite);
+        if (is_remove) emit_range(true, S, C, start, end, pr, rewrite);
         if constexpr (LOC) {
             if (is_remove) {
                 for (int i = lane; i < n; i += 64) s.flags[s.order[i]] &= (uint8_t)~MT_SF_OVW;
@@ -1292,15 +1390,16 @@ struct Wave {
             s.lc.own = C;
             sync();
         }
-        // (the editing client may be short id 0, the reference's own id, client.ts:1057-1062)
-        if (C != s.lc.own || C >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, -1);
+        // (the editing client may be short id 0, the reference's own id, client.ts:1057-1062; its
+        // document stays narrow: the editing form has no wide state)
+        if (C != s.lc.own || C >= MT_MAX_CLIENTS || (op.type & MT_OP_WIDE)) return fail(MT_DERR_LIMITS, -1);
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, -1);
         if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, -1);
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
-        const uint8_t* pairs = pay + tlen;
+        const Pairs pr{pay + tlen, np, false};
         for (int q = 0; q < np; q++)
-            if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, -1);
+            if (pr.key(q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, -1);
         mt_op_rec o = op;
         o.ref_seq = s.cur_seq;
         s.evseq = -1;  // (a local edit's callbacks: seq -1)
@@ -1311,10 +1410,10 @@ struct Wave {
         sync();
         if (op.type == MT_OP_INSERT) {
             if (o.pos1 < 0 || o.pos1 > L) return fail(MT_DERR_INSERT_FAILED, -1);
-            op_insert(o, pay, tlen, pairs, np);
+            op_insert(o, pay, tlen, pr);
         } else {
             if (o.pos1 < 0 || o.pos2 > L || o.pos1 >= o.pos2) return fail(MT_DERR_BAD_OP, -1);  // getValidOpRange
-            op_range(o, pairs, np);
+            op_range(o, pr);
         }
         if (ev && s.evn > (int)evcap) fail(MT_DERR_EVENTS, -1);
     }
@@ -1324,6 +1423,7 @@ struct Wave {
         s.evseq = S;
         if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                                  // client.ts:824
         if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);           // :826
+        if (op.type & MT_OP_WIDE) return fail(MT_DERR_LIMITS, S);
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
         op_ack(op, payload + op.payload_off + (op.payload_len - 2 * np), np);
         if (s.err) return;
@@ -1334,38 +1434,44 @@ struct Wave {
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
         const int np = MT_OP_NPAIRS(op.flags);
         const int32_t S = op.seq;
+        const int type = MT_OP_TYPE(op);
+        const bool wop = (op.type & MT_OP_WIDE) != 0;
         if constexpr (LOC) {
             if (S == MT_SEQ_REGEN) return op_regen(op, payload);
-            if (op.type <= MT_OP_ANNOTATE && S == -1) return apply_local(op, payload);
-            if (s.lc.own >= 0 && (int)op.client == s.lc.own && op.type <= MT_OP_ANNOTATE && !MT_OP_IS_NOOP(op))
+            if (type <= MT_OP_ANNOTATE && S == -1) return apply_local(op, payload);
+            if (s.lc.own >= 0 && (int)op.client == s.lc.own && type <= MT_OP_ANNOTATE && !MT_OP_IS_NOOP(op))
                 return apply_ack(op, payload);
         }
-        if (op.type > MT_OP_LOAD) return fail(MT_DERR_BAD_OP, S);
+        if (type > MT_OP_LOAD) return fail(MT_DERR_BAD_OP, S);
+        // (a wide op reaches only the wide form: mt_bin_kernel routes its document there)
+        if (wop && !W) return fail(MT_DERR_LIMITS, S);
+        constexpr int kClients = W ? MT_MAX_CLIENTS_WIDE : MT_MAX_CLIENTS;
         // MT_OP_LOAD: MergeTree.insertSegments from SnapshotLoader.loadBody (snapshotLoader.ts:192-224),
         // no Client around it: no window asserts and no updateSeqNumbers
-        const bool load = op.type == MT_OP_LOAD;
+        const bool load = type == MT_OP_LOAD;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
         const int C = op.client & 0xFF;
+        const uint32_t plen = MT_OP_PAIRS_LEN(op);
         s.evseq = S;
         if (load) {
-            const bool ok = (C == MT_CLIENT_NONCOLLAB || (C >= 1 && C < MT_MAX_CLIENTS)) &&
-                            (op.pos2 < 0 || ((op.client >> 8) >= 1 && (op.client >> 8) < MT_MAX_CLIENTS));
+            const bool ok = (C == MT_CLIENT_NONCOLLAB || (C >= 1 && C < kClients)) &&
+                            (op.pos2 < 0 || ((op.client >> 8) >= 1 && (op.client >> 8) < kClients));
             if (!ok) return fail(MT_DERR_LIMITS, S);
-            if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+            if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u))) return fail(MT_DERR_BAD_OP, S);
         } else if (!noop) {
-            if (op.client == 0 || op.client >= MT_MAX_CLIENTS) return fail(MT_DERR_LIMITS, S);
-            if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+            if (op.client == 0 || op.client >= kClients) return fail(MT_DERR_LIMITS, S);
+            if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u))) return fail(MT_DERR_BAD_OP, S);
         } else {  // every assert of the message before any edit: the document halts before it
             if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);  // client.ts:824
             if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
         }
         const uint8_t* pay = payload + op.payload_off;
-        const int tlen = (int)op.payload_len - 2 * np;
-        const uint8_t* pairs = pay + tlen;
+        const int tlen = (int)((op.payload_len - plen) >> (wop ? 1 : 0));  // text code units
+        const Pairs pr{pay + (op.payload_len - plen), np, wop};
         for (int q = 0; q < np; q++)
-            if (pairs[2 * q] >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
+            if (pr.key(q) >= pr.key_limit()) return fail(MT_DERR_LIMITS, S);
         if (!noop) {
-            if (op.pos1 < 0 || (op.type != MT_OP_INSERT && !load && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
+            if (op.pos1 < 0 || (type != MT_OP_INSERT && !load && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
             const int L = scan(op.ref_seq, C);  // cum for the op's view (no edit yet)
             // the window asserts run after the op in the reference (completeAndLogOp, client.ts:461-464;
             // updateSeqNumbers :826), so a failing insert (mergeTree.ts:2210) is reported first; all of
@@ -1374,10 +1480,10 @@ struct Wave {
             if (load) wc = 0;
             else if (!(s.cur_seq < S)) wc = MT_DERR_SEQ_ORDER;
             else if (!(s.min_seq <= op.msn) || !(op.msn <= S)) wc = MT_DERR_MSN_ORDER;
-            if ((op.type == MT_OP_INSERT || load) && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
+            if ((type == MT_OP_INSERT || load) && tlen > 0 && op.pos1 > L) wc = MT_DERR_INSERT_FAILED;
             if (wc) return fail(wc, S);
-            if (op.type == MT_OP_INSERT || load) op_insert(op, pay, tlen, pairs, np);
-            else op_range(op, pairs, np);
+            if (type == MT_OP_INSERT || load) op_insert(op, pay, tlen, pr);
+            else op_range(op, pr);
         }
         if (s.err) return;
         if (!load && !(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
@@ -1554,7 +1660,17 @@ struct Wave {
             s.hseq[i] = g.hseq[ho + i];
             s.hslot[i] = g.hslot[ho + i];
         }
+        const bool was_wide = (sc.wide & MT_WIDE_DOC) != 0;
+        if constexpr (W) {
+            for (int i = lane; i < n; i += 64) {
+                s.ovx[i] = was_wide ? g.ovx[so + i] : 0ull;
+                s.ph[i] = was_wide ? g.ph[so + i] : 0ull;
+                s.pxl[i] = was_wide ? g.pxl[so + i] : 0ull;
+                s.pxh[i] = was_wide ? g.pxh[so + i] : 0ull;
+            }
+        }
         if (lane == 0) {
+            s.wide = sc.wide;
             s.n = n;
             s.nlev = sc.nlev;
             for (int L = 0; L < MT_MAXLEV; L++) s.nb[L] = sc.nb[L];
@@ -1595,6 +1711,48 @@ struct Wave {
         }
         sync();
         arena = abase + (size_t)s.text_half * textcap;
+        if constexpr (W) {
+            if (!was_wide) promote();
+        }
+    }
+
+    // A narrow document enters the wide form (include/mtgpu.h "limits"): its Latin-1 text becomes
+    // UTF-16 code units in the other arena half (compacted, in document order; a half holds
+    // textcap units); the overlap ids >= 64 and the wide property words start empty (load).  When the
+    // text does not fit, the document halts with MT_DERR_TEXT_ARENA and stays narrow.
+    MT_DEV void promote() {
+        if constexpr (W) {
+            const int n = s.n;
+            const uint32_t tcb = textcap * (uint32_t)sizeof(TC);  // bytes per half
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(abase) + (size_t)s.text_half * tcb;
+            int total = 0;
+            for (int base = 0; base < n; base += 64) total += wave_sum(base + lane < n ? (int)s.len[base + lane] : 0);
+            if ((uint32_t)total > textcap) return fail(MT_DERR_TEXT_ARENA, s.cur_seq);
+            TC* dst = abase + (size_t)(s.text_half ^ 1u) * textcap;
+            uint32_t carry = 0;
+            for (int base = 0; base < n; base += 64) {
+                const int i = base + lane;
+                const int l = i < n ? (int)s.len[i] : 0;
+                const int incl = wave_incl_scan(l);
+                const uint32_t at = carry + (uint32_t)(incl - l);
+                if (i < n) {
+                    const uint8_t* t = src + s.toff[i];
+                    for (int q = 0; q < l; q++) dst[at + q] = (TC)t[q];
+                }
+                sync();
+                if (i < n) s.toff[i] = at;
+                carry += (uint32_t)wave_last(incl);
+            }
+            __threadfence_block();
+            sync();
+            if (lane == 0) {
+                s.text_half = s.text_half ^ 1u;
+                s.text_top = carry;
+                s.wide = s.wide | MT_WIDE_DOC | MT_WIDE_LDS;
+            }
+            sync();
+            arena = dst;
+        }
     }
 
     MT_DEV void store(const mt_gstate& g, uint32_t d) {
@@ -1648,6 +1806,16 @@ struct Wave {
             sc.text_half = s.text_half;
             sc.n_empty = (uint32_t)nempty;
             if (g.evn) g.evn[d] = (uint32_t)s.evn;
+            if (W) sc.wide = s.wide;
+        }
+        if constexpr (W) {
+            for (int i = lane; i < nn; i += 64) {
+                const int sl = s.order[i];
+                g.ovx[so + i] = s.ovx[sl];
+                g.ph[so + i] = s.ph[sl];
+                g.pxl[so + i] = s.pxl[sl];
+                g.pxh[so + i] = s.pxh[sl];
+            }
         }
         if constexpr (LOC) {
             if (s.lc.own >= 0) {
@@ -1704,6 +1872,13 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     if (a >= b) return;
     if (LOC) {  // the editing form has one capacity: a document that could outgrow it halts
         const mt_doc_scalars& sc = g.sc[d];
+        if (sc.wide & MT_WIDE_DOC) {  // (and no wide state: a wide document cannot take local edits)
+            if (threadIdx.x == 0 && !sc.err) {
+                g.sc[d].err = MT_DERR_LIMITS;
+                g.sc[d].err_seq = ops[a].seq;
+            }
+            return;
+        }
         const int nops = (int)(b - a);
         int ib_need = 0;
         for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
@@ -1760,7 +1935,8 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
 // Documents above 2048 segments: the same engine with the document's structure in a per-wave
 // HBM workspace (ws + w * sizeof(Lds<CAP>)) instead of LDS.  Latency-bound like the LDS form but
 // without its 160 KiB-per-CU ceiling; such documents are rare, so a handful of waves serve them.
-template <int CAP>
+// W: wide documents (include/mtgpu.h "limits"), every capacity class from 2048 segments up.
+template <int CAP, bool W = false>
 __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                      const uint8_t* __restrict__ payload,
                                                      const uint32_t* __restrict__ row_ptr,
@@ -1769,9 +1945,10 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
-    Lds<CAP>& st = *reinterpret_cast<Lds<CAP>*>(ws + (size_t)w * sizeof(Lds<CAP>));
-    Wave<CAP, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap, g.ev ? g.ev + (size_t)d * g.evcap : nullptr,
-                       g.evcap);
+    using LS = Lds<CAP, false, W>;
+    LS& st = *reinterpret_cast<LS*>(ws + (size_t)w * sizeof(LS));
+    Wave<CAP, true, false, W> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
+                                 g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -1853,6 +2030,39 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
             return hipErrorInvalidValue;
     }
 #undef MT_LAUNCH_BIG
+}
+
+// wide documents (mt_bin_kernel's wide buckets; workspace: n_docs * mt_lds_bytes_wide(cap_class))
+extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
+                                           hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    dim3 grid(n_docs), block(64);
+#define MT_LAUNCH_WIDE(CAPV)                                                                                 \
+    case CAPV:                                                                                               \
+        hipLaunchKernelGGL((mt::apply_kernel_g<CAPV, true>), grid, block, 0, stream, *g, ops, payload, row_ptr, \
+                           doc_ids, n_docs, op_lo, op_cnt, ws);                                              \
+        return hipGetLastError();
+    switch (cap_class) {
+        MT_LAUNCH_WIDE(2048)
+        MT_LAUNCH_WIDE(4096)
+        MT_LAUNCH_WIDE(8192)
+        MT_LAUNCH_WIDE(16384)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef MT_LAUNCH_WIDE
+}
+
+extern "C" size_t mt_lds_bytes_wide(int cap_class) {
+    switch (cap_class) {
+        case 2048: return sizeof(mt::Lds<2048, false, true>);
+        case 4096: return sizeof(mt::Lds<4096, false, true>);
+        case 8192: return sizeof(mt::Lds<8192, false, true>);
+        case 16384: return sizeof(mt::Lds<16384, false, true>);
+        default: return 0;
+    }
 }
 
 // documents with an editing client (mt_bin_kernel's last bucket): the LDS engine's editing form

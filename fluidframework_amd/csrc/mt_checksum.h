@@ -4,8 +4,11 @@
 #pragma once
 #include <stdint.h>
 #include "mt_synth.h"  // mt_mix64, MT_HD
+#include "mt_state.h"
 
-MT_HD static inline uint64_t mt_fnv1a_step(uint64_t h, uint8_t c) { return (h ^ c) * 0x100000001B3ull; }
+// fnv1a over the text's UTF-16 code units (h ^= unit): for text up to U+00FF it is the fnv1a of
+// the Latin-1 bytes, so narrow and wide documents of the same state hash alike
+MT_HD static inline uint64_t mt_fnv1a_step(uint64_t h, uint32_t c) { return (h ^ c) * 0x100000001B3ull; }
 #define MT_FNV_INIT 0xCBF29CE484222325ull
 // a Marker's "text hash": the fnv1a of its one ReferenceType byte, xor this tag
 #define MT_MARKER_TAG 0x4D41524B45520000ull
@@ -21,6 +24,18 @@ MT_HD static inline uint64_t mt_seg_hash(uint64_t idx, uint64_t text_hash, int32
     h = mt_mix64(h ^ props_lo ^ ((uint64_t)props_defined << 63));
     return h;
 }
+// The overlap term: the ids < 64 as a bitmask; a wide document's ids >= 64 (ovx: ascending from the
+// low byte, 0 = none) hashed in.  The props term: the low bytes of the value ids of keys 0..7 (the
+// narrow u64); a wide document's high bytes (hi) and keys 8..15 (xlo, xhi) hashed in.  Both are the
+// narrow word itself whenever the wide part is empty.
+MT_HD static inline uint64_t mt_ovl_term(uint64_t mask, uint64_t ovx) {
+    return ovx ? mask ^ mt_mix64(ovx ^ 0x4F56584944530000ull) : mask;
+}
+MT_HD static inline uint64_t mt_props_term(uint64_t lo, uint64_t hi, uint64_t xlo, uint64_t xhi) {
+    if (!(hi | xlo | xhi)) return lo;
+    return lo ^ mt_mix64(mt_mix64(hi ^ 0x1111111111111111ull) ^ mt_mix64(xlo ^ 0x2222222222222222ull) ^
+                         mt_mix64(xhi ^ 0x3333333333333333ull));
+}
 // canonical client id of a stored short id: NonCollabClient (snapshot loads) is -2
 MT_HD static inline int32_t mt_canon_client(uint32_t c) { return c == 0xFEu ? -2 : (int32_t)c; }
 MT_HD static inline uint64_t mt_tree_term(uint64_t count, uint64_t b, uint64_t depth) {
@@ -31,4 +46,34 @@ MT_HD static inline uint64_t mt_finish_checksum(uint64_t seg_sum, uint64_t tree_
     uint64_t s = mt_mix64(seg_sum) ^ mt_mix64(tree_sum ^ 0x5851F42D4C957F2Dull);
     s ^= mt_mix64((uint64_t)(uint32_t)cur_seq | ((uint64_t)(uint32_t)min_seq << 32));
     return mt_mix64(s ^ nsegs);
+}
+
+// ---- readers of a document's HBM state, narrow or wide (mt_state.h) ------------------------------
+// segment at HBM index i (= doc * segcap + position): value id of key k
+MT_HD static inline uint32_t mt_gprop(const mt_gstate& g, bool wide, size_t i, int k) {
+    const int sh = 8 * (k & 7);
+    if (!wide) return k < 8 ? (uint32_t)((g.props[i] >> sh) & 0xFFu) : 0u;
+    const uint64_t lo = k < 8 ? g.props[i] : g.pxl[i], hi = k < 8 ? g.ph[i] : g.pxh[i];
+    return (uint32_t)((lo >> sh) & 0xFFu) | ((uint32_t)((hi >> sh) & 0xFFu) << 8);
+}
+// matchProperties' value comparison of two segments (properties.ts:62-93)
+MT_HD static inline bool mt_gprops_eq(const mt_gstate& g, bool wide, size_t a, size_t b) {
+    if (g.props[a] != g.props[b]) return false;
+    return !wide || (g.ph[a] == g.ph[b] && g.pxl[a] == g.pxl[b] && g.pxh[a] == g.pxh[b]);
+}
+MT_HD static inline uint64_t mt_gprops_term(const mt_gstate& g, bool wide, size_t i) {
+    return wide ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i]) : g.props[i];
+}
+MT_HD static inline uint64_t mt_govl_term(const mt_gstate& g, bool wide, size_t i) {
+    return wide ? mt_ovl_term(g.ovl[i], g.ovx[i]) : g.ovl[i];
+}
+// a wide document's overlap list (ascending bytes, 0 = none) holds client c
+MT_HD static inline bool mt_ovx_has(uint64_t x, uint32_t c) {
+    const uint64_t t = x ^ (0x0101010101010101ull * (uint64_t)(c & 0xFFu));
+    return ((t - 0x0101010101010101ull) & ~t & 0x8080808080808080ull) != 0;
+}
+// code unit q of the text at arena unit offset `off` of document d (its current half)
+MT_HD static inline uint32_t mt_gtext(const mt_gstate& g, uint32_t d, const mt_doc_scalars& sc, uint32_t off) {
+    const uint8_t* a = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    return (sc.wide & MT_WIDE_DOC) ? (uint32_t)reinterpret_cast<const uint16_t*>(a)[off] : (uint32_t)a[off];
 }

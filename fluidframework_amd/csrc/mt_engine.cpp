@@ -34,14 +34,19 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
                                           hipStream_t stream);
+extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
+                                           hipStream_t stream);
+extern "C" size_t mt_lds_bytes_wide(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
                                      const mt_load_seg* segs, const uint8_t* text, const int32_t* min_seq,
                                      const int32_t* cur_seq, hipStream_t st);
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
-                                    uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
-                                    hipStream_t st);
+                                    int first_wide, uint32_t* counts, uint32_t* ids, const mt_op_rec* ops,
+                                    unsigned long long* acc, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
 extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* q, uint32_t n, uint32_t cap,
                                        mt_stack_item* items, uint32_t* depth, hipStream_t st);
@@ -69,6 +74,11 @@ constexpr int kNumClasses = 19;
 constexpr int kLdsClasses = 16;  // classes an LDS-resident kernel serves (the generator's)
 constexpr int kFirstLds = 15;    // index of the 2048 class: the first the register engine does not serve
 constexpr int kMaxSegCap = 16384;
+// bins of a tick (mt_bin_kernel): the classes, the editing documents, and the wide documents of the
+// classes from 2048 up (the LDS engine's wide form, include/mtgpu.h "limits")
+constexpr int kFirstWide = kFirstLds;
+constexpr int kWideClasses = kNumClasses - kFirstWide;
+constexpr int kBuckets = kNumClasses + 1 + kWideClasses;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -87,6 +97,7 @@ struct mt_batch {
     uint64_t n_ops = 0, payload_bytes = 0;
     uint32_t n_docs = 0;
     uint32_t max_ops_per_doc = 0;
+    bool wide = false;  // some record needs the wide form (its documents' wide state is allocated first)
 };
 
 struct mt_engine {
@@ -154,9 +165,41 @@ static mt_status dalloc(mt_engine* e, T** p, size_t count) {
     return MT_OK;
 }
 
+// The wide documents' extra per-segment state (mt_state.h), allocated for every document the first
+// time an engine sees wide content (a wide record or snapshot segment)
+static mt_status ensure_wide(mt_engine* e) {
+    if (e->g.ovx) return MT_OK;
+    const size_t S = (size_t)e->cfg.max_docs * e->g.segcap;
+    mt_gstate& g = e->g;
+    mt_status st = MT_OK;
+    if ((st = dalloc(e, &g.ph, S)) || (st = dalloc(e, &g.pxl, S)) || (st = dalloc(e, &g.pxh, S)) ||
+        (st = dalloc(e, &g.ovx, S))) {
+        g.ovx = nullptr;  // (the kernels test ovx; the others are freed with the engine)
+        return st;
+    }
+    return MT_OK;
+}
+// a record beyond the narrow limits (include/mtgpu.h "limits")
+static bool wide_rec(const mt_op_rec& o) {
+    if (o.type & MT_OP_WIDE) return true;
+    if (MT_OP_TYPE(o) == MT_OP_LOAD) {
+        const uint32_t c0 = o.client & 0xFFu, c1 = o.client >> 8;
+        return (c0 != MT_CLIENT_NONCOLLAB && c0 >= MT_MAX_CLIENTS) || (o.pos2 >= 0 && c1 >= MT_MAX_CLIENTS);
+    }
+    return !MT_OP_IS_NOOP(o) && o.client >= MT_MAX_CLIENTS;
+}
+static bool wide_load_seg(const mt_load_seg& sg) {
+    if ((sg.flags & MT_LSF_U16) || (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) ||
+        (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS))
+        return true;
+    for (int k = 0; k < 16; k++)
+        if ((sg.flags & MT_SF_PDEF) && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255)) return true;
+    return false;
+}
+
 extern "C" {
 
-const char* mt_version(void) { return "libmtgpu 0.1 (gfx950)"; }
+const char* mt_version(void) { return "libmtgpu 0.2 (gfx950)"; }
 
 mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     if (!cfg || !out || cfg->max_docs == 0) return MT_ERR_ARG;
@@ -192,14 +235,14 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.ct, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
         (st = dalloc(e, &g.lsq, D * MT_LOC_CAP)) || (st = dalloc(e, &g.rg, D * MT_RG_RECS)) ||
         (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) ||
-        // (+1: the editing documents' bucket after the capacity classes)
-        (st = dalloc(e, &e->d_counts, kNumClasses + 1)) || (st = dalloc(e, &e->d_acc, kNumClasses + 1)) ||
-        (st = dalloc(e, &e->d_ids, D * (kNumClasses + 1)))) {
+        // (the editing documents' and the wide documents' buckets after the capacity classes)
+        (st = dalloc(e, &e->d_counts, kBuckets)) || (st = dalloc(e, &e->d_acc, kBuckets)) ||
+        (st = dalloc(e, &e->d_ids, D * kBuckets))) {
         mt_engine_destroy(e);
         return st;
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&e->h_counts, (kNumClasses + 1) * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_counts, kBuckets * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_ERR_HIP;
@@ -274,7 +317,7 @@ mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
 mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const uint32_t* seg_row_ptr,
                        const mt_load_seg* segs, const uint8_t* text, uint64_t text_bytes, const int32_t* min_seq,
                        const int32_t* cur_seq) {
-    static_assert(sizeof(mt_load_seg) == 32, "mt_load_seg is 32 bytes");
+    static_assert(sizeof(mt_load_seg) == 64, "mt_load_seg is 64 bytes");
     if (!e || (n && (!doc_ids || !seg_row_ptr || !min_seq || !cur_seq))) return MT_ERR_ARG;
     if (n == 0) return MT_OK;
     const uint64_t n_segs = seg_row_ptr[n] - seg_row_ptr[0];
@@ -283,13 +326,20 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
         if (doc_ids[i] >= e->n_docs || seg_row_ptr[i + 1] < seg_row_ptr[i]) return MT_ERR_ARG;
         if (!(min_seq[i] <= cur_seq[i])) return MT_ERR_ARG;
     }
+    bool wide = false;
     for (uint64_t k = 0; k < n_segs; k++) {  // every text range inside `text`, ids in range
         const mt_load_seg& sg = segs[seg_row_ptr[0] + k];
-        if ((uint64_t)sg.text_off + sg.text_len > text_bytes) return MT_ERR_ARG;
-        if (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) return MT_ERR_ARG;
-        if (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS) return MT_ERR_ARG;
+        const uint64_t tb = (uint64_t)sg.text_len * ((sg.flags & MT_LSF_U16) ? 2u : 1u);
+        if ((uint64_t)sg.text_off + tb > text_bytes) return MT_ERR_ARG;
+        if (sg.client >= MT_MAX_CLIENTS_WIDE && sg.client != MT_CLIENT_NONCOLLAB) return MT_ERR_ARG;
+        if (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS_WIDE) return MT_ERR_ARG;
+        wide = wide || wide_load_seg(sg);
     }
     HIP_OK(hipSetDevice(e->cfg.device));
+    if (wide) {
+        const mt_status ws = ensure_wide(e);
+        if (ws) return ws;
+    }
     e->gen++;
     // one staging allocation: ids, rebased row pointers, windows, segments, text
     std::vector<uint32_t> rp(n + 1);
@@ -385,7 +435,7 @@ mt_status mt_range_stacks(mt_engine* e, const mt_tile_query* q, uint32_t n, uint
 }
 
 mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
-    static_assert(sizeof(mt_event) == 32, "mt_event is 32 bytes");
+    static_assert(sizeof(mt_event) == 64, "mt_event is 64 bytes");
     if (!e) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     HIP_OK(hipStreamSynchronize(e->stream));
@@ -491,6 +541,7 @@ mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, co
         delete b;
         return MT_ERR_ARG;
     }
+    for (uint64_t i = 0; i < n_ops && !b->wide; i++) b->wide = wide_rec(ops[i]);
     if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
         hipMalloc(&b->payload, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||
         hipMalloc(&b->row_ptr, (b->n_docs + 1) * sizeof(uint32_t)) != hipSuccess) {
@@ -521,27 +572,36 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     if (!e || !b || b->n_docs != e->n_docs) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     e->gen++;
+    if (b->wide) {
+        const mt_status ws = ensure_wide(e);
+        if (ws) return ws;
+    }
     const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     e->last_launches = 0;
     uint32_t nk = 0;
-    HIP_OK(hipMemsetAsync(e->d_acc, 0, (kNumClasses + 1) * sizeof(unsigned long long), e->stream));
+    HIP_OK(hipMemsetAsync(e->d_acc, 0, kBuckets * sizeof(unsigned long long), e->stream));
     e->kev_cls.clear();
     HIP_OK(hipEventRecord(e->ev0, e->stream));
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
-        HIP_OK(hipMemsetAsync(e->d_counts, 0, (kNumClasses + 1) * sizeof(uint32_t), e->stream));
+        HIP_OK(hipMemsetAsync(e->d_counts, 0, kBuckets * sizeof(uint32_t), e->stream));
         HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, e->n_classes, e->first_lds,
-                             e->d_counts, e->d_ids, b->ops, e->d_acc, e->stream));
-        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, (kNumClasses + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             kFirstWide, e->d_counts, e->d_ids, b->ops, e->d_acc, e->stream));
+        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kBuckets * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
         // the classes above 2048 segments keep each document's structure in an HBM workspace
         // (one region per class: their kernels may run concurrently)
-        size_t ws_off[kNumClasses] = {}, need = 0;
+        // (the wide documents' form keeps its structure in the workspace at every class)
+        size_t ws_off[kNumClasses] = {}, wws_off[kNumClasses] = {}, need = 0;
         for (int c = kLdsClasses; c < e->n_classes; c++) {
             ws_off[c] = need;
             need += (size_t)e->h_counts[c] * mt_lds_bytes(kClasses[c]);
+        }
+        for (int c = kFirstWide; c < e->n_classes; c++) {
+            wws_off[c] = need;
+            need += (size_t)e->h_counts[e->n_classes + 1 + (c - kFirstWide)] * mt_lds_bytes_wide(kClasses[c]);
         }
         if (need > e->ws_bytes) {
             HIP_OK(hipDeviceSynchronize());
@@ -590,6 +650,23 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         if (const uint32_t cnt = e->h_counts[e->n_classes])
             HIP_OK(mt_launch_apply_loc(&e->g, b->ops, b->payload, b->row_ptr, e->d_ids + (size_t)e->n_classes * b->n_docs,
                                        cnt, lo, per, e->stream));
+        // wide documents: the LDS engine's wide form, per class
+        for (int c = kFirstWide; c < e->n_classes; c++) {
+            const int k = e->n_classes + 1 + (c - kFirstWide);
+            const uint32_t cnt = e->h_counts[k];
+            if (!cnt) continue;
+            while (e->kev.size() < 2 * (nk + 1)) {
+                hipEvent_t ev;
+                HIP_OK(hipEventCreate(&ev));
+                e->kev.push_back(ev);
+            }
+            HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
+            HIP_OK(mt_launch_apply_wide(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                        e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], e->stream));
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
+            e->kev_cls.push_back(c);
+            nk++;
+        }
     }
     HIP_OK(mt_launch_fixup(&e->g, b->ops, b->n_docs, e->stream));  // error precedence, see mt_service.hip
     HIP_OK(hipEventRecord(e->ev1, e->stream));
@@ -607,8 +684,9 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         e->cls_launches[e->kev_cls[k]]++;
     }
     HIP_OK(hipEventElapsedTime(&e->last_wall_ms, e->ev0, e->ev1));
-    unsigned long long acc[kNumClasses];
+    unsigned long long acc[kBuckets];
     HIP_OK(hipMemcpy(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost));
+    for (int c = kFirstWide; c < e->n_classes; c++) acc[c] += acc[e->n_classes + 1 + (c - kFirstWide)];
     e->last_ms = kms;
     e->last_launches = nk;
     e->last_bytes = 0;
@@ -661,10 +739,10 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
     if (r == hipSuccess) r = hipMemsetAsync(pay_used, 0, (size_t)n * sizeof(uint32_t), e->stream);
     const uint32_t tick = 64;
     for (uint32_t lo = 0; r == hipSuccess && lo < per; lo += tick) {
-        r = hipMemsetAsync(e->d_counts, 0, (kNumClasses + 1) * sizeof(uint32_t), e->stream);
+        r = hipMemsetAsync(e->d_counts, 0, kBuckets * sizeof(uint32_t), e->stream);
         if (r == hipSuccess)
             r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, std::min(e->n_classes, kLdsClasses), 0,
-                              e->d_counts, e->d_ids, nullptr, nullptr, e->stream);
+                              kFirstWide, e->d_counts, e->d_ids, nullptr, nullptr, e->stream);
         if (r == hipSuccess)
             r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                e->stream);
@@ -853,13 +931,33 @@ mt_status mt_doc_error(mt_engine* e, uint32_t doc, int32_t* code, int32_t* seq) 
 
 // ------------------------------------------------------------------- canonical readout
 namespace {
+// A document's state on the host, narrow or wide (mt_state.h): text as UTF-16 code units, props as
+// a value id per key, overlap as a sorted client list
 struct HostDoc {
     mt_doc_scalars sc;
+    bool wide = false;
     std::vector<int32_t> seq, rseq;
     std::vector<uint32_t> len, toff;
-    std::vector<uint64_t> ovl, props;
-    std::vector<uint8_t> client, rclient, flags, text;
+    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
+    std::vector<uint8_t> client, rclient, flags;
+    std::vector<uint16_t> text;                // the arena's current half, in code units
     std::vector<std::vector<uint8_t>> levels;  // per level child counts (level 0 = leaf blocks)
+    uint32_t prop(int i, int k) const {
+        const int sh = 8 * (k & 7);
+        if (!wide) return k < 8 ? (uint32_t)((props[i] >> sh) & 0xFF) : 0u;
+        const uint64_t lo = k < 8 ? props[i] : pxl[i], hi = k < 8 ? ph[i] : pxh[i];
+        return (uint32_t)((lo >> sh) & 0xFF) | ((uint32_t)((hi >> sh) & 0xFF) << 8);
+    }
+    std::vector<int> overlap(int i) const {
+        std::vector<int> v;
+        for (int c = 0; c < 64; c++)
+            if ((ovl[i] >> c) & 1) v.push_back(c);
+        if (wide)
+            for (int b = 0; b < 8; b++)
+                if (const int c = (int)((ovx[i] >> (8 * b)) & 0xFF)) v.push_back(c);
+        return v;
+    }
+    const uint16_t* units(int i) const { return text.data() + toff[i]; }
 };
 
 template <class T>
@@ -869,10 +967,29 @@ hipError_t fetch(std::vector<T>& v, const T* base, size_t off, size_t n, hipStre
     return hipMemcpyAsync(v.data(), base + off, n * sizeof(T), hipMemcpyDeviceToHost, st);
 }
 
+// the current arena half of document d as code units (a narrow document's bytes widened)
+mt_status fetch_text(mt_engine* e, uint32_t d, const mt_doc_scalars& sc, std::vector<uint16_t>& out) {
+    const mt_gstate& g = e->g;
+    const size_t base = ((size_t)d * 2 + sc.text_half) * g.textcap;
+    if (sc.wide & MT_WIDE_DOC) {
+        out.resize(sc.text_top);
+        if (sc.text_top)
+            HIP_OK(hipMemcpyAsync(out.data(), g.text + base, (size_t)sc.text_top * 2, hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        return MT_OK;
+    }
+    std::vector<uint8_t> b;
+    HIP_OK(fetch(b, g.text, base, sc.text_top, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    out.assign(b.begin(), b.end());
+    return MT_OK;
+}
+
 mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
     const mt_gstate& g = e->g;
     HIP_OK(hipMemcpyAsync(&h.sc, g.sc + d, sizeof h.sc, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
+    h.wide = (h.sc.wide & MT_WIDE_DOC) != 0 && g.ovx;
     const size_t so = (size_t)d * g.segcap, n = (size_t)h.sc.nseg;
     HIP_OK(fetch(h.seq, g.seq, so, n, e->stream));
     HIP_OK(fetch(h.rseq, g.rseq, so, n, e->stream));
@@ -880,32 +997,47 @@ mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
     HIP_OK(fetch(h.toff, g.toff, so, n, e->stream));
     HIP_OK(fetch(h.ovl, g.ovl, so, n, e->stream));
     HIP_OK(fetch(h.props, g.props, so, n, e->stream));
+    if (h.wide) {
+        HIP_OK(fetch(h.ovx, g.ovx, so, n, e->stream));
+        HIP_OK(fetch(h.ph, g.ph, so, n, e->stream));
+        HIP_OK(fetch(h.pxl, g.pxl, so, n, e->stream));
+        HIP_OK(fetch(h.pxh, g.pxh, so, n, e->stream));
+    }
     HIP_OK(fetch(h.client, g.client, so, n, e->stream));
     HIP_OK(fetch(h.rclient, g.rclient, so, n, e->stream));
     HIP_OK(fetch(h.flags, g.flags, so, n, e->stream));
-    HIP_OK(fetch(h.text, g.text, ((size_t)d * 2 + h.sc.text_half) * g.textcap, h.sc.text_top, e->stream));
     h.levels.resize(h.sc.nlev);
     for (int L = 0; L < h.sc.nlev; L++) {
         if (L == 0) HIP_OK(fetch(h.levels[0], g.lbcnt, (size_t)d * g.lbcap, h.sc.nb[0], e->stream));
         else HIP_OK(fetch(h.levels[L], g.ibcnt, ((size_t)d * (MT_MAXLEV - 1) + (L - 1)) * g.ibcap, h.sc.nb[L], e->stream));
     }
     HIP_OK(hipStreamSynchronize(e->stream));
-    return MT_OK;
+    return fetch_text(e, d, h.sc, h.text);
 }
 
-void json_str(std::string& o, const uint8_t* p, size_t n) {
+// A JSON string of UTF-16 code units, ASCII only: printable ASCII as itself, \" \\ and the short
+// forms JSON.stringify uses (ECMA-262 QuoteJSONString), every other unit -- non-ASCII and surrogate
+// halves included -- as \uXXXX.  It parses to the same string the reference's JSON holds.
+void json_units(std::string& o, const uint16_t* p, size_t n) {
     o += '"';
     for (size_t i = 0; i < n; i++) {
-        unsigned char c = p[i];
-        if (c == '"' || c == '\\') {
-            o += '\\';
-            o += (char)c;
-        } else if (c < 0x20) {
-            char buf[8];
-            snprintf(buf, sizeof buf, "\\u%04x", c);
-            o += buf;
-        } else {
-            o += (char)c;
+        const unsigned c = p[i];
+        switch (c) {
+            case '"': o += "\\\""; break;
+            case '\\': o += "\\\\"; break;
+            case '\b': o += "\\b"; break;
+            case '\t': o += "\\t"; break;
+            case '\n': o += "\\n"; break;
+            case '\f': o += "\\f"; break;
+            case '\r': o += "\\r"; break;
+            default:
+                if (c < 0x20 || c >= 0x7F) {
+                    char buf[8];
+                    snprintf(buf, sizeof buf, "\\u%04x", c);
+                    o += buf;
+                } else {
+                    o += (char)c;
+                }
         }
     }
     o += '"';
@@ -917,27 +1049,26 @@ std::string state_json(const HostDoc& h) {
         if (i) o += ',';
         o += '[';
         if (h.flags[i] & MT_SF_MARKER)  // a Marker: {"marker": refType}
-            o += "{\"marker\":" + std::to_string(h.text[h.toff[i]]) + "}";
+            o += "{\"marker\":" + std::to_string(h.units(i)[0]) + "}";
         else
-            json_str(o, h.text.data() + h.toff[i], h.len[i]);
+            json_units(o, h.units(i), h.len[i]);
         const bool rm = h.flags[i] & MT_SF_REMOVED;
         o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(mt_canon_client(h.client[i])) + ',';
         o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient[i]) : "-1") + ",[";
         bool f = true;
-        for (int c = 0; c < 64; c++)
-            if ((h.ovl[i] >> c) & 1) {
-                if (!f) o += ',';
-                f = false;
-                o += std::to_string(c);
-            }
+        for (int c : h.overlap(i)) {
+            if (!f) o += ',';
+            f = false;
+            o += std::to_string(c);
+        }
         o += "],";
         if (!(h.flags[i] & MT_SF_PDEF)) {
             o += "null";
         } else {
             o += '{';
             bool f2 = true;
-            for (int k = 0; k < MT_MAX_KEYS; k++) {
-                const unsigned v = (unsigned)((h.props[i] >> (8 * k)) & 0xFF);
+            for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) {
+                const unsigned v = h.prop(i, k);
                 if (!v) continue;
                 if (!f2) o += ',';
                 f2 = false;
@@ -962,40 +1093,12 @@ std::string state_json(const HostDoc& h) {
     return o;
 }
 
-
-// JSON.stringify's string escaping (ECMA-262 QuoteJSONString): \b \t \n \f \r short forms,
-// other control characters as \u00xx
-void js_str(std::string& o, const uint8_t* p, size_t n) {
-    o += '"';
-    for (size_t i = 0; i < n; i++) {
-        const unsigned char c = p[i];
-        switch (c) {
-            case '"': o += "\\\""; break;
-            case '\\': o += "\\\\"; break;
-            case '\b': o += "\\b"; break;
-            case '\t': o += "\\t"; break;
-            case '\n': o += "\\n"; break;
-            case '\f': o += "\\f"; break;
-            case '\r': o += "\\r"; break;
-            default:
-                if (c < 0x20) {
-                    char buf[8];
-                    snprintf(buf, sizeof buf, "\\u%04x", c);
-                    o += buf;
-                } else {
-                    o += (char)c;
-                }
-        }
-    }
-    o += '"';
-}
-
 // props as the reference's map: keys "k<id>" (interned key ids), values = interned value ids
-void props_json(std::string& o, uint64_t props) {
+void props_json(std::string& o, const HostDoc& h, int i) {
     o += '{';
     bool first = true;
-    for (int k = 0; k < MT_MAX_KEYS; k++) {
-        const unsigned v = (unsigned)((props >> (8 * k)) & 0xFF);
+    for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) {
+        const unsigned v = h.prop(i, k);
         if (!v) continue;
         if (!first) o += ',';
         first = false;
@@ -1006,22 +1109,22 @@ void props_json(std::string& o, uint64_t props) {
 
 // TextSegment.toJSONObject (textSegment.ts:47-53) of `text` with the props of segment i;
 // Marker.toJSONObject (mergeTree.ts:652-656) for a marker: {marker: {refType}, props?}
-void seg_json(std::string& o, const HostDoc& h, int i, const std::string& text) {
+void seg_json(std::string& o, const HostDoc& h, int i, const std::vector<uint16_t>& text) {
     if (h.flags[i] & MT_SF_MARKER) {
-        o += "{\"marker\":{\"refType\":" + std::to_string(h.text[h.toff[i]]) + "}";
+        o += "{\"marker\":{\"refType\":" + std::to_string(h.units(i)[0]) + "}";
         if (h.flags[i] & MT_SF_PDEF) {
             o += ",\"props\":";
-            props_json(o, h.props[i]);
+            props_json(o, h, i);
         }
         o += '}';
     } else if (h.flags[i] & MT_SF_PDEF) {
         o += "{\"text\":";
-        js_str(o, (const uint8_t*)text.data(), text.size());
+        json_units(o, text.data(), text.size());
         o += ",\"props\":";
-        props_json(o, h.props[i]);
+        props_json(o, h, i);
         o += '}';
     } else {
-        js_str(o, (const uint8_t*)text.data(), text.size());
+        json_units(o, text.data(), text.size());
     }
 }
 
@@ -1041,11 +1144,11 @@ std::string snapshot_json(const HostDoc& h, const std::vector<uint32_t>& sp, uin
         const int pos = (int)sp[3 * k];
         const int cnt = (int)(sp[3 * k + 1] >> 1);
         const bool meta = sp[3 * k + 1] & 1u;
-        std::string text;
+        std::vector<uint16_t> text;
         for (int i = pos; i < pos + cnt; i++) {
             // elided inside the run: removed at or below the MSN, or a pending local insert / removal
             if (h.seq[i] == -1 || ((h.flags[i] & MT_SF_REMOVED) && h.rseq[i] <= h.sc.min_seq)) continue;
-            text.append((const char*)h.text.data() + h.toff[i], h.len[i]);
+            text.insert(text.end(), h.units(i), h.units(i) + h.len[i]);
         }
         lens[k] = sp[3 * k + 2];
         std::string& o = specs[k];
@@ -1107,27 +1210,35 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
     const size_t S = (size_t)n * g.segcap, so = (size_t)d0 * g.segcap;
     std::vector<int32_t> seq, rseq;
     std::vector<uint32_t> len, toff;
-    std::vector<uint64_t> ovl, props;
+    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
     std::vector<uint8_t> client, rclient, flags, lb, ib;
+    bool any_wide = false;
+    for (uint32_t i = 0; i < n; i++) any_wide = any_wide || ((sc[i].wide & MT_WIDE_DOC) && g.ovx);
     HIP_OK(fetch(seq, g.seq, so, S, e->stream));
     HIP_OK(fetch(rseq, g.rseq, so, S, e->stream));
     HIP_OK(fetch(len, g.len, so, S, e->stream));
     HIP_OK(fetch(toff, g.toff, so, S, e->stream));
     HIP_OK(fetch(ovl, g.ovl, so, S, e->stream));
     HIP_OK(fetch(props, g.props, so, S, e->stream));
+    if (any_wide) {
+        HIP_OK(fetch(ovx, g.ovx, so, S, e->stream));
+        HIP_OK(fetch(ph, g.ph, so, S, e->stream));
+        HIP_OK(fetch(pxl, g.pxl, so, S, e->stream));
+        HIP_OK(fetch(pxh, g.pxh, so, S, e->stream));
+    }
     HIP_OK(fetch(client, g.client, so, S, e->stream));
     HIP_OK(fetch(rclient, g.rclient, so, S, e->stream));
     HIP_OK(fetch(flags, g.flags, so, S, e->stream));
     HIP_OK(fetch(lb, g.lbcnt, (size_t)d0 * g.lbcap, (size_t)n * g.lbcap, e->stream));
     HIP_OK(fetch(ib, g.ibcnt, (size_t)d0 * (MT_MAXLEV - 1) * g.ibcap, (size_t)n * (MT_MAXLEV - 1) * g.ibcap, e->stream));
     out.assign(n, HostDoc());
-    for (uint32_t i = 0; i < n; i++) {
-        out[i].sc = sc[i];
-        HIP_OK(fetch(out[i].text, g.text, ((size_t)(d0 + i) * 2 + sc[i].text_half) * g.textcap, sc[i].text_top, e->stream));
-    }
     HIP_OK(hipStreamSynchronize(e->stream));
     for (uint32_t i = 0; i < n; i++) {
         HostDoc& h = out[i];
+        h.sc = sc[i];
+        h.wide = (sc[i].wide & MT_WIDE_DOC) && g.ovx;
+        mt_status st = fetch_text(e, d0 + i, sc[i], h.text);
+        if (st) return st;
         const size_t a = (size_t)i * g.segcap, m = (size_t)h.sc.nseg;
         h.seq.assign(seq.begin() + a, seq.begin() + a + m);
         h.rseq.assign(rseq.begin() + a, rseq.begin() + a + m);
@@ -1135,6 +1246,12 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
         h.toff.assign(toff.begin() + a, toff.begin() + a + m);
         h.ovl.assign(ovl.begin() + a, ovl.begin() + a + m);
         h.props.assign(props.begin() + a, props.begin() + a + m);
+        if (h.wide) {
+            h.ovx.assign(ovx.begin() + a, ovx.begin() + a + m);
+            h.ph.assign(ph.begin() + a, ph.begin() + a + m);
+            h.pxl.assign(pxl.begin() + a, pxl.begin() + a + m);
+            h.pxh.assign(pxh.begin() + a, pxh.begin() + a + m);
+        }
         h.client.assign(client.begin() + a, client.begin() + a + m);
         h.rclient.assign(rclient.begin() + a, rclient.begin() + a + m);
         h.flags.assign(flags.begin() + a, flags.begin() + a + m);
@@ -1302,10 +1419,13 @@ mt_status mt_get_text(mt_engine* e, uint32_t doc, char* buf, uint64_t cap, uint6
     HostDoc h;
     mt_status st = read_doc(e, doc, h);
     if (st) return st;
-    std::string t;
+    std::string t;  // UTF-16 code units, little endian
     for (int i = 0; i < h.sc.nseg; i++)
         if (!(h.flags[i] & (MT_SF_REMOVED | MT_SF_MARKER)))  // gatherText: text segments only
-            t.append((const char*)h.text.data() + h.toff[i], h.len[i]);
+            for (uint32_t q = 0; q < h.len[i]; q++) {
+                t += (char)(h.units(i)[q] & 0xFF);
+                t += (char)(h.units(i)[q] >> 8);
+            }
     return copy_out(t, buf, cap, len);
 }
 

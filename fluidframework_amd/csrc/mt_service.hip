@@ -64,8 +64,27 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
     if (ns > (int)g.segcap) err = MT_DERR_CAPACITY;
     const size_t so = (size_t)d * g.segcap;
     uint8_t* arena = g.text + (size_t)d * 2 * g.textcap;  // half 0
+    // a document with any segment beyond the narrow limits loads in the wide form (UTF-16 text,
+    // u16 value ids, keys < 16, client ids < 254; include/mtgpu.h "limits")
+    bool wdoc = false, lds = false;
+    for (int base = 0; base < ns; base += 64) {
+        const int i = base + lane;
+        bool w = false, l32 = false;
+        if (i < ns) {
+            const mt_load_seg& sg = segs[r0 + i];
+            const bool pdef = sg.flags & MT_SF_PDEF;
+            w = (sg.flags & MT_LSF_U16) || (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) ||
+                (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS);
+            for (int k = 0; k < 16; k++) w = w || (pdef && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255));
+            l32 = (sg.client > 32 && sg.client != MT_CLIENT_NONCOLLAB) || (sg.rseq >= 0 && sg.rclient > 32);
+        }
+        wdoc = wdoc || wave_ballot(w) != 0;
+        lds = lds || wave_ballot(l32) != 0;
+    }
+    if (wdoc && !g.ovx) err = MT_DERR_LIMITS;  // (the engine allocates the wide state before it loads)
+    const uint32_t ucap = wdoc ? g.textcap / 2 : g.textcap;  // code units per arena half
+    uint16_t* arena16 = reinterpret_cast<uint16_t*>(arena);
     uint32_t carry = 0;
-    bool wide = false;
     for (int base = 0; base < ns && !err; base += 64) {
         const int i = base + lane;
         mt_load_seg sg{};
@@ -74,30 +93,43 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
         const uint32_t incl = (uint32_t)wave_incl_scan((int)l);
         const uint32_t at = carry + incl - l;
         carry += (uint32_t)wave_last((int)incl);
-        if (carry > g.textcap) {
+        if (carry > ucap) {
             err = MT_DERR_TEXT_ARENA;
             break;
         }
-        wide = wide || __ballot(i < ns && ((sg.client > 32 && sg.client < MT_MAX_CLIENTS) ||
-                                           (sg.rseq >= 0 && sg.rclient > 32))) != 0;
         if (i < ns) {
+            const bool u16 = sg.flags & MT_LSF_U16;
+            const uint8_t* t = text + sg.text_off;
+            auto unit = [&](uint32_t q) -> uint32_t { return u16 ? (uint32_t)t[2 * q] | ((uint32_t)t[2 * q + 1] << 8) : t[q]; };
             bool nl = false;
             for (uint32_t q = 0; q < l; q++) {
-                const uint8_t c = text[sg.text_off + q];
-                arena[at + q] = c;
+                const uint32_t c = unit(q);
+                if (wdoc) arena16[at + q] = (uint16_t)c;
+                else arena[at + q] = (uint8_t)c;
                 nl = nl || c == '\n';
             }
             const bool rm = sg.rseq >= 0;
-            const bool mk = sg.flags & MT_SF_MARKER;  // a Marker spec: one byte, its ReferenceType
+            const bool mk = sg.flags & MT_SF_MARKER;  // a Marker spec: one unit, its ReferenceType
             uint8_t fl = (uint8_t)((rm ? MT_SF_REMOVED : 0u) | (sg.flags & (MT_SF_PDEF | MT_SF_MARKER)) |
                                    (nl && !mk ? MT_SF_HASNL : 0u));
-            if (!mk && l && text[sg.text_off + l - 1] == '\n') fl |= MT_SF_NL;
+            if (!mk && l && unit(l - 1) == '\n') fl |= MT_SF_NL;
+            uint64_t w4[4] = {0, 0, 0, 0};  // props as the narrow word + the wide words
+            for (int k = 0; k < 16; k++) {
+                w4[(k >> 3) * 2] |= (uint64_t)(sg.props[k] & 0xFFu) << (8 * (k & 7));
+                w4[(k >> 3) * 2 + 1] |= (uint64_t)(sg.props[k] >> 8) << (8 * (k & 7));
+            }
             g.seq[so + i] = sg.seq;
             g.rseq[so + i] = rm ? sg.rseq : 0;
             g.len[so + i] = l;
             g.toff[so + i] = at;
             g.ovl[so + i] = 0;  // removedClientOverlap is not part of a snapshot
-            g.props[so + i] = sg.props;
+            g.props[so + i] = w4[0];
+            if (wdoc) {
+                g.ovx[so + i] = 0;
+                g.ph[so + i] = w4[1];
+                g.pxl[so + i] = w4[2];
+                g.pxh[so + i] = w4[3];
+            }
             g.client[so + i] = sg.client;
             g.rclient[so + i] = rm ? sg.rclient : 0;
             g.flags[so + i] = fl;
@@ -133,7 +165,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             for (int L = 0; L < nlev; L++) sc.nb[L] = nb[L];
             sc.n_empty = ns == 0 ? 1u : 0u;
             sc.text_top = carry;
-            sc.wide = wide ? 1u : 0u;
+            sc.wide = (lds || wdoc ? MT_WIDE_LDS : 0u) | (wdoc ? MT_WIDE_DOC : 0u);
         }
         sc.cur_seq = cur_seq[w];
         sc.min_seq = min_seq[w];
@@ -147,11 +179,13 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // adds at most 2 segments (a boundary split + an insert, or two boundary splits), at most 2 leaf
 // blocks, and a handful of heap entries; the register engine also pads one slot per empty leaf
 // block.  classes[k] = {CAP, LB, IB, H}.  Documents that ever see a client id above 32 go to the
-// last class (the LDS engine, 64-client overlap sets).  Binning is wave-aggregated: one atomic
-// per (wave, class).
+// last class (the LDS engine, 64-client overlap sets).  Buckets: 0 .. n_classes-1 the capacity
+// classes, n_classes the editing documents, then one per class from first_wide on for the wide
+// documents (include/mtgpu.h "limits"; promoted here by their first wide op or client id >= 64).
+// Binning is wave-aggregated: one atomic per (wave, bucket).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
-                              uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
+                              int first_wide, uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
                               const mt_op_rec* __restrict__ ops, unsigned long long* __restrict__ acc) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     int c = -1;
@@ -173,8 +207,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 int32_t cur = sc.cur_seq, mn = sc.min_seq;
                 for (uint32_t i = a; i < b; i++) {
                     const mt_op_rec o = ops[i];
-                    if (o.type == MT_OP_LOAD) continue;  // snapshot body append: no window update
-                    if (o.type > MT_OP_LOAD) break;
+                    if (MT_OP_TYPE(o) == MT_OP_LOAD) continue;  // snapshot body append: no window update
+                    if (MT_OP_TYPE(o) > MT_OP_LOAD) break;
                     if (o.seq == -1) {
                         if (own < 0) own = o.client;
                         continue;
@@ -194,20 +228,25 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 }
             }
             bool wide = sc.wide != 0;
+            bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
             // snapshot body appends (MT_OP_LOAD, SnapshotLoader.loadBody) are applied by the LDS
             // engine only: the register engine's hot loop stays free of them
             bool lds_only = false;
             if (ops)
-                for (uint32_t i = a; i < b && !lds_only; i++) lds_only = ops[i].type == MT_OP_LOAD;
-            if (!wide && ops) {
+                for (uint32_t i = a; i < b && !lds_only; i++) lds_only = MT_OP_TYPE(ops[i]) == MT_OP_LOAD;
+            if ((!wide || !wdoc) && ops) {
                 for (uint32_t i = a; i < b; i++) {
-                    const uint32_t c = ops[i].client;
-                    wide = wide || (ops[i].type == MT_OP_LOAD
-                                        ? (((c & 0xFFu) > 32 && (c & 0xFFu) != MT_CLIENT_NONCOLLAB) ||
-                                           (ops[i].pos2 >= 0 && (c >> 8) > 32))
-                                        : c > 32);
+                    const mt_op_rec& o = ops[i];
+                    const uint32_t c = o.client;
+                    const bool load = MT_OP_TYPE(o) == MT_OP_LOAD;
+                    const uint32_t c0 = load ? (c & 0xFFu) : c, c1 = load ? (c >> 8) : 0u;
+                    const bool has0 = !load || c0 != MT_CLIENT_NONCOLLAB, has1 = load && o.pos2 >= 0;
+                    wide = wide || (has0 && c0 > 32) || (has1 && c1 > 32);
+                    wdoc = wdoc || (o.type & MT_OP_WIDE) ||
+                           (load ? ((has0 && c0 >= MT_MAX_CLIENTS) || (has1 && c1 >= MT_MAX_CLIENTS))
+                                 : (!MT_OP_IS_NOOP(o) && c >= MT_MAX_CLIENTS));
                 }
-                if (wide) g.sc[d].wide = 1u;
+                if (wide && !(sc.wide & MT_WIDE_LDS)) g.sc[d].wide = sc.wide | MT_WIDE_LDS;
             }
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
@@ -225,6 +264,27 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     break;
                 }
             }
+            if (wdoc && !editing) {
+                // the wide form, from the 2048 class up (the wide state is the engine's to allocate:
+                // without it the document halts)
+                if (!g.ovx) {
+                    g.sc[d].err = MT_DERR_LIMITS;
+                    g.sc[d].err_seq = ops ? ops[a].seq : 0;
+                    c = -1;
+                } else {
+                    c = n_classes - 1;
+                    for (int k = first_wide; k < n_classes; k++) {
+                        const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
+                                  h = classes[4 * k + 3];
+                        if (sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb &&
+                            ib_need + nops + 1 <= ib && sc.heap_n + 4 * nops + 16 <= h) {
+                            c = k;
+                            break;
+                        }
+                    }
+                    c = n_classes + 1 + (c - first_wide);
+                }
+            }
             if (editing) c = n_classes;  // the editing documents' bucket (mt_launch_apply_loc)
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
@@ -240,7 +300,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    for (int k = 0; k <= n_classes; k++) {
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0);
+    for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;
         const int leader = first_lane(m);
@@ -268,16 +329,16 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const mt_doc_scalars sc = g.sc[d];
     if (sc.win_op < 0 || (sc.err != MT_DERR_SEQ_ORDER && sc.err != MT_DERR_MSN_ORDER)) return;
     const mt_op_rec o = ops[sc.win_op];
-    const int np = MT_OP_NPAIRS(o.flags);
-    if (o.seq != sc.err_seq || o.type != MT_OP_INSERT || (int)o.payload_len - 2 * np <= 0) return;
+    if (o.seq != sc.err_seq || MT_OP_TYPE(o) != MT_OP_INSERT || o.payload_len <= MT_OP_PAIRS_LEN(o)) return;
     const size_t so = (size_t)d * g.segcap;
     const int32_t R = o.ref_seq;
     const uint32_t C = o.client;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     int64_t len = 0;
     for (int i = 0; i < sc.nseg; i++) {  // nodeLength leaf branch (mergeTree.ts:1667-1697)
         const bool seen = g.client[so + i] == C || g.seq[so + i] <= R;
-        const bool hid = (g.flags[so + i] & MT_SF_REMOVED) &&
-                         (g.rclient[so + i] == C || ((g.ovl[so + i] >> C) & 1ull) || g.rseq[so + i] <= R);
+        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0 : (wdoc && mt_ovx_has(g.ovx[so + i], C));
+        const bool hid = (g.flags[so + i] & MT_SF_REMOVED) && (g.rclient[so + i] == C || ov || g.rseq[so + i] <= R);
         if (seen && !hid) len += g.len[so + i];
     }
     if ((int64_t)o.pos1 > len) g.sc[d].err = MT_DERR_INSERT_FAILED;
@@ -290,18 +351,18 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
     const int lane = lane_id();
     const mt_doc_scalars sc = g.sc[d];
     const size_t so = (size_t)d * g.segcap;
-    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     uint64_t seg_sum = 0;
     for (int i = lane; i < sc.nseg; i += 64) {
         uint64_t h = MT_FNV_INIT;
         const uint32_t t0 = g.toff[so + i], tl = g.len[so + i];
-        for (uint32_t q = 0; q < tl; q++) h = mt_fnv1a_step(h, text[t0 + q]);
+        for (uint32_t q = 0; q < tl; q++) h = mt_fnv1a_step(h, mt_gtext(g, d, sc, t0 + q));
         const uint8_t f = g.flags[so + i];
         if (f & MT_SF_MARKER) h ^= MT_MARKER_TAG;  // a Marker: its ReferenceType byte, tagged
         const bool rm = f & MT_SF_REMOVED;
         seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(g.client[so + i]), rm ? g.rseq[so + i] : -1,
-                               rm ? (int32_t)g.rclient[so + i] : -1, g.ovl[so + i], g.props[so + i],
-                               (f & MT_SF_PDEF) ? 1u : 0u);
+                               rm ? (int32_t)g.rclient[so + i] : -1, mt_govl_term(g, wdoc, so + i),
+                               mt_gprops_term(g, wdoc, so + i), (f & MT_SF_PDEF) ? 1u : 0u);
     }
     uint64_t tree_sum = 0;
     for (int L = 0; L < sc.nlev; L++) {
@@ -332,10 +393,10 @@ extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint3
 }
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
-                                    uint32_t* counts, uint32_t* ids, const mt_op_rec* ops, unsigned long long* acc,
-                                    hipStream_t st) {
+                                    int first_wide, uint32_t* counts, uint32_t* ids, const mt_op_rec* ops,
+                                    unsigned long long* acc, hipStream_t st) {
     hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
-                       classes, n_classes, first_lds, counts, ids, ops, acc);
+                       classes, n_classes, first_lds, first_wide, counts, ids, ops, acc);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st) {
@@ -355,12 +416,13 @@ __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile
     const mt_doc_scalars sc = g.sc[d];
     const int n = sc.nseg;
     const size_t so = (size_t)d * g.segcap;
-    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     const int pos = qq.pos;
     auto labeled = [&](int i) -> bool {  // refHasTileLabel (mergeTree.ts:581-597)
-        if (qq.key >= MT_MAX_KEYS || !(g.flags[so + i] & MT_SF_MARKER) || !(text[g.toff[so + i]] & 1u)) return false;
-        const uint32_t v = (uint32_t)(g.props[so + i] >> (8 * qq.key)) & 0xFFu;
-        return v != 0 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
+        if (qq.key >= MT_MAX_KEYS_WIDE || !(g.flags[so + i] & MT_SF_MARKER) || !(mt_gtext(g, d, sc, g.toff[so + i]) & 1u))
+            return false;
+        const uint32_t v = mt_gprop(g, wdoc, so + i, qq.key);
+        return v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
     };
     auto local_len = [&](int i) -> int { return (g.flags[so + i] & MT_SF_REMOVED) ? 0 : (int)g.len[so + i]; };
     int res = -1, rpos = -1;
@@ -460,7 +522,7 @@ __global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_til
     const mt_doc_scalars sc = g.sc[d];
     const int n = sc.nseg;
     const size_t so = (size_t)d * g.segcap;
-    const uint8_t* text = g.text + ((size_t)d * 2 + sc.text_half) * g.textcap;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     const int pos = qq.pos;
     mt_stack_item* out = items + (size_t)w * cap;
     int a = 0, t = 0, carry = 0;
@@ -472,10 +534,10 @@ __global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_til
         const int start = carry + incl - ll;
         uint32_t rt = 0;
         bool cand = false;
-        if (i < n && ll > 0 && start <= pos && qq.key < MT_MAX_KEYS && (g.flags[so + i] & MT_SF_MARKER)) {
-            rt = text[g.toff[so + i]];
-            const uint32_t v = (uint32_t)(g.props[so + i] >> (8 * qq.key)) & 0xFFu;
-            cand = (rt & 6u) && v != 0 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
+        if (i < n && ll > 0 && start <= pos && qq.key < MT_MAX_KEYS_WIDE && (g.flags[so + i] & MT_SF_MARKER)) {
+            rt = mt_gtext(g, d, sc, g.toff[so + i]);
+            const uint32_t v = mt_gprop(g, wdoc, so + i, qq.key);
+            cand = (rt & 6u) && v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
         }
         uint64_t m = wave_ballot(cand);
         touched |= m != 0;
@@ -548,12 +610,13 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
     const int n = sc.nseg;
     const int32_t msn = sc.min_seq;
     const size_t so = (size_t)d * g.segcap;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     uint32_t* out = specs + (size_t)w * cap * 3;
     int k = 0;
     bool have = false;
     int ps = 0, pc = 0;
     uint32_t plen = 0, pfl = 0;
-    uint64_t pprops = 0;
+    uint64_t pprops = 0;  // the run's props (narrow word; a wide document compares all words in HBM)
     auto emit = [&](int pos, int cnt, bool meta, uint32_t len) {
         if (lane == 0 && k < (int)cap) {
             out[3 * k] = (uint32_t)pos;
@@ -593,7 +656,7 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), j) << 32);
             if (have && !((pfl | fj) & MT_SF_MARKER) && !(pfl & MT_SF_NL) && (plen <= 256u || lj <= 256u) &&
                 ((pfl ^ fj) & MT_SF_PDEF) == 0 &&
-                pprops == pj) {
+                pprops == pj && (!wdoc || mt_gprops_eq(g, true, so + ps, so + base + j))) {
                 pc = base + j - ps + 1;  // span from the run's first segment (elided ones inside it skipped by the reader)
                 plen += lj;
                 pfl = (pfl & ~MT_SF_NL) | (fj & MT_SF_NL);

@@ -37,10 +37,14 @@ struct mt_doc_scalars {      // 80 bytes
     uint32_t text_top;       // bytes used in the current half of the document's text arena
     uint32_t text_half;      // which half of the double-buffered arena is current (0/1)
     uint32_t n_empty;        // leaf blocks without children (the register engine pads one slot each)
-    uint32_t wide;           // a client id above 32 was seen: the document stays on the LDS engine
+    uint32_t wide;           // MT_WIDE_LDS: a client id above 32 was seen (the document stays on the LDS
+                             // engine); MT_WIDE_DOC: the wide representation (include/mtgpu.h "limits")
     int32_t win_op;          // batch index of the first op failing a window assert (binning's
                              // replay of the window), -1 if none: mt_fixup_kernel's input
 };
+
+#define MT_WIDE_LDS 1u
+#define MT_WIDE_DOC 2u
 
 // An editing client's document (client.ts:163-214, 588-625): its local
 // edits are pending until their acks.  Pending edit ordinals [glo, ghi) (at most 64 at once) index
@@ -69,8 +73,16 @@ struct mt_gstate {
     int32_t* rseq;
     uint32_t* len;
     uint32_t* toff;    // text view: arena offset
-    uint64_t* ovl;     // removedClientOverlap as a bitmask over short client ids
-    uint64_t* props;   // 8 keys x u8 value id
+    uint64_t* ovl;     // removedClientOverlap as a bitmask over short client ids < 64
+    uint64_t* props;   // 8 keys x u8 value id (a wide document: the low bytes of keys 0..7's u16 ids)
+    // a wide document's extra state (MT_WIDE_DOC; [doc][segcap], allocated on first need, else null):
+    // ovx = its overlapping removers >= 64 (up to MT_OVX_IDS ids, ascending from the low byte, 0 =
+    // none); ph = the high bytes of keys 0..7's value ids; pxl / pxh = keys 8..15, low / high bytes.
+    // Its text arena holds UTF-16 code units (2 bytes each; toff / len / text_top in units).
+    uint64_t* ovx;
+    uint64_t* ph;
+    uint64_t* pxl;
+    uint64_t* pxh;
     uint8_t* client;
     uint8_t* rclient;
     uint8_t* flags;

@@ -342,12 +342,15 @@ class MergeEngine:
         _check(lib().mt_doc_error(self.h, doc, ctypes.byref(code), ctypes.byref(seq)), 'mt_doc_error')
         return code.value, seq.value
 
-    def _string(self, fn, doc):
+    def _raw(self, fn, doc):
         n = ctypes.c_uint64()
         _check(fn(self.h, doc, None, 0, ctypes.byref(n)), fn.__name__)
         buf = ctypes.create_string_buffer(n.value + 1)
         _check(fn(self.h, doc, buf, n.value + 1, ctypes.byref(n)), fn.__name__)
-        return buf.raw[:n.value].decode('latin-1')
+        return buf.raw[:n.value]
+
+    def _string(self, fn, doc):
+        return self._raw(fn, doc).decode('latin-1')
 
     def state(self, doc):
         return json.loads(self._string(lib().mt_get_state, doc))
@@ -397,7 +400,8 @@ class MergeEngine:
         return ms.value, cnt.value
 
     def text(self, doc):
-        return self._string(lib().mt_get_text, doc)
+        """MergeTreeTextHelper.getText: the UTF-16 code units as a str (surrogate halves kept)."""
+        return self._raw(lib().mt_get_text, doc).decode('utf-16-le', 'surrogatepass')
 
     def length(self, doc):
         n = ctypes.c_uint32()

@@ -22,8 +22,26 @@ NPAIRS_SHIFT = 3        # bits 3..6: property pairs in the payload
 REF_TILE, REF_NEST_BEGIN, REF_NEST_END = 1, 2, 4
 
 
+OP_WIDE = 0x80          # type bit 7 (MT_OP_WIDE): UTF-16 text, 3-byte pairs (key u8, value u16 LE)
+
+
 def npairs(flags):
     return (int(flags) >> NPAIRS_SHIFT) & 15
+
+
+def encode_text(text, force_wide=False):
+    """(bytes, wide) of a str as the engine carries text: one Latin-1 byte per UTF-16 code unit when
+    every unit fits, else the UTF-16 code units little endian (lone surrogates kept)."""
+    if not force_wide:
+        try:
+            return text.encode('latin-1'), False
+        except UnicodeEncodeError:
+            pass
+    return text.encode('utf-16-le', 'surrogatepass'), True
+
+
+def decode_text(b, wide):
+    return b.decode('utf-16-le', 'surrogatepass') if wide else b.decode('latin-1')
 
 MAGIC = b'MTLOG001'
 

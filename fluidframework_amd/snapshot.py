@@ -17,8 +17,10 @@ SnapshotLoader.specToSegment (snapshotLoader.ts:85-117) does: without merge info
 (UniversalSequenceNumber 0, NonCollabClient); with it, its seq / client / removedSeq / removedClient.
 Long client ids and property keys / values are interned per document by the caller's interners.
 Marker specs ({marker: {refType}, props}, Marker.toJSONObject mergeTree.ts:652-656) load as markers
-(one byte, the ReferenceType, up to 255).  Text beyond U+00FF is refused (ValueError): one byte per
-UTF-16 code unit (textSegment.ts:45).
+(one byte, the ReferenceType, up to 255).  Text is carried as UTF-16 code units (cachedLength =
+text.length, textSegment.ts:45): Latin-1 bytes when every unit fits, else 2 bytes per unit
+(MT_LSF_U16; the document loads in the engine's wide form, include/mtgpu.h "limits"), as are keys
+>= 8, value ids >= 256 and client ids >= 64.
 """
 import ctypes
 import json
@@ -26,18 +28,19 @@ import json
 import numpy as np
 
 from .engine import _check, _ptr, lib
-from .oplog import F_MARKER, F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OpBatch
+from .oplog import F_MARKER, F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OP_WIDE, OpBatch, encode_text
 
 MT_OP_LOAD = 4
 NONCOLLAB = 0xFE            # MT_CLIENT_NONCOLLAB: NonCollabClient (constants.ts:15)
 UNIVERSAL_SEQ = 0           # UniversalSequenceNumber (constants.ts:11)
 SF_PDEF = 2
 SF_MARKER = 16
+LSF_U16 = 64                # MT_LSF_U16: the segment's text is UTF-16 code units
 
 LOAD_SEG_DTYPE = np.dtype([('seq', '<i4'), ('rseq', '<i4'), ('client', 'u1'), ('rclient', 'u1'), ('flags', 'u1'),
                            ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('pad2', '<u4'),
-                           ('props', '<u8')])
-assert LOAD_SEG_DTYPE.itemsize == 32
+                           ('props', '<u2', (16,)), ('pad3', '<u8')])
+assert LOAD_SEG_DTYPE.itemsize == 64
 
 
 class Interner:
@@ -58,13 +61,19 @@ class Interner:
 
 
 class DocInterners:
-    """Per-document id spaces: long client ids -> short ids (1..63), property keys -> 0..7,
-    property values -> 1..255 (0 = absent)."""
+    """Per-document id spaces: long client ids -> short ids (1..253), property keys -> 0..15, and
+    per key its values -> 1..65535 (0 = absent; ids are opaque, only equality matters,
+    properties.ts:62-93)."""
 
     def __init__(self):
-        self.client = Interner(1, 64)
-        self.key = Interner(0, 8)
-        self.value = Interner(1, 256)
+        self.client = Interner(1, 254)
+        self.key = Interner(0, 16)
+        self.values = {}
+
+    def value(self, kid, v):
+        if kid not in self.values:
+            self.values[kid] = Interner(1, 65536)
+        return self.values[kid](v)
 
 
 def _blobs(tree):
@@ -129,8 +138,8 @@ class LoadedDoc:
 
 
 def _spec(spec, it):
-    """specToSegment (snapshotLoader.ts:85-117) -> (text bytes, seq, client, rseq, rclient, pdef, props,
-    marker)"""
+    """specToSegment (snapshotLoader.ts:85-117) -> (text, seq, client, rseq, rclient, pdef, props
+    {key id: value id}, marker)"""
     merge = isinstance(spec, dict) and 'json' in spec
     js = spec['json'] if merge else spec
     marker = False
@@ -145,16 +154,13 @@ def _spec(spec, it):
         text, props, marker = chr(rt), js.get('props'), True
     else:
         raise ValueError(f'not a text or marker segment spec: {json.dumps(js)[:80]}')
-    try:
-        tb = text.encode('latin-1')
-    except UnicodeEncodeError:
-        raise ValueError('text beyond U+00FF is not device-representable') from None
-    pv = 0
+    pv = {}
     if props is not None:
         for k, v in props.items():
             if v is None:  # a null value never reaches a stored property set
                 continue
-            pv |= it.value(v) << (8 * it.key(k))
+            kid = it.key(k)
+            pv[kid] = it.value(kid, v)
     if merge:
         seq = spec['seq'] if spec.get('seq') is not None else UNIVERSAL_SEQ
         client = it.client(spec['client']) if spec.get('client') is not None else NONCOLLAB
@@ -162,7 +168,12 @@ def _spec(spec, it):
         rclient = it.client(spec['removedClient']) if spec.get('removedClient') is not None else 0
     else:
         seq, client, rseq, rclient = UNIVERSAL_SEQ, NONCOLLAB, -1, 0
-    return tb, seq, client, rseq, rclient, props is not None, pv, marker
+    return text, seq, client, rseq, rclient, props is not None, pv, marker
+
+
+def _wide_seg(units_wide, client, rseq, rclient, pv):
+    return (units_wide or (client >= 64 and client != NONCOLLAB) or (rseq >= 0 and rclient >= 64) or
+            any(k >= 8 or v > 255 for k, v in pv.items()))
 
 
 def build_load(docs, interners=None):
@@ -174,39 +185,46 @@ def build_load(docs, interners=None):
     for doc, it in zip(docs, interners):
         local = 0  # root.cachedLength: the local (non-removed) length
         for spec in doc.header:
-            tb, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
-            segs.append((seq, rseq, client, rclient, (SF_PDEF if pdef else 0) | (SF_MARKER if mk else 0), 0,
-                         len(text), len(tb), 0, pv))
+            t, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
+            tb, wide_text = encode_text(t)
+            n = len(tb) // 2 if wide_text else len(tb)
+            props = [pv.get(k, 0) for k in range(16)]
+            segs.append((seq, rseq, client, rclient,
+                         (SF_PDEF if pdef else 0) | (SF_MARKER if mk else 0) | (LSF_U16 if wide_text else 0), 0,
+                         len(text), n, 0, props, 0))
             text += tb
-            local += 0 if rseq >= 0 else len(tb)
+            local += 0 if rseq >= 0 else n
         row_ptr.append(len(segs))
         # loadBody (snapshotLoader.ts:192-224): a run of segments without merge info is one
         # insertSegments at root.cachedLength, each next one at insertPos += cachedLength
         # (mergeTree.ts:2219); any other segment is its own insertSegments call
         batch_pos = None
         for spec in doc.body:
-            tb, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
+            t, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
+            tb, wide_text = encode_text(t)
+            n = len(tb) // 2 if wide_text else len(tb)
+            wide = _wide_seg(wide_text, client, rseq, rclient, pv)
+            if wide and not wide_text:  # a wide record carries its text as UTF-16 units
+                tb, wide_text = encode_text(t, force_wide=True)
             batched = client == NONCOLLAB and seq == UNIVERSAL_SEQ
             if batched:
                 pos = local if batch_pos is None else batch_pos
-                batch_pos = pos + len(tb)
+                batch_pos = pos + n
             else:
                 pos = local
                 batch_pos = None
-            local += 0 if rseq >= 0 else len(tb)
+            local += 0 if rseq >= 0 else n
             pairs = b''
             flags = 0
             if pdef:
-                for k in range(8):
-                    v = (pv >> (8 * k)) & 0xFF
-                    if v:
-                        pairs += bytes([k, v])
-                flags = F_PROPS | ((len(pairs) // 2) << NPAIRS_SHIFT)
+                for k in sorted(pv):
+                    pairs += bytes([k, pv[k] & 0xFF, pv[k] >> 8]) if wide else bytes([k, pv[k]])
+                flags = F_PROPS | (len(pv) << NPAIRS_SHIFT)
             if mk:
                 flags |= F_MARKER
             data = tb + pairs
-            recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8), MT_OP_LOAD, flags,
-                         pos, rseq, len(payload), len(data)))
+            recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8),
+                         MT_OP_LOAD | (OP_WIDE if wide else 0), flags, pos, rseq, len(payload), len(data)))
             payload += data
         body_rp.append(len(recs))
     segs_a = np.array(segs, dtype=LOAD_SEG_DTYPE) if segs else np.zeros(0, dtype=LOAD_SEG_DTYPE)

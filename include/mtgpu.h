@@ -49,15 +49,25 @@ enum mt_op_flags {
 };
 #define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload */
 #define MT_OP_NPAIRS(flags) (((flags) >> MT_F_NPAIRS_SHIFT) & 0xF)
+/* Wide payload (type bit 7): the op's text is UTF-16 code units (2 bytes each, little endian:
+ * cachedLength = text.length, textSegment.ts:45 -- any string, surrogate halves included) and each
+ * property pair is 3 bytes (key u8 < MT_MAX_KEYS_WIDE, value id u16 LE).  The host sets it on every
+ * op whose text, keys or value ids do not fit the narrow form ([Latin-1 bytes][key u8 < 8, value u8]).
+ * A document that receives a wide op, or a client id >= MT_MAX_CLIENTS, becomes a WIDE document for
+ * good (see "limits" below); narrow-form ops apply to wide documents unchanged. */
+#define MT_OP_WIDE 0x80u
+#define MT_OP_TYPE(o) ((o).type & 0x7Fu)
+#define MT_OP_PAIR_BYTES(o) (((o).type & MT_OP_WIDE) ? 3u : 2u)
+#define MT_OP_PAIRS_LEN(o) (MT_OP_PAIR_BYTES(o) * MT_OP_NPAIRS((o).flags))
 /* An insert whose segment spec is the empty string is dropped by Client.applyInsertOp before it
  * touches the tree (`if (op.seg)`, client.ts:403-407: no boundary split, no completeAndLogOp
  * asserts, no callback); only updateSeqNumbers runs.  Such a record (text insert, no props, no
  * text bytes) is applied exactly as an MT_OP_NOOP.  An empty text WITH a props object is a real
  * insert: the boundary split happens and blockInsert skips the zero-length segment. */
 #define MT_OP_IS_EMPTY_INSERT(o)                                                      \
-    ((o).type == MT_OP_INSERT && !((o).flags & (MT_F_PROPS | MT_F_MARKER)) &&         \
-     (o).payload_len <= 2u * MT_OP_NPAIRS((o).flags))
-#define MT_OP_IS_NOOP(o) ((o).type == MT_OP_NOOP || MT_OP_IS_EMPTY_INSERT(o))
+    (MT_OP_TYPE(o) == MT_OP_INSERT && !((o).flags & (MT_F_PROPS | MT_F_MARKER)) &&    \
+     (o).payload_len <= MT_OP_PAIRS_LEN(o))
+#define MT_OP_IS_NOOP(o) (MT_OP_TYPE(o) == MT_OP_NOOP || MT_OP_IS_EMPTY_INSERT(o))
 /* An editing client.  A record with seq = MT_SEQ_LOCAL is a local edit of the
  * document's editing client (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
  * client.ts:163-214): INSERT / REMOVE / ANNOTATE at positions of its local view, applied at once
@@ -92,17 +102,31 @@ typedef struct mt_op_rec {
     int32_t pos1;         /* insert position / range start                                      */
     int32_t pos2;         /* range end (remove, annotate)                                       */
     uint32_t payload_off; /* byte offset into the batch payload                                 */
-    uint32_t payload_len; /* text bytes + 2*npairs: [text][key u8, value u8]*; value 0 = null   */
+    uint32_t payload_len; /* text bytes + 2*npairs: [text][key u8, value u8]*; value 0 = null
+                             (MT_OP_WIDE: 2 * text units + 3 * npairs)                            */
 } mt_op_rec;
 
 /* NonCollabClient (constants.ts:15): the client of a segment loaded from a snapshot below the
  * MSN (snapshotLoader.ts:107-114); canonical state and checksum report it as -2 */
 #define MT_CLIENT_NONCOLLAB 0xFE
 
-/* ---- limits of the device representation (checked; violations become per-doc errors) ------ */
-#define MT_MAX_CLIENTS 64      /* short client ids 0..63 (overlap set is a u64 bitmask)          */
-#define MT_MAX_KEYS 8          /* property keys per document (u8 value id per key)              */
-#define MT_MAX_VALUES 255      /* property value ids 1..255 per document (0 = absent/null)      */
+/* ---- limits of the device representation (checked; violations become per-doc errors) ------
+ * A NARROW document (every document starts narrow) holds short client ids < 64 (overlap sets as a
+ * u64 bitmask), keys < 8 with u8 value ids and one byte per text code unit (Latin-1): the register
+ * engine's and the LDS engine's fast forms.  A WIDE document (promoted for good by its first wide
+ * op, client id >= 64 or wide snapshot segment) holds client ids < 254 (u8; 0xFE is NonCollabClient),
+ * keys < 16 with u16 value ids, UTF-16 text (2 bytes per code unit in the same arena: half the
+ * units), and overlap sets of the ids < 64 plus at most MT_OVX_IDS ids >= 64 per segment.  Wide
+ * documents run on the LDS engine's wide form (its structure in an HBM workspace); their extra
+ * per-segment state (32 B) is allocated by the engine on first need.  Value ids are opaque
+ * (equality only) and may be interned per key. */
+#define MT_MAX_CLIENTS 64      /* narrow: short client ids 0..63 (overlap set is a u64 bitmask)  */
+#define MT_MAX_KEYS 8          /* narrow: property keys per document (u8 value id per key)      */
+#define MT_MAX_VALUES 255      /* narrow: property value ids 1..255 (0 = absent/null)           */
+#define MT_MAX_CLIENTS_WIDE 254 /* wide: short client ids 0..253                                */
+#define MT_MAX_KEYS_WIDE 16    /* wide: property keys 0..15                                      */
+#define MT_MAX_VALUES_WIDE 65535 /* wide: property value ids 1..65535 per key                    */
+#define MT_OVX_IDS 8           /* wide: overlapping removers with ids >= 64 per segment          */
 #define MT_MAX_TEXTCAP (512u * 1024u) /* text arena bytes per document half (mt_cfg.text_capacity) */
 
 typedef enum mt_status {
@@ -159,26 +183,31 @@ mt_status mt_docs_init(mt_engine* eng, uint32_t n_docs);
 /* ---- snapshot load ---------------------------------------------------
  * One segment of a snapshot's header chunk (IJSONSegmentWithMergeInfo, snapshotChunks.ts:60-66,
  * after SnapshotLoader.specToSegment, snapshotLoader.ts:85-117): 32 bytes. */
-typedef struct mt_load_seg {
+typedef struct mt_load_seg {  /* 64 bytes */
     int32_t seq;          /* spec.seq, or UniversalSequenceNumber (0) without merge info            */
     int32_t rseq;         /* spec.removedSeq; -1 = not removed                                      */
     uint8_t client;       /* short id of spec.client, or MT_CLIENT_NONCOLLAB                        */
     uint8_t rclient;      /* short id of spec.removedClient (when removed)                          */
     uint8_t flags;        /* MT_SF_PDEF (2) when the spec carries props, MT_SF_MARKER (16) for a
-                             Marker spec (text_len 1: its ReferenceType byte)  (mt_state.h)        */
+                             Marker spec (text_len 1: its ReferenceType byte), MT_LSF_U16 (64):
+                             the text is UTF-16 code units (2 bytes each, LE)  (mt_state.h)        */
     uint8_t pad;
-    uint32_t text_off;    /* the segment's text in the batch's text bytes                           */
-    uint32_t text_len;
+    uint32_t text_off;    /* the segment's text: byte offset in the batch's text bytes              */
+    uint32_t text_len;    /* code units (= bytes without MT_LSF_U16)                                */
     uint32_t pad2;
-    uint64_t props;       /* 8 keys x u8 value id (0 = absent)                                       */
+    uint16_t props[16];   /* value id per key (0 = absent)                                           */
+    uint64_t pad3;
 } mt_load_seg;
+#define MT_LSF_U16 64u
 
 /* SnapshotLoader.loadHeader for documents doc_ids[0..n): MergeTree.reloadFromSegments (mergeTree.ts:
  * 1195-1251: the leaves in blocks of MaxNodesInBlock - 1 = 7, levels built bottom-up until one
  * block is left) then startOrUpdateCollaboration(id, min_seq[i], cur_seq[i]) (snapshotLoader.ts:
  * 138-154, client.ts:1051-1071; an empty LRU heap, every block's needsScour undefined).  Document
  * i's segments are segs[seg_row_ptr[i] .. seg_row_ptr[i+1]) in order; texts are byte ranges of
- * `text` (Latin-1, one byte per UTF-16 unit).  Built on the device, one wave per document.
+ * `text` (Latin-1, one byte per UTF-16 unit, or UTF-16 LE with MT_LSF_U16).  A document with any
+ * segment beyond the narrow limits (UTF-16 text, key >= 8, value id >= 256, client id >= 64) loads
+ * as a wide document.  Built on the device, one wave per document.
  * The body chunks (and catch-up ops) follow through mt_submit as MT_OP_LOAD records (and normal
  * ops).  A document over the engine's capacities gets MT_DERR_CAPACITY / MT_DERR_TEXT_ARENA. */
 mt_status mt_docs_load(mt_engine* eng, uint32_t n, const uint32_t* doc_ids, const uint32_t* seg_row_ptr,
@@ -199,11 +228,13 @@ mt_status mt_submit(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops,
                     const uint8_t* payload, uint64_t payload_bytes, const uint32_t* doc_row_ptr);
 mt_status mt_sync(mt_engine* eng);
 
-/* Readout (synchronises).  Text = MergeTreeTextHelper.getText for the observer. */
+/* Readout (synchronises).  Text = MergeTreeTextHelper.getText for the observer, as UTF-16 code
+ * units (2 bytes each, little endian; *len in bytes) -- the JS string, surrogate halves included. */
 mt_status mt_get_length(mt_engine* eng, uint32_t doc, uint32_t* len);
 mt_status mt_get_text(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uint64_t* len);
 /* Canonical state (JSON, see DESIGN.md "Canonical state"): L1 text, L2 linked leaves,
- * L3 block shape, currentSeq/minSeq. */
+ * L3 block shape, currentSeq/minSeq.  ASCII JSON: non-ASCII code units as \uXXXX (here and in the
+ * snapshot blobs: the same JSON values the reference's JSON.stringify writes). */
 mt_status mt_get_state(mt_engine* eng, uint32_t doc, char* buf, uint64_t cap, uint64_t* len);
 /* Per-document 64-bit checksum of the canonical state (DESIGN.md "Checksum"). */
 mt_status mt_checksums(mt_engine* eng, uint64_t* out, uint32_t n_docs);
@@ -266,7 +297,7 @@ mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
 typedef struct mt_tile_query {  /* 48 bytes */
     uint32_t doc;
     int32_t pos;                /* startPos */
-    uint8_t key;                /* key id of "referenceTileLabels" in this document (>= 8: no tiles) */
+    uint8_t key;                /* key id of "referenceTileLabels" in this document (>= 16: no tiles) */
     uint8_t preceding;
     uint8_t pad[2];
     uint32_t vmask[8];          /* bit v: value id v's label array holds the label */
@@ -276,6 +307,8 @@ typedef struct mt_tile_result {
     int32_t pos;                /* the tile's local position (getPosition), -1: none */
     int32_t ordinal;            /* its index among the document's segments, -1: none */
 } mt_tile_result;
+/* (vmask covers value ids 0..255 of the label key: a host interning that key's values past 255
+ * refuses the query, so a label never goes unmatched silently) */
 mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_tile_result* out);
 
 /* The ops document `doc` regenerated at its MT_SEQ_REGEN records since the last drain (at most 256
@@ -326,7 +359,8 @@ mt_status mt_range_stacks(mt_engine* eng, const mt_tile_query* q, uint32_t n, ui
  *          maintenance callbacks: -1,
  *   len  = segment.cachedLength at callback time (APPEND: the first segment's grown length).
  * ANNOTATE records carry propertyDeltas as a key mask + the previous value id per key (0 =
- * null: the key was absent).  Recording routes every document to the LDS engine. */
+ * null: the key was absent).  Recording routes every document to the LDS engine (wide documents:
+ * its wide form). */
 enum mt_event_op {
     MT_EV_INSERT = 0, MT_EV_REMOVE = 1, MT_EV_ANNOTATE = 2,   /* MergeTreeDeltaType (ops.ts:17-24)   */
     MT_EV_APPEND = -1, MT_EV_SPLIT = -2, MT_EV_UNLINK = -3    /* MergeTreeMaintenanceType            */
@@ -335,17 +369,17 @@ enum mt_event_op {
 #define MT_EVF_NOPD 4u  /* ANNOTATE delta segment whose propertyDeltas is undefined (a remote annotate
                          dropped while the editing client's rewrite is pending) */
 #define MT_EVF_EMPTY 2u   /* the callback's deltaSegments is empty (no segment in this record) */
-typedef struct mt_event {   /* 32 bytes */
+typedef struct mt_event {   /* 64 bytes */
     int32_t seq;            /* sequenceNumber of the message being applied                        */
     int8_t op;              /* mt_event_op                                                        */
     uint8_t flags;          /* MT_EVF_*                                                           */
-    uint8_t pmask;          /* ANNOTATE: keys present in propertyDeltas (bit k = key id k)        */
-    uint8_t pad;
+    uint16_t pmask;         /* ANNOTATE: keys present in propertyDeltas (bit k = key id k)        */
     int32_t leaf;
     int32_t pos;
     uint32_t len;
-    uint32_t pad2;
-    uint64_t pvals;         /* ANNOTATE: previous value id of key k in byte k (0 = null)          */
+    uint32_t pad;
+    uint16_t pvals[16];     /* ANNOTATE: previous value id of key k (0 = null)                    */
+    uint64_t pad2;
 } mt_event;
 /* Start recording: `per_doc` records per document between drains (0 stops recording).  A
  * document that would exceed it halts with MT_DERR_EVENTS. */

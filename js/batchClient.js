@@ -24,8 +24,11 @@ const native = require(path.join(__dirname, "mtgpu.node"));
 
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
 const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
-const MAX_CLIENTS = 64, MAX_KEYS = 8, MAX_VALUES = 255;
-const REC = 32;
+const OP_WIDE = 0x80;  // MT_OP_WIDE: UTF-16 text, (key u8, value u16) pairs
+// include/mtgpu.h "limits": the wide form's (a document goes wide with its first op beyond the narrow
+// ones: client id >= 64, key >= 8, value id >= 256 or a code unit above U+00FF)
+const MAX_CLIENTS = 254, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
+const REC = 32, EVREC = 64;
 
 function canonicalJson(v) {
     if (Array.isArray(v)) return "[" + v.map(canonicalJson).join(",") + "]";
@@ -130,8 +133,8 @@ class BatchClient {
         this.longIds = [];
         this.keyIds = new Map();        // property key -> id
         this.keys = [];
-        this.valueIds = new Map();      // JSON(value) -> id
-        this.values = [undefined];
+        this.valueIds = [];             // per key id: JSON(value) -> id (ids are per key: only equality matters)
+        this.values = [];               // per key id: id -> value
         this.currentSeq = 0;
         this.minSeq = 0;
         this.msgQueue = [];
@@ -148,7 +151,7 @@ class BatchClient {
     _deliver(rows, lo, hi) {
         const cbs = [];
         for (let i = lo; i < hi; i++) {
-            const o = 32 * i;
+            const o = EVREC * i;
             const op = rows.readInt8(o + 4), flags = rows.readUInt8(o + 5);
             if (flags & 1) cbs.push({ seq: rows.readInt32LE(o), operation: op, deltaSegments: [] });
             if (flags & 2) continue;  // a callback without delta segments
@@ -156,12 +159,12 @@ class BatchClient {
             if (op >= 0) segment.position = rows.readInt32LE(o + 12);
             const delta = { segment };
             if (op === ANNOTATE && !(flags & 4)) {  // (MT_EVF_NOPD: propertyDeltas undefined)
-                const mask = rows.readUInt8(o + 6), vals = rows.readBigUInt64LE(o + 24);
+                const mask = rows.readUInt16LE(o + 6);
                 delta.propertyDeltas = {};
                 for (let k = 0; k < MAX_KEYS; k++) {
                     if (!((mask >> k) & 1)) continue;
-                    const v = Number((vals >> BigInt(8 * k)) & 0xffn);
-                    delta.propertyDeltas[this.keys[k]] = v ? this.values[v] : null;
+                    const v = rows.readUInt16LE(o + 24 + 2 * k);
+                    delta.propertyDeltas[this.keys[k]] = v ? this.values[k][v] : null;
                 }
             }
             cbs[cbs.length - 1].deltaSegments.push(delta);
@@ -206,6 +209,8 @@ class BatchClient {
                 if (kid >= MAX_KEYS) throw new Error(`BatchClient: more than ${MAX_KEYS} property keys`);
                 this.keyIds.set(k, kid);
                 this.keys.push(k);
+                this.valueIds.push(new Map());
+                this.values.push([undefined]);
             }
             const v = props[k];
             let vid = 0;
@@ -216,12 +221,12 @@ class BatchClient {
                 // objects and arrays (e.g. referenceTileLabels) are interned by content with sorted
                 // keys: matchProperties compares them structurally (properties.ts:62-93)
                 const key = canonicalJson(v);
-                vid = this.valueIds.get(key);
+                vid = this.valueIds[kid].get(key);
                 if (vid === undefined) {
-                    vid = this.values.length;
-                    if (vid > MAX_VALUES) throw new Error(`BatchClient: more than ${MAX_VALUES} property values`);
-                    this.valueIds.set(key, vid);
-                    this.values.push(v);
+                    vid = this.values[kid].length;
+                    if (vid > MAX_VALUES) throw new Error(`BatchClient: more than ${MAX_VALUES} values of property "${k}"`);
+                    this.valueIds[kid].set(key, vid);
+                    this.values[kid].push(v);
                 }
             }
             out.push(kid, vid);
@@ -250,15 +255,12 @@ class BatchClient {
                 if (op.seg.props) { r.flags |= F_PROPS; pairs = this._pairs(op.seg.props); }
             } else throw new Error("BatchClient: only text and marker segments are supported");
             if (typeof text !== "string") throw new Error("BatchClient: segment text must be a string");
-            // the device arena holds one byte per UTF-16 code unit, so lengths and positions equal the
-            // reference's cachedLength = text.length (textSegment.ts:45) only up to U+00FF: anything
-            // wider is refused here rather than stored truncated
-            if (/[^\u0000-\u00ff]/.test(text)) {
-                throw new Error("BatchClient: text with UTF-16 code units above U+00FF is not supported by the device engine");
-            }
+            // lengths and positions are UTF-16 code units (cachedLength = text.length, textSegment.ts:45):
+            // Latin-1 bytes when every unit fits, else the wide form's 2 bytes per unit
             r.type = INSERT; r.pos1 = op.pos1;
             r.npairs = pairs.length / 2;
-            r.payload = Buffer.concat([Buffer.from(text, "latin1"), Buffer.from(pairs)]);
+            r.text = text;
+            r.pairs = pairs;
         } else if (op.type === REMOVE || op.type === ANNOTATE) {
             if (op.relativePos1 || op.relativePos2 || op.register) throw new Error("BatchClient: unsupported op form");
             r.type = op.type; r.pos1 = op.pos1; r.pos2 = op.pos2;
@@ -269,10 +271,28 @@ class BatchClient {
                 }
                 const pairs = this._pairs(op.props);
                 r.npairs = pairs.length / 2;
-                r.payload = Buffer.from(pairs);
+                r.text = "";
+                r.pairs = pairs;
             }
         } else {
             throw new Error(`BatchClient: op type ${op.type} unsupported`);
+        }
+        if (r.pairs) {  // the payload, narrow or wide (include/mtgpu.h MT_OP_WIDE)
+            let wide = /[^\u0000-\u00ff]/.test(r.text);
+            for (let q = 0; q < r.pairs.length; q += 2) wide = wide || r.pairs[q] >= NARROW_KEYS || r.pairs[q + 1] > 255;
+            if (wide) {
+                const pb = Buffer.alloc(3 * r.npairs);
+                for (let q = 0; q < r.npairs; q++) {
+                    pb.writeUInt8(r.pairs[2 * q], 3 * q);
+                    pb.writeUInt16LE(r.pairs[2 * q + 1], 3 * q + 1);
+                }
+                r.type |= OP_WIDE;
+                r.payload = Buffer.concat([Buffer.from(r.text, "utf16le"), pb]);
+            } else {
+                r.payload = Buffer.concat([Buffer.from(r.text, "latin1"), Buffer.from(r.pairs)]);
+            }
+            delete r.text;
+            delete r.pairs;
         }
         return r;
     }
@@ -285,6 +305,9 @@ class BatchClient {
         const msg = { sequenceNumber: -1, referenceSequenceNumber: this.currentSeq, minimumSequenceNumber: 0 };
         const r = this._record(msg, op, this._shortId(this.longClientId), false);
         if (r.type === NOOP) return undefined;  // insertSegmentLocal: nothing for an empty segment
+        if ((r.type & OP_WIDE) || r.client >= NARROW_CLIENTS) {
+            throw new Error("BatchClient: an editing client's document stays within the narrow limits (include/mtgpu.h)");
+        }
         this.queue.push(r);
         if (this.engine.recording) this.expect.push({ op });  // a local edit's callback: no sequencedMessage
         this.engine.pending += 1;
@@ -327,7 +350,7 @@ class BatchClient {
             const props = {};
             for (let q = 0; q < np; q++) {
                 const k = pay.readUInt8(off + len - 2 * np + 2 * q), v = pay.readUInt8(off + len - 2 * np + 2 * q + 1);
-                props[this.keys[k]] = v ? this.values[v] : null;
+                props[this.keys[k]] = v ? this.values[k][v] : null;
             }
             if (type === INSERT) {
                 const text = pay.toString("latin1", off, off + len - 2 * np);
@@ -410,8 +433,11 @@ class BatchClient {
         const kid = this.keyIds.get(key);
         q.writeUInt8(kid === undefined ? 0xff : kid, off + 8);
         q.writeUInt8(preceding ? 1 : 0, off + 9);
-        for (let v = 1; v < this.values.length; v++) {
-            const labels = this.values[v];
+        const vals = kid === undefined ? [undefined] : this.values[kid];
+        // (the query's label mask covers value ids below 256 of the label key)
+        if (vals.length > 256) throw new Error(`BatchClient: more than 255 values of "${key}" for a label query`);
+        for (let v = 1; v < vals.length; v++) {
+            const labels = vals[v];
             if (Array.isArray(labels) && labels.includes(label)) {
                 const o = off + 12 + 4 * (v >> 5);
                 q.writeUInt32LE((q.readUInt32LE(o) | (1 << (v & 31))) >>> 0, o);
@@ -468,7 +494,10 @@ class BatchClient {
             s[5] = s[5].map((x) => this.longIds[x]);
             if (s[6]) {
                 const p = {};
-                for (const k of Object.keys(s[6])) p[this.keys[parseInt(k.slice(1), 10)]] = this.values[s[6][k]];
+                for (const k of Object.keys(s[6])) {
+                    const kid = parseInt(k.slice(1), 10);
+                    p[this.keys[kid]] = this.values[kid][s[6][k]];
+                }
                 s[6] = p;
             }
         }

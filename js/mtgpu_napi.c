@@ -275,7 +275,9 @@ static napi_value get_string(napi_env env, napi_callback_info info, string_fn fn
         free(buf);
         return throw_status(env, what, st);
     }
-    napi_status ns = napi_create_string_latin1(env, buf, n, &out);
+    /* mt_get_text: UTF-16 code units (little endian, as x86 and gfx950 are); the state JSON: ASCII */
+    napi_status ns = fn == mt_get_text ? napi_create_string_utf16(env, (const char16_t*)buf, n / 2, &out)
+                                       : napi_create_string_latin1(env, buf, n, &out);
     free(buf);
     NAPI_CALL(env, ns);
     return out;
@@ -420,7 +422,7 @@ static napi_value regen_drain(napi_env env, napi_callback_info info) {
     return out;
 }
 
-/* docsLoad(engine, docIdsU32, segRowPtrU32, segs (32-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
+/* docsLoad(engine, docIdsU32, segRowPtrU32, segs (64-byte mt_load_seg rows), text, minSeqI32, curSeqI32):
  * SnapshotLoader.loadHeader for a batch of documents (mt_docs_load) */
 static napi_value docs_load(napi_env env, napi_callback_info info) {
     size_t argc = 7;
@@ -465,7 +467,7 @@ static napi_value events_enable(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
-/* eventsDrain(engine, nDocs) -> [Buffer of 32-byte mt_event rows, Buffer of nDocs+1 u32 row pointers] */
+/* eventsDrain(engine, nDocs) -> [Buffer of 64-byte mt_event rows, Buffer of nDocs+1 u32 row pointers] */
 static napi_value events_drain(napi_env env, napi_callback_info info) {
     size_t argc = 2;
     napi_value argv[2], out, rows, rp;

@@ -36,12 +36,22 @@ function tileLabels(v) {
     return out;
 }
 
-function propsOf(log, r, opts) {
+// a record's payload: [text][pairs]; narrow: Latin-1 bytes and (key u8, value u8) pairs; wide
+// (type bit 7, MT_OP_WIDE): UTF-16 LE code units and (key u8, value u16 LE) pairs
+const pairBytes = (r) => (r.type & 0x80 ? 3 : 2);
+function textOf(log, r) {
     const np = (r.flags >> 3) & 15;
-    const start = log.payOff + r.poff + r.plen - 2 * np;
+    const a = log.payOff + r.poff, b = a + r.plen - pairBytes(r) * np;
+    return log.buf.toString(r.type & 0x80 ? "utf16le" : "latin1", a, b);
+}
+
+function propsOf(log, r, opts) {
+    const np = (r.flags >> 3) & 15, pb = pairBytes(r);
+    const start = log.payOff + r.poff + r.plen - pb * np;
     const props = {};
     for (let q = 0; q < np; q++) {
-        const k = log.buf.readUInt8(start + 2 * q), v = log.buf.readUInt8(start + 2 * q + 1);
+        const k = log.buf.readUInt8(start + pb * q);
+        const v = pb === 3 ? log.buf.readUInt16LE(start + 3 * q + 1) : log.buf.readUInt8(start + 2 * q + 1);
         if (opts && opts.tileKey === k) props.referenceTileLabels = v === 0 ? null : tileLabels(v);
         else if (opts && opts.rangeKey === k) props.referenceRangeLabels = v === 0 ? null : tileLabels(v);
         else props["k" + k] = v === 0 ? null : v;
@@ -50,18 +60,18 @@ function propsOf(log, r, opts) {
 }
 
 function toOp(log, r, opts) {
-    const np = (r.flags >> 3) & 15;
-    if (r.type === 0 && (r.flags & 128)) {
-        const seg = { marker: { refType: log.buf.readUInt8(log.payOff + r.poff) } };
+    const type = r.type & 0x7f;
+    if (type === 0 && (r.flags & 128)) {
+        const seg = { marker: { refType: textOf(log, r).charCodeAt(0) } };
         if (r.flags & 2) seg.props = propsOf(log, r, opts);
         return { type: 0, pos1: r.pos1, seg };
     }
-    if (r.type === 0) {
-        const text = log.buf.toString("latin1", log.payOff + r.poff, log.payOff + r.poff + r.plen - 2 * np);
+    if (type === 0) {
+        const text = textOf(log, r);
         return { type: 0, pos1: r.pos1, seg: (r.flags & 2) ? { text, props: propsOf(log, r, opts) } : text };
     }
-    if (r.type === 1) return { type: 1, pos1: r.pos1, pos2: r.pos2 };
-    if (r.type === 2) {
+    if (type === 1) return { type: 1, pos1: r.pos1, pos2: r.pos2 };
+    if (type === 2) {
         const op = { type: 2, pos1: r.pos1, pos2: r.pos2, props: propsOf(log, r, opts) };
         if (r.flags & 1) op.combiningOp = { name: "rewrite" };
         return op;

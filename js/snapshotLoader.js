@@ -17,8 +17,8 @@
 // specToSegment (snapshotLoader.ts:85-117): without merge info a segment is (seq 0, NonCollabClient).
 const native = require("./mtgpu.node");
 
-const MT_OP_LOAD = 4, F_PROPS = 2, F_MARKER = 128;
-const NONCOLLAB = 0xfe, UNIVERSAL_SEQ = 0, SF_PDEF = 2, SF_MARKER = 16;
+const MT_OP_LOAD = 4, F_PROPS = 2, F_MARKER = 128, OP_WIDE = 0x80;
+const NONCOLLAB = 0xfe, UNIVERSAL_SEQ = 0, SF_PDEF = 2, SF_MARKER = 16, LSF_U16 = 64, LOAD_SEG = 64;
 
 function blobs(tree) {
     if (tree && Array.isArray(tree.entries)) {
@@ -86,9 +86,8 @@ function spec(client, s) {
     } else {
         throw new Error("snapshotLoader: not a text or marker segment spec");
     }
-    if (/[^\u0000-\u00ff]/.test(text)) {
-        throw new Error("snapshotLoader: text with UTF-16 code units above U+00FF is not supported by the device engine");
-    }
+    // UTF-16 code units (cachedLength = text.length, textSegment.ts:45): Latin-1 bytes when they fit
+    const u16 = /[^\u0000-\u00ff]/.test(text);
     let pairs = [];
     if (props !== undefined && props !== null) {
         const nonNull = {};
@@ -102,8 +101,10 @@ function spec(client, s) {
         if (s.removedSeq !== undefined && s.removedSeq !== null) rseq = s.removedSeq;
         if (s.removedClient !== undefined && s.removedClient !== null) rc = client._shortId(s.removedClient);
     }
-    return { bytes: Buffer.from(text, "latin1"), seq, client: c, rseq, rclient: rc,
-        pdef: props !== undefined && props !== null, pairs, marker };
+    let wide = u16 || (c >= 64 && c !== NONCOLLAB) || (rseq >= 0 && rc >= 64);  // the wide form (include/mtgpu.h)
+    for (let q = 0; q < pairs.length; q += 2) wide = wide || pairs[q] >= 8 || pairs[q + 1] > 255;
+    return { bytes: Buffer.from(text, wide ? "utf16le" : "latin1"), units: text.length, u16: wide, seq, client: c,
+        rseq, rclient: rc, pdef: props !== undefined && props !== null, pairs, marker, wide };
 }
 
 /**
@@ -127,20 +128,15 @@ function loadSnapshots(engine, entries) {
         let local = 0;  // root.cachedLength: the local (non-removed) length
         for (const s of doc.header) {
             const x = spec(client, s);
-            const row = Buffer.alloc(32);
+            const row = Buffer.alloc(LOAD_SEG);  // mt_load_seg (include/mtgpu.h)
             row.writeInt32LE(x.seq, 0); row.writeInt32LE(x.rseq, 4);
             row.writeUInt8(x.client, 8); row.writeUInt8(x.rclient, 9);
-            row.writeUInt8((x.pdef ? SF_PDEF : 0) | (x.marker ? SF_MARKER : 0), 10);
-            row.writeUInt32LE(textOff, 12); row.writeUInt32LE(x.bytes.length, 16);
-            let lo = 0, hi = 0;
-            for (let q = 0; q < x.pairs.length; q += 2) {
-                const k = x.pairs[q], v = x.pairs[q + 1];
-                if (k < 4) lo |= v << (8 * k); else hi |= v << (8 * (k - 4));
-            }
-            row.writeUInt32LE(lo >>> 0, 24); row.writeUInt32LE(hi >>> 0, 28);
+            row.writeUInt8((x.pdef ? SF_PDEF : 0) | (x.marker ? SF_MARKER : 0) | (x.u16 ? LSF_U16 : 0), 10);
+            row.writeUInt32LE(textOff, 12); row.writeUInt32LE(x.units, 16);
+            for (let q = 0; q < x.pairs.length; q += 2) row.writeUInt16LE(x.pairs[q + 1], 24 + 2 * x.pairs[q]);
             segRows.push(row); texts.push(x.bytes);
             textOff += x.bytes.length; nseg++;
-            if (x.rseq < 0) local += x.bytes.length;
+            if (x.rseq < 0) local += x.units;
         }
         segRow[i + 1] = nseg;
         minSeq[i] = doc.minSeq; curSeq[i] = doc.seq;
@@ -153,20 +149,23 @@ function loadSnapshots(engine, entries) {
             let pos;
             if (batched) {
                 pos = batchPos === null ? local : batchPos;
-                batchPos = pos + x.bytes.length;
+                batchPos = pos + x.units;
             } else {
                 pos = local;
                 batchPos = null;
             }
-            if (x.rseq < 0) local += x.bytes.length;
+            if (x.rseq < 0) local += x.units;
             const sorted = [];
             for (let q = 0; q < x.pairs.length; q += 2) sorted.push([x.pairs[q], x.pairs[q + 1]]);
             sorted.sort((a, b) => a[0] - b[0]);
-            const pairs = [].concat(...sorted);
+            const pb = Buffer.alloc((x.wide ? 3 : 2) * sorted.length);
+            sorted.forEach(([k, v], q) => {
+                if (x.wide) { pb.writeUInt8(k, 3 * q); pb.writeUInt16LE(v, 3 * q + 1); } else { pb.writeUInt8(k, 2 * q); pb.writeUInt8(v, 2 * q + 1); }
+            });
             client.queue.push({ seq: x.seq, ref: UNIVERSAL_SEQ, msn: 0,
-                client: x.client | ((x.rseq >= 0 ? x.rclient : 0) << 8), type: MT_OP_LOAD,
-                flags: (x.pdef ? F_PROPS : 0) | (x.marker ? F_MARKER : 0), npairs: pairs.length / 2, pos1: pos,
-                pos2: x.rseq, payload: Buffer.concat([x.bytes, Buffer.from(pairs)]) });
+                client: x.client | ((x.rseq >= 0 ? x.rclient : 0) << 8), type: MT_OP_LOAD | (x.wide ? OP_WIDE : 0),
+                flags: (x.pdef ? F_PROPS : 0) | (x.marker ? F_MARKER : 0), npairs: sorted.length, pos1: pos,
+                pos2: x.rseq, payload: Buffer.concat([x.bytes, pb]) });
             engine.pending++;
         }
         client.currentSeq = doc.seq;

@@ -32,23 +32,47 @@ def seg_hash(idx, text_hash, seq, client, rseq, rclient, overlap, props_lo, prop
     return h
 
 
+def ovl_term(mask, ovx):
+    """the overlap term: ids < 64 as a bitmask, ids >= 64 (ascending bytes from the low one) hashed in"""
+    return mask ^ mix64(ovx ^ 0x4F56584944530000) if ovx else mask
+
+
+def props_term(lo, hi, xlo, xhi):
+    """the props term: low bytes of keys 0..7; high bytes and keys 8..15 hashed in"""
+    if not (hi | xlo | xhi):
+        return lo
+    return lo ^ mix64(mix64(hi ^ 0x1111111111111111) ^ mix64(xlo ^ 0x2222222222222222) ^
+                      mix64(xhi ^ 0x3333333333333333))
+
+
+def utf16_units(text):
+    """a str as its UTF-16 code units (lone surrogates included, as JSON carries them)"""
+    b = text.encode('utf-16-le', 'surrogatepass')
+    return [b[i] | (b[i + 1] << 8) for i in range(0, len(b), 2)]
+
+
 def checksum(state):
     """state: canonical JSON dict {"seq","msn","segs":[[text,seq,client,rseq,rclient,[ov],props]],"tree"}"""
     seg_sum = 0
     for i, (text, seq, client, rseq, rclient, ov, props) in enumerate(state['segs']):
-        overlap = 0
-        for o in ov:
-            overlap |= 1 << o
-        props_lo = 0
+        mask, ovx, nx = 0, 0, 0
+        for o in sorted(ov):
+            if o < 64:
+                mask |= 1 << o
+            else:
+                ovx |= o << (8 * nx)
+                nx += 1
+        w = [0, 0, 0, 0]
         if props is not None:
             for k, v in props.items():
-                kid = int(k[1:])
-                if kid < 8:
-                    props_lo |= (int(v) & 0xFF) << (8 * kid)
+                kid, v = int(k[1:]), int(v)
+                w[(kid >> 3) * 2] |= (v & 0xFF) << (8 * (kid & 7))
+                w[(kid >> 3) * 2 + 1] |= (v >> 8) << (8 * (kid & 7))
+        overlap, props_lo = ovl_term(mask, ovx), props_term(*w)
         if isinstance(text, dict):  # a Marker {"marker": refType}: its refType byte, tagged
             th = fnv1a(bytes([text['marker']])) ^ MARKER_TAG
         else:
-            th = fnv1a(text.encode('latin-1'))
+            th = fnv1a(utf16_units(text))
         seg_sum = (seg_sum + seg_hash(i, th, seq, client, rseq, rclient, overlap, props_lo,
                                       props is not None)) & M64
     tree_sum = 0

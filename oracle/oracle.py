@@ -175,7 +175,7 @@ class Oracle:
         n = lib().mto_doc_text(self.h, doc, None, 0)
         buf = ctypes.create_string_buffer(int(n))
         lib().mto_doc_text(self.h, doc, buf, n)
-        return buf.value.decode()
+        return json.loads(buf.value.decode())  # (a JSON string: any UTF-16 text, lone surrogates included)
 
     def nsegs(self, doc):
         return lib().mto_doc_nsegs(self.h, doc)

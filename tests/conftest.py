@@ -15,6 +15,9 @@ def pytest_configure(config):
 
 GOLDEN = os.path.join(REPO, 'tests', 'golden')
 GOLDEN_SETS = ['scenarios', 'markers', 'synth_c1', 'synth_c2', 'synth_c3', 'synth_c4', 'synth_tiny', 'synth_markers']
+# beyond the narrow limits (include/mtgpu.h "limits"): UTF-16 text, > 100 client ids, u16 value ids,
+# keys 8..15 -- tests/golden/make_wide.py
+WIDE_SETS = ['wide', 'wide_synth']
 
 
 def load_golden(name):

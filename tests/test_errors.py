@@ -147,11 +147,11 @@ def _device_limit_batch(oracle_lib, faulty=True):
                 int(o['pos2']), data, int(o['flags']))
         if not faulty:
             continue
-        if d == 1:   # client id 65 (short ids < 64: MT_DERR_LIMITS)
-            rec(201, 200, m, 65, INSERT, 0, 0, b'x')
+        if d == 1:   # client id 254 (short ids < 254 -- 0xFE is NonCollabClient: MT_DERR_LIMITS)
+            rec(201, 200, m, 254, INSERT, 0, 0, b'x')
         if d == 3:   # unknown op type (MT_DERR_BAD_OP)
             rec(201, 200, m, 1, 9)
-        if d == 5:   # property key 8 (8 keys per document on the device: MT_DERR_LIMITS)
+        if d == 5:   # property key 8 in a narrow-form op (keys < 8; the wide form carries < 16: MT_DERR_LIMITS)
             rec(201, 200, m, 2, INSERT, 0, 0, b'ab' + bytes([8, 1]), 2 | (1 << 3))
         if d == 7:   # negative position (MT_DERR_BAD_OP)
             rec(201, 200, m, 2, REMOVE, -3, 2)
@@ -166,11 +166,11 @@ def _device_limit_batch(oracle_lib, faulty=True):
 
 
 def test_oracle_flags_malformed_records(oracle_lib):
-    """The oracle shares the record-level checks (client ids, op type, positions); its tree and
-    key table are unbounded (32 keys), so the key-8 and > 2048-segment documents replay fine."""
+    """The oracle shares the record-level checks (client ids, op type, the key limit of the op's
+    form, positions); its tree is unbounded, so the > 2048-segment document replays fine."""
     batch, _ = _device_limit_batch(oracle_lib)
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)
-    want = {1: (6, 201), 3: (7, 201), 7: (7, 201)}
+    want = {1: (6, 201), 3: (7, 201), 5: (6, 201), 7: (7, 201)}
     for d in range(batch.n_docs):
         assert o.error(d) == want.get(d, (0, 0)), d
 

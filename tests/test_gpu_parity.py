@@ -4,7 +4,7 @@ synthetic logs.  Run on the GPU box:  python -m pytest tests -m gpu"""
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_SETS, load_golden
+from conftest import GOLDEN_SETS, WIDE_SETS, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +22,7 @@ def _diff(a, b):
 
 
 @pytest.mark.parametrize('b', [0, 32, 5])
-@pytest.mark.parametrize('name', GOLDEN_SETS)
+@pytest.mark.parametrize('name', GOLDEN_SETS + WIDE_SETS)
 def test_golden_bit_exact(name, b):
     from fluidframework_amd.engine import MergeEngine
     batch, exp = load_golden(name)
@@ -122,3 +122,76 @@ def test_snapshot_matches_restatement_on_fuzz(oracle_lib):
         got = eng.snapshots(5, 40, chunk, names)
         for i, d in enumerate(range(5, 45)):
             assert got[i] == snapshot.emit(o.state(d), chunk or snapshot.DEFAULT_CHUNK), (chunk, d)
+
+
+@pytest.mark.parametrize('b', [32, 7])
+def test_wide_and_narrow_documents_share_an_engine(oracle_lib, b):
+    """Wide documents (tests/golden/wide*: UTF-16 text, 120 client ids, u16 value ids, keys 8..15) in
+    one engine with narrow C3 documents on the register engine: each kind on its own form, both
+    bit-exact; the narrow documents' checksums equal the oracle's."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import CONFIGS, OpBatch
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 400
+    narrow = oracle_lib.generate(64, seed=8, **cfg)
+    wides = [load_golden(n) for n in WIDE_SETS]
+    batch = OpBatch.concat([narrow] + [w for w, _ in wides])
+    eng = MergeEngine(batch.n_docs, ops_per_launch=b)
+    eng.apply(batch)
+    o = oracle_lib.Oracle(64).apply(narrow, threads=8)
+    assert np.array_equal(eng.checksums()[:64], o.checksums())
+    d0 = 64
+    for w, exp in wides:
+        for r in exp:
+            d = d0 + r['doc']
+            assert eng.error(d) == (0, 0), (d, eng.error(d))
+            assert eng.state(d) == r['state'], _diff(eng.state(d), r['state'])
+            assert eng.text(d) == r['text']
+        d0 += w.n_docs
+
+
+def test_narrow_documents_promote_to_wide_mid_batch(oracle_lib):
+    """Narrow C3 documents replayed halfway, then a wide record (a CJK insert, a client id >= 64, a
+    value id past 255, or a key past 7) arrives: each document moves to the wide form with its state
+    (text widened in place of the arena) and the rest of its log applies bit-exact with the oracle."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import CONFIGS, OP_WIDE, OpBatch, INSERT, ANNOTATE
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 512
+    n = 48
+    full = oracle_lib.generate(n, seed=19, **cfg)
+    # the same logs with one record per document turned wide at op 256
+    ops = full.ops.copy()
+    payload = bytearray(full.payload.tobytes())
+    for d in range(n):
+        i = int(full.row_ptr[d]) + 256
+        o = ops[i]
+        kind = d % 4
+        if kind == 1 and o['type'] != 3:
+            ops[i]['client'] = 64 + d          # a client id >= 64 (its first appearance)
+            continue
+        # rewrite the record as a wide insert of two CJK units (payload appended)
+        text = '中文'.encode('utf-16-le')
+        pairs = b''
+        if kind == 2:
+            pairs = bytes([1, 0x2C, 0x01])     # key 1 -> value id 300
+        elif kind == 3:
+            pairs = bytes([11, 5, 0])          # key 11 -> value id 5
+        off = len(payload)
+        payload += text + pairs
+        ops[i]['type'] = INSERT | OP_WIDE
+        ops[i]['flags'] = (2 | (1 << 3)) if pairs else 0
+        ops[i]['pos1'] = 0
+        ops[i]['payload_off'] = off
+        ops[i]['payload_len'] = len(text) + len(pairs)
+    batch = OpBatch(ops, np.frombuffer(bytes(payload), np.uint8), full.row_ptr)
+    o = oracle_lib.Oracle(n).apply(batch, threads=8)
+    eng = MergeEngine(n, ops_per_launch=32)
+    eng.apply(batch)
+    got, want = eng.checksums(), o.checksums()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(d), eng.error(int(d)), o.error(int(d)), _diff(eng.state(int(d)), o.state(int(d))))
+                           for d in bad[:3]]
+    assert all(eng.error(d) == o.error(d) for d in range(n))

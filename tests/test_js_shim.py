@@ -80,24 +80,29 @@ def test_deli_sequencer_replays_lambda_spec():
     assert nacked[4][0] == 'nack' and nacked[4][3] == 'Nonexistent client'
 
 
-def test_batchclient_refuses_text_beyond_latin1():
-    """The device arena stores one byte per UTF-16 code unit: text above U+00FF (CJK, a surrogate
-    pair) must throw at applyMsg, never be stored truncated (textSegment.ts:45 cachedLength =
-    text.length); Latin-1 text is accepted.  No device work: the record is refused on the host."""
+def test_batchclient_encodes_wide_records():
+    """Text is UTF-16 code units (textSegment.ts:45 cachedLength = text.length): Latin-1 text goes out
+    narrow (one byte per unit); CJK or a surrogate pair -- or a value id past 255, a key past 7 -- makes
+    the record wide (MT_OP_WIDE: 2 bytes per unit, 3-byte pairs).  No device work: host encoding only."""
     if not _addon():
         pytest.skip('node headers absent')
     js = ("const {BatchClient}=require('./js/batchClient.js');"
           "const c=new BatchClient({pending:0},0);c.startOrUpdateCollaboration('observer');"
-          "const bad=[];for (const t of ['\\u4e2d\\u6587','a\\ud83d\\ude00b']) {"
-          " try {c.insertTextRemote(0,t,undefined,1,0,'w');bad.push(t);} catch(e) {"
-          "  if (!/U\\+00FF/.test(e.message)) throw e;}}"
           "c.insertTextRemote(0,'caf\\u00e9',undefined,1,0,'w');"
-          "if (bad.length) throw new Error('accepted '+JSON.stringify(bad));"
-          "if (c.queue.length!==1||c.queue[0].payload.length!==4) throw new Error('latin-1 record');"
-          "console.log('ok')")
+          "c.insertTextRemote(0,'\\u4e2d\\u6587',undefined,2,1,'w');"
+          "c.insertTextRemote(0,'a\\ud83d\\ude00b',{k:1},3,2,'w');"
+          "const props={};for (let i=0;i<300;i++) props['v'+i]=undefined;"
+          "for (let i=0;i<300;i++) c.applyMsg(c.makeOpMessage({type:2,pos1:0,pos2:1,props:{m:'id'+i}},4+i,3,'w'));"
+          "const q=c.queue.map((r)=>[r.type,r.flags,r.payload.length]);"
+          "console.log(JSON.stringify([q[0],q[1],q[2],q[3+254],q[3+255]]))")
     out = subprocess.run([NODE, '-e', js], cwd=REPO, capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.strip() == 'ok'
+    q = json.loads(out.stdout.strip())
+    assert q[0] == [0, 0, 4]                       # narrow: 4 Latin-1 bytes
+    assert q[1] == [0x80, 0, 4]                    # wide: 2 units x 2 bytes
+    assert q[2] == [0x80, 2, 8 + 3]                # wide: a, surrogate pair, b = 4 units; one 3-byte pair
+    assert q[3] == [2, 0, 2]                       # value id 255 of key "m": a narrow pair
+    assert q[4] == [0x82, 0, 3]                    # value id 256: a wide annotate
 
 
 @pytest.mark.gpu

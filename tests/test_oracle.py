@@ -13,10 +13,10 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_SETS, REPO, load_golden
+from conftest import GOLDEN_SETS, REPO, WIDE_SETS, load_golden
 
 
-@pytest.mark.parametrize('name', GOLDEN_SETS)
+@pytest.mark.parametrize('name', GOLDEN_SETS + WIDE_SETS)
 def test_oracle_matches_reference_golden(oracle_lib, name):
     from oracle import canon
     batch, exp = load_golden(name)

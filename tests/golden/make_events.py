@@ -19,8 +19,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 
-FULL = ['scenarios', 'markers', 'errors', 'empty_inserts']
-DIGEST = ['synth_tiny', 'synth_c3', 'synth_c4', 'synth_markers']
+FULL = ['scenarios', 'markers', 'errors', 'empty_inserts', 'wide']
+DIGEST = ['synth_tiny', 'synth_c3', 'synth_c4', 'synth_markers', 'wide_synth']
 
 
 def canonical(events):

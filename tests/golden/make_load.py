@@ -8,8 +8,8 @@ Runs in the build container only (needs /root/reference and node):
      (oracle/tsref/replay_ref.js `load`).  Stored: the emitted snapshot (input) and the loaded
      client's final canonical state and error (expected output).
   2. ref_snapshots/ -- the reference's own snapshot test data (packages/dds/sequence/src/test/
-     snapshots/{v1,legacy,legacyWithCatchUp}/*.json, data files the reference's snapshotVersion
-     spec loads; text, annotated text and markers) that fit the device, and expected.jsonl: the
+     snapshots/{v1,legacy,legacyWithCatchUp}/*.json, all 15 data files the reference's snapshotVersion
+     spec loads; text, a large body, annotated text and markers), and expected.jsonl: the
      reference loader's state after loading each and applying ref_followup.mtlog (the spec's
      edits -- NEWTEXT every 50 characters, a replace of everything, a remove of everything --
      as sequenced remote ops).
@@ -32,10 +32,9 @@ REF_SNAP = '/root/reference/packages/dds/sequence/src/test/snapshots'
 # (set, message index k, mergeTreeSnapshotChunkSize (0 = default))
 LOG_SETS = [('synth_tiny', 384, 0), ('synth_c3', 256, 300), ('synth_c4', 512, 0), ('scenarios', 3, 0),
             ('synth_c1', 1024, 400), ('markers', 4, 0), ('synth_markers', 320, 250)]
-# the fixtures within 64 KB of text (largeBody's single 88,890-character segment is not)
-REF_FILES = ['v1/headerOnly', 'v1/headerAndBody', 'v1/withAnnotations', 'v1/withMarkers', 'legacy/headerOnly',
-             'legacy/headerAndBody', 'legacy/withAnnotations', 'legacy/withMarkers', 'legacyWithCatchUp/headerAndBody',
-             'legacyWithCatchUp/withAnnotations', 'legacyWithCatchUp/withMarkers']
+# every data file snapshotVersion.spec.ts loads (sequence/src/test/snapshots/{v1,legacy,legacyWithCatchUp}/*)
+REF_FILES = [f'{v}/{k}' for v in ('v1', 'legacy', 'legacyWithCatchUp')
+             for k in ('headerOnly', 'headerAndBody', 'largeBody', 'withAnnotations', 'withMarkers')]
 
 
 def followup(length, seq0=0):
@@ -86,7 +85,7 @@ def main():
         res = subprocess.run(['node', replay, 'loadtree', src, logf], check=True, capture_output=True, text=True)
         r = json.loads(res.stdout)
         r['file'] = fn
-        r['loaded'] = st if 'withMarkers' not in fn else None  # (not device-representable: see the test)
+        r['loaded'] = st
         lines.append(json.dumps(r, separators=(',', ':')))
         print(fn, 'length', length, 'ops', log.n_ops, 'err', r['err'])
     with open(os.path.join(dst, 'expected.jsonl'), 'w') as f:

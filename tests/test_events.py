@@ -18,7 +18,8 @@ import pytest
 
 from conftest import GOLDEN, load_golden
 
-LOGS = ['scenarios', 'markers', 'errors', 'empty_inserts', 'synth_tiny', 'synth_c3', 'synth_c4', 'synth_markers']
+LOGS = ['scenarios', 'markers', 'errors', 'empty_inserts', 'synth_tiny', 'synth_c3', 'synth_c4', 'synth_markers', 'wide',
+        'wide_synth']
 
 
 def _golden_events():

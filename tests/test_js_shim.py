@@ -40,7 +40,7 @@ def _to_log_ids(state):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['scenarios', 'synth_c3', 'synth_tiny'])
+@pytest.mark.parametrize('name', ['scenarios', 'synth_c3', 'synth_tiny', 'wide', 'wide_synth'])
 def test_batchclient_replays_golden(name):
     assert _addon()
     _, exp = load_golden(name)
@@ -50,7 +50,9 @@ def test_batchclient_replays_golden(name):
     got = [json.loads(x) for x in out.stdout.strip().split('\n')]
     for r, e in zip(got, exp):
         assert r['text'] == e['text']
-        assert r['length'] == len(e['text'])
+        # getLength: UTF-16 code units of the live segments, a marker counting 1 (getText skips markers)
+        assert r['length'] == sum(1 if isinstance(sg[0], dict) else len(sg[0].encode('utf-16-le', 'surrogatepass')) // 2
+                                  for sg in e['state']['segs'] if sg[3] == -1)
         assert _to_log_ids(r['state']) == e['state'], (name, r['doc'])
 
 
@@ -140,7 +142,8 @@ def test_deli_reuses_short_ids_after_leave():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['scenarios', 'markers', 'errors', 'empty_inserts', 'synth_tiny', 'synth_c4'])
+@pytest.mark.parametrize('name', ['scenarios', 'markers', 'errors', 'empty_inserts', 'synth_tiny', 'synth_c4', 'wide',
+                                  'wide_synth'])
 def test_batchclient_delivers_reference_callbacks(name):
     """mergeTreeDeltaCallback / mergeTreeMaintenanceCallback on BatchClient (flushes every 40
     messages, 32 ops per launch) deliver exactly the callbacks the reference's own Client fired
@@ -194,8 +197,9 @@ def test_batchclient_loads_reference_snapshots(name):
 
 @pytest.mark.gpu
 def test_batchclient_loads_reference_snapshot_files():
-    """The reference's own snapshot test files (v1 / legacy / legacy with catch-up ops, header-only
-    and header + body, annotated) through BatchClient: the loaded state, then the spec's edits."""
+    """All 15 of the reference's own snapshot test files (v1 / legacy / legacy with catch-up ops;
+    header-only, header + body, large body, annotated, markers with a markerId each) through
+    BatchClient: the loaded state, then the spec's edits."""
     from test_snapshot_load import REF_DIR, err_code
     assert _addon()
     with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
@@ -205,7 +209,7 @@ def test_batchclient_loads_reference_snapshot_files():
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [json.loads(x) for x in out.stdout.strip().split('\n')]
-    assert len(lines) >= 6
+    assert len(lines) == 15
     for g in lines:
         c = cases[g['file']]
         assert _js_state_to_log(g['loaded']) == c['loaded'], g['file']

@@ -101,12 +101,12 @@ def translate_props(state, it):
     return out
 
 
-def ref_cases(representable=True):
-    """The reference snapshot files; representable=True: those the device holds (withMarkers gives
-    each of its 564 markers its own markerId value, past the 255 value ids of a document)."""
+def ref_cases():
+    """All 15 of the reference's snapshot data files (snapshotVersion.spec.ts): v1, legacy and legacy
+    with catch-up ops; header only, header + body, one 88,890-character segment, annotated, and
+    withMarkers (564 markers, each its own markerId value: a wide document, u16 value ids)."""
     with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
-        cases = [json.loads(x) for x in f if x.strip()]
-    return [c for c in cases if ('withMarkers' not in c['file']) == representable]
+        return [json.loads(x) for x in f if x.strip()]
 
 
 # ----------------------------------------------------------------------------------- CPU (oracle)
@@ -177,10 +177,19 @@ def test_engine_load_matches_reference(name, b):
             assert eng.state(d) == r['state'], (name, d)
 
 
+def test_all_reference_snapshot_files_are_covered():
+    """The fixture set holds every data file of sequence/src/test/snapshots (15 files)."""
+    files = {c['file'] for c in ref_cases()}
+    assert len(files) == 15
+    assert {f.split('_', 1)[1] for f in files} == {'headerOnly.json', 'headerAndBody.json', 'largeBody.json',
+                                                   'withAnnotations.json', 'withMarkers.json'}
+
+
 @pytest.mark.gpu
 def test_engine_loads_reference_snapshot_files(oracle_lib):
-    """All the reference's text-only snapshot files in one engine (one document each, loaded in one
-    mt_docs_load + one body batch), then the spec's edits; checksums against the oracle too."""
+    """All 15 of the reference's snapshot files in one engine (one document each, loaded in one
+    mt_docs_load + one body batch), then the spec's edits; states equal to the reference loader's
+    (snapshotLoader.ts:35-225) after the load and after the edits."""
     from fluidframework_amd import snapshot
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import OpBatch
@@ -189,8 +198,9 @@ def test_engine_loads_reference_snapshot_files(oracle_lib):
     for c in cases:
         with open(os.path.join(REF_DIR, c['file'])) as f:
             trees.append(json.load(f))
-    # (a 38,890-character document whose appends copy runs of up to its whole text: a larger arena)
-    eng = MergeEngine(len(cases), ops_per_launch=32, text_capacity=256 * 1024)
+    # (an 88,890-character segment, and documents whose appends copy runs of up to their whole text:
+    # a larger arena; the follow-up edits split the large bodies into a few thousand segments)
+    eng = MergeEngine(len(cases), ops_per_launch=32, text_capacity=512 * 1024, seg_capacity=8192)
     its, catchup = snapshot.load_docs(eng, trees)
     assert all(x == [] for x in catchup)
     for d, c in enumerate(cases):

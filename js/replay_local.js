@@ -26,6 +26,10 @@ function tuple(op) {
 
 const log = loadLog(process.argv[2]);
 const withEvents = process.argv[3] === "events";
+// "seqdelta": SequenceDeltaEvents (js/sequenceDeltaEvent.js) from a "sequenceDelta" listener, one record
+// per event in replay_ref.js's seqdelta form
+const withSeqDelta = process.argv[3] === "seqdelta";
+const { SequenceEvents } = require("./sequenceDeltaEvent.js");
 const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16 });
 const sortKeys = (pd) => {
     const o = {};
@@ -48,6 +52,16 @@ for (let d = 0; d < log.nDocs; d++) {
             args.deltaSegments.map((x) => seg(x, args.operation === 2 && x.propertyDeltas ? sortKeys(x.propertyDeltas) : null))]);
         c.mergeTreeMaintenanceCallback = (args) => c.events.push([args.sequenceNumber, args.operation,
             args.deltaSegments.map((x) => seg(x, null))]);
+    }
+    if (withSeqDelta) {
+        const seqEvents = new SequenceEvents(c);
+        seqEvents.on("sequenceDelta", (ev) => {
+            const ranges = ev.ranges.map((r) => [r.operation, r.segment.ordinal, r.position, r.segment.cachedLength,
+                r.propertyDeltas ? sortKeys(r.propertyDeltas) : null]);
+            const m = ev.opArgs.sequencedMessage;
+            c.events.push([m ? m.sequenceNumber : -1, ev.deltaOperation, ev.isLocal, ev.isEmpty, ev.clientId, ranges,
+                ev.first ? ev.first.segment.ordinal : null, ev.last ? ev.last.segment.ordinal : null]);
+        });
     }
     for (const it of items) {
         if (it.regen) {  // reconnect: the op to resubmit, as record tuples
@@ -79,7 +93,7 @@ const out = clients.map((c, d) => {
     let err = null, state = null;
     try { state = c.getState(); } catch (e) { err = String(e.message || e); }
     const line = c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state };
-    if (withEvents) line.events = c.events;
+    if (withEvents || withSeqDelta) line.events = c.events;
     return JSON.stringify(line);
 });
 process.stdout.write(out.join("\n") + "\n");

@@ -3,7 +3,8 @@
 
 TEST INFRASTRUCTURE ONLY (see oracle/README.md).  Type-strips (tsstrip.py) exactly the
 reference files the observer apply path needs -- packages/dds/merge-tree/src/*.ts and its
-test harness (TestClient, farm runner, the unit-test specs) -- plus the two helpers it uses
+test harness (TestClient, farm runner, the unit-test specs), and the sequence package's
+SequenceDeltaEvent (sequenceDeltaEvent.ts, the delta-event wrapper) -- plus the two helpers it uses
 from @fluidframework/common-utils (assert.ts:12-16, trace.ts:12-31), the protocol enums
 (protocol-definitions/src/protocol.ts) and test-runtime-utils' MockStorage.  Everything else
 the imports name (loggers, container enums, base64, random-js for the farm specs) gets a small
@@ -70,6 +71,15 @@ exports.listBlobsAtTreePath = async function (tree, path) {
   }
   return t.entries.filter((e) => e.type === "Blob").map((e) => e.path);
 };
+''',
+    # the sequence package's SequenceDeltaEvent (sequenceDeltaEvent.ts) imports the merge-tree by name
+    'node_modules/@fluidframework/merge-tree/index.js': r'''
+"use strict";
+module.exports = require("../../../merge-tree/src/index.js");
+''',
+    'node_modules/@fluidframework/merge-tree/dist/test/index.js': r'''
+"use strict";
+module.exports = require("../../../../../merge-tree/src/test/index.js");
 ''',
     'node_modules/@fluidframework/test-runtime-utils/index.js': r'''
 "use strict";
@@ -161,6 +171,10 @@ def main():
     for name in sorted(os.listdir(os.path.join(MT, 'test'))):
         if name.endswith('.ts'):
             strip_to(os.path.join(MT, 'test', name), os.path.join(OUT, 'merge-tree/src/test', name[:-3] + '.js'))
+    strip_to(os.path.join(REF, 'packages/dds/sequence/src/sequenceDeltaEvent.ts'),
+             os.path.join(OUT, 'sequence/src/sequenceDeltaEvent.js'))
+    strip_to(os.path.join(REF, 'packages/dds/sequence/src/test/sequenceDeltaEvent.spec.ts'),
+             os.path.join(OUT, 'sequence/src/test/sequenceDeltaEvent.spec.js'))
     cu = os.path.join(REF, 'common/lib/common-utils/src')
     strip_to(os.path.join(cu, 'assert.ts'), os.path.join(OUT, 'node_modules/@fluidframework/common-utils/assert.js'))
     strip_to(os.path.join(cu, 'trace.ts'), os.path.join(OUT, 'node_modules/@fluidframework/common-utils/trace.js'))

@@ -423,6 +423,77 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "seqdelta") {
+        // SequenceDeltaEvent (packages/dds/sequence/src/sequenceDeltaEvent.ts, transpiled) around every
+        // delta callback of the document's client (an editing client for a local_* log, else the
+        // observer), its ranges read inside the listener as SharedString users do: one record per
+        // event [seq (-1: local edit), deltaOperation, isLocal, isEmpty, clientId, [[operation, leaf,
+        // position, cachedLength, propertyDeltas | null], ...], first leaf | null, last leaf | null]
+        const { SequenceDeltaEvent } = require(path.join(__dirname, "..", "_tsref", "sequence", "src",
+            "sequenceDeltaEvent.js"));
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const items = [...messages(log, d)];
+            const own = items.find((x) => x.local);
+            const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+            const c = new Client(specToSegment, logger);
+            c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+            const seqRef = { seq: 0 };
+            const leafOf = (seg) => {
+                let ord = 0, found = -1;
+                const walk = (b) => {
+                    for (let i = 0; i < b.childCount && found < 0; i++) {
+                        const ch = b.children[i];
+                        if (!ch.isLeaf()) { walk(ch); continue; }
+                        if (ch.parent === undefined) continue;
+                        if (ch === seg) { found = ord; return; }
+                        ord++;
+                    }
+                };
+                walk(c.mergeTree.root);
+                return found;
+            };
+            const pdelta = (pd) => {
+                if (!pd) return null;
+                const o = {};
+                for (const k of Object.keys(pd).sort((a, b) => parseInt(a.slice(1)) - parseInt(b.slice(1)))) {
+                    o[k] = pd[k] === undefined ? null : pd[k];
+                }
+                return o;
+            };
+            const events = [];
+            c.mergeTreeDeltaCallback = (opArgs, deltaArgs) => {
+                const ev = new SequenceDeltaEvent(opArgs, deltaArgs, c);
+                const ranges = ev.ranges.map((r) => [r.operation, leafOf(r.segment), r.position, r.segment.cachedLength,
+                    pdelta(r.propertyDeltas)]);
+                events.push([seqRef.seq, ev.deltaOperation, ev.isLocal, ev.isEmpty, ev.clientId, ranges,
+                    ev.first ? leafOf(ev.first.segment) : null, ev.last ? leafOf(ev.last.segment) : null]);
+            };
+            let err = null;
+            try {
+                for (const it of items) {
+                    if (it.regen) {
+                        seqRef.seq = -2;
+                        c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+                    } else if (it.local) {
+                        seqRef.seq = -1;
+                        const op = it.op;
+                        if (op.type === 0) c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                        else if (op.type === 1) c.removeRangeLocal(op.pos1, op.pos2);
+                        else c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+                    } else {
+                        seqRef.seq = it.sequenceNumber;
+                        c.applyMsg(it);
+                    }
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            out.push(JSON.stringify({ doc: d, err, events }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "stacks") {
         // getStackContext (client.ts:946-948, mergeTree.ts:1750-1760): the NestBegin / NestEnd stack of
         // each label L0..L3 at a spread of positions, range labels on key <rangeKey>; each stack as

@@ -5,7 +5,8 @@ const path = require("path");
 const root = path.join(__dirname, "..", "_tsref");
 const shim = require(path.join(root, "mocha_shim.js"));
 const names = process.argv.slice(2);
-const files = names.map((n) => path.join(root, "merge-tree/src/test", n.endsWith(".js") ? n : n + ".js"));
+// (a name with a "/" is relative to oracle/_tsref, e.g. sequence/src/test/sequenceDeltaEvent.spec)
+const files = names.map((n) => path.join(root, n.includes("/") ? "" : "merge-tree/src/test", n.endsWith(".js") ? n : n + ".js"));
 shim.run(files).then((res) => {
   let pass = 0, fail = 0, skip = 0;
   for (const r of res) {

@@ -289,3 +289,87 @@ def test_batchclient_editing_client_callbacks_match_reference(name):
             assert ev == g['events'], (name, g['doc'])
         assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
             g['sha256'], (name, g['doc'])
+
+
+SEQDELTA_LOGS = ['seqdelta', 'local_rounds', 'local_lag', 'local_big', 'local_markers', 'local_reconnect', 'scenarios',
+                 'markers', 'wide', 'synth_c1']
+
+
+def _seqdelta_gold():
+    with open(os.path.join(GOLDEN, 'seqdelta.expected.jsonl')) as f:
+        return [json.loads(x) for x in f if x.strip()]
+
+
+def test_seqdelta_fixture_covers_the_spec():
+    """tests/golden/seqdelta.expected.jsonl holds the reference's SequenceDeltaEvents for every `it` of
+    sequenceDeltaEvent.spec.ts (59 documents) and for the editing / observer logs; spot-check facts the
+    spec asserts (positions after a concurrent remote edit, two ranges for a split removal)."""
+    gold = _seqdelta_gold()
+    assert {g['log'] for g in gold} == set(SEQDELTA_LOGS)
+    spec = [g for g in gold if g['log'] == 'seqdelta']
+    assert len(spec) == 59 and all(g['err'] is None for g in spec)
+    # collab insert "separate regions, local before remote": the remote insert lands at 23 + 12
+    ev = spec[3]['events']
+    assert ev[1][2] is True and ev[1][5] == [[0, 1, 4, 12, None]]
+    assert ev[2][2] is False and ev[2][5][0][2] == 35 and ev[2][5][0][3] == 5
+    # combination "insertPos is deleteRangeStart, insertLocal deleteRemote": "brown " and "fox " as two ranges
+    two = [e for g in spec for e in g['events'] if e[1] == 1 and len(e[5]) == 2 and e[5][0][3] == 6 and e[5][1][3] == 4]
+    assert two and two[0][5][1][2] == 4 + 11
+    # .ranges "multiple noncontinuous segments": the remote remove's five ranges at 4, 8, ..., 20
+    last = spec[-1]['events'][-1]
+    assert last[2] is False and [r[2] for r in last[5]] == [4, 8, 12, 16, 20]
+
+
+def test_sequence_events_install_and_remove_callbacks():
+    """SequenceEvents (js/sequenceDeltaEvent.js) installs the client's callback with the first listener,
+    wraps each callback in a SequenceDeltaEvent (ranges sorted by ordinal, one per segment, isLocal
+    without a sequenced message) and uninstalls with the last listener -- no device needed."""
+    src = r"""
+const { SequenceEvents, SequenceDeltaEvent } = require('./js/sequenceDeltaEvent.js');
+const client = { longClientId: 'c7' };
+const seq = new SequenceEvents(client);
+if (client.mergeTreeDeltaCallback) throw 'installed early';
+const seen = [];
+const fn = (ev) => seen.push(ev);
+seq.on('sequenceDelta', fn);
+const s = (ordinal, position, cachedLength) => ({ ordinal, position, cachedLength });
+client.mergeTreeDeltaCallback({ sequencedMessage: undefined }, { operation: 2, deltaSegments: [
+    { segment: s(5, 9, 2), propertyDeltas: { k0: null } }, { segment: s(3, 4, 1), propertyDeltas: { k0: 1 } },
+    { segment: s(5, 9, 2), propertyDeltas: { k0: 7 } }] });
+client.mergeTreeDeltaCallback({ sequencedMessage: { sequenceNumber: 4 } }, { operation: 1, deltaSegments: [] });
+const [a, b] = seen;
+if (!(a instanceof SequenceDeltaEvent) || !a.isLocal || a.isEmpty || a.clientId !== 'c7') throw 'event a';
+if (a.ranges.map((r) => r.segment.ordinal).join() !== '3,5' || a.first.position !== 4 || a.last.position !== 9) throw 'ranges';
+if (a.ranges[1].propertyDeltas.k0 !== null || a.ranges[0].operation !== 2) throw 'first range per segment';
+if (b.isLocal || !b.isEmpty || b.first !== undefined || b.deltaOperation !== 1) throw 'event b';
+seq.off('sequenceDelta', fn);
+if (client.mergeTreeDeltaCallback) throw 'not uninstalled';
+console.log('ok');
+"""
+    out = subprocess.run([NODE, '-e', src], cwd=REPO, capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == 'ok', out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', SEQDELTA_LOGS)
+def test_batchclient_sequence_delta_events_match_reference(name):
+    """SequenceDeltaEvents ("sequenceDelta" listeners of js/sequenceDeltaEvent.js over an editing or
+    observer BatchClient): operation, isLocal, isEmpty, clientId, every range's leaf / position /
+    cachedLength / propertyDeltas and first / last, read in the listener -- the reference's
+    SequenceDeltaEvent over the reference client (tests/golden/seqdelta.expected.jsonl; seqdelta.mtlog is
+    sequenceDeltaEvent.spec.ts re-expressed as logs)."""
+    import hashlib
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          'seqdelta'], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    gold = [g for g in _seqdelta_gold() if g['log'] == name]
+    assert gold
+    for g in gold:
+        ev = got[g['doc']]['events']
+        if 'events' in g:
+            assert ev == g['events'], (name, g['doc'])
+        else:
+            assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+                g['sha256'], (name, g['doc'])

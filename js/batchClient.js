@@ -504,6 +504,117 @@ class BatchClient {
         return st;
     }
 
+    // ---- the read surface over the applied state (client.ts:275-311, 838-847, 1004-1040) --------
+    // A segment is a plain descriptor of the state it was read from -- {ordinal, position (local
+    // view), cachedLength, seq, clientId, removedSeq, removedClientId (short ids), properties,
+    // text | refType} -- named by its ordinal (its index among the document's linked segments): the
+    // device keeps no segment objects, so a descriptor is valid until the document next changes.
+    _segments() {
+        const st = this.getState();
+        let pos = 0;
+        return st.segs.map((s, i) => {
+            const marker = s[0] !== null && typeof s[0] === "object";
+            const len = marker ? 1 : s[0].length;
+            const removed = s[4] !== -1;
+            const d = { ordinal: i, position: pos, cachedLength: len, seq: s[1],
+                clientId: typeof s[2] === "string" ? this._shortId(s[2]) : s[2],
+                removedSeq: removed ? s[3] : undefined, removedClientId: removed ? this._shortId(s[4]) : undefined,
+                removedClientOverlap: s[5].length ? s[5].map((x) => this._shortId(x)) : undefined,
+                properties: s[6] || undefined };
+            if (marker) d.refType = s[0].marker; else d.text = s[0];
+            if (!removed) pos += len;
+            return d;
+        });
+    }
+    // nodeLength of a leaf (mergeTree.ts:1659-1697): the local view (localNetLength) or a remote
+    // client's view at refSeq
+    static _viewLength(d, refSeq, clientId, local) {
+        const removed = d.removedSeq !== undefined;
+        if (local) return removed ? 0 : d.cachedLength;
+        if (!(d.clientId === clientId || (d.seq !== -1 && d.seq <= refSeq))) return 0;
+        if (removed && (d.removedClientId === clientId || (d.removedClientOverlap || []).includes(clientId) ||
+            (d.removedSeq !== -1 && d.removedSeq <= refSeq))) return 0;
+        return d.cachedLength;
+    }
+    _containing(segs, pos, refSeq, clientId, local) {  // MergeTree.getContainingSegment (mergeTree.ts:1623-1634)
+        for (const d of segs) {
+            const len = BatchClient._viewLength(d, refSeq, clientId, local);
+            if (pos < len) return { segment: d, offset: pos };
+            pos -= len;
+        }
+        return { segment: undefined, offset: undefined };
+    }
+    /** Client.getContainingSegment (client.ts:1004-1007): {segment, offset} in the local view. */
+    getContainingSegment(pos) { return this._containing(this._segments(), pos, 0, 0, true); }
+    /** Client.getPropertiesAtPosition (client.ts:1009-1023). */
+    getPropertiesAtPosition(pos) {
+        const seg = this.getContainingSegment(pos).segment;
+        return seg ? seg.properties : undefined;
+    }
+    /** Client.getRangeExtentsOfPosition (client.ts:1024-1040). */
+    getRangeExtentsOfPosition(pos) {
+        const seg = this.getContainingSegment(pos).segment;
+        return seg ? { posStart: seg.position, posAfterEnd: seg.position + seg.cachedLength }
+            : { posStart: undefined, posAfterEnd: undefined };
+    }
+    /** Client.getPosition (client.ts:290-292): the local-view position of the segment (by ordinal). */
+    getPosition(segment) {
+        const segs = this._segments();
+        const d = segs[segment.ordinal];
+        return d ? d.position : 0;
+    }
+    /**
+     * Client.walkSegments (client.ts:275-284, MergeTree.mapRange / nodeMap mergeTree.ts:2903-2960):
+     * handler(segment, pos, refSeq, clientId, start, end, accum) for every segment of the local view
+     * overlapping [start, end) (start / end relative to the segment), until it returns a falsy value.
+     * splitRange (which splits segments in place) is not supported.
+     */
+    walkSegments(handler, start, end, accum, splitRange = false) {
+        if (splitRange) throw new Error("BatchClient.walkSegments: splitRange is not supported");
+        const segs = this._segments();
+        if (start === undefined) start = 0;
+        if (end === undefined) end = segs.reduce((a, d) => a + (d.removedSeq === undefined ? d.cachedLength : 0), 0);
+        let pos = 0;
+        for (const d of segs) {
+            const len = d.removedSeq === undefined ? d.cachedLength : 0;
+            if (end > 0 && len > 0 && start < len && !handler(d, pos, this.currentSeq, this.getClientId(), start, end, accum)) {
+                break;
+            }
+            pos += len;
+            start -= len;
+            end -= len;
+        }
+    }
+    /**
+     * Client.getMarkerFromId (client.ts:311-313): the marker whose "markerId" property is id.  The
+     * reference's id map keeps markers after their removal; here a removed marker is found while it
+     * is still in the document (until zamboni unlinks it), a live one first.
+     */
+    getMarkerFromId(id) {
+        let found;
+        for (const d of this._segments()) {
+            if (d.refType !== undefined && d.properties && d.properties.markerId === id &&
+                (found === undefined || d.removedSeq === undefined || found.removedSeq !== undefined)) {
+                found = d;
+            }
+        }
+        return found;
+    }
+    /**
+     * Client.resolveRemoteClientPosition (client.ts:838-847, mergeTree.ts:2105-2127): a remote
+     * client's position at its refSeq, as a local position (undefined past its length).
+     */
+    resolveRemoteClientPosition(remoteClientPosition, remoteClientRefSeq, remoteClientId) {
+        const cid = this._shortId(remoteClientId);
+        const local = cid === this._shortId(this.longClientId);  // (nodeLength: the own client sees the local view)
+        const segs = this._segments();
+        const r = this._containing(segs, remoteClientPosition, remoteClientRefSeq, cid, local);
+        if (r.segment) return r.segment.position + r.offset;
+        const rlen = segs.reduce((a, d) => a + BatchClient._viewLength(d, remoteClientRefSeq, cid, local), 0);
+        if (remoteClientPosition === rlen) return segs.reduce((a, d) => a + BatchClient._viewLength(d, 0, 0, true), 0);
+        return undefined;
+    }
+
     // ---- TestClient helpers (src/test/testClient.ts:112-234) --------------------------------
     makeOpMessage(op, seq = -1, refSeq = this.currentSeq, longClientId, minSeqNumber = 0) {
         return { clientId: longClientId === undefined ? this.longClientId : longClientId, clientSequenceNumber: 1,
@@ -513,6 +624,12 @@ class BatchClient {
     }
     insertTextRemote(pos, text, props, seq, refSeq, longClientId) {
         const seg = props ? { text, props } : text;
+        this.applyMsg(this.makeOpMessage({ type: INSERT, pos1: pos, seg }, seq, refSeq, longClientId));
+    }
+    /** TestClient.insertMarkerRemote (testClient.ts:190-207). */
+    insertMarkerRemote(pos, markerDef, props, seq, refSeq, longClientId) {
+        const seg = { marker: { refType: markerDef.refType } };
+        if (props) seg.props = props;
         this.applyMsg(this.makeOpMessage({ type: INSERT, pos1: pos, seg }, seq, refSeq, longClientId));
     }
     removeRangeRemote(start, end, seq, refSeq, longClientId) {

@@ -64,6 +64,33 @@ if (mode === "sets") {
         return JSON.stringify({ file: c.file, loaded: loaded[i], err, state: clients[i].getState() });
     });
     process.stdout.write(out.join("\n") + "\n");
+} else if (mode === "markers") {
+    // getMarkerFromId (client.ts:311-313) after loading the reference's snapshot files: every markerId
+    // of the loaded state, then an id that is not there; lines {file, found: [[id, ordinal, position,
+    // refType] | [id, null], ...]}
+    const cases = readJsonl(process.argv[3]);
+    const dir = process.argv[4];
+    const eng = new BatchEngine({ maxDocs: cases.length, opsPerLaunch: 32, textCapacity: 512 * 1024, segCapacity: 8192 });
+    const clients = cases.map(() => {
+        const c = eng.createClient();
+        c.startOrUpdateCollaboration("observer");
+        return c;
+    });
+    loadSnapshots(eng, cases.map((c, i) => ({ client: clients[i],
+        snapshot: JSON.parse(fs.readFileSync(path.join(dir, c.file), "utf8")) })));
+    const out = cases.map((c, i) => {
+        const ids = [];
+        for (const s of clients[i].getState().segs) {
+            if (s[0] !== null && typeof s[0] === "object" && s[6] && s[6].markerId !== undefined) ids.push(s[6].markerId);
+        }
+        ids.push("no such marker");
+        const found = ids.map((id) => {
+            const m = clients[i].getMarkerFromId(id);
+            return m ? [id, m.ordinal, clients[i].getPosition(m), m.refType] : [id, null];
+        });
+        return JSON.stringify({ file: c.file, found });
+    });
+    process.stdout.write(out.join("\n") + "\n");
 } else {
-    throw new Error("mode: sets | files");
+    throw new Error("mode: sets | files | markers");
 }

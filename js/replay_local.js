@@ -29,6 +29,8 @@ const withEvents = process.argv[3] === "events";
 // "seqdelta": SequenceDeltaEvents (js/sequenceDeltaEvent.js) from a "sequenceDelta" listener, one record
 // per event in replay_ref.js's seqdelta form
 const withSeqDelta = process.argv[3] === "seqdelta";
+// "read": the read surface over each document's final state, in replay_ref.js's read form
+const withRead = process.argv[3] === "read";
 const { SequenceEvents } = require("./sequenceDeltaEvent.js");
 const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16 });
 const sortKeys = (pd) => {
@@ -63,7 +65,9 @@ for (let d = 0; d < log.nDocs; d++) {
                 ev.first ? ev.first.segment.ordinal : null, ev.last ? ev.last.segment.ordinal : null]);
         });
     }
+    c.remoteIds = new Set();
     for (const it of items) {
+        if (!it.local && !it.regen) c.remoteIds.add(it.clientId);
         if (it.regen) {  // reconnect: the op to resubmit, as record tuples
             const op = c.regeneratePendingOp(it.op);
             regen.push([it.index, (op.type === 3 ? op.ops : [op]).map(tuple)]);
@@ -89,7 +93,52 @@ for (let d = 0; d < log.nDocs; d++) {
     c.regen = regen;
     clients.push(c);
 }
+function readSurface(c, d) {
+    const pset = (seg) => (seg && seg.properties ? sortKeys(seg.properties) : null);
+    const len = c.getLength();
+    const positions = [];
+    const stride = Math.max(1, Math.floor((len + 2) / 48));
+    for (let p = 0; p <= len + 1; p += stride) positions.push(p);
+    if (positions[positions.length - 1] !== len) positions.push(len);
+    const contain = positions.map((p) => {
+        const r = c.getContainingSegment(p);
+        return r.segment ? [r.segment.ordinal, r.offset] : null;
+    });
+    const props = positions.map((p) => pset(c.getContainingSegment(p).segment));
+    const extents = positions.map((p) => {
+        const e = c.getRangeExtentsOfPosition(p);
+        return [e.posStart === undefined ? null : e.posStart, e.posAfterEnd === undefined ? null : e.posAfterEnd];
+    });
+    const walks = [];
+    for (const [a, b, stop] of [[undefined, undefined, 0], [Math.floor(len / 3), Math.floor((2 * len) / 3) + 1, 0],
+        [1, len, 3], [len, len + 5, 0]]) {
+        const calls = [];
+        c.walkSegments((seg, pos, refSeq, clientId, start, end) => {
+            calls.push([seg.ordinal, pos, start, end]);
+            return stop === 0 || calls.length < stop;
+        }, a, b);
+        walks.push(calls);
+    }
+    const getpos = c._segments().map((seg) => c.getPosition(seg));
+    const remote = [];
+    const seq = c.getCurrentSeq();
+    for (const id of [...c.remoteIds].sort().slice(0, 4)) {
+        for (const refSeq of (c.longClientId !== "observer") ? [seq] : [Math.max(c.getState().msn, seq - 5), seq]) {
+            const cid = c._shortId(id);
+            const local = cid === c._shortId(c.longClientId);
+            const rl = c._segments().reduce((acc, x) => acc + c.constructor._viewLength(x, refSeq, cid, local), 0);
+            for (const p of [0, Math.floor(rl / 2), rl, rl + 1]) {
+                const r = c.resolveRemoteClientPosition(p, refSeq, id);
+                remote.push([id, refSeq, p, r === undefined ? null : r]);
+            }
+        }
+    }
+    return { doc: d, err: null, len, positions, contain, props, extents, walks, getpos, remote };
+}
 const out = clients.map((c, d) => {
+    if (withRead) {
+        try { return JSON.stringify(readSurface(c, d)); } catch (e) { return JSON.stringify({ doc: d, err: String(e.message || e) }); }
+    }
     let err = null, state = null;
     try { state = c.getState(); } catch (e) { err = String(e.message || e); }
     const line = c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state };

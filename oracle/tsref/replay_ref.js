@@ -494,6 +494,99 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "read") {
+        // the client's read surface over its final state (client.ts:275-311, 838-847, 1004-1040):
+        // getContainingSegment / getPropertiesAtPosition / getRangeExtentsOfPosition at a spread of
+        // positions, walkSegments over a few ranges, getPosition of every leaf and
+        // resolveRemoteClientPosition for a few (pos, refSeq, client) -- segments as their leaf ordinal
+        const out = [];
+        for (let d = 0; d < log.nDocs; d++) {
+            const items = [...messages(log, d)];
+            const own = items.find((x) => x.local);
+            const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+            const c = new Client(specToSegment, logger);
+            c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+            let err = null;
+            const clients = new Set();
+            try {
+                for (const it of items) {
+                    if (it.regen) {
+                        c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+                    } else if (it.local) {
+                        const op = it.op;
+                        if (op.type === 0) c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                        else if (op.type === 1) c.removeRangeLocal(op.pos1, op.pos2);
+                        else c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+                    } else {
+                        c.applyMsg(it);
+                        clients.add(it.clientId);
+                    }
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            if (err) {
+                out.push(JSON.stringify({ doc: d, err }));
+                continue;
+            }
+            const leaves = [];
+            const walk = (b) => {
+                for (let i = 0; i < b.childCount; i++) {
+                    const ch = b.children[i];
+                    if (!ch.isLeaf()) walk(ch); else leaves.push(ch);
+                }
+            };
+            walk(c.mergeTree.root);
+            const ord = (seg) => leaves.indexOf(seg);
+            const pset = (seg) => {
+                if (!seg || !seg.properties) return null;
+                const o = {};
+                for (const k of Object.keys(seg.properties).sort((a, b) => parseInt(a.slice(1)) - parseInt(b.slice(1)))) {
+                    o[k] = seg.properties[k] === undefined ? null : seg.properties[k];
+                }
+                return o;
+            };
+            const len = c.getLength();
+            const positions = [];
+            const stride = Math.max(1, Math.floor((len + 2) / 48));
+            for (let p = 0; p <= len + 1; p += stride) positions.push(p);
+            if (positions[positions.length - 1] !== len) positions.push(len);
+            const contain = positions.map((p) => {
+                const r = c.getContainingSegment(p);
+                return r.segment ? [ord(r.segment), r.offset] : null;
+            });
+            const props = positions.map((p) => pset(c.getContainingSegment(p).segment));
+            const extents = positions.map((p) => {
+                const e = c.getRangeExtentsOfPosition(p);
+                return [e.posStart === undefined ? null : e.posStart, e.posAfterEnd === undefined ? null : e.posAfterEnd];
+            });
+            const walks = [];
+            for (const [a, b, stop] of [[undefined, undefined, 0], [Math.floor(len / 3), Math.floor((2 * len) / 3) + 1, 0],
+                [1, len, 3], [len, len + 5, 0]]) {
+                const calls = [];
+                c.walkSegments((seg, pos, refSeq, clientId, start, end) => {
+                    calls.push([ord(seg), pos, start, end]);
+                    return stop === 0 || calls.length < stop;
+                }, a, b);
+                walks.push(calls);
+            }
+            const getpos = leaves.map((seg) => c.getPosition(seg));
+            const remote = [];
+            const seq = c.getCurrentSeq();
+            for (const id of [...clients].sort().slice(0, 4)) {
+                for (const refSeq of (own) ? [seq] : [Math.max(c.getCollabWindow().minSeq, seq - 5), seq]) {
+                    const rl = c.mergeTree.getLength(refSeq, c.getOrAddShortClientId(id));
+                    for (const p of [0, Math.floor(rl / 2), rl, rl + 1]) {
+                        const r = c.resolveRemoteClientPosition(p, refSeq, id);
+                        remote.push([id, refSeq, p, r === undefined ? null : r]);
+                    }
+                }
+            }
+            out.push(JSON.stringify({ doc: d, err, len, positions, contain, props, extents, walks, getpos, remote }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "stacks") {
         // getStackContext (client.ts:946-948, mergeTree.ts:1750-1760): the NestBegin / NestEnd stack of
         // each label L0..L3 at a spread of positions, range labels on key <rangeKey>; each stack as

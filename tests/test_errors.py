@@ -83,7 +83,7 @@ def _engine(n, b, engine=None):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('engine', [None, 'lds'])
-@pytest.mark.parametrize('b', [0, 2])
+@pytest.mark.parametrize('b', [0, 2, 7, 32])  # 32: the production ops-per-launch (errors mid-launch, fixup after)
 @pytest.mark.parametrize('fixture', FIXTURES)
 def test_engine_matches_reference_errors(engine, b, fixture):
     batch, exp = load_golden(fixture)

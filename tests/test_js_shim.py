@@ -373,3 +373,79 @@ def test_batchclient_sequence_delta_events_match_reference(name):
         else:
             assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
                 g['sha256'], (name, g['doc'])
+
+
+READ_LOGS = ['scenarios', 'markers', 'synth_markers', 'wide', 'synth_c1', 'local_lag', 'local_markers',
+             'local_reconnect']
+
+
+def _read_gold():
+    with open(os.path.join(GOLDEN, 'read.expected.jsonl')) as f:
+        return [json.loads(x) for x in f if x.strip()]
+
+
+def test_read_fixture_covers_logs():
+    gold = _read_gold()
+    assert {g['log'] for g in gold} == set(READ_LOGS)
+    full = [g for g in gold if 'contain' in g]
+    assert full and all(g['err'] is None for g in full)
+    # the fixture exercises misses (positions past the end), props, stopped walks and unresolvable
+    # remote positions
+    assert any(x is None for g in full for x in g['contain'])
+    assert any(x is not None for g in full for x in g['props'])
+    assert any(len(g['walks'][2]) == 3 for g in full)
+    assert any(r[3] is None for g in full for r in g['remote'])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', READ_LOGS)
+def test_batchclient_read_surface_matches_reference(name):
+    """getContainingSegment / getPropertiesAtPosition / getRangeExtentsOfPosition, walkSegments,
+    getPosition and resolveRemoteClientPosition on BatchClient over the device state equal the
+    reference client's on the same logs (tests/golden/read.expected.jsonl, make_read.py)."""
+    import hashlib
+    assert _addon()
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          'read'], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    gold = [g for g in _read_gold() if g['log'] == name]
+    assert gold
+    for g in gold:
+        r = got[g['doc']]
+        if 'sha256' in g:
+            assert hashlib.sha256(json.dumps(r, separators=(',', ':')).encode()).hexdigest() == g['sha256'], \
+                (name, g['doc'])
+        else:
+            e = {k: v for k, v in g.items() if k != 'log'}
+            for k in e:
+                assert r[k] == e[k], (name, g['doc'], k)
+
+
+@pytest.mark.gpu
+def test_batchclient_get_marker_from_id_on_reference_snapshots():
+    """getMarkerFromId (client.ts:311-313) after loading the reference's withMarkers snapshots (564
+    markers, each with its markerId): every id resolves to its marker at its position in the
+    reference loader's state; an unknown id to undefined."""
+    from test_snapshot_load import REF_DIR
+    assert _addon()
+    with open(os.path.join(REF_DIR, 'expected.jsonl')) as f:
+        cases = {c['file']: c for c in (json.loads(x) for x in f if x.strip())}
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_load.js'), 'markers',
+                          os.path.join(REF_DIR, 'expected.jsonl'), REF_DIR], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    n_markers = 0
+    for g in (json.loads(x) for x in out.stdout.strip().split('\n')):
+        segs = cases[g['file']]['loaded']['segs']
+        exp, pos = [], 0
+        for i, s in enumerate(segs):
+            live = s[4] == -1
+            if isinstance(s[0], dict) and s[6] and 'markerId' in s[6]:
+                exp.append([s[6]['markerId'], i, pos, s[0]['marker']])
+            if live:
+                pos += 1 if isinstance(s[0], dict) else len(s[0].encode('utf-16-le', 'surrogatepass')) // 2
+        exp.append(['no such marker', None])
+        assert g['found'] == exp, g['file']
+        n_markers += len(exp) - 1
+    assert n_markers >= 3 * 564

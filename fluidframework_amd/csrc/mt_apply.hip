@@ -84,6 +84,8 @@ struct Lds {
     uint64_t pxl[W ? CAP : 1];
     uint64_t pxh[W ? CAP : 1];
     uint32_t wide;                // the document's mt_doc_scalars.wide bits
+    uint32_t lkeys;               // its declared label keys (mt_doc_scalars.label_keys)
+    uint32_t slab[CAP];           // a stale marker's cached label value ids (mt_gstate.slab)
 };
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
@@ -197,6 +199,33 @@ struct Wave {
         for (int q = 0; q < pr.np; q++) pset(sl, pr.key(q), pr.val(q));
     }
     static constexpr int kKeys = W ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS;
+
+    // ------------------------------------------------------------ block caches
+    // The HierMergeBlock label caches (rightmostTiles / leftmostTiles / rangeStacks, mergeTree.ts:
+    // 263-318) of a document with declared label keys (mt_set_label_keys): blockUpdate rebuilds a
+    // leaf block's from its live markers' labels; annotateRange changes labels without one
+    // (mergeTree.ts:2565-2605).  A marker annotated since its leaf block's last rebuild is "stale":
+    // its flags carry MT_SF_STALE and slab the tile / range label value ids the caches still hold.
+    MT_DEV bool track() const { return s.lkeys != MT_NO_LABEL_KEYS; }
+    // (lane-parallel, before an annotate changes the slot's props)
+    MT_DEV void mark_stale(int sl) {
+        const uint8_t f = s.flags[sl];
+        if ((f & MT_SF_MARKER) && !(f & MT_SF_STALE)) {
+            const uint32_t kt = s.lkeys & 0xFFu, kr = (s.lkeys >> 8) & 0xFFu;
+            const bool def = (f & MT_SF_PDEF) != 0;
+            const uint32_t vt = def && kt < (uint32_t)kKeys ? pval(sl, (int)kt) : 0u;
+            const uint32_t vr = def && kr < (uint32_t)kKeys ? pval(sl, (int)kr) : 0u;
+            s.slab[sl] = vt | (vr << 16);
+            s.flags[sl] = (uint8_t)(f | MT_SF_STALE);
+        }
+    }
+    // blockUpdate of the leaf block(s) holding positions [k0, k1): their caches are current again
+    MT_DEV void refresh(int k0, int k1) {
+        if (!track()) return;
+        sync();
+        for (int i = k0 + lane; i < k1; i += 64) s.flags[s.order[i]] &= (uint8_t)~MT_SF_STALE;
+        sync();
+    }
 
     // ------------------------------------------------------------ delta events
     // One callback record (mt_event, include/mtgpu.h), written by lane 0 in firing order: the
@@ -632,7 +661,10 @@ struct Wave {
         // MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2231-2236): [segment, next-to-be-linked]
         emit(MT_EV_SPLIT, MT_EVF_FIRST, k, -1, (uint32_t)off);
         emit(MT_EV_SPLIT, 0, k + 1, -1, s.len[t]);
-        return insert_at(k + 1, b, t, old_end, seq);
+        const int bs = s.bst[b], bc = s.lbcnt[b];
+        if (!insert_at(k + 1, b, t, old_end, seq)) return false;
+        refresh(bs, bs + bc + 1);  // insertingWalk: blockUpdateLength of the split's block (or both halves)
+        return true;
     }
 
     // ------------------------------------------------------------------- heap
@@ -836,7 +868,10 @@ struct Wave {
             sync();
             if (lane == 0) lvl(L + 1)[P] = (uint8_t)cc;
             sync();
-            if (L == 0) block_starts();
+            if (L == 0) {
+                block_starts();
+                refresh(s.bst[first_child], s.bst[first_child + cc]);  // every packed block is new
+            }
             // underflow(parent) && parent.parent
             if (cc < kMaxNodes / 2 && (L + 1) < s.nlev - 1) {
                 int fc = 0;
@@ -882,6 +917,8 @@ struct Wave {
                 int fc = 0;
                 const int P = parent_of(0, b, &fc);
                 pack(0, P, fc);
+            } else if (kept < cnt) {
+                refresh(s.bst[b], s.bst[b] + kept);  // blockUpdatePathLengths(block)
             }
             if (s.err) return;
         }
@@ -1014,6 +1051,7 @@ struct Wave {
             const int idx = k - st;  // index inside block b before a possible split
             const int before_nb = s.nb[0];
             if (!insert_at(k, b, t, -1, S)) return;
+            refresh(st, st + c + 1);  // insertingWalk: blockUpdateLength of the insert's block (or both halves)
             const int bb = (s.nb[0] > before_nb && idx >= kMaxNodes / 2) ? b + 1 : b;
             if (S > s.min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
                 if (!add_lru(bb, t, S)) return;
@@ -1061,6 +1099,7 @@ struct Wave {
                     if constexpr (LOC) {
                         if (local) s.gm[sl] |= gbit;
                     }
+                    if (!is_remove && track()) mark_stale(sl);
                     if (LOC && !is_remove) {
                         annotate_loc(sl, pr.p, pr.np, rewrite, local);
                     } else if (is_remove) {
@@ -1091,6 +1130,24 @@ struct Wave {
         }
         if (wave_ballot(over)) return fail(MT_DERR_LIMITS, S);
         sync();
+        if (is_remove && track()) {  // markRangeRemoved's post action: blockUpdate of every block mapRange enters
+            block_starts();
+            const int nb = s.nb[0];
+            for (int base = 0; base < nb; base += 64) {
+                const int j = base + lane;
+                if (j < nb) {
+                    const int st = s.bst[j], c = s.lbcnt[j];
+                    bool any = false;
+                    for (int q = 0; q < c; q++) {
+                        const int ce = s.cum[st + q], cs = cstart(st + q);
+                        any = any || (ce > cs && cs < end && ce > start);
+                    }
+                    if (any)
+                        for (int q = 0; q < c; q++) s.flags[s.order[st + q]] &= (uint8_t)~MT_SF_STALE;
+                }
+            }
+            sync();
+        }
         if (is_remove) emit_range(true, S, C, start, end, pr, rewrite);
         if constexpr (LOC) {
             if (is_remove) {
@@ -1188,7 +1245,9 @@ struct Wave {
                 }
             }
             sync();
-            add_lru(block_of_pos(k), sl, S);
+            const int b = block_of_pos(k);
+            add_lru(b, sl, S);
+            refresh(s.bst[b], s.bst[b] + s.lbcnt[b]);  // ackPendingSegment: blockUpdatePathLengths(parent)
         }
     }
     MT_DEV void op_ack(const mt_op_rec& op, const uint8_t* pairs, int np) {
@@ -1646,6 +1705,8 @@ struct Wave {
             s.flags[i] = g.flags[so + i];
             s.order[i] = (uint16_t)i;
         }
+        const bool trk = sc.label_keys != MT_NO_LABEL_KEYS && g.slab;
+        for (int i = lane; i < n; i += 64) s.slab[i] = trk ? g.slab[so + i] : 0u;
         const size_t lo = (size_t)d * g.lbcap;
         for (int i = lane; i < sc.nb[0]; i += 64) {
             s.lbcnt[i] = g.lbcnt[lo + i];
@@ -1671,6 +1732,7 @@ struct Wave {
         }
         if (lane == 0) {
             s.wide = sc.wide;
+            s.lkeys = trk ? sc.label_keys : MT_NO_LABEL_KEYS;
             s.n = n;
             s.nlev = sc.nlev;
             for (int L = 0; L < MT_MAXLEV; L++) s.nb[L] = sc.nb[L];
@@ -1771,6 +1833,7 @@ struct Wave {
             g.client[so + i] = s.client[sl];
             g.rclient[so + i] = s.rclient[sl];
             g.flags[so + i] = s.flags[sl];
+            if (track()) g.slab[so + i] = s.slab[sl];
             s.cum[sl] = i;  // slot -> position for the heap remap
         }
         sync();

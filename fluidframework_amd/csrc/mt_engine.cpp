@@ -40,6 +40,7 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
                                            hipStream_t stream);
 extern "C" size_t mt_lds_bytes_wide(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
+extern "C" hipError_t mt_launch_label_keys(const mt_gstate* g, uint32_t d0, uint32_t d1, uint32_t keys, hipStream_t st);
 extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
                                      const mt_load_seg* segs, const uint8_t* text, const int32_t* min_seq,
                                      const int32_t* cur_seq, hipStream_t st);
@@ -135,6 +136,7 @@ struct mt_engine {
     hipStream_t side[kNumClasses] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
     uint64_t gen = 0;  // bumped by every call that can change document state (snap_cache's key)
+    std::vector<uint16_t> lkeys;  // per document: its declared label keys (mt_set_label_keys), host copy
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
         uint64_t gen = 0;
@@ -309,8 +311,40 @@ mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
     HIP_OK(hipSetDevice(e->cfg.device));
     e->n_docs = n_docs;
     e->gen++;
+    e->lkeys.assign(e->cfg.max_docs, (uint16_t)MT_NO_LABEL_KEYS);
     HIP_OK(mt_launch_init(&e->g, n_docs, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
+    return MT_OK;
+}
+
+mt_status mt_set_label_keys(mt_engine* e, uint32_t doc, int tile_key, int range_key) {
+    if (!e || tile_key < -1 || tile_key >= MT_MAX_KEYS_WIDE || range_key < -1 || range_key >= MT_MAX_KEYS_WIDE)
+        return MT_ERR_ARG;
+    const uint32_t keys = (tile_key < 0 ? 0xFFu : (uint32_t)tile_key) | ((range_key < 0 ? 0xFFu : (uint32_t)range_key) << 8);
+    const uint32_t d0 = doc == MT_ALL_DOCS ? 0 : doc, d1 = doc == MT_ALL_DOCS ? e->n_docs : doc + 1;
+    if (d0 >= e->n_docs && doc != MT_ALL_DOCS) return MT_ERR_ARG;
+    if (keys == MT_NO_LABEL_KEYS) return MT_OK;
+    if (e->lkeys.size() < e->cfg.max_docs) e->lkeys.resize(e->cfg.max_docs, (uint16_t)MT_NO_LABEL_KEYS);
+    auto merge = [](uint32_t old, uint32_t req) {  // each key: declared once, or left as it is (0xFF)
+        uint32_t out = 0;
+        for (int h = 0; h < 16; h += 8) {
+            const uint32_t o = (old >> h) & 0xFFu, r = (req >> h) & 0xFFu;
+            if (r != 0xFFu && o != 0xFFu && o != r) return 0xFFFFFFFFu;
+            out |= (r != 0xFFu ? r : o) << h;
+        }
+        return out;
+    };
+    for (uint32_t d = d0; d < d1; d++)
+        if (merge(e->lkeys[d], keys) == 0xFFFFFFFFu) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    if (!e->g.slab) {
+        uint32_t* p = nullptr;
+        if (dalloc(e, &p, (size_t)e->cfg.max_docs * e->g.segcap)) return MT_ERR_NOMEM;
+        e->g.slab = p;
+    }
+    for (uint32_t d = d0; d < d1; d++) e->lkeys[d] = (uint16_t)merge(e->lkeys[d], keys);
+    e->gen++;
+    HIP_OK(mt_launch_label_keys(&e->g, d0, d1, keys, e->stream));
     return MT_OK;
 }
 

@@ -19,11 +19,29 @@ __global__ void mt_init_kernel(mt_gstate g, uint32_t n_docs) {
     sc.nb[0] = 1;
     sc.n_empty = 1;  // the root leaf block starts empty
     sc.win_op = -1;
+    sc.label_keys = MT_NO_LABEL_KEYS;
     g.sc[d] = sc;
     g.loc[d].own = -1;  // an observer until its first local edit
     g.loc[d].glo = g.loc[d].ghi = g.loc[d].stamp = g.loc[d].lseq = g.loc[d].rgn = g.loc[d].rgpn = 0;
     g.lbcnt[(size_t)d * g.lbcap] = 0;
     g.lbscour[(size_t)d * g.lbcap] = MT_SC_UNDEF;
+}
+
+// mt_set_label_keys: documents [d0, d1) track the block caches of their tile / range labels and run
+// on the LDS engine from now on
+__global__ void mt_label_keys_kernel(mt_gstate g, uint32_t d0, uint32_t d1, uint32_t keys) {
+    const uint32_t d = d0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= d1) return;
+    const uint32_t old = g.sc[d].label_keys;  // (a key left undeclared, 0xFF, keeps its value; the host
+    uint32_t nk = 0;                         // refused conflicting declarations)
+    for (int h = 0; h < 16; h += 8) nk |= (((keys >> h) & 0xFFu) != 0xFFu ? (keys >> h) & 0xFFu : (old >> h) & 0xFFu) << h;
+    g.sc[d].label_keys = nk;
+    g.sc[d].wide |= MT_WIDE_LDS;
+}
+extern "C" hipError_t mt_launch_label_keys(const mt_gstate* g, uint32_t d0, uint32_t d1, uint32_t keys, hipStream_t st) {
+    if (d1 <= d0) return hipSuccess;
+    hipLaunchKernelGGL(mt_label_keys_kernel, dim3((d1 - d0 + 255) / 256), dim3(256), 0, st, *g, d0, d1, keys);
+    return hipGetLastError();
 }
 
 // SnapshotLoader.loadHeader (snapshotLoader.ts:119-157) for a batch of documents, one wave per
@@ -148,9 +166,11 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             m = nb[L];
         }
     }
+    const uint32_t lkeys = g.sc[d].label_keys;  // (declared keys outlive a load)
     if (lane == 0) {
         mt_doc_scalars sc{};
         sc.win_op = -1;
+        sc.label_keys = lkeys;
         if (err) {  // the document keeps an empty tree and reports the error
             sc.nlev = 1;
             sc.nb[0] = 1;
@@ -165,7 +185,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             for (int L = 0; L < nlev; L++) sc.nb[L] = nb[L];
             sc.n_empty = ns == 0 ? 1u : 0u;
             sc.text_top = carry;
-            sc.wide = (lds || wdoc ? MT_WIDE_LDS : 0u) | (wdoc ? MT_WIDE_DOC : 0u);
+            sc.wide = (lds || wdoc || lkeys != MT_NO_LABEL_KEYS ? MT_WIDE_LDS : 0u) | (wdoc ? MT_WIDE_DOC : 0u);
         }
         sc.cur_seq = cur_seq[w];
         sc.min_seq = min_seq[w];
@@ -404,6 +424,54 @@ extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, 
     hipLaunchKernelGGL(mt_fixup_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, ops, n_docs);
     return hipGetLastError();
 }
+// The leaf block holding segment ib, as its position range [*lo, *hi) ([n, n) for ib < 0)
+MT_DEV void mt_leaf_block_of(const mt_gstate& g, uint32_t d, const mt_doc_scalars& sc, int ib, int* lo, int* hi) {
+    *lo = *hi = sc.nseg;
+    if (ib < 0) return;
+    const uint8_t* cnt = g.lbcnt + (size_t)d * g.lbcap;
+    const int nb = sc.nb[0];
+    int carry = 0;
+    for (int base = 0; base < nb; base += 64) {
+        const int b = base + lane_id();
+        const int c = b < nb ? (int)cnt[b] : 0;
+        const int incl = wave_incl_scan(c) + carry;
+        const uint64_t m = wave_ballot(b < nb && c > 0 && incl - c <= ib && ib < incl);
+        if (m) {
+            const int l = first_lane(m);
+            *lo = __builtin_amdgcn_readlane(incl - c, l);
+            *hi = __builtin_amdgcn_readlane(incl, l);
+            return;
+        }
+        carry = wave_last(incl);
+    }
+}
+// The value id of label key `key` of segment i as the query sees it: a stale marker (MT_SF_STALE) outside
+// the search path's leaf block [blo, bhi) answers with the labels its block's caches still hold
+// (HierMergeBlock rightmostTiles / leftmostTiles / rangeStacks, rebuilt by blockUpdate only)
+MT_DEV uint32_t mt_label_vid(const mt_gstate& g, bool wdoc, size_t so, int i, uint32_t key, uint32_t lkeys, int blo,
+                             int bhi) {
+    uint32_t v = mt_gprop(g, wdoc, so + i, key);
+    if (lkeys != MT_NO_LABEL_KEYS && g.slab && (i < blo || i >= bhi) && (g.flags[so + i] & MT_SF_STALE)) {
+        const uint32_t sl = g.slab[so + i];
+        if (key == (lkeys & 0xFFu)) v = sl & 0xFFFFu;
+        else if (key == ((lkeys >> 8) & 0xFFu)) v = sl >> 16;
+    }
+    return v;
+}
+// the segment whose local-view range holds pos (the leaf search() stops on), -1 past the end
+MT_DEV int mt_containing(const mt_gstate& g, size_t so, int n, int pos) {
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane_id();
+        const int ll = (i < n && !(g.flags[so + i] & MT_SF_REMOVED)) ? (int)g.len[so + i] : 0;
+        const int incl = wave_incl_scan(ll) + carry;
+        const uint64_t m = wave_ballot(i < n && ll > 0 && incl - ll <= pos && pos < incl);
+        if (m) return base + first_lane(m);
+        carry = wave_last(incl);
+    }
+    return -1;
+}
+
 // mt_find_tiles: Client.findTile for a batch of queries, one wave per query, over the document's
 // compact HBM state in the local view (include/mtgpu.h; mergeTree.ts:1763-1870, 996-1035)
 __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile_query* __restrict__ q, uint32_t nq,
@@ -418,10 +486,11 @@ __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile
     const size_t so = (size_t)d * g.segcap;
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     const int pos = qq.pos;
+    int blo = n, bhi = n;  // the search path's leaf block (its tiles answer with their current labels)
     auto labeled = [&](int i) -> bool {  // refHasTileLabel (mergeTree.ts:581-597)
         if (qq.key >= MT_MAX_KEYS_WIDE || !(g.flags[so + i] & MT_SF_MARKER) || !(mt_gtext(g, d, sc, g.toff[so + i]) & 1u))
             return false;
-        const uint32_t v = mt_gprop(g, wdoc, so + i, qq.key);
+        const uint32_t v = mt_label_vid(g, wdoc, so, i, qq.key, sc.label_keys, blo, bhi);
         return v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
     };
     auto local_len = [&](int i) -> int { return (g.flags[so + i] & MT_SF_REMOVED) ? 0 : (int)g.len[so + i]; };
@@ -429,6 +498,7 @@ __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile
     if (qq.preceding) {
         // search: the last live tile at a position <= pos (shifted children's rightmostTiles, then
         // the leaf holding pos)
+        if (sc.label_keys != MT_NO_LABEL_KEYS) mt_leaf_block_of(g, d, sc, mt_containing(g, so, n, pos), &blo, &bhi);
         int carry = 0;
         for (int base = 0; base < n; base += 64) {
             const int i = base + lane;
@@ -471,6 +541,7 @@ __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile
             // ... unless a trailing empty leaf block comes after it at that same position
             const bool trailing_empty = is == n - 1 && pos == total && sc.nb[0] > 0 &&
                                         g.lbcnt[(size_t)d * g.lbcap + sc.nb[0] - 1] == 0;
+            if (sc.label_keys != MT_NO_LABEL_KEYS) mt_leaf_block_of(g, d, sc, is, &blo, &bhi);
             if (!trailing_empty) {
                 if (labeled(is)) {  // recordTileStart: removed or not
                     res = is;
@@ -527,6 +598,8 @@ __global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_til
     mt_stack_item* out = items + (size_t)w * cap;
     int a = 0, t = 0, carry = 0;
     bool touched = false;
+    int blo = n, bhi = n;  // the search path's leaf block (its markers fold with their current labels)
+    if (sc.label_keys != MT_NO_LABEL_KEYS) mt_leaf_block_of(g, d, sc, mt_containing(g, so, n, pos), &blo, &bhi);
     for (int base = 0; base < n; base += 64) {
         const int i = base + lane;
         const int ll = (i < n && !(g.flags[so + i] & MT_SF_REMOVED)) ? (int)g.len[so + i] : 0;
@@ -536,7 +609,7 @@ __global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_til
         bool cand = false;
         if (i < n && ll > 0 && start <= pos && qq.key < MT_MAX_KEYS_WIDE && (g.flags[so + i] & MT_SF_MARKER)) {
             rt = mt_gtext(g, d, sc, g.toff[so + i]);
-            const uint32_t v = mt_gprop(g, wdoc, so + i, qq.key);
+            const uint32_t v = mt_label_vid(g, wdoc, so, i, qq.key, sc.label_keys, blo, bhi);
             cand = (rt & 6u) && v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
         }
         uint64_t m = wave_ballot(cand);

@@ -20,6 +20,9 @@
 #define MT_SF_NL 4u          // text ends with "\n" (TextSegment.canAppend, textSegment.ts:63-68)
 #define MT_SF_HASNL 8u       // text contains a "\n" somewhere (a split of a segment without one needs no text read)
 #define MT_SF_MARKER 16u     // a Marker (length 1; its one arena byte is its ReferenceType)
+#define MT_SF_STALE 32u      // a marker annotated since its leaf block's last blockUpdate: the block caches
+                             // (HierMergeBlock rightmostTiles / leftmostTiles / rangeStacks) still hold the
+                             // label value ids in `slab` (documents with declared label keys only)
 #define MT_SF_OVW 128u       // (within one op only) a pending local removal this remote removal took over
 
 // needsScour tri-state (mergeTree.ts:63, 1279, 1438, 1445)
@@ -27,7 +30,7 @@
 #define MT_SC_TRUE 1
 #define MT_SC_FALSE 2
 
-struct mt_doc_scalars {      // 80 bytes
+struct mt_doc_scalars {      // 84 bytes
     int32_t nseg;            // linked segments
     int32_t nlev;            // block levels (1 = the root is the only, leaf, block)
     int32_t nb[MT_MAXLEV];   // blocks per level (level 0 = leaf blocks)
@@ -41,7 +44,10 @@ struct mt_doc_scalars {      // 80 bytes
                              // engine); MT_WIDE_DOC: the wide representation (include/mtgpu.h "limits")
     int32_t win_op;          // batch index of the first op failing a window assert (binning's
                              // replay of the window), -1 if none: mt_fixup_kernel's input
+    uint32_t label_keys;     // key ids of "referenceTileLabels" (bits 0-7) and "referenceRangeLabels"
+                             // (bits 8-15), 0xFF: none; MT_NO_LABEL_KEYS: block caches not tracked
 };
+#define MT_NO_LABEL_KEYS 0xFFFFu
 
 #define MT_WIDE_LDS 1u
 #define MT_WIDE_DOC 2u
@@ -83,6 +89,8 @@ struct mt_gstate {
     uint64_t* ph;
     uint64_t* pxl;
     uint64_t* pxh;
+    uint32_t* slab;    // [doc][segcap] a stale marker's cached label value ids: tile key (low 16 bits),
+                       // range key (high 16) -- allocated on the first mt_set_label_keys, else null
     uint8_t* client;
     uint8_t* rclient;
     uint8_t* flags;

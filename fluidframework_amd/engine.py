@@ -98,13 +98,14 @@ def lib():
         L.mt_regen_drain.argtypes = [vp, u32, vp, u32, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.mt_events_enable.argtypes = [vp, u32]
         L.mt_events_drain.argtypes = [vp, vp, u64, vp, ctypes.POINTER(u64)]
+        L.mt_set_label_keys.argtypes = [vp, u32, i32, i32]
         L.mt_version.restype = ctypes.c_char_p
         for name in ('mt_engine_create', 'mt_engine_destroy', 'mt_docs_init', 'mt_batch_upload', 'mt_batch_apply',
                      'mt_batch_free', 'mt_submit', 'mt_sync', 'mt_get_length', 'mt_get_text', 'mt_get_state',
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
                      'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_range_stacks', 'mt_regen_drain', 'mt_set_concurrent_classes',
-                     'mt_events_enable', 'mt_events_drain'):
+                     'mt_events_enable', 'mt_events_drain', 'mt_set_label_keys'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -251,6 +252,13 @@ class MergeEngine:
         return buf.value.decode()
 
     # -- findTile (include/mtgpu.h) --------------------------------------------------------
+    def set_label_keys(self, tile_key, range_key, doc=None):
+        """Declare the key ids of "referenceTileLabels" / "referenceRangeLabels" (-1: unused) for one
+        document or all (mt_set_label_keys): its findTile / getStackContext then follow the reference's
+        block caches after label annotates."""
+        _check(lib().mt_set_label_keys(self.h, 0xFFFFFFFF if doc is None else doc, tile_key, range_key),
+               'mt_set_label_keys')
+
     def find_tiles(self, queries):
         """Client.findTile for a batch of TILE_QUERY_DTYPE rows: TILE_RESULT_DTYPE rows (pos -1: none)."""
         q = np.ascontiguousarray(queries, dtype=TILE_QUERY_DTYPE)

@@ -291,9 +291,16 @@ mt_status mt_seg_counts(mt_engine* eng, uint32_t* out, uint32_t n_docs);
  * is a tile, otherwise the first live tile after it.  A tile is a Marker whose refType has Tile
  * (ops.ts:8) and whose "referenceTileLabels" property (key id `key` of the document) holds the
  * label; the host passes the label as the set of value ids whose label arrays contain it.
- * The reference answers through HierMergeBlock caches that annotateRange does not refresh
- * (mergeTree.ts:2584): after an annotate that changes a tile's labels it can report the old labels
- * until the block is next updated; the engine answers from the current labels. */
+ * The reference answers through HierMergeBlock caches (rightmostTiles / leftmostTiles,
+ * mergeTree.ts:263-318) that blockUpdate rebuilds whenever a block's children change -- inserts,
+ * boundary splits, removes (every block the removal's mapRange enters), zamboni scours that unlink
+ * or append, packs, acks -- but annotateRange does not (mergeTree.ts:2565-2605): a tile found by
+ * shifting over a block answers with the labels its markers had at that block's last rebuild, a tile
+ * in the leaf block of the search path with its current labels.  The engine reproduces this for the
+ * documents whose label keys the host declared (mt_set_label_keys): a marker annotated since its leaf
+ * block's last rebuild keeps the tile / range label value ids it had then (a "stale" marker), and the
+ * queries read those outside the search path's leaf block.  Without declared keys the engine
+ * answers from the current labels. */
 typedef struct mt_tile_query {  /* 48 bytes */
     uint32_t doc;
     int32_t pos;                /* startPos */
@@ -332,8 +339,9 @@ mt_status mt_regen_drain(mt_engine* eng, uint32_t doc, mt_op_rec* recs, uint32_t
  * entries) and its full depth to depth[i] & MT_STACK_DEPTH; MT_STACK_TOUCHED is set when any such
  * marker was folded (the reference's RangeStackMap then holds the label, possibly with an empty
  * stack; otherwise the label is absent).  q.preceding is ignored.  Like findTile, the reference
- * folds HierMergeBlock rangeStacks caches that annotateRange does not refresh (mergeTree.ts:2584);
- * the engine answers from the current labels. */
+ * folds HierMergeBlock rangeStacks caches that annotateRange does not refresh; with declared label
+ * keys the engine folds the markers of other leaf blocks with their labels as of their block's last
+ * rebuild, as findTile does. */
 #define MT_STACK_DEPTH 0x7FFFFFFFu
 #define MT_STACK_TOUCHED 0x80000000u
 typedef struct mt_stack_item {  /* 12 bytes */
@@ -343,6 +351,16 @@ typedef struct mt_stack_item {  /* 12 bytes */
 } mt_stack_item;
 mt_status mt_range_stacks(mt_engine* eng, const mt_tile_query* q, uint32_t n, uint32_t cap, mt_stack_item* items,
                           uint32_t* depth);
+
+/* Declare the key ids of "referenceTileLabels" (tile_key) and "referenceRangeLabels" (range_key) in
+ * document `doc` (MT_ALL_DOCS: every document), -1 for a key the document does not use.  From then on
+ * the engine tracks the reference's block caches for those labels (see findTile above); the host calls
+ * it when it interns either key for a document, before submitting the op that first carries it (-1
+ * leaves a key as it is, so the two may be declared by separate calls).  A document with declared keys
+ * runs on the LDS engine.  A key is declared once per document: declaring it again as a different id
+ * returns MT_ERR_ARG. */
+#define MT_ALL_DOCS 0xFFFFFFFFu
+mt_status mt_set_label_keys(mt_engine* eng, uint32_t doc, int tile_key, int range_key);
 
 /* ---- delta / maintenance events -------------------------------------
  * What Client.mergeTreeDeltaCallback and mergeTreeMaintenanceCallback receive

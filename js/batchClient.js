@@ -49,6 +49,7 @@ class BatchEngine {
         this.pending = 0;
         this.recording = false;
         this.eventsPerDoc = opts.eventsPerDoc || (1 << 16);
+        this.labelDecl = [];  // [doc, tile key, range key] to declare before the next submit
     }
 
     _enableEvents() {
@@ -76,6 +77,8 @@ class BatchEngine {
     }
 
     _encode() {
+        for (const [doc, tk, rk] of this.labelDecl) native.setLabelKeys(this.handle, doc, tk, rk);
+        this.labelDecl = [];
         const n = this.maxDocs;
         const rowPtr = new Uint32Array(n + 1);
         let nops = 0, nbytes = 0;
@@ -211,6 +214,12 @@ class BatchClient {
                 this.keys.push(k);
                 this.valueIds.push(new Map());
                 this.values.push([undefined]);
+                // the label keys whose block caches the engine tracks (mt_set_label_keys), declared
+                // before the batch that carries the key's first op is submitted (BatchEngine._encode)
+                if (k === "referenceTileLabels" || k === "referenceRangeLabels") {
+                    this.engine.labelDecl.push([this.doc, k === "referenceTileLabels" ? kid : -1,
+                        k === "referenceRangeLabels" ? kid : -1]);
+                }
             }
             const v = props[k];
             let vid = 0;

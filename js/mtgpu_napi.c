@@ -578,6 +578,26 @@ static napi_value deli_error(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* setLabelKeys(engine, doc, tileKey, rangeKey): mt_set_label_keys (-1: a key left as it is) */
+static napi_value set_label_keys(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 4 ? get_box(env, argv[0]) : NULL;
+    if (!b) {
+        napi_throw_type_error(env, NULL, "setLabelKeys(engine, doc, tileKey, rangeKey)");
+        return NULL;
+    }
+    uint32_t doc = 0;
+    int32_t tk = -1, rk = -1;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[2], &tk));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[3], &rk));
+    mt_status st = mt_set_label_keys(b->e, doc, tk, rk);
+    if (st) return throw_status(env, "mt_set_label_keys", st);
+    return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor d[] = {
         {"createEngine", NULL, create_engine, NULL, NULL, NULL, napi_default, NULL},
@@ -592,6 +612,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"eventsEnable", NULL, events_enable, NULL, NULL, NULL, napi_default, NULL},
         {"docsLoad", NULL, docs_load, NULL, NULL, NULL, napi_default, NULL},
         {"findTiles", NULL, find_tiles, NULL, NULL, NULL, napi_default, NULL},
+        {"setLabelKeys", NULL, set_label_keys, NULL, NULL, NULL, napi_default, NULL},
         {"rangeStacks", NULL, range_stacks, NULL, NULL, NULL, napi_default, NULL},
         {"regenDrain", NULL, regen_drain, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},

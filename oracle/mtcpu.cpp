@@ -135,10 +135,19 @@ Pay decodePay(const mt_op_rec& op, const uint8_t* payload) {
 
 enum Scour : int8_t { kUndef = 0, kTrue = 1, kFalse = 2 };
 
+// One entry of a block's label caches: a live marker under the block and its properties when the
+// caches were last rebuilt (HierMergeBlock rightmostTiles / leftmostTiles / rangeStacks,
+// mergeTree.ts:263-318, hold the markers keyed by their labels at that time)
+struct Snap {
+    const Seg* seg;
+    uint16_t props[kMaxKeys];
+};
+
 struct Block : Node {
     int childCount = 0;
     Node* children[kMaxNodes] = {nullptr};
     int8_t needsScour = kUndef;
+    std::vector<Snap> snap;  // the block's label caches as of its last blockUpdate, in document order
     Block() : Node(false) {}
 };
 
@@ -303,6 +312,31 @@ struct Doc {
         b->children[i] = child;
     }
 
+    // blockUpdate's cache half (mergeTree.ts:2748-2768, addNodeReferences :263-318): a leaf child that
+    // is a live marker (localNetLength > 0) enters with its properties now; a block child contributes
+    // its own caches as they stand
+    static void blockUpdate(Block* b) {
+        b->snap.clear();
+        for (int i = 0; i < b->childCount; i++) {
+            const Node* ch = b->children[i];
+            if (ch->leaf) {
+                const Seg* x = static_cast<const Seg*>(ch);
+                if (x->marker && localLen(x) > 0) {
+                    Snap e{x, {0}};
+                    if (x->props_defined) std::memcpy(e.props, x->props, sizeof(e.props));
+                    b->snap.push_back(e);
+                }
+            } else {
+                const Block* c = static_cast<const Block*>(ch);
+                b->snap.insert(b->snap.end(), c->snap.begin(), c->snap.end());
+            }
+        }
+    }
+    // blockUpdatePathLengths (mergeTree.ts:2770-2779): the block and every ancestor
+    static void pathUpdate(Block* b) {
+        for (; b; b = b->parent) blockUpdate(b);
+    }
+
     // split, mergeTree.ts:2476-2489
     Block* split(Block* node) {
         const int half = kMaxNodes / 2;
@@ -313,6 +347,8 @@ struct Doc {
             assign(nb, node->children[half + i], i);
             node->children[half + i] = nullptr;
         }
+        blockUpdate(node);  // nodeUpdateLengthNewStructure of both halves
+        blockUpdate(nb);
         return nb;
     }
 
@@ -324,6 +360,7 @@ struct Doc {
         assign(nr, root, 0);
         assign(nr, splitNode, 1);
         root = nr;
+        blockUpdate(nr);
     }
 
     // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
@@ -370,7 +407,10 @@ struct Doc {
                         pos -= len;
                         continue;
                     }
-                    if (!sp) return nullptr;
+                    if (!sp) {
+                        blockUpdate(b);  // blockUpdateLength on the way back up
+                        return nullptr;
+                    }
                     newNode = sp;
                     ci++;
                 } else {
@@ -406,7 +446,10 @@ struct Doc {
         }
         assign(b, newNode, ci);
         b->childCount++;
-        if (b->childCount < kMaxNodes) return nullptr;
+        if (b->childCount < kMaxNodes) {
+            blockUpdate(b);
+            return nullptr;
+        }
         return split(b);
     }
 
@@ -528,11 +571,13 @@ struct Doc {
             for (int q = 0; q < nc; q++) assign(pb, hold[rd++], q);
             pb->parent = parent;
             packed[ni] = pb;
+            blockUpdate(pb);  // nodeUpdateLengthNewStructure(packedBlock)
         }
         for (int j = 0; j < kMaxNodes; j++) parent->children[j] = nullptr;
         for (int j = 0; j < cc; j++) assign(parent, packed[j], j);
         parent->childCount = cc;
         if (underflow(parent) && parent->parent) pack(parent);
+        else pathUpdate(parent);
     }
 
     // zamboniSegments, mergeTree.ts:1422-1478
@@ -551,20 +596,22 @@ struct Doc {
                     b->childCount = (int)hold.size();
                     for (int j = 0; j < b->childCount; j++) assign(b, hold[j], j);
                     if (underflow(b) && b->parent) pack(b);
+                    else pathUpdate(b);
                 }
             }
         }
     }
 
     // ------------------------------------------------------------------- mapRange
+    // (post: markRangeRemoved's post action, a blockUpdate of every block entered, mergeTree.ts:2656-2663)
     template <class F>
-    bool nodeMap(Block* node, int32_t R, int32_t C, int start, int end, F&& leaf) {
+    bool nodeMap(Block* node, int32_t R, int32_t C, int start, int end, F&& leaf, bool post = false) {
         for (int ci = 0; ci < node->childCount; ci++) {
             Node* child = node->children[ci];
             int len = viewLen(child, R, C);
             if (end > 0 && len > 0 && start < len) {
                 if (!child->leaf) {
-                    nodeMap(static_cast<Block*>(child), R, C, start, end, leaf);
+                    nodeMap(static_cast<Block*>(child), R, C, start, end, leaf, post);
                 } else {
                     leaf(static_cast<Seg*>(child));
                 }
@@ -572,6 +619,7 @@ struct Doc {
             start -= len;
             end -= len;
         }
+        if (post) blockUpdate(node);
         return true;
     }
 
@@ -621,6 +669,7 @@ struct Doc {
                 for (size_t i = 0; i < nodes.size(); i += per) {
                     Block* b = newBlock();
                     for (size_t j = i; j < std::min(nodes.size(), i + per); j++) assign(b, nodes[j], b->childCount++);
+                    blockUpdate(b);
                     blocks.push_back(b);
                 }
                 if (blocks.size() == 1) {
@@ -763,7 +812,7 @@ struct Doc {
                     x->lrseq = L;
                 }
                 if (x->removed && x->rseq == kUnassigned) join(g, x);
-            });
+            }, true);
         } else {
             const bool rewrite = op.flags & MT_F_REWRITE;
             nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* x) {
@@ -880,6 +929,10 @@ struct Doc {
                 }
                 addToLRUSet(x, S);
             }
+            std::vector<Block*> nodes;  // blockUpdatePathLengths of each member's parent (mergeTree.ts:1908-1915)
+            for (Seg* x : g.segs)
+                if (x->parent && std::find(nodes.begin(), nodes.end(), x->parent) == nodes.end()) nodes.push_back(x->parent);
+            for (Block* b : nodes) pathUpdate(b);
             pending.pop_front();
         }
         zamboni();
@@ -984,7 +1037,7 @@ struct Doc {
                             delta.push_back(s);          // removedSegments (mergeTree.ts:2637)
                         }
                         addToLRUSet(s, S);
-                    });
+                    }, true);
                 } else {
                     const bool rewrite = op.flags & MT_F_REWRITE;
                     nodeMap(root, R, C, op.pos1, op.pos2, [&](Seg* s) {
@@ -1091,24 +1144,27 @@ struct Doc {
     // HierMergeBlock's rightmostTiles / leftmostTiles (the right- / leftmost live tile of the
     // block, addNodeReferences :263-318).  A tile: a Marker whose refType has Tile (ops.ts:8) and
     // whose "referenceTileLabels" (property `key`) value id is in `vmask` (refHasTileLabel :588).
+    // A shifted block answers from its caches (the labels its markers had at its last blockUpdate,
+    // Block::snap); a leaf from its current properties.
     struct TileQ {
         int key;
         const uint8_t* vmask;  // 256 bits
+        bool hasv(int v) const { return v != 0 && v < 256 && ((vmask[v >> 3] >> (v & 7)) & 1); }
         bool has(const Seg* s) const {
             if (!s->marker || !(s->text.size() && ((uint8_t)s->text[0] & 1u))) return false;
-            const int v = s->props[key];
-            return v != 0 && v < 256 && ((vmask[v >> 3] >> (v & 7)) & 1);
+            return hasv(s->props[key]);
         }
+        bool has(const Snap& e) const { return ((uint8_t)e.seg->text[0] & 1u) && hasv(e.props[key]); }
     };
     static const Seg* edgeTile(const Node* n, const TileQ& q, bool rightmost) {
         if (n->leaf) {
             const Seg* s = static_cast<const Seg*>(n);
             return localLen(s) > 0 && q.has(s) ? s : nullptr;
         }
-        const Block* b = static_cast<const Block*>(n);
-        for (int i = 0; i < b->childCount; i++) {
-            const Seg* t = edgeTile(b->children[rightmost ? b->childCount - 1 - i : i], q, rightmost);
-            if (t) return t;
+        const std::vector<Snap>& sn = static_cast<const Block*>(n)->snap;  // rightmostTiles / leftmostTiles
+        for (size_t i = 0; i < sn.size(); i++) {
+            const Snap& e = sn[rightmost ? sn.size() - 1 - i : i];
+            if (q.has(e)) return e.seg;
         }
         return nullptr;
     }
@@ -1176,10 +1232,11 @@ struct Doc {
     }
     static bool rangeMarker(const Seg* s, const TileQ& q) {
         if (!s->marker || !s->text.size() || !((uint8_t)s->text[0] & 6u)) return false;
-        const int v = s->props[q.key];
-        return v != 0 && v < 256 && ((q.vmask[v >> 3] >> (v & 7)) & 1);
+        return q.hasv(s->props[q.key]);
     }
-    // a block's rangeStacks entry for the label, recomputed from its children
+    // a shifted leaf's contribution, or a block's rangeStacks entry for the label: the fold of its
+    // cached markers (Block::snap, with their labels at its last blockUpdate; folding the block's
+    // reduced stack is folding its markers, applyStackDelta)
     static std::vector<const Seg*> blockStack(const Node* n, const TileQ& q) {
         std::vector<const Seg*> st;
         if (n->leaf) {
@@ -1187,9 +1244,8 @@ struct Doc {
             if (localLen(s) > 0 && rangeMarker(s, q)) applyRange(st, s);
             return st;
         }
-        const Block* b = static_cast<const Block*>(n);
-        for (int i = 0; i < b->childCount; i++)
-            for (const Seg* m : blockStack(b->children[i], q)) applyRange(st, m);  // applyStackDelta
+        for (const Snap& e : static_cast<const Block*>(n)->snap)
+            if (((uint8_t)e.seg->text[0] & 6u) && q.hasv(e.props[q.key])) applyRange(st, e.seg);
         return st;
     }
     void searchRange(const Block* b, int pos, const TileQ& q, std::vector<const Seg*>& st) const {

@@ -17,6 +17,8 @@ mergeTree.ts:1750-1760) on the same logs with range labels on key 1 ("referenceR
 """
 import json
 import os
+
+import numpy as np
 import subprocess
 import sys
 
@@ -86,12 +88,64 @@ def synthetic():
                            p_insert=0.6, p_remove=0.4, p_overlap=0.4, p_insert_props=0.6, p_marker=0.4)
 
 
+def annotated():
+    """label annotates between structural changes: an annotate that changes a marker's tile / range
+    labels refreshes no block (annotateRange, mergeTree.ts:2565-2605), so the reference answers from
+    the labels a block's caches were last rebuilt with until an insert, split, remove, scour, pack or
+    ack rebuilds that block (mergeTree.ts:2748-2768)"""
+    docs = []
+    # ten tiles (labels L0 = 1) with text between them, three leaf blocks; then the middle tiles'
+    # labels change to L1 (2) while the blocks stay as they are, and queries from the last block
+    # shift over the first ones
+    d, s = [], 0
+    for k in range(10):
+        s += 1
+        d.append(M(s, s - 1, 0, 1, 2 * k, REF_TILE, {TILE_KEY: 1}))
+        s += 1
+        d.append(I(s, s - 1, 0, 1, 2 * k + 1, 'x'))
+    for a in (4, 8, 12):
+        s += 1
+        d.append(A(s, s - 1, 0, 2, a, a + 1, {TILE_KEY: 2}))
+    docs.append(d)
+    # the same, then an insert into the first block rebuilds it (and only it)
+    docs.append(d + [I(s + 1, s, 0, 3, 1, 'ins')])
+    # a remove in the middle block rebuilds every block it enters
+    docs.append(d + [R(s + 1, s, 0, 3, 9, 10)])
+    # range markers: begins labelled R0 (1) re-annotated to R1 (2) and an end gaining R0
+    R1 = RANGE_KEY
+    d2, s = [], 0
+    for k in range(12):
+        s += 1
+        d2.append(M(s, s - 1, 0, 1, 2 * k, REF_NEST_BEGIN if k % 3 else REF_NEST_END, {R1: 1 if k % 3 else 2}))
+        s += 1
+        d2.append(I(s, s - 1, 0, 1, 2 * k + 1, 'y'))
+    for a, v in ((2, 2), (6, 1), (14, 2)):
+        s += 1
+        d2.append(A(s, s - 1, 0, 2, a, a + 1, {R1: v}))
+    docs.append(d2)
+    docs.append(d2 + [N(s + 1, s), N(s + 2, s + 1)])
+    hand = build_log(docs)
+    synth = oracle.generate(20, seed=606, n_clients=8, ops_per_doc=400, max_lag=16, n_keys=2, n_values=15,
+                            p_insert=0.5, p_remove=0.2, p_overlap=0.3, p_null=0.1, p_rewrite=0.05,
+                            p_insert_props=0.7, p_marker=0.45)
+    return _concat(hand, synth)
+
+
+def _concat(a, b):
+    """one log holding a's documents, then b's"""
+    from fluidframework_amd.oplog import OpBatch
+    ops_b = b.ops.copy()
+    ops_b['payload_off'] += len(a.payload)
+    return OpBatch(np.concatenate([a.ops, ops_b]), np.concatenate([a.payload, b.payload]),
+                   np.concatenate([a.row_ptr, b.row_ptr[1:] + a.row_ptr[-1]]).astype(np.uint32))
+
+
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
     oracle.build()
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
     out = []
-    for name, batch in (('tiles_scenarios', scenarios()), ('tiles_synth', synthetic())):
+    for name, batch in (('tiles_scenarios', scenarios()), ('tiles_synth', synthetic()), ('tiles_annot', annotated())):
         path = os.path.join(HERE, name + '.mtlog')
         batch.save(path)
         res = subprocess.run(['node', replay, 'tiles', path, str(TILE_KEY)], check=True, capture_output=True,
@@ -104,7 +158,7 @@ def main():
         f.write('\n'.join(out) + '\n')
     # getStackContext on the same logs, range labels on key 1
     out = []
-    for name in ('tiles_scenarios', 'tiles_synth'):
+    for name in ('tiles_scenarios', 'tiles_synth', 'tiles_annot'):
         res = subprocess.run(['node', replay, 'stacks', os.path.join(HERE, name + '.mtlog'), str(RANGE_KEY)],
                              check=True, capture_output=True, text=True)
         for line in res.stdout.strip().split('\n'):

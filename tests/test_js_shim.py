@@ -23,7 +23,7 @@ def test_addon_loads_and_exports():
         pytest.skip('node headers absent')
     out = subprocess.run([NODE, '-e', "const b=require('./js/batchClient.js');"
                           "for (const f of ['createEngine','submit','submitAsync','getText','getState','getLength',"
-                          "'docError','checksums','version','eventsEnable','eventsDrain','findTiles','rangeStacks','docsLoad','regenDrain']) if (typeof b.native[f] !== 'function') throw f;"
+                          "'docError','checksums','version','eventsEnable','eventsDrain','findTiles','rangeStacks','docsLoad','regenDrain','setLabelKeys']) if (typeof b.native[f] !== 'function') throw f;"
                           "console.log(b.native.version())"], cwd=REPO, capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
     assert 'gfx950' in out.stdout
@@ -218,7 +218,7 @@ def test_batchclient_loads_reference_snapshot_files():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth'])
+@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth', 'tiles_annot'])
 def test_batchclient_find_tile_matches_reference(name):
     """BatchClient.findTile (mt_find_tiles via the addon; label arrays interned by content) gives
     the reference Client.findTile answers of tests/golden/tiles.expected.jsonl."""
@@ -234,7 +234,7 @@ def test_batchclient_find_tile_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth'])
+@pytest.mark.parametrize('name', ['tiles_scenarios', 'tiles_synth', 'tiles_annot'])
 def test_batchclient_stack_context_matches_reference(name):
     """BatchClient.getStackContext (mt_range_stacks via the addon) gives the reference
     Client.getStackContext stacks of tests/golden/stacks.expected.jsonl."""

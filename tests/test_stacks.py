@@ -58,6 +58,7 @@ def test_engine_range_stacks_match_reference(name):
     from fluidframework_amd.oplog import OpBatch
     batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
     eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    eng.set_label_keys(0, 1)  # (tile labels on key 0, range labels on key 1)
     eng.apply(batch)
     rows = load_stacks()[name]
     masks = [label_mask(k) for k in range(4)]
@@ -79,6 +80,7 @@ def test_engine_range_stacks_match_oracle_on_fuzz(oracle_lib):
                                 p_insert_props=0.6, p_marker=0.5)
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)
     eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.set_label_keys(0, 1)  # (tile labels on key 0, range labels on key 1)
     eng.apply(batch)
     masks = [label_mask(k) for k in range(4)]
     q, want = [], []

@@ -2,7 +2,8 @@
 (client.ts:1073-1076 -> mergeTree.ts:1763-1789) for the own client, pinned by the reference itself:
 tests/golden/tiles.expected.jsonl holds the answers the reference's observer Client gave on the
 tiles_* logs (tests/golden/make_tiles.py) -- the client.spec.ts findTile cases restated as remote
-ops, and marker-heavy synthetic logs.  Labels ride on property key 0 (value id v = the labels L<i>
+ops, marker-heavy synthetic logs, and tiles_annot: label annotates that leave the reference's
+HierMergeBlock caches stale (146 of its 2,176 answers differ from an answer from the current labels).  Labels ride on property key 0 (value id v = the labels L<i>
 of its bits i, js/mtlog.js tileLabels); a query's label becomes the set of value ids whose label
 arrays hold it (`label_mask`).  The oracle restates search / backwardSearch over its pointer tree;
 the engine answers a batch of queries on the device (mt_find_tiles)."""
@@ -15,7 +16,7 @@ import pytest
 from conftest import GOLDEN
 
 TILE_KEY = 0
-LOGS = ['tiles_scenarios', 'tiles_synth']
+LOGS = ['tiles_scenarios', 'tiles_synth', 'tiles_annot']
 
 
 def label_mask(label):
@@ -72,6 +73,7 @@ def test_engine_find_tiles_match_reference(name):
     from fluidframework_amd.oplog import OpBatch
     batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
     eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    eng.set_label_keys(0, 1)  # (tile labels on key 0, range labels on key 1)
     eng.apply(batch)
     rows = load_tiles()[name]
     masks = [label_mask(k) for k in range(4)]
@@ -91,6 +93,7 @@ def test_engine_find_tiles_match_oracle_on_fuzz(oracle_lib):
                                 p_insert_props=0.6, p_marker=0.4)
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)
     eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.set_label_keys(0, 1)  # (tile labels on key 0, range labels on key 1)
     eng.apply(batch)
     masks = [label_mask(k) for k in range(4)]
     q, want = [], []

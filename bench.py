@@ -84,6 +84,9 @@ def parse():
     p.add_argument('--devices', default='', help='device of each local rank, e.g. "0,0" (default: rank i -> GPU i)')
     p.add_argument('--no-h2d', action='store_true', help='skip the extra step whose op log is uploaded from '
                                                          'host memory inside the timed region (value_with_h2d)')
+    p.add_argument('--no-slow-paths', action='store_true',
+                   help='skip the N=1 side lines for the LDS-engine paths (C3 with delta events recorded, C3 '
+                        'with 48 clients, the editing-client farm at 100K documents)')
     return p.parse_args()
 
 
@@ -228,8 +231,12 @@ def main():
         assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
 
     value_h2d = None
-    if not args.no_h2d and deli is None:
-        value_h2d = h2d_step(eng, dev, n_total * ops_per_doc, barrier, comm)
+    if not args.no_h2d:
+        if deli is None:
+            value_h2d = h2d_step(eng, dev, n_total * ops_per_doc, barrier, comm)
+        else:
+            value_h2d = h2d_step_deli(eng, dev, deli, d_msgs, d_mrow, n_msgs, d_tick, n_total * ops_per_doc,
+                                      barrier, comm, cs)
 
     # final per-document checksum gather to rank 0 (RCCL ncclGather from HBM; the only collective)
     parts = comm.gather_checksums(eng, max_docs)
@@ -252,8 +259,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(dev, cs, n_docs, args.cpu_seconds)
 
+    slow = None
+    if world == 1 and args.config == 'C3' and not args.no_slow_paths and not args.docs and not args.ops:
+        # the main engine's HBM goes back before the side lines allocate theirs
+        kname_main = eng.class_kernel(max(rcls, key=lambda c: rcls[c][0]))
+        dev.free()
+        eng.close()
+        slow = slow_paths(device, docs_per_gpu, args.seed)
+
     if rank == 0:
-        kname = eng.class_kernel(dom)
+        kname = kname_main if slow is not None else eng.class_kernel(dom)
         line = {
             'metric': METRIC,
             'value': round(value, 1),
@@ -286,7 +301,7 @@ def main():
                 'measured_in': 'an extra untimed step with the capacity classes serialized'
                                if rcls is not cls else 'the timed steps (classes serialized)',
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
-                'class_ms_serialized': {str(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
+                'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
                 'all_apply_kernels': {'launches': launches, 'kernel_ms': round(kern_ms, 2),
                                       'achieved_GBps': round(all_achieved, 1),
                                       'apply_wall_ms': round(wall_ms, 2),
@@ -300,6 +315,7 @@ def main():
                 'tickets_per_s_kernel': round(n_msgs / (deli_ms / args.steps * 1e-3), 1) if deli_ms else None,
                 'share_of_step': round(deli_ms / (elapsed * 1e3), 4)},
             'value_with_h2d': value_h2d,
+            'slow_paths': slow,
             'cpu_baseline': cpu,
             'parity': parity,
             'doc_errors_sampled': errs,
@@ -308,6 +324,152 @@ def main():
         }
         print(json.dumps(line), flush=True)
     comm.close()
+
+
+MT_CLASS_EDITING = 0x40000000  # include/mtgpu.h: the editing documents' bucket in the class stats
+MT_CLASS_LDS = 0x20000000      # the LDS engine inside a register class (client ids above 32, label keys)
+
+
+def class_label(cap):
+    if cap & MT_CLASS_EDITING:
+        return f'editing{cap & ~MT_CLASS_EDITING}'
+    if cap & MT_CLASS_LDS:
+        return f'lds{cap & ~MT_CLASS_LDS}'
+    return str(cap)
+
+
+def roofline_of(eng, rcls):
+    """The dominant kernel of one serialized step: its average launch time and algorithmic bytes
+    per launch against the HBM peak (the main line's accounting)."""
+    dom = max(rcls, key=lambda c: rcls[c][0])
+    ms, n, b = rcls[dom]
+    avg = ms / max(1, n)
+    per = b / max(1, n)
+    ach = per / (avg * 1e-3) / 1e9 if n and avg else 0.0
+    return {'bound': 'hbm', 'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(ach / HBM_PEAK_GBS, 4), 'traffic': None, 'kernel': eng.class_kernel(dom), 'launches': n,
+            'avg_launch_ms': round(avg, 4), 'alg_bytes_per_launch': int(per),
+            'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]}}
+
+
+def timed_side_step(eng, dbatch, warmup=1, after=None):
+    """Warm-up, one timed replay (reset + apply of the HBM-resident batch), then one serialized
+    replay for the dominant kernel's roofline; `after(timed)` runs after every replay (the events
+    line drains there, timing the drain of the timed replay).  Returns (seconds, roofline, the
+    timed replay's after() result)."""
+    from fluidframework_amd.hipmem import device_synchronize
+    for _ in range(warmup):
+        eng.reset()
+        eng.apply_staged(dbatch)
+        if after:
+            after(False)
+    device_synchronize()
+    t0 = time.perf_counter()
+    eng.reset()
+    eng.apply_staged(dbatch)
+    device_synchronize()
+    el = time.perf_counter() - t0
+    res = after(True) if after else None
+    eng.set_concurrent_classes(False)
+    eng.reset()
+    eng.apply_staged(dbatch)
+    eng.set_concurrent_classes(True)
+    rcls = {cap: [ms, n, b] for cap, ms, n, b in eng.last_class_stats()}
+    if after:
+        after(False)
+    return el, roofline_of(eng, rcls), res
+
+
+def slow_paths(device, n_docs, seed):
+    """N = 1 side lines for the paths that run on the LDS engine instead of the register engine
+    (DESIGN.md §7): C3 with the delta callbacks recorded (any SharedString with a sequenceDelta
+    listener), C3 with 48 clients (overlap sets past the register engine's 32 bits), and the
+    editing-client farm (local edits + remote ops + acks) tiled over 100K documents.  Each is a
+    full replay of HBM-resident logs, checked against the generation state or the oracle."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import CONFIGS, OpBatch
+    out = {}
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    ops = n_docs * cfg['ops_per_doc']
+
+    # C3 with delta events: every callback recorded on the device; the drain (one CSR gather + D2H
+    # of every record) is timed on its own
+    eng = MergeEngine(n_docs, device=device, ops_per_launch=32)
+    eng.enable_events(per_doc=8192)  # a C3 document fires <= ~6.5 K callbacks per replay
+    dev = eng.synthesize(seed=seed, **cfg)
+    gen_cs = eng.checksums()
+    eng.drain_event_rows()
+
+    def drain(timed):
+        t0 = time.perf_counter()
+        rows, rp = eng.drain_event_rows()
+        return (time.perf_counter() - t0, int(rp[-1])) if timed else None
+    el, rf, (drain_s, n_ev) = timed_side_step(eng, dev, after=drain)
+    ok = bool(np.array_equal(eng.checksums(), gen_cs))
+    errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 256)) if eng.error(d)[0])
+    out['C3_events'] = {'workload': f'C3 ({n_docs} docs x 32 clients x 1024 ops) with every delta callback recorded '
+                                    '(mt_events_enable; LDS engine)',
+                        'value': round(ops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
+                        'events_per_step': n_ev, 'drain_s': round(drain_s, 3),
+                        'note': 'the drain (CSR gather of every callback record + D2H) follows the timed replay',
+                        'roofline': rf, 'parity': {'replay_equals_generation': ok, 'doc_errors_sampled': errs}}
+    dev.free()
+    eng.close()
+
+    # C3 with 48 clients: client ids past 32 (the register engine's overlap set) -> LDS engine
+    cfg48 = dict(cfg, n_clients=48)
+    eng = MergeEngine(n_docs, device=device, ops_per_launch=32)
+    dev = eng.synthesize(seed=seed, **cfg48)
+    gen_cs = eng.checksums()
+    el, rf, _ = timed_side_step(eng, dev)
+    cs = eng.checksums()
+    par = {'replay_equals_generation': bool(np.array_equal(cs, gen_cs))}
+    try:
+        from oracle import oracle
+        k = 256
+        o = oracle.Oracle(k).apply(dev.to_host(0, k), threads=int(os.environ.get('OMP_NUM_THREADS') or 8))
+        par.update(docs_checked=k, mismatches=int(np.count_nonzero(o.checksums() != cs[:k])), against='oracle/mtcpu.cpp')
+    except Exception as ex:  # the checker is optional on a box without a compiler
+        par['oracle'] = f'unavailable: {ex}'
+    out['C3_48_clients'] = {'workload': f'C3 with 48 clients ({n_docs} docs x 1024 ops; LDS engine)',
+                            'value': round(ops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
+                            'roofline': rf, 'parity': par}
+    dev.free()
+    eng.close()
+
+    # the editing-client farm (tests/golden/local_big: reference clients' logs as one of them sees
+    # them) tiled over n_docs documents
+    src = OpBatch.load(os.path.join(HERE, 'tests', 'golden', 'local_big.mtlog'))
+    lens = np.diff(src.row_ptr.astype(np.int64))
+    pick = np.arange(n_docs) % src.n_docs
+    starts = src.row_ptr[:-1].astype(np.int64)[pick]
+    rp = np.concatenate([[0], np.cumsum(lens[pick])]).astype(np.int64)
+    idx = np.repeat(starts - rp[:-1], lens[pick]) + np.arange(rp[-1])
+    batch = OpBatch(src.ops[idx], src.payload, rp.astype(np.uint32))
+    n_rec = int(rp[-1])
+    eng = MergeEngine(n_docs, device=device, ops_per_launch=32)
+    dev = eng.stage(batch)
+    del batch, idx
+    el, rf, _ = timed_side_step(eng, dev)
+    cs = eng.checksums()
+    par = {}
+    try:
+        from oracle import oracle
+        o = oracle.Oracle(src.n_docs).apply(src, threads=int(os.environ.get('OMP_NUM_THREADS') or 8))
+        par = {'docs_checked': n_docs, 'mismatches': int(np.count_nonzero(o.checksums()[pick] != cs)),
+               'against': 'oracle/mtcpu.cpp on the source logs'}
+    except Exception as ex:
+        par['oracle'] = f'unavailable: {ex}'
+    errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 256)) if eng.error(d)[0])
+    par['doc_errors_sampled'] = errs
+    out['editing_farm'] = {'workload': f'tests/golden/local_big (reference editing-client farm logs: local edits, '
+                                       f'remote ops, acks) tiled over {n_docs} docs ({n_rec} records)',
+                           'value': round(n_rec / el, 1), 'unit': 'records/s', 'ms_per_step': round(el * 1e3, 2),
+                           'roofline': rf, 'parity': par}
+    dev.free()
+    eng.close()
+    return out
 
 
 def h2d_step(eng, dev, job_ops, barrier, comm):
@@ -340,6 +502,55 @@ def h2d_step(eng, dev, job_ops, barrier, comm):
     return {'value': round(job_ops / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3),
             'step_s': round(el, 3), 'bytes_uploaded': int(len(pinned.ops) * 32 + len(pinned.payload)),
             'note': 'op log from page-locked host memory: validation + H2D + apply in the timed region'}
+
+
+def h2d_step_deli(eng, dev, deli, d_msgs, d_mrow, n_msgs, d_tick, job_ops, barrier, comm, want_cs):
+    """C5's step with its inputs starting in page-locked host memory: the raw client messages
+    (joins + ops) and the op contents they carry are uploaded (validation + H2D), deli tickets the
+    messages and stamps seq / msn into the uploaded op records, then the apply; all timed.  The
+    result must equal the HBM-resident step's."""
+    from fluidframework_amd.deli import RAW_DTYPE
+    from fluidframework_amd.engine import DeviceBatch
+    from fluidframework_amd.hipmem import DeviceBuffer, PinnedArray
+    from fluidframework_amd.oplog import OpBatch
+    host = dev.to_host()
+    msgs = d_msgs.download(RAW_DTYPE, n_msgs)
+    mrow = d_mrow.download(np.uint32, eng.n_docs + 1)
+    pins = [PinnedArray(len(host.ops), host.ops.dtype), PinnedArray(len(host.payload), np.uint8),
+            PinnedArray(len(host.row_ptr), np.uint32), PinnedArray(len(msgs), RAW_DTYPE),
+            PinnedArray(len(mrow), np.uint32)]
+    for p, a in zip(pins, (host.ops, host.payload, host.row_ptr, msgs, mrow)):
+        p.a[:] = a
+    pinned = OpBatch(pins[0].a, pins[1].a, pins[2].a)
+    nbytes = int(len(host.ops) * 32 + len(host.payload) + msgs.nbytes + mrow.nbytes)
+    del host, msgs
+    d_m2, d_r2 = DeviceBuffer(pins[3].a.nbytes), DeviceBuffer(pins[4].a.nbytes)
+    barrier()
+    t0 = time.perf_counter()
+    eng.reset()
+    deli.restore_all(seq=0, clients={})
+    staged = DeviceBatch(eng, pinned)
+    d_m2.upload(pins[3].a)
+    d_r2.upload(pins[4].a)
+    t1 = time.perf_counter()
+    from fluidframework_amd.deli import batch_device_ptrs
+    d_ops2 = batch_device_ptrs(staged)[0]
+    deli.ticket_device(d_m2.ptr, d_r2.ptr, eng.n_docs, d_tick.ptr, d_ops2, staged.n_ops)
+    deli.sync()
+    eng.apply_staged(staged)
+    barrier()
+    el = comm.max(time.perf_counter() - t0)
+    up = comm.max(t1 - t0)
+    assert np.array_equal(eng.checksums(), want_cs), 'the host-fed C5 step differs from the HBM-resident one'
+    staged.free()
+    d_m2.free()
+    d_r2.free()
+    for p in pins:
+        p.free()
+    return {'value': round(job_ops / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3), 'step_s': round(el, 3),
+            'bytes_uploaded': nbytes,
+            'note': 'raw client messages + op contents from page-locked host memory: validation + H2D + deli '
+                    'ticketing + apply in the timed region'}
 
 
 def cpu_baseline(dev, gpu_cs, n_docs, budget_s):

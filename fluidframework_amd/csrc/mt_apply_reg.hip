@@ -46,6 +46,10 @@ constexpr uint32_t F_PDEF = (uint32_t)MT_SF_PDEF << 16;
 constexpr uint32_t F_NL = (uint32_t)MT_SF_NL << 16;
 constexpr uint32_t F_HASNL = (uint32_t)MT_SF_HASNL << 16;
 constexpr uint32_t F_MARKER = (uint32_t)MT_SF_MARKER << 16;
+// register-only flag: ENDS_WITH_NEWLINE not yet known.  A boundary split leaves the left part's last
+// character unread (the text is in HBM: one dependent global load per split); the flag is resolved
+// where it is read -- scour's append decisions (the block's children at once) and the store.
+constexpr uint32_t F_NLQ = 1u << 21;
 constexpr uint32_t kEmptyCf = 0xFFu;     // padding: client 255 never matches (and the slot is dead)
 constexpr uint16_t kDead = 0xFFFFu;
 
@@ -60,9 +64,10 @@ MT_DEV int wave_total(int v) { return wave_last(wave_incl_scan(v)); }
 // ---- optional per-phase cycle accounting (diagnostic build: -DMT_PROF; never in the product)
 enum { P_LOAD, P_SCAN, P_BOUND, P_INSERT, P_RANGE, P_ZAMBONI, P_SCOUR, P_STORE, P_OPS, P_ZPOP, P_REPACK,
        P_B_GET, P_B_BLK, P_B_TXT, P_B_INS, P_N_SCOUR, P_N_UNLINK, P_N_APPEND, P_N_SPLIT,
-       P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_B_SRCH, P_B_LEAF, P_NSLOT };
+       P_COMPACT, P_N_COMPACT, P_N_APPBYTES, P_B_SRCH, P_B_LEAF, P_OP, P_NSLOT };
+[[maybe_unused]] constexpr int kProfStride = 32;  // slots per class in mt_prof_acc
 #ifdef MT_PROF
-__device__ unsigned long long mt_prof_acc[384];  // [K - 1 = 0..15][24 slots]
+__device__ unsigned long long mt_prof_acc[16 * kProfStride];  // [K - 1 = 0..15][slot]
 MT_DEV uint64_t prof_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -70,11 +75,22 @@ MT_DEV uint64_t prof_now() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
-#define PROF_BEGIN(v) const uint64_t v = prof_now()
-#define PROF_END(arr, slot, v) arr[slot] += prof_now() - (v)
+// -DMT_PROF_ONLY=<slot>: only that phase's stamps run (one stamp pair per phase execution, so its
+// overhead is a constant that the P_OP-only build calibrates); default: every stamp
+#ifndef MT_PROF_ONLY
+#define MT_PROF_ONLY -1
+#endif
+#define PROF_ON(s) (MT_PROF_ONLY < 0 || MT_PROF_ONLY == (s))
+#define PROF_BEGIN(v, s) const uint64_t v = PROF_ON(s) ? prof_now() : 0
+#define PROF_BEGIN2(v, s1, s2) const uint64_t v = (PROF_ON(s1) || PROF_ON(s2)) ? prof_now() : 0
+#define PROF_END(arr, slot, v) \
+    do {                       \
+        if (PROF_ON(slot)) arr[slot] += prof_now() - (v); \
+    } while (0)
 #define PROF_CNT(slot, v) prof[slot] += (v)
 #else
-#define PROF_BEGIN(v)
+#define PROF_BEGIN(v, s)
+#define PROF_BEGIN2(v, s1, s2)
 #define PROF_END(arr, slot, v)
 #define PROF_CNT(slot, v)
 #endif
@@ -89,6 +105,7 @@ struct RLds {
     int32_t scr[CAP + 1];   // scratch by slot / position / leaf block (load, store, compaction)
     int32_t hseq[H];
     uint16_t toff[CAP];     // by segment id: text view offset (at store: id -> position)
+    uint32_t tln[CAP];      // by segment id: text length while linked, 0 once unlinked (compaction)
     uint16_t hslot[H];      // heap entry -> segment id
     uint8_t ibcnt[MT_MAXLEV - 1][IB];  // interior levels: level L's child counts in ibcnt[L - 1]
     uint8_t lbsc[LB + 1];   // store staging: needsScour per leaf block
@@ -115,7 +132,6 @@ struct RWave {
     L& s;
     const int lane;
     uint8_t* const abase;
-    uint8_t* arena;
     const uint32_t textcap;
 
     // ---- document state in registers (blocked: slot i = lane * K + j).  ext vectors: SSA values
@@ -136,7 +152,9 @@ struct RWave {
 #endif
 
     MT_DEV RWave(L& lds, uint8_t* a, uint32_t tc)
-        : s(lds), lane(lane_id()), abase(a), arena(a), textcap(tc), dirty(false) {}
+        : s(lds), lane(lane_id()), abase(a), textcap(tc), dirty(false) {}
+    // the current arena half
+    MT_DEV uint8_t* arena() const { return abase + (size_t)text_half * textcap; }
 
     MT_DEV int idx(int j) const { return lane * K + j; }
 
@@ -199,13 +217,13 @@ struct RWave {
         const int lk = first_lane(hit);
         uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, lk);
         for (int q = r - __builtin_amdgcn_readlane(incl - c, lk); q > 0; q--) mm &= mm - 1;
-        return lk * K + (int)__builtin_ctz(mm);
+        return uni(lk * K + (int)__builtin_ctz(mm));
     }
     // minimum over the lanes of a per-lane slot index (0x7fffffff = none): lane l's slots all
     // precede lane l + 1's, so it is the value of the first lane that has one
     MT_DEV static int first_hit(int v) {
         const uint64_t m = wave_ballot(v != 0x7fffffff);
-        return m ? __builtin_amdgcn_readlane(v, first_lane(m)) : 0x7fffffff;
+        return uni(m ? __builtin_amdgcn_readlane(v, first_lane(m)) : 0x7fffffff);
     }
     // first slot >= from whose bit is set in m; ns if none
     MT_DEV int first_from(uint32_t m, int from) const {
@@ -213,28 +231,30 @@ struct RWave {
         const uint64_t hit = wave_ballot(x != 0);
         if (!hit) return ns;
         const int lk = first_lane(hit);
-        return lk * K + (int)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)x, lk));
+        return uni(lk * K + (int)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)x, lk)));
     }
     // ------------------------------------------------------------ leaf blocks
-    MT_DEV int leaf_of(int k) const { return wave_total(__popc(bs_bits() & below(k + 1))) - 1; }
+    MT_DEV int leaf_of(int k) const { return uni(wave_total(__popc(bs_bits() & below(k + 1))) - 1); }
     MT_DEV int bs_slot(int b) const { return b >= nb0 ? ns : nth_slot(bs_bits(), b); }
     // ---- navigation by slot: a ballot and a readlane or two, no wave-wide scan.  A leaf block
     // is the slot range from its start mark to the next one (or ns); slot 0 always starts block 0.
     MT_DEV int block_start(int k) const {  // start of the leaf block holding slot k
         const uint32_t m = bsm & below(k + 1);
         const int l = 63 - __builtin_clzll(wave_ballot(m != 0));
-        return l * K + (31 - __builtin_clz((uint32_t)__builtin_amdgcn_readlane((int)m, l)));
+        return uni(l * K + (31 - __builtin_clz((uint32_t)__builtin_amdgcn_readlane((int)m, l))));
     }
     MT_DEV int next_start(int k) const { return first_from(bsm, k + 1); }  // end of the block holding k
     // set bits of the lanes' masks m inside slots [a, e) (a block spans one or two lanes almost always)
     MT_DEV int count_in(uint32_t m, int a, int e) const {
+        a = uni(a);
+        e = uni(e);
         if (e <= a) return 0;
         const uint32_t x = m & below(e) & ~below(a);
         const int la = a / K, lb = (e - 1) / K;
-        if (lb - la > 1) return wave_total(__popc(x));
+        if (lb - la > 1) return uni(wave_total(__popc(x)));
         int c = __popc((uint32_t)__builtin_amdgcn_readlane((int)x, la));
         if (lb != la) c += __popc((uint32_t)__builtin_amdgcn_readlane((int)x, lb));
-        return c;
+        return uni(c);
     }
     MT_DEV int live_in(int a, int e) const { return count_in(lvm, a, e); }
     // slot of the r-th (0-based) set bit of m inside [a, e); -1 if there is none
@@ -448,7 +468,7 @@ struct RWave {
     MT_DEV bool insert_at(int k, int a, int en, Elem e, int32_t sq) {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
         const bool front = k == a;  // new first child: it takes over the block's marks
-        PROF_BEGIN(ti0);
+        PROF_BEGIN(ti0, P_B_INS);
         shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
         if (front) {
             set_bs(k + 1, false);
@@ -456,11 +476,11 @@ struct RWave {
         }
         PROF_END(prof, P_B_INS, ti0);
         nlive += 1;
-        PROF_BEGIN(ti1);
+        PROF_BEGIN(ti1, P_B_LEAF);
         const bool over = live_in(a, en + 1) >= kMaxNodes;
         PROF_END(prof, P_B_LEAF, ti1);
         if (!over) return true;
-        PROF_BEGIN(ti2);
+        PROF_BEGIN(ti2, P_COMPACT);
         PROF_CNT(P_N_COMPACT, 1);
         const bool r = split_leaf(a, en + 1, sq);
         PROF_END(prof, P_COMPACT, ti2);
@@ -486,31 +506,30 @@ struct RWave {
         arena_sync();
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t i = base + lane;
-            if (i < cnt) arena[dst + i] = arena[src + i];
+            if (i < cnt) arena()[dst + i] = arena()[src + i];
         }
         dirty = true;
     }
-    // relocate every linked segment's text, in slot order, into the other arena half
-    MT_DEV void compact_text() {
-        PROF_BEGIN(tc);
+    // relocate every linked segment's text into the other arena half, in segment-id order: from the
+    // per-id lengths and offsets in LDS alone, so no register state is live in here (the content of
+    // every segment is what counts; its place in the arena is free)
+    MT_DEV void compact_text(int nid) {  // ids [0, nid) are the segments
+        PROF_BEGIN(tc, P_COMPACT);
         PROF_CNT(P_N_COMPACT, 1);
         arena_sync();
-#pragma unroll
-        for (int j = 0; j < K; j++) s.scr[idx(j)] = (int32_t)(((lvm >> j) & 1u) ? li[j] : kEmptyLi);
-        wave_sync();
+        const uint8_t* src0 = arena();
         uint8_t* dst = abase + (size_t)(text_half ^ 1u) * textcap;
         uint32_t carry = 0;
-        for (int base = 0; base < ns; base += 64) {
+        for (int base = 0; base < nid; base += 64) {
             const int i = base + lane;
-            const uint32_t v = i < ns ? (uint32_t)s.scr[i] : 0u;
-            const uint32_t l = len_of(v);
+            const uint32_t l = i < nid ? s.tln[i] : 0u;
             const uint32_t incl = (uint32_t)wave_incl_scan((int)l);
             const uint32_t at = carry + incl - l;
             if (l) {
-                const uint32_t id = id_of(v);
-                const uint8_t* src = arena + s.toff[id];
+                const uint8_t* src = src0 + s.toff[i];
+#pragma clang loop unroll(disable) vectorize(disable)
                 for (uint32_t q = 0; q < l; q++) dst[at + q] = src[q];
-                s.toff[id] = (uint16_t)at;
+                s.toff[i] = (uint16_t)at;
             }
             carry += (uint32_t)wave_last((int)incl);
         }
@@ -518,12 +537,11 @@ struct RWave {
         wave_sync();
         text_half ^= 1u;
         text_top = carry;
-        arena = dst;
         PROF_END(prof, P_COMPACT, tc);
     }
-    MT_DEV bool arena_reserve(uint32_t need, int32_t sq) {
+    MT_DEV bool arena_reserve(uint32_t need, int32_t sq, int nid) {
         if (text_top + need <= textcap) return true;
-        compact_text();
+        compact_text(nid);
         if (text_top + need <= textcap) return true;
         fail(MT_DERR_TEXT_ARENA, sq);
         return false;
@@ -533,7 +551,7 @@ struct RWave {
     // visible to the op's view that strictly contains pos, cut it (left part in place, cum kept
     // valid for the view) and return its right part r, to be inserted at slot k1 of leaf block b.
     MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& ba, int& be) {
-        PROF_BEGIN(ts0);
+        PROF_BEGIN(ts0, P_B_SRCH);
         int cs = cs0();
         int hitj = -1;
 #pragma unroll
@@ -545,7 +563,7 @@ struct RWave {
         PROF_END(prof, P_B_SRCH, ts0);
         if (!m) return false;
         PROF_CNT(P_N_SPLIT, 1);
-        PROF_BEGIN(tb0);
+        PROF_BEGIN(tb0, P_B_GET);
         const int lk = first_lane(m);
         const int k = lk * K + __builtin_amdgcn_readlane(hitj, lk);
         const Elem e = get(k);
@@ -554,27 +572,36 @@ struct RWave {
         const int off = pos - (e.cum - (int)len);
         const int t = alloc_id(sq);
         if (t < 0) return false;
-        PROF_BEGIN(tb1);
+        PROF_BEGIN(tb1, P_B_BLK);
         ba = block_start(k);
         be = next_start(k);
         PROF_END(prof, P_B_BLK, tb1);
-        PROF_BEGIN(tb2);
+        PROF_BEGIN(tb2, P_B_TXT);
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
         const uint32_t id = id_of(e.li);
         const uint32_t to = uniu(s.toff[id]);
+#ifdef MT_NO_NLQ
         uint8_t last = 0;  // a segment without any "\n" needs no text read
         if (e.cf & F_HASNL) {
             arena_sync();
-            last = arena[to + (uint32_t)off - 1];
+            last = arena()[to + (uint32_t)off - 1];
         }
+#endif
         if (lane == 0) {
             s.props[t] = s.props[id];
             s.toff[t] = (uint16_t)(to + (uint32_t)off);
+            s.tln[id] = (uint32_t)off;
+            s.tln[t] = len - (uint32_t)off;
         }
         r = e;
         r.li = (len - (uint32_t)off) | ((uint32_t)t << kLenBits);
         r.cf = e.cf;
+#ifdef MT_NO_NLQ
         set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & ~F_NL) | (last == '\n' ? F_NL : 0u));
+#else
+        // the left part ends in "\n" only if the segment has one: otherwise known now
+        set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & F_HASNL) ? ((e.cf & ~F_NL) | F_NLQ) : (e.cf & ~(F_NL | F_NLQ)));
+#endif
         set_cum(k, pos);
         wave_sync();
         PROF_END(prof, P_B_TXT, tb2);
@@ -703,7 +730,7 @@ struct RWave {
             const bool adj = __ballot(in_run && myt != pt + (incl - myl)) == 0;
             if (adj) break;  // nothing to copy
             if (pass == 0) {
-                if (!arena_reserve(total, cur_seq)) return;
+                if (!arena_reserve(total, cur_seq, next_id)) return;
                 continue;    // a compaction lays the run out contiguously
             }
             const uint32_t top = text_top;
@@ -721,6 +748,7 @@ struct RWave {
             text_top = top + total;
             wave_sync();
         }
+        if (lane == 0) s.tln[pid_] = total;
         const uint32_t pcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, p);
         const uint32_t lcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, (int)lastq);
         const uint32_t anynl = __ballot(in_run && (vcf & F_HASNL)) ? F_HASNL : 0u;
@@ -749,9 +777,17 @@ struct RWave {
         const bool mine = lane < cnt;
         const int4 z = mine ? s.zrec[lane] : make_int4(0, 0, 0, 0);
         const int32_t vsq = z.x;
-        const uint32_t vli = (uint32_t)z.y, vcf = (uint32_t)z.z;
+        const uint32_t vli = (uint32_t)z.y;
+        uint32_t vcf = (uint32_t)z.z;
         const int vslot = z.w;
         const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
+        if (__ballot(mine && (vcf & F_NLQ))) {  // the children's pending ENDS_WITH_NEWLINE, in one load
+            arena_sync();
+            if (mine && (vcf & F_NLQ)) {
+                const uint8_t c = arena()[(uint32_t)s.toff[id_of(vli)] + len_of(vli) - 1];
+                vcf = (vcf & ~(F_NL | F_NLQ)) | (c == '\n' ? F_NL : 0u);
+            }
+        }
         // scourNode's decisions (mergeTree.ts:1289-1365), lane-parallel: child q is unlinked if it
         // is a tombstone at or below the MSN; it is appended to the run before it if both are live,
         // acked at or below the MSN and non-empty, the run does not end in "\n", the props match
@@ -804,6 +840,7 @@ struct RWave {
         }
         // unlink: the slots become dead in place (their block marks stay)
         const bool gone = mine && ((unlink >> lane) & 1u);
+        if (gone) s.tln[id_of(vli)] = 0u;
         uint64_t gm = __ballot(gone);
         uint32_t kill = 0;
         while (gm) {
@@ -858,23 +895,16 @@ struct RWave {
         int cc = min(kMaxNodes - 1, total / half);
         if (cc < 1) cc = 1;
         const int base = total / cc, extra = total % cc;
-        const uint32_t lb = live_bits() & below(E) & ~below(A);
-        const int c = __popc(lb);
-        const int rbase = wave_incl_scan(c) - c;
-        uint32_t nbs = 0;  // the new block starts; every new block: needsScour undefined
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            bool v = idx(j) == A;
-            if ((lb >> j) & 1u) {
-                const int r = rbase + __popc(lb & ((1u << j) - 1u));
-                for (int t = 1; t < cc; t++) v = v || r == t * base + min(t, extra);
-            }
-            nbs |= v ? (1u << j) : 0u;
-        }
+        // the new block starts: slot A, then the live children of ranks t * base + min(t, extra)
+        // (one uniform lookup per new block, not a compare network per register); every new block:
+        // needsScour undefined
         const uint32_t rng = below(E) & ~below(A);
-        bsm = (bsm & ~rng) | (nbs & rng);
+        bsm &= ~rng;
         sc0 &= ~rng;
         sc1 &= ~rng;
+        set_bs(A, true);
+#pragma clang loop unroll(disable)
+        for (int t = 1; t < cc; t++) set_bs(nth_in(lvm, A, E, t * base + min(t, extra)), true);
         nb0 += cc - m;
         if (lane == 0) s.ibcnt[0][P] = (uint8_t)cc;
         wave_sync();
@@ -894,7 +924,7 @@ struct RWave {
     MT_DEV void zamboni() {
         for (int it = 0; it < 2; it++) {
             if (heap_n == 0 || uni(s.hseq[1]) > min_seq) break;
-            PROF_BEGIN(tz);
+            PROF_BEGIN(tz, P_ZPOP);
             const int id = heap_pop();
             if (id == (int)kDead) continue;
             const int k = slot_of_id(id);
@@ -911,7 +941,7 @@ struct RWave {
                     aa = step == 1 ? A : ee;
                     ee = next_start(aa);
                 }
-                PROF_BEGIN(ts);
+                PROF_BEGIN(ts, P_SCOUR);
                 PROF_CNT(P_N_SCOUR, 1);
                 const int kept = scour(aa, ee);
                 PROF_END(prof, P_SCOUR, ts);
@@ -927,7 +957,7 @@ struct RWave {
                 }
                 if (step == m) break;
             }
-            PROF_BEGIN(tr);
+            PROF_BEGIN(tr, P_REPACK);
             if (P >= 0) repack_leaf(P, fc, m, total, A, ee);
             PROF_END(prof, P_REPACK, tr);
             if (err) return;
@@ -994,13 +1024,14 @@ struct RWave {
         k = best != 0x7fffffff ? best : e;
         const int t = alloc_id(S);
         if (t < 0) return -1;
-        if (!arena_reserve((uint32_t)tlen, S)) return -1;
+        if (!arena_reserve((uint32_t)tlen, S, t)) return -1;  // (t's text is not written yet)
         const uint32_t top = text_top;
         bool hasnl = false;
+        uint8_t* const ar = arena();
         for (int base = 0; base < tlen; base += 64) {
             const int i = base + lane;
             const uint8_t c = i < tlen ? (uint8_t)(base == 0 ? pb : pay[i]) : 0;
-            if (i < tlen) arena[top + i] = c;
+            if (i < tlen) ar[top + i] = c;
             hasnl = hasnl || __ballot(i < tlen && c == '\n') != 0;
         }
         dirty = true;
@@ -1015,6 +1046,7 @@ struct RWave {
         if (lane == 0) {
             s.props[t] = p;
             s.toff[t] = (uint16_t)top;
+            s.tln[t] = (uint32_t)tlen;
         }
         text_top = top + (uint32_t)tlen;
         wave_sync();
@@ -1035,6 +1067,17 @@ struct RWave {
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = op.flags & MT_F_REWRITE;
         const uint32_t cbit = 1u << (C - 1);
+        // the op's (key, value) pairs as one uniform clear mask and set value: later pairs win, as
+        // applied in order (properties.ts:95-116)
+        uint64_t pclr = 0, pset = 0;
+        if (!is_remove) {
+            for (int q = 0; q < np; q++) {
+                const int k = (int)pbyte(pay, tlen + 2 * q);
+                const uint64_t m = 0xFFull << (8 * k);
+                pclr |= m;
+                pset = (pset & ~m) | ((uint64_t)pbyte(pay, tlen + 2 * q + 1) << (8 * k));
+            }
+        }
         uint32_t tm = 0;  // touched slots of this lane
         {
             int cs = cs0();
@@ -1055,9 +1098,8 @@ struct RWave {
                 cf[j] = mark ? ((f & ~0xFF00u) | F_RM | ((uint32_t)C << 8)) : (annot ? (f | F_PDEF) : f);
                 if (annot) {  // SegmentPropertiesManager.addProperties (remote, no combining op)
                     const uint32_t id = id_of(li[j]);
-                    uint64_t p = (f & F_PDEF) ? s.props[id] : 0;
-                    if (rewrite) p = 0;
-                    s.props[id] = apply_pairs(p, pay, tlen, np);
+                    const uint64_t p = ((f & F_PDEF) && !rewrite) ? s.props[id] : 0;
+                    s.props[id] = (p & ~pclr) | pset;
                 }
                 cs = ce;
             }
@@ -1097,14 +1139,14 @@ struct RWave {
             if (!(cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);
             if (!(min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);
             if (!(op.msn <= S)) return fail(MT_DERR_MSN_ORDER, S);
-            PROF_BEGIN(t0);
+            PROF_BEGIN(t0, P_SCAN);
             scan(op.ref_seq, op.client);
             PROF_END(prof, P_SCAN, t0);
             // insertion steps: the boundary splits (ensureIntervalBoundary), then for an insert
             // the new segment; every step ends in the one insert_at call site
             const int nsteps = ins ? (tlen > 0 ? 2 : 1) : 2;
             for (int step = 0; step < nsteps; step++) {
-                PROF_BEGIN(t1);
+                PROF_BEGIN2(t1, P_BOUND, P_INSERT);
                 const bool placing = ins && step == 1;
                 Elem e;
                 int k = 0, ba = 0, be = 0, t = -1;
@@ -1117,6 +1159,12 @@ struct RWave {
                     t = place_prep(op, pay, tlen, np, e, k, ba, be);
                     if (t < 0) return;
                 }
+                // (uniform by construction; the phi that merges the two prep paths is not
+                // provably so, and its users would run on the VALU)
+                k = uni(k);
+                ba = uni(ba);
+                be = uni(be);
+                t = uni(t);
                 const bool ok = insert_at(k, ba, be, e, S);
                 if (placing) {
                     PROF_END(prof, P_INSERT, t1);
@@ -1130,7 +1178,7 @@ struct RWave {
                 }
             }
             if (!ins) {
-                PROF_BEGIN(t2);
+                PROF_BEGIN(t2, P_RANGE);
                 range_action(op, pay, tlen, np);
                 PROF_END(prof, P_RANGE, t2);
             }
@@ -1149,7 +1197,7 @@ struct RWave {
                 if (!(msn > min_seq)) break;
                 min_seq = msn;
             }
-            PROF_BEGIN(t3);
+            PROF_BEGIN(t3, P_ZAMBONI);
             zamboni();
             PROF_END(prof, P_ZAMBONI, t3);
             if (err) return;
@@ -1225,6 +1273,7 @@ struct RWave {
         for (int i = lane; i < n; i += 64) {
             s.props[i] = g.props[so + i];
             s.toff[i] = (uint16_t)g.toff[so + i];
+            s.tln[i] = g.len[so + i];
             s.scr[i] = 0;
         }
         for (int Lv = 1; Lv < nlev; Lv++) {
@@ -1351,7 +1400,6 @@ struct RWave {
                 }
             }
         }
-        arena = abase + (size_t)text_half * textcap;
     }
 
     // one register field -> HBM in position order, staged through LDS (scattered LDS writes,
@@ -1375,6 +1423,21 @@ struct RWave {
         const int incl = wave_incl_scan(c);
         const int pbase = incl - c;
         const int nn = wave_last(incl);
+        {  // pending ENDS_WITH_NEWLINE flags (F_NLQ) from the text
+            uint32_t q = 0;
+#pragma unroll
+            for (int j = 0; j < K; j++) q |= ((cf[j] & F_NLQ) && ((lb >> j) & 1u)) ? (1u << j) : 0u;
+            if (__ballot(q != 0)) {
+                arena_sync();
+#pragma unroll
+                for (int j = 0; j < K; j++) {
+                    if ((q >> j) & 1u) {
+                        const uint8_t ch = arena()[(uint32_t)s.toff[id_of(li[j])] + len_of(li[j]) - 1];
+                        cf[j] = (cf[j] & ~(F_NL | F_NLQ)) | (ch == '\n' ? F_NL : 0u);
+                    }
+                }
+            }
+        }
         store_field(seq, lb, pbase, nn, [&](int i, uint32_t v) { g.seq[so + i] = (int32_t)v; });
         store_field(rseq, lb, pbase, nn, [&](int i, uint32_t v) { g.rseq[so + i] = (int32_t)v; });
         store_field(ov, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] = (uint64_t)v << 1; });
@@ -1492,34 +1555,29 @@ MT_DEV const mt_gstate& kernarg_gstate() {
     return *p;
 }
 
-// (tools/variants.sh A/Bs other choices on MI355X: K = 12 at 3 / 4 waves spills 150-400 VGPRs and
-// runs C3 at 0.63x / 0.39x; K = 8 at 2 / 4 waves runs C4 at 0.87x / 0.72x; K = 4 at 3 waves runs
-// C5 at 0.92x)
-#ifndef MT_WPE12
-#define MT_WPE12 2
+// Waves per SIMD by class.  The register state is 6 K VGPRs per lane and the op path needs ~110
+// more (text compaction reads no register state: compact_text), so K <= 5 fits 128 VGPRs (4 waves),
+// K <= 9 fits 168 (3), larger classes 256 (2).  MT_WPE_K<n>=w overrides one class for A/Bs.
+constexpr int wpe_default(int K) { return K <= 3 ? 5 : K <= 5 ? 4 : K <= 9 ? 3 : 2; }
+#define MT_WPE_OR(n, d) (MT_WPE_K##n > 0 ? MT_WPE_K##n : (d))
+#ifndef MT_WPE_K9
+#define MT_WPE_K9 0
 #endif
-#ifndef MT_WPE8
-#define MT_WPE8 3
+#ifndef MT_WPE_K10
+#define MT_WPE_K10 0
 #endif
-#ifndef MT_WPE4
-#define MT_WPE4 4
+#ifndef MT_WPE_K5
+#define MT_WPE_K5 0
 #endif
-#ifndef MT_WPE7
-#define MT_WPE7 MT_WPE8
+#ifndef MT_WPE_K3
+#define MT_WPE_K3 0
 #endif
-#ifndef MT_WPE6
-#define MT_WPE6 MT_WPE8
-#endif
-#ifndef MT_WPE5
-#define MT_WPE5 MT_WPE6
-#endif
-#ifndef MT_WPE10
-#define MT_WPE10 MT_WPE12
-#endif
+constexpr int wpe(int K) {
+    return K == 9 ? MT_WPE_OR(9, wpe_default(9)) : K == 10 ? MT_WPE_OR(10, wpe_default(10))
+         : K == 5 ? MT_WPE_OR(5, wpe_default(5)) : K <= 3 ? MT_WPE_OR(3, wpe_default(K)) : wpe_default(K);
+}
 template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
-    K >= 11 ? MT_WPE12 : K >= 9 ? MT_WPE10 : K == 8 ? MT_WPE8 : K == 7 ? MT_WPE7 : K == 6 ? MT_WPE6 : K == 5 ? MT_WPE5
-                                                                                                 : MT_WPE4))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                        const uint8_t* __restrict__ payload,
                                                        const uint32_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
@@ -1534,7 +1592,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
-    PROF_BEGIN(tl);
+    PROF_BEGIN(tl, P_LOAD);
     wv.load(kernarg_gstate(), d);
     PROF_END(wv.prof, P_LOAD, tl);
     // software pipeline: the records of the next 7..15 ops and the payload of op i+1 are in flight
@@ -1563,18 +1621,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(
             const uint32_t plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j * 8 + 7));
             pb0 = wv.lane < (int)plen ? payload[poff + wv.lane] : 0u;
         }
+        PROF_BEGIN(top, P_OP);
         wv.apply(op, payload);
+        PROF_END(wv.prof, P_OP, top);
 #ifdef MT_PROF
         wv.prof[P_OPS]++;
 #endif
     }
-    PROF_BEGIN(tt);
+    PROF_BEGIN(tt, P_STORE);
     wv.store(kernarg_gstate(), d);
     PROF_END(wv.prof, P_STORE, tt);
 #ifdef MT_PROF
     if (wv.lane == 0)
         for (int q = 0; q < P_NSLOT; q++)
-            atomicAdd(&mt_prof_acc[(K - 1) * 24 + q],
+            atomicAdd(&mt_prof_acc[(K - 1) * kProfStride + q],
                       (unsigned long long)wv.prof[q]);
 #endif
 }
@@ -1618,10 +1678,10 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
 // diagnostic: read (and clear) the per-phase cycle totals of a -DMT_PROF build (zeros otherwise)
 extern "C" int mt_prof_read(unsigned long long* out, int n) {
 #ifdef MT_PROF
-    if (n > 384) n = 384;
+    if (n > 16 * mtr::kProfStride) n = 16 * mtr::kProfStride;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mtr::mt_prof_acc), n * sizeof(unsigned long long)) != hipSuccess)
         return -1;
-    unsigned long long z[384] = {0};
+    unsigned long long z[16 * mtr::kProfStride] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(mtr::mt_prof_acc), z, sizeof z) != hipSuccess) return -1;
     return n;
 #else

@@ -79,7 +79,12 @@ constexpr int kMaxSegCap = 16384;
 // classes from 2048 up (the LDS engine's wide form, include/mtgpu.h "limits")
 constexpr int kFirstWide = kFirstLds;
 constexpr int kWideClasses = kNumClasses - kFirstWide;
-constexpr int kBuckets = kNumClasses + 1 + kWideClasses;
+// ... and, after those, the documents that need the LDS engine inside a register class (any client
+// id above 32, declared label keys): one bucket per register class, run by the LDS engine at that
+// class's capacity (mt_bin_kernel)
+constexpr int kBuckets = kNumClasses + 1 + kWideClasses + kFirstLds;
+// per-class statistics: the classes, the editing bucket, then the LDS engine inside each register class
+constexpr int kStatClasses = kNumClasses + 1 + kFirstLds;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -115,9 +120,10 @@ struct mt_engine {
     std::vector<hipEvent_t> kev;   // per apply launch: start/stop pairs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f, last_wall_ms = 0.f;
-    float cls_ms[kNumClasses] = {0};
-    uint32_t cls_launches[kNumClasses] = {0};
-    uint64_t cls_bytes[kNumClasses] = {0};
+    // per capacity class, plus one entry for the editing documents' bucket (index kNumClasses)
+    float cls_ms[kStatClasses] = {0};
+    uint32_t cls_launches[kStatClasses] = {0};
+    uint64_t cls_bytes[kStatClasses] = {0};
     std::vector<int> kev_cls;
     uint32_t last_launches = 0;
     uint64_t last_bytes = 0;
@@ -553,29 +559,33 @@ mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, co
         }
         b->max_ops_per_doc = std::max(b->max_ops_per_doc, doc_row_ptr[d + 1] - doc_row_ptr[d]);
     }
-    // payload bounds: the kernels trust these (a big batch is checked on all host cores)
-    auto bad_range = [&](uint64_t lo, uint64_t hi) {
-        bool bad = false;
-        for (uint64_t i = lo; i < hi; i++) bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
-        return bad;
+    // payload bounds (the kernels trust these) and whether any record needs the wide document
+    // form, in one pass; a big batch is checked on all host cores.  Result bit 0: bad, bit 1: wide.
+    auto scan_range = [&](uint64_t lo, uint64_t hi) {
+        bool bad = false, wide = false;
+        for (uint64_t i = lo; i < hi; i++) {
+            bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
+            wide |= wide_rec(ops[i]);
+        }
+        return (bad ? 1 : 0) | (wide ? 2 : 0);
     };
-    bool bad = false;
+    int flags = 0;
     const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
     if (n_ops < (1u << 20) || nt == 1) {
-        bad = bad_range(0, n_ops);
+        flags = scan_range(0, n_ops);
     } else {
         std::vector<std::thread> th;
-        std::vector<char> res(nt, 0);
+        std::vector<int> res(nt, 0);
         for (unsigned t = 0; t < nt; t++)
-            th.emplace_back([&, t] { res[t] = bad_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
+            th.emplace_back([&, t] { res[t] = scan_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
         for (auto& x : th) x.join();
-        for (char r : res) bad |= r != 0;
+        for (int r : res) flags |= r;
     }
-    if (bad) {
+    if (flags & 1) {
         delete b;
         return MT_ERR_ARG;
     }
-    for (uint64_t i = 0; i < n_ops && !b->wide; i++) b->wide = wide_rec(ops[i]);
+    b->wide = (flags & 2) != 0;
     if (hipMalloc(&b->ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
         hipMalloc(&b->payload, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||
         hipMalloc(&b->row_ptr, (b->n_docs + 1) * sizeof(uint32_t)) != hipSuccess) {
@@ -612,6 +622,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     }
     const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
+    const int lds_base = e->n_classes + 1 + (e->n_classes > kFirstWide ? e->n_classes - kFirstWide : 0);
     e->last_launches = 0;
     uint32_t nk = 0;
     HIP_OK(hipMemsetAsync(e->d_acc, 0, kBuckets * sizeof(unsigned long long), e->stream));
@@ -675,15 +686,48 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             e->kev_cls.push_back(c);
             nk++;
         }
+        // documents that need the LDS engine inside a register class: the LDS engine at that
+        // class's capacity, on the class's stream after its register launch
+        for (int c = 0; c < e->first_lds && c < e->n_classes; c++) {
+            const uint32_t cnt = e->h_counts[lds_base + c];
+            if (!cnt) continue;
+            hipStream_t st = e->stream;
+            if (e->concurrent) {
+                st = e->side[c];
+                if (!joined[c]) HIP_OK(hipStreamWaitEvent(st, e->fork_ev, 0));
+                joined[c] = true;
+            }
+            while (e->kev.size() < 2 * (nk + 1)) {
+                hipEvent_t ev;
+                HIP_OK(hipEventCreate(&ev));
+                e->kev.push_back(ev);
+            }
+            HIP_OK(hipEventRecord(e->kev[2 * nk], st));
+            HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
+                                   e->d_ids + (size_t)(lds_base + c) * b->n_docs, cnt, lo, per, st));
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], st));
+            e->kev_cls.push_back(kNumClasses + 1 + c);
+            nk++;
+        }
         for (int c = 0; c < kNumClasses; c++) {  // join: the next tick's binning sees every class done
             if (!joined[c]) continue;
             HIP_OK(hipEventRecord(e->join_ev[c], e->side[c]));
             HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
         // documents with an editing client (local edits + acks): the LDS engine's editing form
-        if (const uint32_t cnt = e->h_counts[e->n_classes])
+        if (const uint32_t cnt = e->h_counts[e->n_classes]) {
+            while (e->kev.size() < 2 * (nk + 1)) {
+                hipEvent_t ev;
+                HIP_OK(hipEventCreate(&ev));
+                e->kev.push_back(ev);
+            }
+            HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
             HIP_OK(mt_launch_apply_loc(&e->g, b->ops, b->payload, b->row_ptr, e->d_ids + (size_t)e->n_classes * b->n_docs,
                                        cnt, lo, per, e->stream));
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
+            e->kev_cls.push_back(kNumClasses);
+            nk++;
+        }
         // wide documents: the LDS engine's wide form, per class
         for (int c = kFirstWide; c < e->n_classes; c++) {
             const int k = e->n_classes + 1 + (c - kFirstWide);
@@ -706,7 +750,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     HIP_OK(hipEventRecord(e->ev1, e->stream));
     HIP_OK(hipEventSynchronize(e->ev1));
     float kms = 0.f;
-    for (int c = 0; c < kNumClasses; c++) {
+    for (int c = 0; c < kStatClasses; c++) {
         e->cls_ms[c] = 0.f;
         e->cls_launches[c] = 0;
     }
@@ -725,8 +769,14 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     e->last_launches = nk;
     e->last_bytes = 0;
     for (int c = 0; c < kNumClasses; c++) {
-        e->cls_bytes[c] = acc[c];
-        e->last_bytes += acc[c];
+        e->cls_bytes[c] = c < e->n_classes ? acc[c] : 0;
+        e->last_bytes += e->cls_bytes[c];
+    }
+    e->cls_bytes[kNumClasses] = acc[e->n_classes];  // the editing bucket
+    e->last_bytes += acc[e->n_classes];
+    for (int c = 0; c < kFirstLds; c++) {
+        e->cls_bytes[kNumClasses + 1 + c] = c < e->first_lds && c < e->n_classes ? acc[lds_base + c] : 0;
+        e->last_bytes += e->cls_bytes[kNumClasses + 1 + c];
     }
     return MT_OK;
 }
@@ -896,8 +946,11 @@ mt_status mt_last_apply_stats(mt_engine* e, float* ms, float* wall_ms, uint32_t*
 
 mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes) {
-    if (!e || cls >= (uint32_t)kNumClasses) return MT_ERR_ARG;
-    if (capacity) *capacity = (uint32_t)kClasses[cls];
+    if (!e || cls >= (uint32_t)kStatClasses) return MT_ERR_ARG;
+    if (capacity)
+        *capacity = cls < (uint32_t)kNumClasses    ? (uint32_t)kClasses[cls]
+                    : cls == (uint32_t)kNumClasses ? (MT_CLASS_EDITING | MT_LOC_CAP)
+                                                   : (MT_CLASS_LDS | (uint32_t)kClasses[cls - kNumClasses - 1]);
     if (kernel_ms) *kernel_ms = e->cls_ms[cls];
     if (launches) *launches = e->cls_launches[cls];
     if (alg_bytes) *alg_bytes = e->cls_bytes[cls];
@@ -907,7 +960,11 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
 mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint64_t cap) {
     if (!e || !buf || !cap) return MT_ERR_ARG;
     char tmp[96];
-    if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)
+    if (capacity & MT_CLASS_EDITING)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if (capacity & MT_CLASS_LDS)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_LDS)));
+    else if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)
         snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel<%u>", capacity / 64);
     else if (capacity > 2048)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u>", capacity);

@@ -198,10 +198,12 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // Bin the documents that have ops in this launch by the capacity class they need.  Each op
 // adds at most 2 segments (a boundary split + an insert, or two boundary splits), at most 2 leaf
 // blocks, and a handful of heap entries; the register engine also pads one slot per empty leaf
-// block.  classes[k] = {CAP, LB, IB, H}.  Documents that ever see a client id above 32 go to the
-// last class (the LDS engine, 64-client overlap sets).  Buckets: 0 .. n_classes-1 the capacity
-// classes, n_classes the editing documents, then one per class from first_wide on for the wide
-// documents (include/mtgpu.h "limits"; promoted here by their first wide op or client id >= 64).
+// block.  classes[k] = {CAP, LB, IB, H}.  Buckets: 0 .. n_classes-1 the capacity classes,
+// n_classes the editing documents, then one per class from first_wide on for the wide documents
+// (include/mtgpu.h "limits"; promoted here by their first wide op or client id >= 64), then -- when
+// the register engine serves classes 0 .. first_lds-1 -- one per such class for the documents that
+// need the LDS engine there (a client id above 32: 64-client overlap sets; declared label keys):
+// the LDS engine at that class's capacity, not at first_lds's.
 // Binning is wave-aggregated: one atomic per (wave, bucket).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
@@ -274,8 +276,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             bool editing = own >= 0;
             if (ops)
                 for (uint32_t i = a; i < b && !editing; i++) editing = ops[i].seq == -1 && ops[i].type != MT_OP_LOAD;
-            // (wide documents and snapshot appends start at the first class the LDS engine serves)
-            for (int k = (wide || lds_only) ? first_lds : 0; k < n_classes; k++) {
+            // (snapshot appends start at the first class the LDS engine serves)
+            for (int k = lds_only ? first_lds : 0; k < n_classes; k++) {
                 const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
                           h = classes[4 * k + 3];
                 if (sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= cap && sc.nb[0] + 2 * nops + 1 <= lb &&
@@ -305,6 +307,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     c = n_classes + 1 + (c - first_wide);
                 }
             }
+            if (wide && !wdoc && c < first_lds)  // the LDS engine at a register class's capacity
+                c = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + c;
             if (editing) c = n_classes;  // the editing documents' bucket (mt_launch_apply_loc)
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
@@ -320,7 +324,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0);
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + first_lds;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;

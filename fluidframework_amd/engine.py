@@ -235,9 +235,11 @@ class MergeEngine:
         _check(lib().mt_set_concurrent_classes(self.h, 1 if on else 0), 'mt_set_concurrent_classes')
 
     def last_class_stats(self):
-        """[(capacity, kernel_ms, launches, alg_bytes)] per LDS capacity class of the last apply."""
+        """[(capacity, kernel_ms, launches, alg_bytes)] per capacity class of the last apply (then the
+        editing bucket, MT_CLASS_EDITING | 1024, and the LDS engine inside each register class,
+        MT_CLASS_LDS | capacity: include/mtgpu.h)."""
         out = []
-        for c in range(32):  # classes 0.. until the library reports MT_ERR_ARG
+        for c in range(64):  # classes 0.. until the library reports MT_ERR_ARG
             cap, ms, n, nb = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
             if lib().mt_last_apply_class_stats(self.h, c, ctypes.byref(cap), ctypes.byref(ms), ctypes.byref(n),
                                                ctypes.byref(nb)) != 0:

@@ -90,3 +90,19 @@ def test_concurrent_classes_match_serialized(oracle_lib):
         assert len(classes) >= 3, classes
     assert np.array_equal(sums[0], sums[1])
     assert np.array_equal(sums[0], want)
+
+
+def test_wide_client_documents_use_small_lds_classes(oracle_lib):
+    """Documents with client ids above 32 run on the LDS engine at the capacity of the register
+    class they fit (MT_CLASS_LDS | capacity in the class stats), not all at 2048 segments."""
+    n = 64
+    batch = oracle_lib.generate(n, seed=5150, **WORKLOADS['wide'])
+    want = oracle_lib.Oracle(n).apply(batch, threads=8).checksums()
+    eng = _engine(n, 32)
+    eng.apply(batch)
+    assert np.array_equal(eng.checksums(), want)
+    used = {cap: launches for cap, _, launches, _ in eng.last_class_stats() if launches}
+    lds = sorted(cap & ~0x20000000 for cap in used if cap & 0x20000000)
+    assert lds and lds[0] < 1024, used
+    assert 2048 not in used, used
+    assert eng.class_kernel(0x20000000 | lds[0]).startswith('mt::apply_kernel<')

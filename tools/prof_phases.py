@@ -16,7 +16,8 @@ from fluidframework_amd.oplog import CONFIGS  # noqa: E402
 
 SLOTS = ['load', 'scan', 'boundary', 'insert', 'range', 'zamboni', 'scour', 'store', 'ops', 'zpop', 'repack',
          'b_get', 'b_blk', 'b_txt', 'b_ins', 'n_scour', 'n_unlink', 'n_append', 'n_split', 'compact',
-         'n_compact', 'n_appbytes', 'b_srch', 'b_leaf']
+         'n_compact', 'n_appbytes', 'b_srch', 'b_leaf', 'op']
+STRIDE = 32  # kProfStride in mt_apply_reg.hip
 
 ap = argparse.ArgumentParser()
 ap.add_argument('--config', default='C3')
@@ -31,15 +32,16 @@ eng = MergeEngine(a.docs, ops_per_launch=32)
 dev = eng.synthesize(seed=5, **cfg)
 L = lib()
 L.mt_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 384)()
-L.mt_prof_read(buf, 384)  # clear
+buf = (ctypes.c_ulonglong * (16 * STRIDE))()
+L.mt_prof_read(buf, 16 * STRIDE)  # clear
 eng.reset()
 eng.apply_staged(dev)
-L.mt_prof_read(buf, 384)
+L.mt_prof_read(buf, 16 * STRIDE)
 for k in range(1, 17):
-    v = list(buf[24 * (k - 1):24 * (k - 1) + len(SLOTS)])
+    v = list(buf[STRIDE * (k - 1):STRIDE * (k - 1) + len(SLOTS)])
     ops = v[SLOTS.index('ops')]
     if not ops:
         continue
-    parts = ' '.join((f'{n}={v[i] / ops:.2f}' if n.startswith('n_') else f'{n}={v[i] / ops:.0f}') for i, n in enumerate(SLOTS) if n != 'ops')
+    parts = ' '.join((f'{n}={v[i] / ops:.2f}' if n.startswith('n_') else f'{n}={v[i] / ops:.0f}') for i, n in enumerate(SLOTS)
+                     if n != 'ops' and (v[i] or n.startswith('n_')))
     print(f'K={k:2d} ops={ops:10d} cycles/op: {parts}')

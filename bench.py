@@ -48,7 +48,8 @@ PROFILES = os.path.join(HERE, 'profiles')
 PMC_ROUND = 'r02'
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
-                'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs'}
+                'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs',
+                'C3W': 'BASELINE.json configs[2] with 48 clients'}
 
 
 def pmc_path(config):
@@ -381,11 +382,12 @@ def timed_side_step(eng, dbatch, warmup=1, after=None):
 
 
 def slow_paths(device, n_docs, seed):
-    """N = 1 side lines for the paths that run on the LDS engine instead of the register engine
-    (DESIGN.md §7): C3 with the delta callbacks recorded (any SharedString with a sequenceDelta
-    listener), C3 with 48 clients (overlap sets past the register engine's 32 bits), and the
-    editing-client farm (local edits + remote ops + acks) tiled over 100K documents.  Each is a
-    full replay of HBM-resident logs, checked against the generation state or the oracle."""
+    """N = 1 side lines for the paths off the register engine's narrow form: C3 with
+    the delta callbacks recorded (any SharedString with a sequenceDelta listener: LDS engine), C3
+    with 48 clients (overlap sets past 32 bits: the register engine's C64 form), and the
+    editing-client farm (local edits + remote ops + acks: the LDS engine's editing form) tiled over
+    100K documents.  Each is a full replay of HBM-resident logs, checked against the generation
+    state or the oracle."""
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import CONFIGS, OpBatch
     out = {}
@@ -418,7 +420,8 @@ def slow_paths(device, n_docs, seed):
     eng.close()
 
     # C3 with 48 clients: client ids past 32 (the register engine's overlap set) -> LDS engine
-    cfg48 = dict(cfg, n_clients=48)
+    cfg48 = dict(CONFIGS['C3W'])
+    cfg48.pop('n_docs')
     eng = MergeEngine(n_docs, device=device, ops_per_launch=32)
     dev = eng.synthesize(seed=seed, **cfg48)
     gen_cs = eng.checksums()
@@ -432,7 +435,8 @@ def slow_paths(device, n_docs, seed):
         par.update(docs_checked=k, mismatches=int(np.count_nonzero(o.checksums() != cs[:k])), against='oracle/mtcpu.cpp')
     except Exception as ex:  # the checker is optional on a box without a compiler
         par['oracle'] = f'unavailable: {ex}'
-    out['C3_48_clients'] = {'workload': f'C3 with 48 clients ({n_docs} docs x 1024 ops; LDS engine)',
+    out['C3_48_clients'] = {'workload': f'C3 with 48 clients ({n_docs} docs x 1024 ops; the register engine\'s C64 '
+                                        'form: 64-bit overlap sets)',
                             'value': round(ops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
                             'roofline': rf, 'parity': par}
     dev.free()

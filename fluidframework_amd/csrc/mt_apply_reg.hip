@@ -35,7 +35,8 @@ namespace mtr {
 
 constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
-constexpr int kNarrowClients = 32;     // register overlap set: clients 1..32 at bit C-1
+constexpr int kNarrowClients = 32;     // register overlap set: clients 1..32 at bit C-1 of ov
+constexpr int kC64Clients = 63;        // ... and 33..63 at bit C-33 of oh (the C64 instantiation)
 constexpr uint32_t kLenBits = 17;      // li = len | id << 17  (len <= textcap <= 65536)
 constexpr uint32_t kLenMask = (1u << kLenBits) - 1;
 constexpr uint32_t kNoId = 0x7FFFu;    // id of a padding slot
@@ -115,11 +116,13 @@ struct RLds {
 
 struct Elem {
     int32_t seq, rseq;
-    uint32_t li, cf, ov;
+    uint32_t li, cf, ov, oh;
     int32_t cum;
 };
 
-template <int K>
+// W: documents with client ids above 32 (any up to 63): the overlap set takes a second register
+// per slot (oh), otherwise the same engine
+template <int K, bool W = false>
 struct RWave {
     using L = RLds<K>;
     static constexpr int CAP = L::CAP;
@@ -138,6 +141,7 @@ struct RWave {
     // end to end, and a wave-uniform dynamic index becomes s_set_gpr_idx register indexing.
     VI seq, rseq;
     VU li, cf, ov;
+    VU oh;   // (W only) overlap clients 33..63
     VI cum;  // per-op scratch: inclusive visible prefix for the op's view
     // ---- uniform document scalars
     int ns, nlive, nb0, nlev, heap_n, cur_seq, min_seq, err, err_seq, next_id;
@@ -281,6 +285,7 @@ struct RWave {
         r.li = (uint32_t)__builtin_amdgcn_readlane((int)li[jk], lk);
         r.cf = (uint32_t)__builtin_amdgcn_readlane((int)cf[jk], lk);
         r.ov = (uint32_t)__builtin_amdgcn_readlane((int)ov[jk], lk);
+        if constexpr (W) r.oh = (uint32_t)__builtin_amdgcn_readlane((int)oh[jk], lk);
         r.cum = __builtin_amdgcn_readlane(cum[jk], lk);
         return r;
     }
@@ -306,6 +311,7 @@ struct RWave {
         const int32_t c_seq = shr1(seq[K - 1], 0), c_rseq = shr1(rseq[K - 1], 0);
         const uint32_t c_li = (uint32_t)shr1((int)li[K - 1], 0), c_cf = (uint32_t)shr1((int)cf[K - 1], 0);
         const uint32_t c_ov = (uint32_t)shr1((int)ov[K - 1], 0);
+        const uint32_t c_oh = W ? (uint32_t)shr1((int)oh[K - 1], 0) : 0u;
         const int32_t c_cum = CUM ? shr1(cum[K - 1], 0) : 0;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
@@ -318,6 +324,10 @@ struct RWave {
             li[j] = mv ? pli : (at ? e.li : li[j]);
             cf[j] = mv ? pcf : (at ? e.cf : cf[j]);
             ov[j] = mv ? pov : (at ? e.ov : ov[j]);
+            if constexpr (W) {
+                const uint32_t poh = j ? oh[j - 1] : c_oh;
+                oh[j] = mv ? poh : (at ? e.oh : oh[j]);
+            }
             if (CUM) {
                 const int32_t pcm = j ? cum[j - 1] : c_cum;
                 cum[j] = mv ? pcm : (at ? e.cum : cum[j]);
@@ -332,7 +342,8 @@ struct RWave {
         // bitwise, not short-circuit: no branch per slot
         const uint32_t f = cf[j];
         const bool seen = ((f & 0xFFu) == (uint32_t)C) | (seq[j] <= R);
-        const bool hid = ((f & F_RM) != 0) & ((((f >> 8) & 0xFFu) == (uint32_t)C) | (((ov[j] >> (C - 1)) & 1u) != 0) |
+        const uint32_t ovw = (W && C > kNarrowClients) ? oh[j] : ov[j];
+        const bool hid = ((f & F_RM) != 0) & ((((f >> 8) & 0xFFu) == (uint32_t)C) | (((ovw >> ((C - 1) & 31)) & 1u) != 0) |
                                               (rseq[j] <= R));
         return (seen & !hid & (((lvm >> j) & 1u) != 0)) ? (int)len_of(li[j]) : 0;
     }
@@ -1055,6 +1066,7 @@ struct RWave {
         en.li = (uint32_t)tlen | ((uint32_t)t << kLenBits);
         en.cf = (uint32_t)C | fl;
         en.ov = 0;
+        en.oh = 0;
         en.cum = pos + tlen;
         return t;
     }
@@ -1066,7 +1078,8 @@ struct RWave {
         const int C = op.client, start = op.pos1, end = op.pos2;
         const bool is_remove = op.type == MT_OP_REMOVE;
         const bool rewrite = op.flags & MT_F_REWRITE;
-        const uint32_t cbit = 1u << (C - 1);
+        const uint32_t cbit = 1u << ((C - 1) & 31);
+        const bool hic = W && C > kNarrowClients;  // (W) the client's bit is in oh
         // the op's (key, value) pairs as one uniform clear mask and set value: later pairs win, as
         // applied in order (properties.ts:95-116)
         uint64_t pclr = 0, pset = 0;
@@ -1093,7 +1106,8 @@ struct RWave {
                 const bool mark = touched && is_remove && !was_rm;  // first remover wins
                 const bool overlap = touched && is_remove && was_rm;  // addOverlappingClient
                 const bool annot = touched && !is_remove;
-                ov[j] = overlap ? (ov[j] | cbit) : ov[j];
+                ov[j] = (overlap && !hic) ? (ov[j] | cbit) : ov[j];
+                if constexpr (W) oh[j] = (overlap && hic) ? (oh[j] | cbit) : oh[j];
                 rseq[j] = mark ? S : rseq[j];
                 cf[j] = mark ? ((f & ~0xFF00u) | F_RM | ((uint32_t)C << 8)) : (annot ? (f | F_PDEF) : f);
                 if (annot) {  // SegmentPropertiesManager.addProperties (remote, no combining op)
@@ -1126,7 +1140,7 @@ struct RWave {
         const int tlen = (int)op.payload_len - 2 * np;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
         if (!noop) {
-            if (op.client == 0 || op.client > kNarrowClients) return fail(MT_DERR_LIMITS, S);
+            if (op.client == 0 || op.client > (W ? kC64Clients : kNarrowClients)) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
             for (int q = 0; q < np; q++)
                 if (pbyte(pay, tlen + 2 * q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
@@ -1316,6 +1330,7 @@ struct RWave {
             li[j] = kEmptyLi;
             cf[j] = kEmptyCf;
             ov[j] = 0;
+            if constexpr (W) oh[j] = 0;
             cum[j] = 0;
         }
         if (i0 < n) {
@@ -1341,7 +1356,10 @@ struct RWave {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (K % 2 == 1) {
 #pragma unroll
-                for (int j = 0; j < K; j++) ov[j] = (uint32_t)(g.ovl[so + i0 + j] >> 1);
+                for (int j = 0; j < K; j++) {
+                    ov[j] = (uint32_t)(g.ovl[so + i0 + j] >> 1);
+                    if constexpr (W) oh[j] = (uint32_t)(g.ovl[so + i0 + j] >> 33);
+                }
             } else {
                 const uint32_t* op = reinterpret_cast<const uint32_t*>(g.ovl + so + i0);
 #pragma unroll
@@ -1349,6 +1367,10 @@ struct RWave {
                     const U4 x = reinterpret_cast<const U4*>(op)[c];  // two u64: (lo, hi), (lo, hi)
                     ov[2 * c] = (x[0] >> 1) | (x[1] << 31);
                     ov[2 * c + 1] = (x[2] >> 1) | (x[3] << 31);
+                    if constexpr (W) {
+                        oh[2 * c] = x[1] >> 1;
+                        oh[2 * c + 1] = x[3] >> 1;
+                    }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -1391,6 +1413,7 @@ struct RWave {
                         ph.li = kEmptyLi;
                         ph.cf = kEmptyCf;
                         ph.ov = 0;
+                        ph.oh = 0;
                         ph.cum = 0;
                         shift_in<false>(__builtin_amdgcn_readlane(incl - c, fl) + placed, ph, true,
                                         __builtin_amdgcn_readlane(scv, fl), false);
@@ -1441,6 +1464,8 @@ struct RWave {
         store_field(seq, lb, pbase, nn, [&](int i, uint32_t v) { g.seq[so + i] = (int32_t)v; });
         store_field(rseq, lb, pbase, nn, [&](int i, uint32_t v) { g.rseq[so + i] = (int32_t)v; });
         store_field(ov, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] = (uint64_t)v << 1; });
+        if constexpr (W)  // (after the low half: the same rows, read back and completed)
+            store_field(oh, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] |= (uint64_t)v << 33; });
         store_field(cf, lb, pbase, nn, [&](int i, uint32_t v) {
             g.client[so + i] = (uint8_t)(v & 0xFFu);
             g.rclient[so + i] = (uint8_t)((v >> 8) & 0xFFu);
@@ -1576,18 +1601,16 @@ constexpr int wpe(int K) {
     return K == 9 ? MT_WPE_OR(9, wpe_default(9)) : K == 10 ? MT_WPE_OR(10, wpe_default(10))
          : K == 5 ? MT_WPE_OR(5, wpe_default(5)) : K <= 3 ? MT_WPE_OR(3, wpe_default(K)) : wpe_default(K);
 }
-template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops,
-                                                       const uint8_t* __restrict__ payload,
-                                                       const uint32_t* __restrict__ row_ptr,
-                                                       const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
-                                                       uint32_t op_lo, uint32_t op_cnt) {
+template <int K, bool W>
+MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restrict__ ops,
+                      const uint8_t* __restrict__ payload, const uint32_t* __restrict__ row_ptr,
+                      const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     RLds<K>& lds = *reinterpret_cast<RLds<K>*>(smem);
-    RWave<K> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap);
+    RWave<K, W> wv(lds, text + (size_t)d * 2 * textcap, textcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -1639,9 +1662,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) vo
 #endif
 }
 
+// the narrow register engine (client ids <= 32) and its C64 form (client ids <= 63: a second overlap
+// register per slot, one occupancy step lower where the state no longer fits)
+constexpr int wpe_c64(int K) { return K <= 3 ? 4 : K <= 7 ? 3 : 2; }
+template <int K>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(
+    mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
+    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
+    uint32_t op_cnt) {
+    reg_apply<K, false>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
+}
+template <int K>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe_c64(K)))) void reg_apply_kernel_c64(
+    mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
+    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
+    uint32_t op_cnt) {
+    reg_apply<K, true>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
+}
+
 }  // namespace mtr
 
-extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstate* g, const mt_op_rec* ops,
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
@@ -1649,8 +1690,12 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, con
 #define MTR_LAUNCH(CAPV)                                                                                     \
     case CAPV: {                                                                                             \
         constexpr int K = CAPV / 64;                                                                         \
-        hipLaunchKernelGGL((mtr::reg_apply_kernel<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g, ops,    \
-                           payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                                \
+        if (c64)                                                                                             \
+            hipLaunchKernelGGL((mtr::reg_apply_kernel_c64<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g, \
+                               ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
+        else                                                                                                 \
+            hipLaunchKernelGGL((mtr::reg_apply_kernel<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g,     \
+                               ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
         return hipGetLastError();                                                                            \
     }
     switch (cap_class) {

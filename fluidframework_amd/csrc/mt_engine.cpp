@@ -23,7 +23,7 @@
 extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
                                       const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
                                       uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
-extern "C" hipError_t mt_launch_apply_reg(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstate* g, const mt_op_rec* ops,
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
@@ -79,12 +79,13 @@ constexpr int kMaxSegCap = 16384;
 // classes from 2048 up (the LDS engine's wide form, include/mtgpu.h "limits")
 constexpr int kFirstWide = kFirstLds;
 constexpr int kWideClasses = kNumClasses - kFirstWide;
-// ... and, after those, the documents that need the LDS engine inside a register class (any client
-// id above 32, declared label keys): one bucket per register class, run by the LDS engine at that
-// class's capacity (mt_bin_kernel)
-constexpr int kBuckets = kNumClasses + 1 + kWideClasses + kFirstLds;
-// per-class statistics: the classes, the editing bucket, then the LDS engine inside each register class
-constexpr int kStatClasses = kNumClasses + 1 + kFirstLds;
+// ... and, after those, per register class: the documents that need the LDS engine there (declared
+// label keys), run by the LDS engine at that class's capacity, then the documents with client ids
+// above 32, run by the register engine's C64 form (mt_bin_kernel)
+constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds;
+// per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
+// the register engine's C64 form per class
+constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -674,7 +675,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], st));
             if (e->use_reg && kClasses[c] <= kRegMaxCap)
-                HIP_OK(mt_launch_apply_reg(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                HIP_OK(mt_launch_apply_reg(kClasses[c], 0, &e->g, b->ops, b->payload, b->row_ptr,
                                            e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
             else if (c >= kLdsClasses)
                 HIP_OK(mt_launch_apply_big(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
@@ -686,10 +687,14 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             e->kev_cls.push_back(c);
             nk++;
         }
-        // documents that need the LDS engine inside a register class: the LDS engine at that
-        // class's capacity, on the class's stream after its register launch
-        for (int c = 0; c < e->first_lds && c < e->n_classes; c++) {
-            const uint32_t cnt = e->h_counts[lds_base + c];
+        // documents that need the LDS engine inside a register class (the LDS engine at that
+        // class's capacity), then those with client ids above 32 (the register engine's C64 form),
+        // on the class's stream after its register launch
+        for (int q = 0; q < 2 * e->first_lds; q++) {
+            const int c = q % e->first_lds;
+            const bool c64 = q >= e->first_lds;
+            if (c >= e->n_classes) continue;
+            const uint32_t cnt = e->h_counts[lds_base + q];
             if (!cnt) continue;
             hipStream_t st = e->stream;
             if (e->concurrent) {
@@ -703,10 +708,14 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], st));
-            HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
-                                   e->d_ids + (size_t)(lds_base + c) * b->n_docs, cnt, lo, per, st));
+            if (c64)
+                HIP_OK(mt_launch_apply_reg(kClasses[c], 1, &e->g, b->ops, b->payload, b->row_ptr,
+                                           e->d_ids + (size_t)(lds_base + q) * b->n_docs, cnt, lo, per, st));
+            else
+                HIP_OK(mt_launch_apply(lds_cap(kClasses[c]), &e->g, b->ops, b->payload, b->row_ptr,
+                                       e->d_ids + (size_t)(lds_base + q) * b->n_docs, cnt, lo, per, st));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], st));
-            e->kev_cls.push_back(kNumClasses + 1 + c);
+            e->kev_cls.push_back(kNumClasses + 1 + (c64 ? kFirstLds : 0) + c);
             nk++;
         }
         for (int c = 0; c < kNumClasses; c++) {  // join: the next tick's binning sees every class done
@@ -774,9 +783,11 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     }
     e->cls_bytes[kNumClasses] = acc[e->n_classes];  // the editing bucket
     e->last_bytes += acc[e->n_classes];
-    for (int c = 0; c < kFirstLds; c++) {
-        e->cls_bytes[kNumClasses + 1 + c] = c < e->first_lds && c < e->n_classes ? acc[lds_base + c] : 0;
-        e->last_bytes += e->cls_bytes[kNumClasses + 1 + c];
+    for (int q = 0; q < 2 * kFirstLds; q++) {
+        const int c = q % kFirstLds;
+        const bool on = e->first_lds == kFirstLds && c < e->n_classes;
+        e->cls_bytes[kNumClasses + 1 + q] = on ? acc[lds_base + (q >= kFirstLds ? e->first_lds : 0) + c] : 0;
+        e->last_bytes += e->cls_bytes[kNumClasses + 1 + q];
     }
     return MT_OK;
 }
@@ -947,10 +958,13 @@ mt_status mt_last_apply_stats(mt_engine* e, float* ms, float* wall_ms, uint32_t*
 mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes) {
     if (!e || cls >= (uint32_t)kStatClasses) return MT_ERR_ARG;
-    if (capacity)
+    if (capacity) {
+        const uint32_t q = cls - kNumClasses - 1;  // (past the editing bucket)
         *capacity = cls < (uint32_t)kNumClasses    ? (uint32_t)kClasses[cls]
                     : cls == (uint32_t)kNumClasses ? (MT_CLASS_EDITING | MT_LOC_CAP)
-                                                   : (MT_CLASS_LDS | (uint32_t)kClasses[cls - kNumClasses - 1]);
+                    : q < (uint32_t)kFirstLds      ? (MT_CLASS_LDS | (uint32_t)kClasses[q])
+                                                   : (MT_CLASS_C64 | (uint32_t)kClasses[q - kFirstLds]);
+    }
     if (kernel_ms) *kernel_ms = e->cls_ms[cls];
     if (launches) *launches = e->cls_launches[cls];
     if (alg_bytes) *alg_bytes = e->cls_bytes[cls];
@@ -962,6 +976,8 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
     char tmp[96];
     if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if (capacity & MT_CLASS_C64)
+        snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel_c64<%u>", (capacity & ~(uint32_t)MT_CLASS_C64) / 64);
     else if (capacity & MT_CLASS_LDS)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_LDS)));
     else if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)

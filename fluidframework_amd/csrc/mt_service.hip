@@ -185,7 +185,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             for (int L = 0; L < nlev; L++) sc.nb[L] = nb[L];
             sc.n_empty = ns == 0 ? 1u : 0u;
             sc.text_top = carry;
-            sc.wide = (lds || wdoc || lkeys != MT_NO_LABEL_KEYS ? MT_WIDE_LDS : 0u) | (wdoc ? MT_WIDE_DOC : 0u);
+            sc.wide = (wdoc || lkeys != MT_NO_LABEL_KEYS ? MT_WIDE_LDS : 0u) | (lds ? MT_WIDE_C64 : 0u) |
+                      (wdoc ? MT_WIDE_DOC : 0u);
         }
         sc.cur_seq = cur_seq[w];
         sc.min_seq = min_seq[w];
@@ -202,8 +203,9 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // n_classes the editing documents, then one per class from first_wide on for the wide documents
 // (include/mtgpu.h "limits"; promoted here by their first wide op or client id >= 64), then -- when
 // the register engine serves classes 0 .. first_lds-1 -- one per such class for the documents that
-// need the LDS engine there (a client id above 32: 64-client overlap sets; declared label keys):
-// the LDS engine at that class's capacity, not at first_lds's.
+// need the LDS engine there (declared label keys):
+// the LDS engine at that class's capacity, not at first_lds's; then one per such class for the
+// documents that only need 64-bit overlap sets (a client id above 32): the register engine's C64 form.
 // Binning is wave-aggregated: one atomic per (wave, bucket).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
@@ -249,26 +251,27 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     }
                 }
             }
-            bool wide = sc.wide != 0;
+            const bool needs_lds = (sc.wide & MT_WIDE_LDS) != 0;
+            bool c64 = (sc.wide & MT_WIDE_C64) != 0;
             bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
             // snapshot body appends (MT_OP_LOAD, SnapshotLoader.loadBody) are applied by the LDS
             // engine only: the register engine's hot loop stays free of them
             bool lds_only = false;
             if (ops)
                 for (uint32_t i = a; i < b && !lds_only; i++) lds_only = MT_OP_TYPE(ops[i]) == MT_OP_LOAD;
-            if ((!wide || !wdoc) && ops) {
+            if (!wdoc && ops) {
                 for (uint32_t i = a; i < b; i++) {
                     const mt_op_rec& o = ops[i];
                     const uint32_t c = o.client;
                     const bool load = MT_OP_TYPE(o) == MT_OP_LOAD;
                     const uint32_t c0 = load ? (c & 0xFFu) : c, c1 = load ? (c >> 8) : 0u;
                     const bool has0 = !load || c0 != MT_CLIENT_NONCOLLAB, has1 = load && o.pos2 >= 0;
-                    wide = wide || (has0 && c0 > 32) || (has1 && c1 > 32);
+                    c64 = c64 || (has0 && c0 > 32) || (has1 && c1 > 32);
                     wdoc = wdoc || (o.type & MT_OP_WIDE) ||
                            (load ? ((has0 && c0 >= MT_MAX_CLIENTS) || (has1 && c1 >= MT_MAX_CLIENTS))
                                  : (!MT_OP_IS_NOOP(o) && c >= MT_MAX_CLIENTS));
                 }
-                if (wide && !(sc.wide & MT_WIDE_LDS)) g.sc[d].wide = sc.wide | MT_WIDE_LDS;
+                if (c64 && !(sc.wide & MT_WIDE_C64)) g.sc[d].wide = sc.wide | MT_WIDE_C64;
             }
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
@@ -307,8 +310,11 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     c = n_classes + 1 + (c - first_wide);
                 }
             }
-            if (wide && !wdoc && c < first_lds)  // the LDS engine at a register class's capacity
-                c = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + c;
+            if (!wdoc && c < first_lds && (needs_lds || c64)) {
+                // the LDS engine at a register class's capacity, or the register engine's C64 form
+                const int lds_base = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0);
+                c = (needs_lds ? lds_base : lds_base + first_lds) + c;
+            }
             if (editing) c = n_classes;  // the editing documents' bucket (mt_launch_apply_loc)
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
@@ -324,7 +330,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + first_lds;
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;

@@ -49,8 +49,9 @@ struct mt_doc_scalars {      // 84 bytes
 };
 #define MT_NO_LABEL_KEYS 0xFFFFu
 
-#define MT_WIDE_LDS 1u
-#define MT_WIDE_DOC 2u
+#define MT_WIDE_LDS 1u  // needs the LDS engine (declared label keys, the wide form)
+#define MT_WIDE_DOC 2u  // the wide document form (include/mtgpu.h "limits")
+#define MT_WIDE_C64 4u  // has seen a client id above 32: 64-bit overlap sets (register engine: its C64 form)
 
 // An editing client's document (client.ts:163-214, 588-625): its local
 // edits are pending until their acks.  Pending edit ordinals [glo, ghi) (at most 64 at once) index

@@ -150,6 +150,9 @@ CONFIGS = {
                p_insert=0.45, p_remove=0.30, p_overlap=0.5, p_null=0.05, p_rewrite=0.02, p_insert_props=0.1),
     'C4': dict(n_docs=100_000, n_clients=8, ops_per_doc=1024, max_lag=256, stall_ops=200,
                p_insert=0.6, p_remove=0.4),
+    # C3 with 48 clients: overlap sets past 32 bits (side line of bench.py)
+    'C3W': dict(n_docs=100_000, n_clients=48, ops_per_doc=1024, max_lag=32, n_keys=8, n_values=16,
+                p_insert=0.45, p_remove=0.30, p_overlap=0.5, p_null=0.05, p_rewrite=0.02, p_insert_props=0.1),
     # 1M documents over the 8 GPUs of a node (n_docs is per GPU): raw client messages go through
     # the deli kernel (seq / msn assigned and stamped into the op records), then the apply.  The
     # 8 clients' joins are the deli checkpoint the documents start from (joined at seq 0).

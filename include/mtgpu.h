@@ -255,10 +255,13 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
 /* The same, per capacity class (cls = 0, 1, ... for 128, 192, 256 ... 1024 segments in steps of 64,
  * then 2048 / 4096 / 8192 / 16384, then one entry for the editing documents' bucket, whose capacity
  * reads MT_CLASS_EDITING | MT_LOC_CAP, then one per register class for the documents the LDS engine
- * runs at that capacity (a client id above 32, declared label keys), reading MT_CLASS_LDS | capacity;
- * MT_ERR_ARG past the last): each class is one kernel instantiation (see mt_class_kernel_name). */
+ * runs at that capacity (declared label keys), reading MT_CLASS_LDS | capacity, then one per register
+ * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),
+ * reading MT_CLASS_C64 | capacity; MT_ERR_ARG past the last): each class is one kernel
+ * instantiation (see mt_class_kernel_name). */
 #define MT_CLASS_EDITING 0x40000000u
 #define MT_CLASS_LDS 0x20000000u
+#define MT_CLASS_C64 0x10000000u
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);
 /* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class

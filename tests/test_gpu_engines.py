@@ -92,9 +92,11 @@ def test_concurrent_classes_match_serialized(oracle_lib):
     assert np.array_equal(sums[0], want)
 
 
-def test_wide_client_documents_use_small_lds_classes(oracle_lib):
-    """Documents with client ids above 32 run on the LDS engine at the capacity of the register
-    class they fit (MT_CLASS_LDS | capacity in the class stats), not all at 2048 segments."""
+def test_wide_client_documents_use_the_c64_register_form(oracle_lib):
+    """Documents with client ids above 32 run on the register engine's C64 form (a second overlap
+    register per slot: MT_CLASS_C64 | capacity in the class stats, mtr::reg_apply_kernel_c64<K>), at
+    the capacity of the class they fit, not on the LDS engine at 2048 segments; label-key documents
+    keep the LDS engine at their class's capacity (MT_CLASS_LDS)."""
     n = 64
     batch = oracle_lib.generate(n, seed=5150, **WORKLOADS['wide'])
     want = oracle_lib.Oracle(n).apply(batch, threads=8).checksums()
@@ -102,7 +104,14 @@ def test_wide_client_documents_use_small_lds_classes(oracle_lib):
     eng.apply(batch)
     assert np.array_equal(eng.checksums(), want)
     used = {cap: launches for cap, _, launches, _ in eng.last_class_stats() if launches}
-    lds = sorted(cap & ~0x20000000 for cap in used if cap & 0x20000000)
-    assert lds and lds[0] < 1024, used
+    c64 = sorted(cap & ~0x10000000 for cap in used if cap & 0x10000000)
+    assert c64 and c64[0] < 1024, used
     assert 2048 not in used, used
-    assert eng.class_kernel(0x20000000 | lds[0]).startswith('mt::apply_kernel<')
+    assert eng.class_kernel(0x10000000 | c64[0]) == 'mtr::reg_apply_kernel_c64<%d>' % (c64[0] // 64)
+    # the same documents with declared label keys: the LDS engine at the register classes' capacities
+    eng2 = _engine(n, 32)
+    eng2.set_label_keys(6, 7)
+    eng2.apply(batch)
+    assert np.array_equal(eng2.checksums(), want)
+    used2 = {cap: launches for cap, _, launches, _ in eng2.last_class_stats() if launches}
+    assert any(cap & 0x20000000 for cap in used2) and not any(cap & 0x10000000 for cap in used2), used2

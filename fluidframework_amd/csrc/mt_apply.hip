@@ -85,7 +85,9 @@ struct Lds {
     uint64_t pxh[W ? CAP : 1];
     uint32_t wide;                // the document's mt_doc_scalars.wide bits
     uint32_t lkeys;               // its declared label keys (mt_doc_scalars.label_keys)
-    uint32_t slab[CAP];           // a stale marker's cached label value ids (mt_gstate.slab)
+    // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
+    // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
+    uint32_t slab[LOC ? 1 : CAP];
 };
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
@@ -116,6 +118,7 @@ struct Wave {
     mt_op_rec* rg = nullptr;  // (LOC) the document's regenerated-op buffer and its payload
     uint8_t* rgp = nullptr;
 
+    uint32_t* xslab = nullptr;  // (LOC) this document's slot-indexed slab in HBM while it tracks labels
     MT_DEV Wave(L& lds, uint8_t* a, uint32_t tc_bytes, mt_event* e = nullptr, uint32_t ec = 0)
         : s(lds), lane(lane_id()), abase(reinterpret_cast<TC*>(a)), arena(reinterpret_cast<TC*>(a)),
           textcap(tc_bytes / (uint32_t)sizeof(TC)), ev(e), evcap(ec) {}
@@ -215,7 +218,10 @@ struct Wave {
             const bool def = (f & MT_SF_PDEF) != 0;
             const uint32_t vt = def && kt < (uint32_t)kKeys ? pval(sl, (int)kt) : 0u;
             const uint32_t vr = def && kr < (uint32_t)kKeys ? pval(sl, (int)kr) : 0u;
-            s.slab[sl] = vt | (vr << 16);
+            if constexpr (LOC)
+                xslab[sl] = vt | (vr << 16);
+            else
+                s.slab[sl] = vt | (vr << 16);
             s.flags[sl] = (uint8_t)(f | MT_SF_STALE);
         }
     }
@@ -1706,7 +1712,15 @@ struct Wave {
             s.order[i] = (uint16_t)i;
         }
         const bool trk = sc.label_keys != MT_NO_LABEL_KEYS && g.slab;
-        for (int i = lane; i < n; i += 64) s.slab[i] = trk ? g.slab[so + i] : 0u;
+        if constexpr (LOC) {
+            xslab = trk ? g.slabx + so : nullptr;
+            if (trk) {
+                for (int i = lane; i < n; i += 64) xslab[i] = g.slab[so + i];
+                __threadfence_block();  // (lanes write and later read each other's slots)
+            }
+        } else {
+            for (int i = lane; i < n; i += 64) s.slab[i] = trk ? g.slab[so + i] : 0u;
+        }
         const size_t lo = (size_t)d * g.lbcap;
         for (int i = lane; i < sc.nb[0]; i += 64) {
             s.lbcnt[i] = g.lbcnt[lo + i];
@@ -1822,6 +1836,8 @@ struct Wave {
         const size_t so = (size_t)d * g.segcap;
         if ((uint32_t)n > g.segcap || s.nb[0] > (int)g.lbcap || s.heap_n >= (int)g.hcap) fail(MT_DERR_CAPACITY, s.cur_seq);
         const int nn = min(n, (int)g.segcap);
+        if constexpr (LOC)
+            if (xslab) __threadfence_block();  // mark_stale's HBM writes, read below by other lanes
         for (int i = lane; i < nn; i += 64) {
             const int sl = s.order[i];
             g.seq[so + i] = s.seq[sl];
@@ -1833,7 +1849,7 @@ struct Wave {
             g.client[so + i] = s.client[sl];
             g.rclient[so + i] = s.rclient[sl];
             g.flags[so + i] = s.flags[sl];
-            if (track()) g.slab[so + i] = s.slab[sl];
+            if (track()) g.slab[so + i] = LOC ? xslab[sl] : s.slab[sl];
             s.cum[sl] = i;  // slot -> position for the heap remap
         }
         sync();

@@ -111,7 +111,11 @@ struct RLds {
     uint8_t ibcnt[MT_MAXLEV - 1][IB];  // interior levels: level L's child counts in ibcnt[L - 1]
     uint8_t lbsc[LB + 1];   // store staging: needsScour per leaf block
     int32_t nb[MT_MAXLEV];  // blocks per interior level (leaf blocks are counted by BS bits)
-    int4 zrec[kMaxNodes];   // scour scratch: live children by rank {seq or rseq, li, cf, slot}
+    // scour scratch: the live children by rank, one array per field (separate 4-byte stores: no
+    // 4-register tuple built per slot, which cost ~20 VGPRs at the scour's register peak)
+    int32_t zsq[kMaxNodes];  // the removal seq of a removed child, else its seq
+    uint32_t zli[kMaxNodes], zcf[kMaxNodes];
+    int32_t zsl[kMaxNodes];  // its slot
 };
 
 struct Elem {
@@ -781,16 +785,18 @@ struct RWave {
         for (int j = 0; j < K; j++) {
             if ((lb >> j) & 1u) {
                 const int q = rbase + __popc(lb & ((1u << j) - 1u));
-                s.zrec[q] = make_int4((cf[j] & F_RM) ? rseq[j] : seq[j], (int)li[j], (int)cf[j], idx(j));
+                s.zsq[q] = (cf[j] & F_RM) ? rseq[j] : seq[j];
+                s.zli[q] = li[j];
+                s.zcf[q] = cf[j];
+                s.zsl[q] = idx(j);
             }
         }
         wave_sync();
         const bool mine = lane < cnt;
-        const int4 z = mine ? s.zrec[lane] : make_int4(0, 0, 0, 0);
-        const int32_t vsq = z.x;
-        const uint32_t vli = (uint32_t)z.y;
-        uint32_t vcf = (uint32_t)z.z;
-        const int vslot = z.w;
+        const int32_t vsq = mine ? s.zsq[lane] : 0;
+        const uint32_t vli = mine ? s.zli[lane] : 0u;
+        uint32_t vcf = mine ? s.zcf[lane] : 0u;
+        const int vslot = mine ? s.zsl[lane] : 0;
         const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
         if (__ballot(mine && (vcf & F_NLQ))) {  // the children's pending ENDS_WITH_NEWLINE, in one load
             arena_sync();
@@ -1582,8 +1588,9 @@ MT_DEV const mt_gstate& kernarg_gstate() {
 
 // Waves per SIMD by class.  The register state is 6 K VGPRs per lane and the op path needs ~110
 // more (text compaction reads no register state: compact_text), so K <= 5 fits 128 VGPRs (4 waves),
-// K <= 9 fits 168 (3), larger classes 256 (2).  MT_WPE_K<n>=w overrides one class for A/Bs.
-constexpr int wpe_default(int K) { return K <= 3 ? 5 : K <= 5 ? 4 : K <= 9 ? 3 : 2; }
+// K <= 9 fits 168 (3), larger classes 256 (2); K = 10 runs at 3 with 48 B of scratch per lane, which
+// measured faster than 2 without (profiles/r03_ab_soa_C3.log).  MT_WPE_K<n>=w overrides one class.
+constexpr int wpe_default(int K) { return K <= 3 ? 5 : K <= 5 ? 4 : K <= 10 ? 3 : 2; }
 #define MT_WPE_OR(n, d) (MT_WPE_K##n > 0 ? MT_WPE_K##n : (d))
 #ifndef MT_WPE_K9
 #define MT_WPE_K9 0
@@ -1594,11 +1601,15 @@ constexpr int wpe_default(int K) { return K <= 3 ? 5 : K <= 5 ? 4 : K <= 9 ? 3 :
 #ifndef MT_WPE_K5
 #define MT_WPE_K5 0
 #endif
+#ifndef MT_WPE_K11
+#define MT_WPE_K11 0
+#endif
 #ifndef MT_WPE_K3
 #define MT_WPE_K3 0
 #endif
 constexpr int wpe(int K) {
     return K == 9 ? MT_WPE_OR(9, wpe_default(9)) : K == 10 ? MT_WPE_OR(10, wpe_default(10))
+         : K == 11 ? MT_WPE_OR(11, wpe_default(11))
          : K == 5 ? MT_WPE_OR(5, wpe_default(5)) : K <= 3 ? MT_WPE_OR(3, wpe_default(K)) : wpe_default(K);
 }
 template <int K, bool W>

@@ -345,9 +345,12 @@ mt_status mt_set_label_keys(mt_engine* e, uint32_t doc, int tile_key, int range_
         if (merge(e->lkeys[d], keys) == 0xFFFFFFFFu) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     if (!e->g.slab) {
-        uint32_t* p = nullptr;
-        if (dalloc(e, &p, (size_t)e->cfg.max_docs * e->g.segcap)) return MT_ERR_NOMEM;
+        uint32_t *p = nullptr, *px = nullptr;
+        if (dalloc(e, &p, (size_t)e->cfg.max_docs * e->g.segcap) ||
+            dalloc(e, &px, (size_t)e->cfg.max_docs * e->g.segcap))
+            return MT_ERR_NOMEM;
         e->g.slab = p;
+        e->g.slabx = px;
     }
     for (uint32_t d = d0; d < d1; d++) e->lkeys[d] = (uint16_t)merge(e->lkeys[d], keys);
     e->gen++;

@@ -92,6 +92,8 @@ struct mt_gstate {
     uint64_t* pxh;
     uint32_t* slab;    // [doc][segcap] a stale marker's cached label value ids: tile key (low 16 bits),
                        // range key (high 16) -- allocated on the first mt_set_label_keys, else null
+    uint32_t* slabx;   // [doc][segcap] the editing form's slot-indexed slab during a launch (its LDS
+                       // has no room for it: mt_apply.hip Lds<.., LOC>); allocated with slab
     uint8_t* client;
     uint8_t* rclient;
     uint8_t* flags;

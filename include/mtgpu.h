@@ -265,7 +265,9 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);
 /* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class
- * `capacity` on this engine: the register engine for <= 1024 segments, else the LDS engine. */
+ * `capacity` on this engine: the register engine for <= 1024 segments, else the LDS engine; with
+ * MT_CLASS_C64 the register engine's 64-bit overlap form, MT_CLASS_LDS / MT_CLASS_EDITING the LDS
+ * engine at that capacity / its editing form. */
 mt_status mt_class_kernel_name(mt_engine* eng, uint32_t capacity, char* buf, uint64_t cap);
 /* Snapshot of one document: what `new SnapshotV1(mergeTree).extractSync()`
  * + `emit()` write (packages/dds/merge-tree/src/snapshotV1.ts:85-247) -- the segments below the
@@ -364,7 +366,7 @@ mt_status mt_range_stacks(mt_engine* eng, const mt_tile_query* q, uint32_t n, ui
  * the engine tracks the reference's block caches for those labels (see findTile above); the host calls
  * it when it interns either key for a document, before submitting the op that first carries it (-1
  * leaves a key as it is, so the two may be declared by separate calls).  A document with declared keys
- * runs on the LDS engine.  A key is declared once per document: declaring it again as a different id
+ * runs on the LDS engine (at its capacity class's size).  A key is declared once per document: declaring it again as a different id
  * returns MT_ERR_ARG. */
 #define MT_ALL_DOCS 0xFFFFFFFFu
 mt_status mt_set_label_keys(mt_engine* eng, uint32_t doc, int tile_key, int range_key);

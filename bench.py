@@ -45,7 +45,8 @@ METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofli
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
-PMC_ROUND = 'r02'
+PMC_ROUND = 'r03'
+CAL_ROUND = 'r02'  # profiles/<round>_js_calibration.json: r of the JS baseline (oracle/tsref/calibrate.py)
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
                 'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs',
@@ -258,7 +259,7 @@ def main():
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(dev, cs, n_docs, args.cpu_seconds)
+        cpu, parity = cpu_baseline(dev, cs, n_docs, args.cpu_seconds, args.config)
 
     slow = None
     if world == 1 and args.config == 'C3' and not args.no_slow_paths and not args.docs and not args.ops:
@@ -557,7 +558,7 @@ def h2d_step_deli(eng, dev, deli, d_msgs, d_mrow, n_msgs, d_tick, job_ops, barri
                     'ticketing + apply in the timed region'}
 
 
-def cpu_baseline(dev, gpu_cs, n_docs, budget_s):
+def cpu_baseline(dev, gpu_cs, n_docs, budget_s, config='C3'):
     """Replay a bounded sample of the same op logs on the CPU oracle (port of the reference's
     observer path) with all of this host's cores; check the GPU checksums of the sample."""
     from oracle import oracle
@@ -587,14 +588,14 @@ def cpu_baseline(dev, gpu_cs, n_docs, budget_s):
            'sample': f'docs [0, {done_docs}) of the same device-generated logs ({ops} ops, {secs:.1f} s), '
                      f'oracle/mtcpu.cpp observer replay (C++), {threads} threads (one per core of the host share)'}
     parity = {'docs_checked': done_docs, 'mismatches': mism, 'against': 'oracle/mtcpu.cpp'}
-    js = js_baseline(dev, n_docs, threads)
+    js = js_baseline(dev, n_docs, threads, config)
     if js is None:
         return cpp, parity
     js['cpp_port'] = cpp
     return js, parity
 
 
-def js_baseline(dev, n_docs, threads, docs=1536):
+def js_baseline(dev, n_docs, threads, config='C3', docs=1536):
     """The reference's own form of the baseline (BASELINE.json north_star: the TypeScript merge-tree
     with one worker_thread per host core): js/observerReplay.js, a JavaScript restatement of the
     observer path, over a sample of the same logs, scaled by r = reference / restatement measured
@@ -616,12 +617,16 @@ def js_baseline(dev, n_docs, threads, docs=1536):
         return None
     finally:
         os.unlink(path)
-    cal = {}
-    try:
-        with open(os.path.join(PROFILES, f'{PMC_ROUND}_js_calibration.json')) as f:
-            cal = json.load(f)
-    except (OSError, ValueError):
-        pass
+    cal, cal_src = {}, None
+    for name in (f'r03_js_calibration_{config}.json', f'{CAL_ROUND}_js_calibration.json'):
+        try:
+            with open(os.path.join(PROFILES, name)) as f:
+                c = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if c.get('config') == config:
+            cal, cal_src = c, name
+            break
     v = res['ops_per_sec']
     line = {'value': round(v, 1), 'unit': 'ops/s', 'cores': threads, 'kind': 'port',
             'sample': f'docs [0, {d1}) of the same device-generated logs ({res["ops"]} ops), js/observerReplay.js '
@@ -632,7 +637,7 @@ def js_baseline(dev, n_docs, threads, docs=1536):
         line['calibration'] = {'r': round(cal['r'], 4), 'reference_ops_per_sec': round(cal['reference_ops_per_sec'], 1),
                                'restatement_ops_per_sec': round(cal['restatement_ops_per_sec'], 1),
                                'threads': cal['threads'], 'config': cal['config'], 'docs': cal['docs'],
-                               'source': f'profiles/{PMC_ROUND}_js_calibration.json (the transpiled reference '
+                               'source': f'profiles/{cal_src} (the transpiled reference '
                                          'vs this restatement, build container, identical logs)'}
     return line
 

@@ -2064,7 +2064,11 @@ static hipError_t launch_any(int cap_class, bool gen, const mt_gstate* g, mt_op_
     switch (cap_class) {
         MT_LAUNCH(128)
         MT_LAUNCH(256)
+        MT_LAUNCH(384)
         MT_LAUNCH(512)
+        MT_LAUNCH(640)
+        MT_LAUNCH(768)
+        MT_LAUNCH(896)
         MT_LAUNCH(1024)
         MT_LAUNCH(2048)
         default:
@@ -2145,15 +2149,26 @@ extern "C" size_t mt_lds_bytes_wide(int cap_class) {
 }
 
 // documents with an editing client (mt_bin_kernel's last bucket): the LDS engine's editing form
-extern "C" hipError_t mt_launch_apply_loc(const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
-                                          const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
-                                          uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
+extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                          const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
+                                          uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     mt::GenArgs ga{};
-    hipLaunchKernelGGL((mt::apply_kernel<MT_LOC_CAP, false, true>), dim3(n_docs), dim3(64),
-                       sizeof(mt::Lds<MT_LOC_CAP, true>), stream, *g, const_cast<mt_op_rec*>(ops),
-                       const_cast<uint8_t*>(payload), row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);
-    return hipGetLastError();
+    // the editing form at 256 / 512 / 1024 slots: its LDS (~79 B per slot) allows 8 / 4 / 2 waves per CU
+#define MT_LAUNCH_LOC(CAPV)                                                                                  \
+    case CAPV:                                                                                               \
+        hipLaunchKernelGGL((mt::apply_kernel<CAPV, false, true>), dim3(n_docs), dim3(64),                     \
+                           sizeof(mt::Lds<CAPV, true>), stream, *g, const_cast<mt_op_rec*>(ops),             \
+                           const_cast<uint8_t*>(payload), row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);     \
+        return hipGetLastError();
+    switch (cap_class) {
+        MT_LAUNCH_LOC(256)
+        MT_LAUNCH_LOC(512)
+        MT_LAUNCH_LOC(MT_LOC_CAP)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef MT_LAUNCH_LOC
 }
 
 extern "C" size_t mt_lds_bytes(int cap_class) {

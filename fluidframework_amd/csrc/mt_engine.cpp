@@ -27,7 +27,7 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstat
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
-extern "C" hipError_t mt_launch_apply_loc(const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
+extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
                                           const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
                                           uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
@@ -82,10 +82,13 @@ constexpr int kWideClasses = kNumClasses - kFirstWide;
 // ... and, after those, per register class: the documents that need the LDS engine there (declared
 // label keys), run by the LDS engine at that class's capacity, then the documents with client ids
 // above 32, run by the register engine's C64 form (mt_bin_kernel)
-constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds;
+// (then the editing documents that fit 256 / 512 slots: the editing form at that size)
+constexpr int kLocSmall = 2;
+const int32_t kLocCaps[kLocSmall] = {256, 512};
+constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocSmall;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
-// the register engine's C64 form per class
-constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds;
+// the register engine's C64 form per class, the small editing forms
+constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocSmall;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -93,8 +96,15 @@ const int32_t kClassParams[kNumClasses * 4] = {
     640, 320, 88, 384, 704, 352, 96, 416, 768, 384, 104, 448, 832, 416, 112, 480,
     896, 448, 120, 512, 960, 480, 128, 544, 1024, 512, 136, 576, 2048, 1024, 264, 1088,
     4096, 2048, 520, 2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256};
-// the LDS engine is instantiated at 128 / 256 / 512 / 1024 / 2048: the next one up serves a class
-int lds_cap(int cap) { return cap <= 128 ? 128 : cap <= 256 ? 256 : cap <= 512 ? 512 : cap <= 1024 ? 1024 : cap; }
+// the LDS engine is instantiated at 128 / 256 / 384 / 512 / 640 / 768 / 896 / 1024 / 2048 slots: the
+// next one up serves a class.  Its LDS (≈ 55 B per slot) sets the waves per CU: the steps between 512
+// and 1024 keep documents of 520-900 slots at 3-4 waves per CU instead of the 1024 form's 2.
+int lds_cap(int cap) {
+    static const int caps[] = {128, 256, 384, 512, 640, 768, 896, 1024};
+    for (int c : caps)
+        if (cap <= c) return c;
+    return cap;
+}
 }  // namespace
 
 struct mt_batch {
@@ -727,17 +737,21 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
         // documents with an editing client (local edits + acks): the LDS engine's editing form
-        if (const uint32_t cnt = e->h_counts[e->n_classes]) {
+        // (the 1024-slot form's bucket at n_classes, the 256 / 512-slot forms' after the C64 buckets)
+        for (int q = -1; q < kLocSmall; q++) {
+            const int bk = q < 0 ? e->n_classes : lds_base + 2 * e->first_lds + q;
+            const uint32_t cnt = e->h_counts[bk];
+            if (!cnt) continue;
             while (e->kev.size() < 2 * (nk + 1)) {
                 hipEvent_t ev;
                 HIP_OK(hipEventCreate(&ev));
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
-            HIP_OK(mt_launch_apply_loc(&e->g, b->ops, b->payload, b->row_ptr, e->d_ids + (size_t)e->n_classes * b->n_docs,
-                                       cnt, lo, per, e->stream));
+            HIP_OK(mt_launch_apply_loc(q < 0 ? MT_LOC_CAP : kLocCaps[q], &e->g, b->ops, b->payload, b->row_ptr,
+                                       e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
-            e->kev_cls.push_back(kNumClasses);
+            e->kev_cls.push_back(q < 0 ? kNumClasses : kNumClasses + 1 + 2 * kFirstLds + q);
             nk++;
         }
         // wide documents: the LDS engine's wide form, per class
@@ -791,6 +805,10 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         const bool on = e->first_lds == kFirstLds && c < e->n_classes;
         e->cls_bytes[kNumClasses + 1 + q] = on ? acc[lds_base + (q >= kFirstLds ? e->first_lds : 0) + c] : 0;
         e->last_bytes += e->cls_bytes[kNumClasses + 1 + q];
+    }
+    for (int q = 0; q < kLocSmall; q++) {
+        e->cls_bytes[kNumClasses + 1 + 2 * kFirstLds + q] = acc[lds_base + 2 * e->first_lds + q];
+        e->last_bytes += acc[lds_base + 2 * e->first_lds + q];
     }
     return MT_OK;
 }
@@ -963,10 +981,11 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
     if (!e || cls >= (uint32_t)kStatClasses) return MT_ERR_ARG;
     if (capacity) {
         const uint32_t q = cls - kNumClasses - 1;  // (past the editing bucket)
-        *capacity = cls < (uint32_t)kNumClasses    ? (uint32_t)kClasses[cls]
-                    : cls == (uint32_t)kNumClasses ? (MT_CLASS_EDITING | MT_LOC_CAP)
-                    : q < (uint32_t)kFirstLds      ? (MT_CLASS_LDS | (uint32_t)kClasses[q])
-                                                   : (MT_CLASS_C64 | (uint32_t)kClasses[q - kFirstLds]);
+        *capacity = cls < (uint32_t)kNumClasses         ? (uint32_t)kClasses[cls]
+                    : cls == (uint32_t)kNumClasses      ? (MT_CLASS_EDITING | MT_LOC_CAP)
+                    : q < (uint32_t)kFirstLds           ? (MT_CLASS_LDS | (uint32_t)kClasses[q])
+                    : q < (uint32_t)(2 * kFirstLds)     ? (MT_CLASS_C64 | (uint32_t)kClasses[q - kFirstLds])
+                                                        : (MT_CLASS_EDITING | (uint32_t)kLocCaps[q - 2 * kFirstLds]);
     }
     if (kernel_ms) *kernel_ms = e->cls_ms[cls];
     if (launches) *launches = e->cls_launches[cls];

@@ -222,48 +222,26 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         if (a < b && !sc.err) {
             const int nops = (int)(b - a);
             int32_t own = g.loc[d].own;
-            if (ops && sc.win_op < 0) {
-                // replay the collab window over this launch's ops (client.ts:461-464, 821-828;
-                // mergeTree.ts:1718-1722) to find the first op the apply will halt on for a window
-                // assert; mt_fixup_kernel decides after the apply whether "insert failed" outranks it.
-                // An editing client's local edits (seq -1) touch no window; its acks assert only in
-                // updateSeqNumbers (client.ts:804-806, 821-828)
-                int32_t cur = sc.cur_seq, mn = sc.min_seq;
-                for (uint32_t i = a; i < b; i++) {
-                    const mt_op_rec o = ops[i];
-                    if (MT_OP_TYPE(o) == MT_OP_LOAD) continue;  // snapshot body append: no window update
-                    if (MT_OP_TYPE(o) > MT_OP_LOAD) break;
-                    if (o.seq == -1) {
-                        if (own < 0) own = o.client;
-                        continue;
-                    }
-                    if (o.seq == MT_SEQ_REGEN) continue;  // reconnect: no window update
-                    const bool ack = (int32_t)o.client == own;
-                    const bool bad = (MT_OP_IS_NOOP(o) || ack) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
-                                                              : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
-                    if (bad) {
-                        g.sc[d].win_op = (int32_t)i;
-                        break;
-                    }
-                    if (!(o.flags & MT_F_GROUP_MORE)) {
-                        cur = o.seq;
-                        mn = o.msn > mn ? o.msn : mn;
-                    }
-                }
-            }
             const bool needs_lds = (sc.wide & MT_WIDE_LDS) != 0;
             bool c64 = (sc.wide & MT_WIDE_C64) != 0;
             bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+            const bool wdoc0 = wdoc;
             // snapshot body appends (MT_OP_LOAD, SnapshotLoader.loadBody) are applied by the LDS
             // engine only: the register engine's hot loop stays free of them
-            bool lds_only = false;
-            if (ops)
-                for (uint32_t i = a; i < b && !lds_only; i++) lds_only = MT_OP_TYPE(ops[i]) == MT_OP_LOAD;
-            if (!wdoc && ops) {
-                for (uint32_t i = a; i < b; i++) {
-                    const mt_op_rec& o = ops[i];
+            bool lds_only = false, editing = own >= 0;
+            unsigned long long ob = 0;
+            // one pass over this launch's records (each is read once: the loops below were separate)
+            bool win = ops && sc.win_op < 0;
+            int32_t cur = sc.cur_seq, mn = sc.min_seq;
+            for (uint32_t i = a; ops && i < b; i++) {
+                const mt_op_rec o = ops[i];
+                const uint32_t ty = MT_OP_TYPE(o);
+                lds_only = lds_only || ty == MT_OP_LOAD;
+                editing = editing || (o.seq == -1 && o.type != MT_OP_LOAD);
+                ob += 32ull + o.payload_len;
+                if (!wdoc0) {
                     const uint32_t c = o.client;
-                    const bool load = MT_OP_TYPE(o) == MT_OP_LOAD;
+                    const bool load = ty == MT_OP_LOAD;
                     const uint32_t c0 = load ? (c & 0xFFu) : c, c1 = load ? (c >> 8) : 0u;
                     const bool has0 = !load || c0 != MT_CLIENT_NONCOLLAB, has1 = load && o.pos2 >= 0;
                     c64 = c64 || (has0 && c0 > 32) || (has1 && c1 > 32);
@@ -271,14 +249,38 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                            (load ? ((has0 && c0 >= MT_MAX_CLIENTS) || (has1 && c1 >= MT_MAX_CLIENTS))
                                  : (!MT_OP_IS_NOOP(o) && c >= MT_MAX_CLIENTS));
                 }
-                if (c64 && !(sc.wide & MT_WIDE_C64)) g.sc[d].wide = sc.wide | MT_WIDE_C64;
+                // replay the collab window over this launch's ops (client.ts:461-464, 821-828;
+                // mergeTree.ts:1718-1722) to find the first op the apply will halt on for a window
+                // assert; mt_fixup_kernel decides after the apply whether "insert failed" outranks it.
+                // An editing client's local edits (seq -1) touch no window; its acks assert only in
+                // updateSeqNumbers (client.ts:804-806, 821-828)
+                if (!win || ty == MT_OP_LOAD) continue;  // snapshot body append: no window update
+                if (ty > MT_OP_LOAD) {
+                    win = false;
+                    continue;
+                }
+                if (o.seq == -1) {
+                    if (own < 0) own = o.client;
+                    continue;
+                }
+                if (o.seq == MT_SEQ_REGEN) continue;  // reconnect: no window update
+                const bool ack = (int32_t)o.client == own;
+                const bool bad = (MT_OP_IS_NOOP(o) || ack) ? (!(cur <= o.seq) || !(o.msn <= o.seq) || !(mn <= o.msn))
+                                                          : (!(cur < o.seq) || !(mn <= o.msn) || !(o.msn <= o.seq));
+                if (bad) {
+                    g.sc[d].win_op = (int32_t)i;
+                    win = false;
+                    continue;
+                }
+                if (!(o.flags & MT_F_GROUP_MORE)) {
+                    cur = o.seq;
+                    mn = o.msn > mn ? o.msn : mn;
+                }
             }
+            if (!wdoc0 && ops && c64 && !(sc.wide & MT_WIDE_C64)) g.sc[d].wide = sc.wide | MT_WIDE_C64;
             int ib_need = 0;
             for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
             c = n_classes - 1;
-            bool editing = own >= 0;
-            if (ops)
-                for (uint32_t i = a; i < b && !editing; i++) editing = ops[i].seq == -1 && ops[i].type != MT_OP_LOAD;
             // (snapshot appends start at the first class the LDS engine serves)
             for (int k = lds_only ? first_lds : 0; k < n_classes; k++) {
                 const int cap = classes[4 * k], lb = classes[4 * k + 1], ib = classes[4 * k + 2],
@@ -289,6 +291,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     break;
                 }
             }
+            const int cls = c;  // the capacity class (before the bucket remaps below)
             if (wdoc && !editing) {
                 // the wide form, from the 2048 class up (the wide state is the engine's to allocate:
                 // without it the document halts)
@@ -315,22 +318,26 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 const int lds_base = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0);
                 c = (needs_lds ? lds_base : lds_base + first_lds) + c;
             }
-            if (editing) c = n_classes;  // the editing documents' bucket (mt_launch_apply_loc)
+            if (editing) {
+                // the editing documents' buckets (mt_launch_apply_loc): the 1024-slot form at n_classes,
+                // the 256 / 512-slot forms after the C64 buckets (when the chosen class fits them)
+                const int cap = classes[4 * cls];
+                const int ebase = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds;
+                c = cap <= 256 ? ebase : cap <= 512 ? ebase + 1 : n_classes;
+            }
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
                 // accounting"): persistent state in + out, op records, payload
                 unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] +
                                         6ull * sc.heap_n + sizeof(mt_doc_scalars);
                 for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
-                unsigned long long ob = 32ull * (b - a);
-                if (ops)
-                    for (uint32_t i = a; i < b; i++) ob += ops[i].payload_len;
+                if (!ops) ob = 32ull * (b - a);  // (with records: summed in the pass above)
                 bytes = 2ull * st + ob;
             }
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds;
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 2;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;

@@ -1587,31 +1587,18 @@ MT_DEV const mt_gstate& kernarg_gstate() {
 }
 
 // Waves per SIMD by class.  The register state is 6 K VGPRs per lane and the op path needs ~110
-// more (text compaction reads no register state: compact_text), so K <= 5 fits 128 VGPRs (4 waves),
-// K <= 9 fits 168 (3), larger classes 256 (2); K = 10 runs at 3 with 48 B of scratch per lane, which
-// measured faster than 2 without (profiles/r03_ab_soa_C3.log).  MT_WPE_K<n>=w overrides one class.
-constexpr int wpe_default(int K) { return K <= 3 ? 5 : K <= 5 ? 4 : K <= 10 ? 3 : 2; }
-#define MT_WPE_OR(n, d) (MT_WPE_K##n > 0 ? MT_WPE_K##n : (d))
-#ifndef MT_WPE_K9
-#define MT_WPE_K9 0
+// more (text compaction reads no register state: compact_text).  The kernels are issue-latency
+// bound, so a class takes the highest occupancy whose spill stays small: K = 4 runs at 5 waves
+// (96 VGPRs, 8 B of scratch per lane), K = 6 and 7 at 4 (128 VGPRs, 8 / 56 B), K = 10 at 3 (48 B);
+// each measured faster than one wave fewer without scratch, while 200+ B of scratch (K = 8 at 4,
+// K = 11 / 12 at 3) measured 1.2-2.6x slower (profiles/r03_ab_occupancy.log).
+constexpr int wpe_default(int K) { return K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2; }
+// MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
+#ifndef MT_WPE_OV
+#define MT_WPE_OV {0}
 #endif
-#ifndef MT_WPE_K10
-#define MT_WPE_K10 0
-#endif
-#ifndef MT_WPE_K5
-#define MT_WPE_K5 0
-#endif
-#ifndef MT_WPE_K11
-#define MT_WPE_K11 0
-#endif
-#ifndef MT_WPE_K3
-#define MT_WPE_K3 0
-#endif
-constexpr int wpe(int K) {
-    return K == 9 ? MT_WPE_OR(9, wpe_default(9)) : K == 10 ? MT_WPE_OR(10, wpe_default(10))
-         : K == 11 ? MT_WPE_OR(11, wpe_default(11))
-         : K == 5 ? MT_WPE_OR(5, wpe_default(5)) : K <= 3 ? MT_WPE_OR(3, wpe_default(K)) : wpe_default(K);
-}
+constexpr int wpe_ov[17] = MT_WPE_OV;
+constexpr int wpe(int K) { return K < 17 && wpe_ov[K] > 0 ? wpe_ov[K] : wpe_default(K); }
 template <int K, bool W>
 MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restrict__ ops,
                       const uint8_t* __restrict__ payload, const uint32_t* __restrict__ row_ptr,
@@ -1675,7 +1662,14 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
 
 // the narrow register engine (client ids <= 32) and its C64 form (client ids <= 63: a second overlap
 // register per slot, one occupancy step lower where the state no longer fits)
-constexpr int wpe_c64(int K) { return K <= 3 ? 4 : K <= 7 ? 3 : 2; }
+#ifndef MT_WPE_C64_OV
+#define MT_WPE_C64_OV {0}
+#endif
+constexpr int wpe_c64_ov[17] = MT_WPE_C64_OV;
+// The C64 form carries K more VGPRs of state; same rule (A/B on C3W in profiles/r03_ab_occupancy.log:
+// K = 3..6 one wave up, K = 8, 9 at 3 with <= 100 B of scratch; K = 7 at 4 would spill ~200 B).
+constexpr int wpe_c64_default(int K) { return K <= 4 ? 5 : K <= 6 ? 4 : K <= 9 ? 3 : 2; }
+constexpr int wpe_c64(int K) { return K < 17 && wpe_c64_ov[K] > 0 ? wpe_c64_ov[K] : wpe_c64_default(K); }
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(
     mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,

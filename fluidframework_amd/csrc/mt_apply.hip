@@ -1777,7 +1777,7 @@ struct Wave {
             sync();
             // (a document that has not edited yet has never stored these arrays)
             const bool has = s.lc.own >= 0;
-            const size_t lo2 = (size_t)d * MT_LOC_CAP;
+            const size_t lo2 = (size_t)d * g.locstride;
             for (int i = lane; i < n; i += 64) {
                 s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
                 s.pk[i] = has ? g.pk[lo2 + i] : 0ull;
@@ -1898,8 +1898,8 @@ struct Wave {
         }
         if constexpr (LOC) {
             if (s.lc.own >= 0) {
-                const size_t lo2 = (size_t)d * MT_LOC_CAP;
-                for (int i = lane; i < min(nn, MT_LOC_CAP); i += 64) {
+                const size_t lo2 = (size_t)d * g.locstride;
+                for (int i = lane; i < min(nn, (int)g.locstride); i += 64) {
                     const int sl = s.order[i];
                     g.gm[lo2 + i] = s.gm[sl];
                     g.pk[lo2 + i] = s.pk[sl];
@@ -1932,6 +1932,34 @@ struct GenArgs {
     const uint32_t* gids; // or the global id of every local document (a hash-routed shard)
 };
 
+// An editing document enters the editing form at CAP slots only if this launch's ops cannot outgrow
+// it (the form cannot move a document between capacities mid-launch); otherwise it halts with
+// MT_DERR_CAPACITY, and a wide document with MT_DERR_LIMITS (no local edits in the wide form).
+template <int CAP>
+MT_DEV bool loc_admit(const mt_gstate& g, const mt_op_rec* ops, uint32_t d, uint32_t a, uint32_t b) {
+    using LS = Lds<CAP, true>;
+    const mt_doc_scalars& sc = g.sc[d];
+    if (sc.wide & MT_WIDE_DOC) {
+        if (threadIdx.x == 0 && !sc.err) {
+            g.sc[d].err = MT_DERR_LIMITS;
+            g.sc[d].err_seq = ops[a].seq;
+        }
+        return false;
+    }
+    const int nops = (int)(b - a);
+    int ib_need = 0;
+    for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
+    if (!(sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= CAP && sc.nb[0] + 2 * nops + 1 <= LS::LB &&
+          ib_need + nops + 1 <= LS::IB && sc.heap_n + 4 * nops + 16 <= LS::H && CAP <= (int)g.locstride)) {
+        if (threadIdx.x == 0 && !sc.err) {
+            g.sc[d].err = MT_DERR_CAPACITY;
+            g.sc[d].err_seq = ops[a].seq;
+        }
+        return false;
+    }
+    return true;
+}
+
 template <int CAP, bool GEN, bool LOC = false>
 __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
                                                    uint8_t* __restrict__ payload,
@@ -1949,27 +1977,7 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
-    if (LOC) {  // the editing form has one capacity: a document that could outgrow it halts
-        const mt_doc_scalars& sc = g.sc[d];
-        if (sc.wide & MT_WIDE_DOC) {  // (and no wide state: a wide document cannot take local edits)
-            if (threadIdx.x == 0 && !sc.err) {
-                g.sc[d].err = MT_DERR_LIMITS;
-                g.sc[d].err_seq = ops[a].seq;
-            }
-            return;
-        }
-        const int nops = (int)(b - a);
-        int ib_need = 0;
-        for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
-        if (!(sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= CAP && sc.nb[0] + 2 * nops + 1 <= Lds<CAP, LOC>::LB &&
-              ib_need + nops + 1 <= Lds<CAP, LOC>::IB && sc.heap_n + 4 * nops + 16 <= Lds<CAP, LOC>::H)) {
-            if (threadIdx.x == 0 && !sc.err) {
-                g.sc[d].err = MT_DERR_CAPACITY;
-                g.sc[d].err_seq = ops[a].seq;
-            }
-            return;
-        }
-    }
+    if (LOC && !loc_admit<CAP>(g, ops, d, a, b)) return;
     wv.load(g, d);
     if (LOC) {
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;
@@ -2015,7 +2023,8 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
 // HBM workspace (ws + w * sizeof(Lds<CAP>)) instead of LDS.  Latency-bound like the LDS form but
 // without its 160 KiB-per-CU ceiling; such documents are rare, so a handful of waves serve them.
 // W: wide documents (include/mtgpu.h "limits"), every capacity class from 2048 segments up.
-template <int CAP, bool W = false>
+// LOC: the editing form above MT_LOC_CAP segments (mt_launch_apply_loc_big).
+template <int CAP, bool W = false, bool LOC = false>
 __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                      const uint8_t* __restrict__ payload,
                                                      const uint32_t* __restrict__ row_ptr,
@@ -2024,18 +2033,24 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
-    using LS = Lds<CAP, false, W>;
+    using LS = Lds<CAP, LOC, W>;
     LS& st = *reinterpret_cast<LS*>(ws + (size_t)w * sizeof(LS));
-    Wave<CAP, true, false, W> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
-                                 g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
+    Wave<CAP, true, LOC, W> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
+                               g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
+    if (LOC && !loc_admit<CAP>(g, ops, d, a, b)) return;
     wv.load(g, d);
+    if (LOC) {
+        wv.rg = g.rg + (size_t)d * MT_RG_RECS;
+        wv.rgp = g.rgp + (size_t)d * MT_RG_BYTES;
+    }
     for (uint32_t i = a; i < b; i++) {
         if (st.err) break;
         const mt_op_rec op = ops[i];
+        if (LOC) wv.rix = i - r0;
         wv.apply(op, payload);
     }
     wv.store(g, d);
@@ -2169,6 +2184,36 @@ extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, con
             return hipErrorInvalidValue;
     }
 #undef MT_LAUNCH_LOC
+}
+
+// editing documents above MT_LOC_CAP segments (mt_bin_kernel's last editing buckets): the editing
+// form with its structure in the HBM workspace (n_docs * mt_lds_bytes_loc(cap_class) bytes)
+extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                              const uint8_t* payload, const uint32_t* row_ptr,
+                                              const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
+                                              uint32_t op_cnt, uint8_t* ws, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    dim3 grid(n_docs), block(64);
+#define MT_LAUNCH_LOCB(CAPV)                                                                                 \
+    case CAPV:                                                                                               \
+        hipLaunchKernelGGL((mt::apply_kernel_g<CAPV, false, true>), grid, block, 0, stream, *g, ops, payload, \
+                           row_ptr, doc_ids, n_docs, op_lo, op_cnt, ws);                                     \
+        return hipGetLastError();
+    switch (cap_class) {
+        MT_LAUNCH_LOCB(2048)
+        MT_LAUNCH_LOCB(4096)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef MT_LAUNCH_LOCB
+}
+
+extern "C" size_t mt_lds_bytes_loc(int cap_class) {
+    switch (cap_class) {
+        case 2048: return sizeof(mt::Lds<2048, true>);
+        case 4096: return sizeof(mt::Lds<4096, true>);
+        default: return 0;
+    }
 }
 
 extern "C" size_t mt_lds_bytes(int cap_class) {

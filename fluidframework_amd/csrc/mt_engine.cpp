@@ -39,6 +39,11 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
                                            uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
                                            hipStream_t stream);
 extern "C" size_t mt_lds_bytes_wide(int cap_class);
+extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+                                              const uint8_t* payload, const uint32_t* row_ptr,
+                                              const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
+                                              uint32_t op_cnt, uint8_t* ws, hipStream_t stream);
+extern "C" size_t mt_lds_bytes_loc(int cap_class);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_label_keys(const mt_gstate* g, uint32_t d0, uint32_t d1, uint32_t keys, hipStream_t st);
 extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
@@ -82,13 +87,14 @@ constexpr int kWideClasses = kNumClasses - kFirstWide;
 // ... and, after those, per register class: the documents that need the LDS engine there (declared
 // label keys), run by the LDS engine at that class's capacity, then the documents with client ids
 // above 32, run by the register engine's C64 form (mt_bin_kernel)
-// (then the editing documents that fit 256 / 512 slots: the editing form at that size)
-constexpr int kLocSmall = 2;
-const int32_t kLocCaps[kLocSmall] = {256, 512};
-constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocSmall;
+// (then the editing documents that fit 256 / 512 slots: the editing form at that size; then those
+// above MT_LOC_CAP = 1024: its HBM-workspace form at 2048 / 4096)
+constexpr int kLocForms = 4;
+const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096};
+constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
-// the register engine's C64 form per class, the small editing forms
-constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocSmall;
+// the register engine's C64 form per class, the other editing forms
+constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocForms;
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -198,6 +204,38 @@ static mt_status ensure_wide(mt_engine* e) {
     }
     return MT_OK;
 }
+// The editing documents' per-segment state (gm / pk / ct / lsq) holds MT_LOC_CAP slots per document
+// until a document's editing form needs a larger class (mt_launch_apply_loc_big): then every
+// document's rows are re-laid at that stride (nothing runs on the engine's streams meanwhile)
+template <class T>
+static mt_status relay_rows(mt_engine* e, T** p, uint32_t from, uint32_t to) {
+    const size_t D = e->cfg.max_docs;
+    T* q = nullptr;
+    if (hipMalloc(&q, D * to * sizeof(T)) != hipSuccess) return MT_ERR_NOMEM;
+    if (hipMemset(q, 0, D * to * sizeof(T)) != hipSuccess ||
+        hipMemcpy2D(q, to * sizeof(T), *p, from * sizeof(T), from * sizeof(T), D, hipMemcpyDeviceToDevice) !=
+            hipSuccess) {
+        (void)hipFree(q);
+        return MT_ERR_HIP;
+    }
+    for (auto& a : e->allocs)
+        if (a == (void*)*p) a = q;
+    HIP_OK(hipFree(*p));
+    *p = q;
+    return MT_OK;
+}
+static mt_status ensure_locstride(mt_engine* e, uint32_t cap) {
+    mt_gstate& g = e->g;
+    if (g.locstride >= cap) return MT_OK;
+    HIP_OK(hipDeviceSynchronize());
+    mt_status st = MT_OK;
+    if ((st = relay_rows(e, &g.gm, g.locstride, cap)) || (st = relay_rows(e, &g.pk, g.locstride, cap)) ||
+        (st = relay_rows(e, &g.ct, g.locstride, cap)) || (st = relay_rows(e, &g.lsq, g.locstride, cap)))
+        return st;  // (a failed relay leaves the arrays it did at the new stride: the engine is unusable)
+    g.locstride = cap;
+    return MT_OK;
+}
+
 // a record beyond the narrow limits (include/mtgpu.h "limits")
 static bool wide_rec(const mt_op_rec& o) {
     if (o.type & MT_OP_WIDE) return true;
@@ -241,6 +279,7 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     g.ibcap = g.segcap / 8 + 8;
     g.hcap = e->cfg.heap_capacity;
     g.textcap = e->cfg.text_capacity;
+    g.locstride = MT_LOC_CAP;
     mt_status st = MT_OK;
     const size_t S = D * g.segcap;
     if ((st = dalloc(e, &g.seq, S)) || (st = dalloc(e, &g.rseq, S)) || (st = dalloc(e, &g.len, S)) ||
@@ -662,6 +701,15 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             wws_off[c] = need;
             need += (size_t)e->h_counts[e->n_classes + 1 + (c - kFirstWide)] * mt_lds_bytes_wide(kClasses[c]);
         }
+        size_t lws_off[kLocForms] = {};
+        for (int q = 0; q < kLocForms; q++) {
+            const uint32_t cnt = e->h_counts[lds_base + 2 * e->first_lds + q];
+            if (kLocCaps[q] <= MT_LOC_CAP || !cnt) continue;
+            const mt_status ls = ensure_locstride(e, (uint32_t)kLocCaps[q]);
+            if (ls) return ls;
+            lws_off[q] = need;
+            need += (size_t)cnt * mt_lds_bytes_loc(kLocCaps[q]);
+        }
         if (need > e->ws_bytes) {
             HIP_OK(hipDeviceSynchronize());
             if (e->ws) HIP_OK(hipFree(e->ws));
@@ -737,8 +785,9 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(hipStreamWaitEvent(e->stream, e->join_ev[c], 0));
         }
         // documents with an editing client (local edits + acks): the LDS engine's editing form
-        // (the 1024-slot form's bucket at n_classes, the 256 / 512-slot forms' after the C64 buckets)
-        for (int q = -1; q < kLocSmall; q++) {
+        // (the 1024-slot form's bucket at n_classes, the 256 / 512-slot forms' after the C64 buckets,
+        // then the 2048 / 4096-slot HBM-workspace forms')
+        for (int q = -1; q < kLocForms; q++) {
             const int bk = q < 0 ? e->n_classes : lds_base + 2 * e->first_lds + q;
             const uint32_t cnt = e->h_counts[bk];
             if (!cnt) continue;
@@ -748,8 +797,13 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
-            HIP_OK(mt_launch_apply_loc(q < 0 ? MT_LOC_CAP : kLocCaps[q], &e->g, b->ops, b->payload, b->row_ptr,
-                                       e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->stream));
+            if (q >= 0 && kLocCaps[q] > MT_LOC_CAP)
+                HIP_OK(mt_launch_apply_loc_big(kLocCaps[q], &e->g, b->ops, b->payload, b->row_ptr,
+                                               e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->ws + lws_off[q],
+                                               e->stream));
+            else
+                HIP_OK(mt_launch_apply_loc(q < 0 ? MT_LOC_CAP : kLocCaps[q], &e->g, b->ops, b->payload, b->row_ptr,
+                                           e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
             e->kev_cls.push_back(q < 0 ? kNumClasses : kNumClasses + 1 + 2 * kFirstLds + q);
             nk++;
@@ -806,7 +860,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         e->cls_bytes[kNumClasses + 1 + q] = on ? acc[lds_base + (q >= kFirstLds ? e->first_lds : 0) + c] : 0;
         e->last_bytes += e->cls_bytes[kNumClasses + 1 + q];
     }
-    for (int q = 0; q < kLocSmall; q++) {
+    for (int q = 0; q < kLocForms; q++) {
         e->cls_bytes[kNumClasses + 1 + 2 * kFirstLds + q] = acc[lds_base + 2 * e->first_lds + q];
         e->last_bytes += acc[lds_base + 2 * e->first_lds + q];
     }
@@ -996,7 +1050,9 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
 mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint64_t cap) {
     if (!e || !buf || !cap) return MT_ERR_ARG;
     char tmp[96];
-    if (capacity & MT_CLASS_EDITING)
+    if ((capacity & MT_CLASS_EDITING) && (capacity & ~(uint32_t)MT_CLASS_EDITING) > MT_LOC_CAP)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_C64)
         snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel_c64<%u>", (capacity & ~(uint32_t)MT_CLASS_C64) / 64);

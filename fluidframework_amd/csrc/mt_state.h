@@ -68,7 +68,7 @@ struct mt_loc {
 };
 #define MT_RG_RECS 256       // regenerated op records per document between drains
 #define MT_RG_BYTES 4096     // and their payload bytes
-#define MT_LOC_CAP 1024      // an editing document runs on the LDS engine at this capacity
+#define MT_LOC_CAP 1024      // the editing form's largest LDS capacity (above: its HBM-workspace form)
 // pending property counts per segment (SegmentPropertiesManager, segmentPropertiesManager.ts:11-12):
 // 7 bits per key id 0..7 at bit 7k, the pending rewrite count in bits 56..63
 #define MT_PK_KEY(pk, k) ((uint32_t)((pk) >> (7 * (k))) & 0x7Fu)
@@ -106,12 +106,15 @@ struct mt_gstate {
     uint8_t* text;     // [doc][2][textcap]  text arena, double-buffered for in-kernel compaction
     struct mt_event* ev;  // [doc][evcap] delta / maintenance events (mt_events_enable), or null
     uint32_t* evn;     // [doc] events recorded since the last drain (may exceed evcap: halted)
-    uint64_t* gm;      // [doc][segcap] editing documents: pending group mask per segment
-    uint64_t* pk;      // [doc][segcap] pending property counts (MT_PK_*)
-    uint32_t* ct;      // [doc][segcap] creation stamp
-    uint64_t* lsq;     // [doc][segcap] localSeq (low 32 bits) / localRemovedSeq (high), 0: undefined
+    // editing documents, [doc][locstride]: MT_LOC_CAP slots per document until a document's editing
+    // form needs a larger class (its HBM-workspace form), then the engine re-lays them at that class
+    uint64_t* gm;      // pending group mask per segment
+    uint64_t* pk;      // pending property counts (MT_PK_*)
+    uint32_t* ct;      // creation stamp
+    uint64_t* lsq;     // localSeq (low 32 bits) / localRemovedSeq (high), 0: undefined
     mt_loc* loc;       // [doc]
     struct mt_op_rec* rg;  // [doc][MT_RG_RECS] regenerated ops (seq = the resetting record's index)
     uint8_t* rgp;      // [doc][MT_RG_BYTES] their payload
     uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;
+    uint32_t locstride;  // slots per document of gm / pk / ct / lsq
 };

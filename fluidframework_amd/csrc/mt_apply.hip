@@ -40,9 +40,23 @@ struct Pairs {
     MT_DEV int key_limit() const { return wide ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS; }
 };
 
+// The editing form's per-document pending-group state with GN group slots (mt_loc's fields; GN = 64
+// is mt_loc itself)
+template <int GN>
+struct LocState {
+    int32_t own;
+    uint32_t glo, ghi;
+    uint32_t stamp;
+    uint32_t gt[GN];
+    uint32_t lseq;
+    uint32_t gls[GN];
+    uint32_t rgn, rgpn;
+};
+
 // W: a wide document (include/mtgpu.h "limits"): per slot also the overlap ids >= 64 (ovx) and the
-// property words ph / pxl / pxh (u16 value ids, keys 8..15); UTF-16 text
-template <int CAP, bool LOC = false, bool W = false>
+// property words ph / pxl / pxh (u16 value ids, keys 8..15); UTF-16 text.  GW: (LOC) group-mask
+// words per slot, 64 GW pending edits at most (GW > 1: MT_WIDE_GROUPS documents, HBM workspace only)
+template <int CAP, bool LOC = false, bool W = false, int GW = 1>
 struct Lds {
     static constexpr int LB = CAP / 2;      // leaf blocks
     static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
@@ -74,8 +88,8 @@ struct Lds {
     uint32_t gpay;          // generator: payload bytes used in this document's region
     // an editing client's document (LOC, mt_loc): per slot the pending group mask, the pending
     // property counts (MT_PK_*) and the creation stamp
-    mt_loc lc;
-    uint64_t gm[LOC ? CAP : 1];
+    typename std::conditional<(GW > 1), LocState<64 * GW>, mt_loc>::type lc;
+    uint64_t gm[LOC ? CAP * GW : 1];
     uint64_t pk[LOC ? CAP : 1];
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
@@ -94,9 +108,26 @@ struct Lds {
 // SURVEY.md §8 a9 "unbounded B-tree"): the same structure lives in a per-wave workspace in HBM
 // (mt_launch_apply_big); lanes exchange it through the vector L1 / L2, so a pass boundary also
 // waits for the wave's outstanding stores (workgroup scope = the wave's CU).
-template <int CAP, bool G = false, bool LOC = false, bool W = false>
+template <int CAP, bool G = false, bool LOC = false, bool W = false, int GW = 1>
 struct Wave {
-    using L = Lds<CAP, LOC, W>;
+    using L = Lds<CAP, LOC, W, GW>;
+    // (LOC) pending-group masks: GW words per slot; pending edit ordinal N is bit N % GN
+    static constexpr uint32_t GN = 64u * GW;
+    MT_DEV uint64_t& gmw(int sl, uint32_t N) { return s.gm[sl * GW + (int)((N % GN) >> 6)]; }
+    MT_DEV bool gm_has(int sl, uint32_t N) { return (gmw(sl, N) >> (N & 63u)) & 1ull; }
+    MT_DEV void gm_set(int sl, uint32_t N) { gmw(sl, N) |= 1ull << (N & 63u); }
+    MT_DEV void gm_clr(int sl, uint32_t N) { gmw(sl, N) &= ~(1ull << (N & 63u)); }
+    MT_DEV bool gm_any(int sl) {
+        uint64_t v = 0;
+        for (int w = 0; w < GW; w++) v |= s.gm[sl * GW + w];
+        return v != 0;
+    }
+    MT_DEV void gm_copy(int t, int sl) {
+        for (int w = 0; w < GW; w++) s.gm[t * GW + w] = s.gm[sl * GW + w];
+    }
+    MT_DEV void gm_zero(int t) {
+        for (int w = 0; w < GW; w++) s.gm[t * GW + w] = 0ull;
+    }
     using TC = typename std::conditional<W, uint16_t, uint8_t>::type;  // a text code unit in the arena
     MT_DEV static void sync() {
         if (G) {
@@ -651,7 +682,7 @@ struct Wave {
             s.toff[t] = s.toff[sl] + (uint32_t)off;
             s.len[sl] = (uint32_t)off;
             if constexpr (LOC) {  // segmentGroups.copyTo + the property manager's counts (mergeTree.ts:555-560)
-                s.gm[t] = s.gm[sl];
+                gm_copy(t, sl);
                 s.pk[t] = s.pk[sl];
                 s.lsq[t] = s.lsq[sl];
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
@@ -754,7 +785,7 @@ struct Wave {
             const int sl = s.order[st + q];
             const uint8_t f = s.flags[sl];
             bool pending = false;
-            if constexpr (LOC) pending = s.gm[sl] != 0;  // segmentGroups not empty: held (mergeTree.ts:1295)
+            if constexpr (LOC) pending = gm_any(sl);  // segmentGroups not empty: held (mergeTree.ts:1295)
             if (pending) {
                 keep[kept++] = (uint16_t)sl;
                 prev = -1;
@@ -1040,14 +1071,15 @@ struct Wave {
                 }
                 s.flags[t] = f;
                 if constexpr (LOC) {  // a local insert is its edit's one pending segment (saveIfLocal)
-                    s.gm[t] = S == -1 ? (1ull << (s.lc.ghi & 63u)) : 0ull;
+                    gm_zero(t);
+                    if (S == -1) gm_set(t, s.lc.ghi);
                     s.pk[t] = 0;
                     s.lsq[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
                     s.lc.stamp = s.lc.stamp + 1;
                     s.ct[t] = s.lc.stamp;
                     if (S == -1) {
-                        s.lc.gt[s.lc.ghi & 63u] = s.ct[t];
-                        s.lc.gls[s.lc.ghi & 63u] = s.lc.lseq;
+                        s.lc.gt[s.lc.ghi % GN] = s.ct[t];
+                        s.lc.gls[s.lc.ghi % GN] = s.lc.lseq;
                         s.lc.ghi = s.lc.ghi + 1;
                     }
                 }
@@ -1080,14 +1112,14 @@ struct Wave {
         const int n = s.n;
         const bool rewrite = op.flags & MT_F_REWRITE;
         const bool local = S == -1;
-        uint64_t gbit = 0;
+        uint32_t gN = 0;
         if constexpr (LOC) {
             if (local) {  // this edit's pending group (addToPendingList, mergeTree.ts:1922-1929)
-                gbit = 1ull << (s.lc.ghi & 63u);
+                gN = s.lc.ghi;
                 sync();
                 if (lane == 0) {
-                    s.lc.gt[s.lc.ghi & 63u] = s.lc.stamp + 1;  // every member existed before it
-                    s.lc.gls[s.lc.ghi & 63u] = s.lc.lseq;
+                    s.lc.gt[gN % GN] = s.lc.stamp + 1;  // every member existed before it
+                    s.lc.gls[gN % GN] = s.lc.lseq;
                 }
                 sync();
                 s.lc.ghi = s.lc.ghi + 1;
@@ -1103,7 +1135,7 @@ struct Wave {
                 if (ce > cs && cs < end && ce > start) {
                     const int sl = s.order[i];
                     if constexpr (LOC) {
-                        if (local) s.gm[sl] |= gbit;
+                        if (local) gm_set(sl, gN);
                     }
                     if (!is_remove && track()) mark_stale(sl);
                     if (LOC && !is_remove) {
@@ -1230,12 +1262,12 @@ struct Wave {
     // editing client's own sequenced message settles its oldest pending edit.  Its group's list
     // order (which the heap pushes follow) is rebuilt: the members that existed when the edit was
     // made (stamp < gt) in document order, then the parts split off later, by stamp.
-    MT_DEV void ack_one(int k, int32_t S, uint64_t bit, uint8_t type, const uint8_t* pairs, int np, bool rewrite) {
+    MT_DEV void ack_one(int k, int32_t S, uint32_t N, uint8_t type, const uint8_t* pairs, int np, bool rewrite) {
         if constexpr (LOC) {
             const int sl = s.order[k];
             sync();
             if (lane == 0) {
-                s.gm[sl] &= ~bit;
+                gm_clr(sl, N);
                 if (type == MT_OP_INSERT) {
                     s.seq[sl] = S;
                     s.lsq[sl] &= ~0xFFFFFFFFull;
@@ -1261,8 +1293,7 @@ struct Wave {
             const int32_t S = op.seq;
             if (s.lc.glo < s.lc.ghi) {
                 const uint32_t Lo = s.lc.glo;
-                const uint64_t bit = 1ull << (Lo & 63u);
-                const uint32_t gt = s.lc.gt[Lo & 63u];
+                const uint32_t gt = s.lc.gt[Lo % GN];
                 const bool rewrite = op.flags & MT_F_REWRITE;
                 block_starts();
                 const int n = s.n;
@@ -1271,13 +1302,13 @@ struct Wave {
                     bool mem = false;
                     if (i < n) {
                         const int sl = s.order[i];
-                        mem = (s.gm[sl] & bit) && s.ct[sl] < gt;
+                        mem = gm_has(sl, Lo) && s.ct[sl] < gt;
                     }
                     uint64_t m = wave_ballot(mem);
                     while (m) {
                         const int fl = first_lane(m);
                         m &= m - 1;
-                        ack_one(base + fl, S, bit, op.type, pairs, np, rewrite);
+                        ack_one(base + fl, S, Lo, op.type, pairs, np, rewrite);
                         if (s.err) return;
                     }
                 }
@@ -1288,7 +1319,7 @@ struct Wave {
                         uint32_t v = 0xFFFFFFFFu;
                         if (i < n) {
                             const int sl = s.order[i];
-                            if (s.gm[sl] & bit) v = s.ct[sl];
+                            if (gm_has(sl, Lo)) v = s.ct[sl];
                         }
                         uint32_t mv = v;
                         for (int o = 32; o; o >>= 1) mv = min(mv, (uint32_t)__shfl_xor((int)mv, o, 64));
@@ -1298,11 +1329,11 @@ struct Wave {
                     int k = -1;
                     for (int base = 0; base < n && k < 0; base += 64) {
                         const int i = base + lane;
-                        const uint64_t hm = wave_ballot(i < n && (s.gm[s.order[i]] & bit) && s.ct[s.order[i]] == best);
+                        const uint64_t hm = wave_ballot(i < n && gm_has(s.order[i], Lo) && s.ct[s.order[i]] == best);
                         if (hm) k = base + first_lane(hm);
                     }
                     if (k < 0) break;
-                    ack_one(k, S, bit, op.type, pairs, np, rewrite);
+                    ack_one(k, S, Lo, op.type, pairs, np, rewrite);
                     if (s.err) return;
                 }
                 sync();
@@ -1327,8 +1358,7 @@ struct Wave {
             const int np = MT_OP_NPAIRS(op.flags);
             const uint8_t* opairs = payload + op.payload_off + (op.payload_len - 2 * np);
             const uint32_t Lo = s.lc.glo;
-            const uint64_t bit = 1ull << (Lo & 63u);
-            const uint32_t Ls = s.lc.gls[Lo & 63u];
+            const uint32_t Ls = s.lc.gls[Lo % GN];
             auto emit_rec = [&](const mt_op_rec& r) -> bool {
                 if (s.lc.rgn >= MT_RG_RECS || s.lc.rgpn + r.payload_len > MT_RG_BYTES) return fail(MT_DERR_CAPACITY, S), false;
                 if (lane == 0) rg[s.lc.rgn] = r;
@@ -1345,7 +1375,7 @@ struct Wave {
             const int n = s.n;
             for (int base = 0; base < n; base += 64) {
                 const int i = base + lane;
-                const bool mem = i < n && (s.gm[s.order[i]] & bit);
+                const bool mem = i < n && gm_has(s.order[i], Lo);
                 uint64_t m = wave_ballot(mem);
                 while (m) {
                     const int k = base + first_lane(m);
@@ -1363,7 +1393,7 @@ struct Wave {
                         pos += wave_sum(v);
                     }
                     sync();
-                    if (lane == 0) s.gm[sl] &= ~bit;
+                    if (lane == 0) gm_clr(sl, Lo);
                     sync();
                     const uint32_t len = s.len[sl];
                     mt_op_rec r{};
@@ -1410,13 +1440,13 @@ struct Wave {
                         for (int q = 0; q < 2 * nkv; q++) rgp[s.lc.rgpn + (op.type == MT_OP_INSERT ? len : 0) + q] = kv[q];
                     if (!emit_rec(r)) return;
                     // its own pending group, same localSeq, at the queue's tail
-                    if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, S);
+                    if (s.lc.ghi - s.lc.glo >= GN) return fail(MT_DERR_CAPACITY, S);
                     sync();
                     if (lane == 0) {
                         const uint32_t N = s.lc.ghi;
-                        s.gm[sl] |= 1ull << (N & 63u);
-                        s.lc.gls[N & 63u] = Ls;
-                        s.lc.gt[N & 63u] = s.ct[sl];
+                        gm_set(sl, N);
+                        s.lc.gls[N % GN] = Ls;
+                        s.lc.gt[N % GN] = s.ct[sl];
                     }
                     sync();
                     s.lc.ghi = s.lc.ghi + 1;
@@ -1459,7 +1489,7 @@ struct Wave {
         // document stays narrow: the editing form has no wide state)
         if (C != s.lc.own || C >= MT_MAX_CLIENTS || (op.type & MT_OP_WIDE)) return fail(MT_DERR_LIMITS, -1);
         if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, -1);
-        if (s.lc.ghi - s.lc.glo >= 64) return fail(MT_DERR_CAPACITY, -1);
+        if (s.lc.ghi - s.lc.glo >= GN) return fail(MT_DERR_CAPACITY, -1);
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
         const Pairs pr{pay + tlen, np, false};
@@ -1772,14 +1802,41 @@ struct Wave {
                 s.lc.rgn = g.loc[d].rgn;
                 s.lc.rgpn = g.loc[d].rgpn;
             }
-            s.lc.gt[lane] = g.loc[d].gt[lane];
-            s.lc.gls[lane] = g.loc[d].gls[lane];
-            sync();
             // (a document that has not edited yet has never stored these arrays)
-            const bool has = s.lc.own >= 0;
+            const bool has = g.loc[d].own >= 0;
             const size_t lo2 = (size_t)d * g.locstride;
+            if constexpr (GW == 1) {
+                s.lc.gt[lane] = g.loc[d].gt[lane];
+                s.lc.gls[lane] = g.loc[d].gls[lane];
+                for (int i = lane; i < n; i += 64) s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
+            } else if (g.sc[d].wide & MT_WIDE_GROUPS) {
+                for (uint32_t j = lane; j < GN; j += 64) {
+                    s.lc.gt[j] = g.locx[d].gt[j];
+                    s.lc.gls[j] = g.locx[d].gls[j];
+                }
+                for (int i = lane; i < n * GW; i += 64) s.gm[i] = g.gmx[lo2 * GW + i];
+            } else {
+                // entering the wide-group form: ordinal N moves from bit / index N % 64 to N % GN
+                // (at most 64 pending, so N % 64 names one ordinal of [glo, ghi))
+                const uint32_t glo = g.loc[d].glo, np = g.loc[d].ghi - glo;
+                for (uint32_t j = lane; j < GN; j += 64) s.lc.gt[j] = s.lc.gls[j] = 0u;
+                sync();
+                if ((uint32_t)lane < np) {
+                    const uint32_t N = glo + (uint32_t)lane;
+                    s.lc.gt[N % GN] = g.loc[d].gt[N & 63u];
+                    s.lc.gls[N % GN] = g.loc[d].gls[N & 63u];
+                }
+                for (int i = lane; i < n; i += 64) {
+                    for (int w = 0; w < GW; w++) s.gm[i * GW + w] = 0ull;
+                    uint64_t m = has ? g.gm[lo2 + i] : 0ull;
+                    while (m) {
+                        const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                        m &= m - 1;
+                        gm_set(i, glo + ((b - glo) & 63u));
+                    }
+                }
+            }
             for (int i = lane; i < n; i += 64) {
-                s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
                 s.pk[i] = has ? g.pk[lo2 + i] : 0ull;
                 s.ct[i] = has ? g.ct[lo2 + i] : 0u;
                 s.lsq[i] = has ? g.lsq[lo2 + i] : 0ull;
@@ -1886,6 +1943,7 @@ struct Wave {
             sc.n_empty = (uint32_t)nempty;
             if (g.evn) g.evn[d] = (uint32_t)s.evn;
             if (W) sc.wide = s.wide;
+            if (GW > 1 && s.lc.own >= 0) sc.wide = sc.wide | MT_WIDE_GROUPS;
         }
         if constexpr (W) {
             for (int i = lane; i < nn; i += 64) {
@@ -1901,7 +1959,11 @@ struct Wave {
                 const size_t lo2 = (size_t)d * g.locstride;
                 for (int i = lane; i < min(nn, (int)g.locstride); i += 64) {
                     const int sl = s.order[i];
-                    g.gm[lo2 + i] = s.gm[sl];
+                    if constexpr (GW == 1) {
+                        g.gm[lo2 + i] = s.gm[sl];
+                    } else {
+                        for (int w = 0; w < GW; w++) g.gmx[(lo2 + i) * GW + w] = s.gm[sl * GW + w];
+                    }
                     g.pk[lo2 + i] = s.pk[sl];
                     g.ct[lo2 + i] = s.ct[sl];
                     g.lsq[lo2 + i] = s.lsq[sl];
@@ -1915,8 +1977,15 @@ struct Wave {
                     g.loc[d].rgn = s.lc.rgn;
                     g.loc[d].rgpn = s.lc.rgpn;
                 }
-                g.loc[d].gt[lane] = s.lc.gt[lane];
-                g.loc[d].gls[lane] = s.lc.gls[lane];
+                if constexpr (GW == 1) {
+                    g.loc[d].gt[lane] = s.lc.gt[lane];
+                    g.loc[d].gls[lane] = s.lc.gls[lane];
+                } else {
+                    for (uint32_t j = lane; j < GN; j += 64) {
+                        g.locx[d].gt[j] = s.lc.gt[j];
+                        g.locx[d].gls[j] = s.lc.gls[j];
+                    }
+                }
             }
         }
     }
@@ -2023,8 +2092,9 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
 // HBM workspace (ws + w * sizeof(Lds<CAP>)) instead of LDS.  Latency-bound like the LDS form but
 // without its 160 KiB-per-CU ceiling; such documents are rare, so a handful of waves serve them.
 // W: wide documents (include/mtgpu.h "limits"), every capacity class from 2048 segments up.
-// LOC: the editing form above MT_LOC_CAP segments (mt_launch_apply_loc_big).
-template <int CAP, bool W = false, bool LOC = false>
+// LOC: the editing form above MT_LOC_CAP segments or past 64 pending edits (GW = 4: MT_WIDE_GROUPS
+// documents; mt_launch_apply_loc_big).
+template <int CAP, bool W = false, bool LOC = false, int GW = 1>
 __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                      const uint8_t* __restrict__ payload,
                                                      const uint32_t* __restrict__ row_ptr,
@@ -2033,15 +2103,16 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
-    using LS = Lds<CAP, LOC, W>;
+    using LS = Lds<CAP, LOC, W, GW>;
     LS& st = *reinterpret_cast<LS*>(ws + (size_t)w * sizeof(LS));
-    Wave<CAP, true, LOC, W> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
-                               g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
+    Wave<CAP, true, LOC, W, GW> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
+                                   g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     if (LOC && !loc_admit<CAP>(g, ops, d, a, b)) return;
+    if (GW > 1 && !(g.gmx && g.locx)) return;  // (the engine allocates them before such a launch)
     wv.load(g, d);
     if (LOC) {
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;
@@ -2188,32 +2259,33 @@ extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, con
 
 // editing documents above MT_LOC_CAP segments (mt_bin_kernel's last editing buckets): the editing
 // form with its structure in the HBM workspace (n_docs * mt_lds_bytes_loc(cap_class) bytes)
-extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+// (gw = 4: the MT_WIDE_GROUPS documents' form, 256 pending edits, at 1024 / 4096 slots)
+extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gstate* g, const mt_op_rec* ops,
                                               const uint8_t* payload, const uint32_t* row_ptr,
                                               const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
                                               uint32_t op_cnt, uint8_t* ws, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     dim3 grid(n_docs), block(64);
-#define MT_LAUNCH_LOCB(CAPV)                                                                                 \
-    case CAPV:                                                                                               \
-        hipLaunchKernelGGL((mt::apply_kernel_g<CAPV, false, true>), grid, block, 0, stream, *g, ops, payload, \
-                           row_ptr, doc_ids, n_docs, op_lo, op_cnt, ws);                                     \
-        return hipGetLastError();
-    switch (cap_class) {
-        MT_LAUNCH_LOCB(2048)
-        MT_LAUNCH_LOCB(4096)
-        default:
-            return hipErrorInvalidValue;
+#define MT_LAUNCH_LOCB(CAPV, GWV)                                                                            \
+    if (cap_class == CAPV && gw == GWV) {                                                                    \
+        hipLaunchKernelGGL((mt::apply_kernel_g<CAPV, false, true, GWV>), grid, block, 0, stream, *g, ops,     \
+                           payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt, ws);                            \
+        return hipGetLastError();                                                                            \
     }
+    MT_LAUNCH_LOCB(2048, 1)
+    MT_LAUNCH_LOCB(4096, 1)
+    MT_LAUNCH_LOCB(1024, 4)
+    MT_LAUNCH_LOCB(4096, 4)
 #undef MT_LAUNCH_LOCB
+    return hipErrorInvalidValue;
 }
 
-extern "C" size_t mt_lds_bytes_loc(int cap_class) {
-    switch (cap_class) {
-        case 2048: return sizeof(mt::Lds<2048, true>);
-        case 4096: return sizeof(mt::Lds<4096, true>);
-        default: return 0;
-    }
+extern "C" size_t mt_lds_bytes_loc(int cap_class, int gw) {
+    if (gw == 1 && cap_class == 2048) return sizeof(mt::Lds<2048, true>);
+    if (gw == 1 && cap_class == 4096) return sizeof(mt::Lds<4096, true>);
+    if (gw == 4 && cap_class == 1024) return sizeof(mt::Lds<1024, true, false, 4>);
+    if (gw == 4 && cap_class == 4096) return sizeof(mt::Lds<4096, true, false, 4>);
+    return 0;
 }
 
 extern "C" size_t mt_lds_bytes(int cap_class) {

@@ -39,11 +39,11 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
                                            uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
                                            hipStream_t stream);
 extern "C" size_t mt_lds_bytes_wide(int cap_class);
-extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
+extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gstate* g, const mt_op_rec* ops,
                                               const uint8_t* payload, const uint32_t* row_ptr,
                                               const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
                                               uint32_t op_cnt, uint8_t* ws, hipStream_t stream);
-extern "C" size_t mt_lds_bytes_loc(int cap_class);
+extern "C" size_t mt_lds_bytes_loc(int cap_class, int gw);
 extern "C" hipError_t mt_launch_init(const mt_gstate* g, uint32_t n_docs, hipStream_t st);
 extern "C" hipError_t mt_launch_label_keys(const mt_gstate* g, uint32_t d0, uint32_t d1, uint32_t keys, hipStream_t st);
 extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint32_t* doc_ids, const uint32_t* row_ptr,
@@ -88,9 +88,11 @@ constexpr int kWideClasses = kNumClasses - kFirstWide;
 // label keys), run by the LDS engine at that class's capacity, then the documents with client ids
 // above 32, run by the register engine's C64 form (mt_bin_kernel)
 // (then the editing documents that fit 256 / 512 slots: the editing form at that size; then those
-// above MT_LOC_CAP = 1024: its HBM-workspace form at 2048 / 4096)
-constexpr int kLocForms = 4;
-const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096};
+// above MT_LOC_CAP = 1024: its HBM-workspace form at 2048 / 4096; then those past 64 pending edits
+// (MT_WIDE_GROUPS): the HBM-workspace form with 4 group-mask words per slot at 1024 / 4096)
+constexpr int kLocForms = 6;
+const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096, 1024, 4096};
+const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, 4, 4};
 constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
 // the register engine's C64 form per class, the other editing forms
@@ -230,9 +232,26 @@ static mt_status ensure_locstride(mt_engine* e, uint32_t cap) {
     HIP_OK(hipDeviceSynchronize());
     mt_status st = MT_OK;
     if ((st = relay_rows(e, &g.gm, g.locstride, cap)) || (st = relay_rows(e, &g.pk, g.locstride, cap)) ||
-        (st = relay_rows(e, &g.ct, g.locstride, cap)) || (st = relay_rows(e, &g.lsq, g.locstride, cap)))
+        (st = relay_rows(e, &g.ct, g.locstride, cap)) || (st = relay_rows(e, &g.lsq, g.locstride, cap)) ||
+        (g.gmx && (st = relay_rows(e, &g.gmx, 4 * g.locstride, 4 * cap))))
         return st;  // (a failed relay leaves the arrays it did at the new stride: the engine is unusable)
     g.locstride = cap;
+    return MT_OK;
+}
+
+// The MT_WIDE_GROUPS documents' group masks (4 words per segment) and group stamps, allocated the
+// first time a document passes 64 pending edits
+static mt_status ensure_groups(mt_engine* e) {
+    mt_gstate& g = e->g;
+    if (g.gmx) return MT_OK;
+    const size_t D = e->cfg.max_docs;
+    mt_status st = MT_OK;
+    if ((st = dalloc(e, &g.locx, D)) || (st = dalloc(e, &g.gmx, D * 4 * g.locstride))) {
+        g.gmx = nullptr;
+        return st;
+    }
+    HIP_OK(hipMemset(g.locx, 0, D * sizeof(mt_locx)));
+    HIP_OK(hipMemset(g.gmx, 0, D * 4 * g.locstride * sizeof(uint64_t)));
     return MT_OK;
 }
 
@@ -704,11 +723,12 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         size_t lws_off[kLocForms] = {};
         for (int q = 0; q < kLocForms; q++) {
             const uint32_t cnt = e->h_counts[lds_base + 2 * e->first_lds + q];
-            if (kLocCaps[q] <= MT_LOC_CAP || !cnt) continue;
-            const mt_status ls = ensure_locstride(e, (uint32_t)kLocCaps[q]);
+            if ((kLocCaps[q] <= MT_LOC_CAP && kLocGW[q] == 1) || !cnt) continue;
+            mt_status ls = ensure_locstride(e, (uint32_t)std::max(kLocCaps[q], MT_LOC_CAP));
+            if (!ls && kLocGW[q] > 1) ls = ensure_groups(e);
             if (ls) return ls;
             lws_off[q] = need;
-            need += (size_t)cnt * mt_lds_bytes_loc(kLocCaps[q]);
+            need += (size_t)cnt * mt_lds_bytes_loc(kLocCaps[q], kLocGW[q]);
         }
         if (need > e->ws_bytes) {
             HIP_OK(hipDeviceSynchronize());
@@ -797,8 +817,8 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
-            if (q >= 0 && kLocCaps[q] > MT_LOC_CAP)
-                HIP_OK(mt_launch_apply_loc_big(kLocCaps[q], &e->g, b->ops, b->payload, b->row_ptr,
+            if (q >= 0 && (kLocCaps[q] > MT_LOC_CAP || kLocGW[q] > 1))
+                HIP_OK(mt_launch_apply_loc_big(kLocCaps[q], kLocGW[q], &e->g, b->ops, b->payload, b->row_ptr,
                                                e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->ws + lws_off[q],
                                                e->stream));
             else
@@ -1039,7 +1059,8 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
                     : cls == (uint32_t)kNumClasses      ? (MT_CLASS_EDITING | MT_LOC_CAP)
                     : q < (uint32_t)kFirstLds           ? (MT_CLASS_LDS | (uint32_t)kClasses[q])
                     : q < (uint32_t)(2 * kFirstLds)     ? (MT_CLASS_C64 | (uint32_t)kClasses[q - kFirstLds])
-                                                        : (MT_CLASS_EDITING | (uint32_t)kLocCaps[q - 2 * kFirstLds]);
+                                                        : (MT_CLASS_EDITING | (kLocGW[q - 2 * kFirstLds] > 1 ? MT_CLASS_GROUPS : 0u) |
+                                                           (uint32_t)kLocCaps[q - 2 * kFirstLds]);
     }
     if (kernel_ms) *kernel_ms = e->cls_ms[cls];
     if (launches) *launches = e->cls_launches[cls];
@@ -1050,8 +1071,11 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
 mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint64_t cap) {
     if (!e || !buf || !cap) return MT_ERR_ARG;
     char tmp[96];
-    if ((capacity & MT_CLASS_EDITING) && (capacity & ~(uint32_t)MT_CLASS_EDITING) > MT_LOC_CAP)
-        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    if ((capacity & MT_CLASS_EDITING) && (capacity & MT_CLASS_GROUPS))
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 4>",
+                 capacity & ~(uint32_t)(MT_CLASS_EDITING | MT_CLASS_GROUPS));
+    else if ((capacity & MT_CLASS_EDITING) && (capacity & ~(uint32_t)MT_CLASS_EDITING) > MT_LOC_CAP)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 1>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_C64)

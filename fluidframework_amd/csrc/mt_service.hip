@@ -206,7 +206,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // need the LDS engine there (declared label keys):
 // the LDS engine at that class's capacity, not at first_lds's; then one per such class for the
 // documents that only need 64-bit overlap sets (a client id above 32): the register engine's C64 form;
-// then the editing documents' 256 / 512-slot forms and their 2048 / 4096-slot HBM-workspace forms.
+// then the editing documents' 256 / 512-slot forms, their 2048 / 4096-slot HBM-workspace forms and
+// the wide-group forms (MT_WIDE_GROUPS: 256 pending edits) at 1024 / 4096 slots.
 // Binning is wave-aggregated: one atomic per (wave, bucket).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
@@ -230,6 +231,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             // snapshot body appends (MT_OP_LOAD, SnapshotLoader.loadBody) are applied by the LDS
             // engine only: the register engine's hot loop stays free of them
             bool lds_only = false, editing = own >= 0;
+            const uint32_t pend = own >= 0 ? g.loc[d].ghi - g.loc[d].glo : 0u;  // pending edits
+            uint32_t nloc = 0, nregen = 0;  // (an editing document: its local edits / reconnects here)
             unsigned long long ob = 0;
             // one pass over this launch's records (each is read once: the loops below were separate)
             bool win = ops && sc.win_op < 0;
@@ -239,6 +242,8 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 const uint32_t ty = MT_OP_TYPE(o);
                 lds_only = lds_only || ty == MT_OP_LOAD;
                 editing = editing || (o.seq == -1 && o.type != MT_OP_LOAD);
+                nloc += o.seq == -1 ? 1u : 0u;
+                nregen += o.seq == MT_SEQ_REGEN ? 1u : 0u;
                 ob += 32ull + o.payload_len;
                 if (!wdoc0) {
                     const uint32_t c = o.client;
@@ -330,6 +335,9 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                     : cap <= 1024 ? n_classes
                     : cap <= 2048 ? ebase + 2
                                   : ebase + 3;
+                // past 64 pending edits (or close: each local edit and each reconnect's op adds a
+                // group): the form with 256 group slots, at 1024 / 4096 slots, for good
+                if ((sc.wide & MT_WIDE_GROUPS) || pend + nloc + 4u * nregen > 48u) c = cap <= 1024 ? ebase + 4 : ebase + 5;
             }
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
@@ -343,7 +351,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 4;
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 6;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;

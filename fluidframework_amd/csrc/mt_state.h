@@ -52,6 +52,8 @@ struct mt_doc_scalars {      // 84 bytes
 #define MT_WIDE_LDS 1u  // needs the LDS engine (declared label keys, the wide form)
 #define MT_WIDE_DOC 2u  // the wide document form (include/mtgpu.h "limits")
 #define MT_WIDE_C64 4u  // has seen a client id above 32: 64-bit overlap sets (register engine: its C64 form)
+#define MT_WIDE_GROUPS 8u  // an editing document past 64 pending edits at once: the editing form with
+                           // MT_LOC_GROUPS_WIDE group slots (its HBM-workspace form), for good
 
 // An editing client's document (client.ts:163-214, 588-625): its local
 // edits are pending until their acks.  Pending edit ordinals [glo, ghi) (at most 64 at once) index
@@ -65,6 +67,14 @@ struct mt_loc {
     uint32_t lseq;           // collabWindow.localSeq (mergeTree.ts:831)
     uint32_t gls[64];        // each pending group's localSeq
     uint32_t rgn, rgpn;      // regenerated op records / payload bytes not drained yet
+};
+// An editing document past 64 pending edits (MT_WIDE_GROUPS) keeps up to MT_LOC_GROUPS_WIDE: its
+// group masks take MT_LOC_GROUPS_WIDE / 64 words per segment (mt_gstate.gmx) and each group's
+// creation stamp and localSeq live here (bit / index = ordinal % MT_LOC_GROUPS_WIDE)
+#define MT_LOC_GROUPS_WIDE 256
+struct mt_locx {
+    uint32_t gt[MT_LOC_GROUPS_WIDE];
+    uint32_t gls[MT_LOC_GROUPS_WIDE];
 };
 #define MT_RG_RECS 256       // regenerated op records per document between drains
 #define MT_RG_BYTES 4096     // and their payload bytes
@@ -113,6 +123,10 @@ struct mt_gstate {
     uint32_t* ct;      // creation stamp
     uint64_t* lsq;     // localSeq (low 32 bits) / localRemovedSeq (high), 0: undefined
     mt_loc* loc;       // [doc]
+    // MT_WIDE_GROUPS documents (allocated on first need, else null): the group masks, 4 words per
+    // segment ([doc][locstride][4]), and the groups' stamps / localSeqs
+    uint64_t* gmx;
+    mt_locx* locx;     // [doc]
     struct mt_op_rec* rg;  // [doc][MT_RG_RECS] regenerated ops (seq = the resetting record's index)
     uint8_t* rgp;      // [doc][MT_RG_BYTES] their payload
     uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;

@@ -78,7 +78,8 @@ enum mt_op_flags {
  * Remote ops see the pending segments as the reference does (nodeLength, breakTie,
  * blockInsert's continuePredicate, pending property keys).  Such a document runs on the LDS
  * engine's editing form (in LDS up to MT_LOC_CAP = 1024 segments, then with its structure in an HBM
- * workspace at 2048 / 4096; at most 4096 segments and at most 64 pending edits; beyond:
+ * workspace at 2048 / 4096; past 64 pending edits at once the workspace form with 256 pending-edit
+ * slots, for good; at most 4096 segments and 256 pending edits; beyond:
  * MT_DERR_CAPACITY); its delta events include the local edits' callbacks (seq -1). */
 #define MT_SEQ_LOCAL (-1)
 /* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =
@@ -259,9 +260,11 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
  * runs at that capacity (declared label keys), reading MT_CLASS_LDS | capacity, then one per register
  * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),
  * reading MT_CLASS_C64 | capacity, then the editing form's other sizes, MT_CLASS_EDITING | 256 / 512
- * (LDS) and | 2048 / 4096 (HBM workspace); MT_ERR_ARG past the last): each class is one kernel
+ * (LDS) and | 2048 / 4096 (HBM workspace), then MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024 / 4096 (the
+ * HBM-workspace form with 256 pending-edit slots); MT_ERR_ARG past the last): each class is one kernel
  * instantiation (see mt_class_kernel_name). */
 #define MT_CLASS_EDITING 0x40000000u
+#define MT_CLASS_GROUPS 0x08000000u  /* with MT_CLASS_EDITING: the form for more than 64 pending edits */
 #define MT_CLASS_LDS 0x20000000u
 #define MT_CLASS_C64 0x10000000u
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,

@@ -9,7 +9,7 @@
 // lags behind the stream.  A run whose clients end with different text is dropped (the reference
 // itself diverges on some lagging-client runs; such logs are not used as fixtures).
 // TEST INFRASTRUCTURE ONLY (this container).
-//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial [markers [reconnect]]]] -> JSON {docs: [[record, ...], ...]}
+//   node local_farm.js <nDocs> <seed> <opsPerDoc> [nClients [partial [markers [reconnect [offline]]]]] -> JSON {docs: [[record, ...], ...]}
 //   record = [seq, ref, msn, client, type, pos1, pos2, text, props {key id: value id | null} | null,
 //             flags]; c1's local edits have seq = -1 (UnassignedSequenceNumber), ref = msn = 0
 const path = require("path");
@@ -63,7 +63,7 @@ function record(seq, ref, msn, client, op) {
         op.combiningOp && op.combiningOp.name === "rewrite" ? F_REWRITE : 0];
 }
 
-function farm(seed, nOps, nClients, partial, markers, reconnect) {
+function farm(seed, nOps, nClients, partial, markers, reconnect, offline) {
     const r = rng(seed);
     const ri = (n) => Math.floor(r() * n);
     const clients = [];
@@ -78,6 +78,7 @@ function farm(seed, nOps, nClients, partial, markers, reconnect) {
     const log = [];        // c1's view
     const regen = [];      // [index of the seq -2 record, regenerated ops]
     let seq = 0, made = 0;
+    let away = 0;          // offline: rounds c1 still stays offline (its messages held, nothing delivered)
     const deliver = (i) => {
         const m = seqd[cursor[i]++];
         clients[i].applyMsg(m);
@@ -115,23 +116,33 @@ function farm(seed, nOps, nClients, partial, markers, reconnect) {
         if (i === 0) log.push(record(-1, 0, 0, 1, op));
         made++;
     };
-    const sequenceAll = () => {
+    const sequenceAll = (hold) => {
+        const held = [];   // (hold: c1 is offline, its messages wait in order)
         while (queue.length) {
             const q = queue.shift();
+            if (hold && q.client === 1) {
+                held.push(q);
+                continue;
+            }
             seq++;
             // no client may still reference a seq below the msn: its in-flight ops included
-            const msn = Math.min(q.ref, ...clients.map((c) => c.getCurrentSeq()), ...queue.map((o) => o.ref));
+            const msn = Math.min(q.ref, ...clients.map((c) => c.getCurrentSeq()), ...queue.map((o) => o.ref),
+                                 ...held.map((o) => o.ref));
             seqd.push({ clientId: "c" + q.client, clientSequenceNumber: 1, contents: q.op, metadata: undefined,
                 minimumSequenceNumber: msn, origin: undefined, referenceSequenceNumber: q.ref, sequenceNumber: seq,
                 timestamp: 0, term: 1, traces: [], type: "op" });
         }
+        queue.push(...held);
     };
     // rounds (mergeTreeOperationRunner.ts): clients edit, the round's ops are sequenced, and every
     // client catches up -- c1 only to a random point when `partial`, so its next edits interleave
     // with the rest of the stream
     while (made < nOps) {
+        // offline: now and then c1 goes offline for 12-24 rounds, editing more per round; its
+        // messages are held (so its pending edits pile up past 64) and it receives nothing
+        if (offline && !away && r() < 0.08) away = 12 + ri(13);
         for (let i = 0; i < nClients; i++) {
-            const k = r() < 0.6 ? 1 + ri(3) : 0;
+            const k = away && i === 0 ? 1 + ri(5) : r() < 0.6 ? 1 + ri(3) : 0;
             for (let q = 0; q < k; q++) localOp(i);
         }
         // reconnect (client.reconnectFarm.spec.ts): c1's messages of this round are never sequenced;
@@ -143,8 +154,12 @@ function farm(seed, nOps, nClients, partial, markers, reconnect) {
             lost = queue.filter((q) => q.client === 1);
             for (let q = queue.length - 1; q >= 0; q--) if (queue[q].client === 1) queue.splice(q, 1);
         }
-        sequenceAll();
+        sequenceAll(away > 0);
         for (let i = 1; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
+        if (away) {
+            away--;
+            continue;
+        }
         const upto = partial ? cursor[0] + ri(seqd.length - cursor[0] + 1) : seqd.length;
         while (cursor[0] < upto) deliver(0);
         for (const q of lost) {
@@ -166,11 +181,18 @@ function farm(seed, nOps, nClients, partial, markers, reconnect) {
     return reconnect ? { log, regen } : log;
 }
 
-const [nDocs, seed, nOps, nClients, partial, markers, reconnect] = process.argv.slice(2).map((x) => parseInt(x, 10));
+const [nDocs, seed, nOps, nClients, partial, markers, reconnect, offline] =
+    process.argv.slice(2).map((x) => parseInt(x, 10));
 const docs = [];
 let dropped = 0;
 for (let d = 0, k = 0; d < nDocs; k++) {
-    const log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1, reconnect === 1);
+    let log = null;
+    try {  // (offline runs: a reference client may throw "MergeTree insert failed" -- dropped like a divergence)
+        log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1, reconnect === 1,
+                   offline === 1);
+    } catch (err) {
+        if (offline !== 1) throw err;
+    }
     if (log) { docs.push(log); d++; } else dropped++;
 }
 process.stderr.write(`local_farm: ${nDocs} documents, ${dropped} runs dropped (clients diverged)\n`);

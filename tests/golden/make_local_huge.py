@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""Regenerate local_huge (build container only): an editing-client farm log FROM THE REFERENCE
-ITSELF whose documents grow past 1024 segments (the editing form's LDS capacity), for the
-editing form's HBM-workspace classes.  Same farm and replay as make_local.py (oracle/tsref/
-local_farm.js, replay_ref.js `local`): 2 documents, 4 clients, c1 lagging, 32000 edits over all
-clients; local_huge.expected.jsonl holds the reference Client c1's canonical state at 6 checkpoints
-and at the end (one JSON line per document, like local.expected.jsonl)."""
+"""Regenerate local_huge and local_offline (build container only): editing-client farm logs FROM
+THE REFERENCE ITSELF beyond the editing form's LDS limits, for its HBM-workspace forms.  Same farm
+and replay as make_local.py (oracle/tsref/local_farm.js, replay_ref.js `local`), 4 clients, c1
+lagging:
+  * local_huge: 2 documents, 32000 edits over all clients: they grow past 1024 segments;
+  * local_offline: 6 documents, 3000 edits; c1 goes offline for 12-24 rounds now and then (its
+    messages held, nothing delivered) so that 110-170 of its edits are pending at once (the
+    reference client throws "MergeTree insert failed" on some such runs: the farm drops those).
+<name>.expected.jsonl holds the reference Client c1's canonical state at 6 checkpoints and at the
+end (one JSON line per document, like local.expected.jsonl); local_offline.events.jsonl the count and
+SHA-256 of c1's delta callbacks per document (like local_events.jsonl)."""
 import json
 import os
 import subprocess
@@ -17,28 +22,47 @@ sys.path.insert(0, HERE)
 
 from make_golden import build_log  # noqa: E402
 
-N_DOCS, SEED, N_OPS, N_CLIENTS, PARTIAL, N_CK = 2, 22, 32000, 4, 1, 6
+LOGS = (('local_huge', 2, 22, 32000, 0), ('local_offline', 6, 33, 3000, 1))
+# (name, docs, seed, edits over all clients, offline); 4 clients, c1 lagging, 6 checkpoints
+N_CLIENTS, PARTIAL, N_CK = 4, 1, 6
 
 
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
+    for name, n_docs, seed, n_ops, offline in LOGS:
+        make(name, n_docs, seed, n_ops, offline)
+
+
+def make(name, n_docs, seed, n_ops, offline):
     farm = os.path.join(REPO, 'oracle/tsref/local_farm.js')
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
-    res = subprocess.run(['node', farm, str(N_DOCS), str(SEED), str(N_OPS), str(N_CLIENTS), str(PARTIAL), '0', '0'],
-                         check=True, capture_output=True, text=True)
+    res = subprocess.run(['node', farm, str(n_docs), str(seed), str(n_ops), str(N_CLIENTS), str(PARTIAL), '0', '0',
+                          str(offline)], check=True, capture_output=True, text=True)
     docs = [[(s, r, m, c, t, p1, p2, text, None if props is None else {int(k): v for k, v in props.items()}, flags)
              for (s, r, m, c, t, p1, p2, text, props, flags) in recs] for recs in json.loads(res.stdout)['docs']]
-    path = os.path.join(HERE, 'local_huge.mtlog')
+    path = os.path.join(HERE, name + '.mtlog')
     build_log(docs).save(path)
     res = subprocess.run(['node', replay, 'local', path, str(N_CK)], check=True, capture_output=True, text=True)
     out = []
     for line in res.stdout.strip().split('\n'):
         r = json.loads(line)
         assert r['err'] is None, r['err']
-        out.append(json.dumps(dict(log='local_huge', **r), separators=(',', ':')))
-        print('doc', r['doc'], 'segments at the checkpoints', [len(st['segs']) for _, st in r['states']])
-    with open(os.path.join(HERE, 'local_huge.expected.jsonl'), 'w') as f:
+        out.append(json.dumps(dict(log=name, **r), separators=(',', ':')))
+        print(name, 'doc', r['doc'], 'segments at the checkpoints', [len(st['segs']) for _, st in r['states']])
+    with open(os.path.join(HERE, name + '.expected.jsonl'), 'w') as f:
         f.write('\n'.join(out) + '\n')
+    if offline:  # the reference client's callbacks (as make_local.py's local_events.jsonl): count + SHA-256
+        import hashlib
+        res = subprocess.run(['node', replay, 'localevents', path], check=True, capture_output=True, text=True)
+        ev_out = []
+        for line in res.stdout.strip().split('\n'):
+            r = json.loads(line)
+            assert r['err'] is None, r['err']
+            ev = r['events']
+            ev_out.append(json.dumps(dict(log=name, doc=r['doc'], n=len(ev), sha256=hashlib.sha256(
+                json.dumps(ev, separators=(',', ':')).encode()).hexdigest()), separators=(',', ':')))
+        with open(os.path.join(HERE, name + '.events.jsonl'), 'w') as f:
+            f.write('\n'.join(ev_out) + '\n')
 
 
 if __name__ == '__main__':

@@ -1,25 +1,38 @@
-"""An editing client whose document grows past the editing form's LDS capacity (MT_LOC_CAP = 1024
-segments): the editing form's HBM-workspace classes (mt_apply.hip apply_kernel_g<CAP, false, true>,
-mt_launch_apply_loc_big; include/mtgpu.h MT_SEQ_LOCAL).
+"""An editing client beyond the editing form's LDS limits: documents past 1024 segments
+(MT_LOC_CAP) and more than 64 pending edits -- the editing form's HBM-workspace forms (mt_apply.hip
+apply_kernel_g<CAP, false, true, GW>, mt_launch_apply_loc_big; include/mtgpu.h MT_SEQ_LOCAL).
 
-Pinned by the reference itself: tests/golden/local_huge.expected.jsonl holds the canonical states
-of a reference Client c1 replaying local_huge.mtlog (tests/golden/make_local_huge.py: the
-local_farm.js farm of reference clients, 32000 edits over 4 clients, c1 lagging), at checkpoints
-and at the end; both documents pass 1024 segments (up to 1609) with edits pending throughout."""
+Pinned by the reference itself: tests/golden/<log>.expected.jsonl holds the canonical states of a
+reference Client c1 replaying <log>.mtlog (tests/golden/make_local_huge.py: the local_farm.js farm
+of reference clients, 4 clients, c1 lagging), at checkpoints and at the end:
+  * local_huge: 32000 edits; both documents pass 1024 segments (up to 1609) with edits pending;
+  * local_offline: c1 goes offline for 12-24 rounds now and then, so 110-170 of its edits are
+    pending at once (acked in order when it comes back)."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 from conftest import GOLDEN
 from test_local import checkpoint_batch, prefix
 
 NAME = 'local_huge'
+OFFLINE = 'local_offline'
 
 
-def load_rows():
-    with open(os.path.join(GOLDEN, NAME + '.expected.jsonl')) as f:
+def load_rows(name=NAME):
+    with open(os.path.join(GOLDEN, name + '.expected.jsonl')) as f:
         return [json.loads(line) for line in f]
+
+
+def max_pending(batch, doc):
+    """the most edits of the document's editing client pending at once (local edits not yet acked)"""
+    a, b = int(batch.row_ptr[doc]), int(batch.row_ptr[doc + 1])
+    ops = batch.ops[a:b]
+    local = ops['seq'] == -1
+    ack = (ops['seq'] > 0) & (ops['client'] == 1) & ((ops['flags'] & 4) == 0)  # (a GROUP acks once)
+    return int(np.max(np.cumsum(local.astype(np.int64) - ack.astype(np.int64))))
 
 
 def test_fixture_grows_past_the_lds_capacity():
@@ -34,16 +47,39 @@ def test_fixture_grows_past_the_lds_capacity():
     assert local.sum() > 5000 and (b.ops['client'][~local] == 1).sum() == local.sum()  # every edit acked
 
 
-def test_oracle_editing_client_matches_reference_past_1024_segments(oracle_lib):
+def test_offline_fixture_has_more_than_64_pending_edits():
     from fluidframework_amd.oplog import OpBatch
-    batch = OpBatch.load(os.path.join(GOLDEN, NAME + '.mtlog'))
+    b = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    rows = load_rows(OFFLINE)
+    assert all(r['err'] is None for r in rows)
+    pend = [max_pending(b, d) for d in range(b.n_docs)]
+    assert min(pend) > 100, pend
+
+
+@pytest.mark.parametrize('name', [NAME, OFFLINE])
+def test_oracle_editing_client_matches_reference_beyond_lds_limits(oracle_lib, name):
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)
-    for r in load_rows():
+    for r in load_rows(name):
         d = r['doc']
         assert o.error(d) == (0, 0), (d, o.error(d))
         assert o.state(d) == r['states'][-1][1], d
         for k, want in r['states'][-3:-1]:
             assert oracle_lib.Oracle(1).apply(prefix(batch, d, k)).state(0) == want, (d, k)
+
+
+def test_oracle_events_past_64_pending_edits_match_reference(oracle_lib):
+    import hashlib
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    o = oracle_lib.Oracle(batch.n_docs).record_events().apply(batch)
+    with open(os.path.join(GOLDEN, OFFLINE + '.events.jsonl')) as f:
+        gold = [json.loads(x) for x in f]
+    for g in gold:
+        ev = o.events(g['doc'])
+        assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+            g['sha256'], g['doc']
 
 
 @pytest.mark.gpu
@@ -67,5 +103,53 @@ def test_engine_editing_form_past_1024_segments_matches_reference(b):
             assert eng.state(i) == r['states'][q][1], (r['doc'], q, b)
         if max(len(r['states'][q][1]['segs']) for r in rows) > 1024 + 2 * b:
             assert used.get(editing_g, 0) > 0, used
-            assert eng.class_kernel(editing_g) == 'mt::apply_kernel_g<2048, false, true>'
+            assert eng.class_kernel(editing_g) == 'mt::apply_kernel_g<2048, false, true, 1>'
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('b', [1, 32])
+def test_engine_editing_form_past_64_pending_edits_matches_reference(b):
+    """110-170 pending edits at once: every checkpoint state and the final state equal the
+    reference's; the documents ran on the form with 256 pending-edit slots (class stats
+    MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024, mt::apply_kernel_g<1024, false, true, 4>), which they
+    enter with edits pending (their group masks and stamps re-laid) and keep for good."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    rows = load_rows(OFFLINE)
+    groups = 0x40000000 | 0x08000000 | 1024
+    for q in range(len(rows[0]['states'])):
+        cb = checkpoint_batch(batch, rows, q)
+        eng = MergeEngine(cb.n_docs, ops_per_launch=b)
+        eng.apply(cb)
+        used = {cap: n for cap, _, n, _ in eng.last_class_stats() if n}
+        for i, r in enumerate(rows):
+            assert eng.error(i) == (0, 0), (r['doc'], q, eng.error(i))
+            assert eng.state(i) == r['states'][q][1], (r['doc'], q, b)
+        if max(max_pending(cb, i) for i in range(cb.n_docs)) > 64:
+            assert used.get(groups, 0) > 0, used
+            assert eng.class_kernel(groups) == 'mt::apply_kernel_g<1024, false, true, 4>'
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_engine_editing_form_past_64_pending_edits_events_match_reference():
+    """The delta callbacks the wide-group form records (mt_events_enable) equal the reference
+    client's (tests/golden/local_offline.events.jsonl: count + SHA-256 per document)."""
+    import hashlib
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16).enable_events(1 << 16)
+    eng.apply(batch)
+    got = eng.drain_events()
+    with open(os.path.join(GOLDEN, OFFLINE + '.events.jsonl')) as f:
+        gold = [json.loads(x) for x in f]
+    for g in gold:
+        d = g['doc']
+        assert eng.error(d) == (0, 0), (d, eng.error(d))
+        ev = got[d]
+        assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
+            g['sha256'], d
+    eng.close()

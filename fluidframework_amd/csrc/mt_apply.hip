@@ -1355,7 +1355,7 @@ struct Wave {
             const int32_t S = MT_SEQ_REGEN;
             if (s.lc.own < 0 || (int)op.client != s.lc.own || op.type > MT_OP_ANNOTATE) return fail(MT_DERR_BAD_OP, S);
             if (s.lc.glo == s.lc.ghi) return fail(MT_DERR_BAD_OP, S);
-            const int np = MT_OP_NPAIRS(op.flags);
+            const int np = MT_OP_NPAIRS(op);
             const uint8_t* opairs = payload + op.payload_off + (op.payload_len - 2 * np);
             const uint32_t Lo = s.lc.glo;
             const uint32_t Ls = s.lc.gls[Lo % GN];
@@ -1478,7 +1478,7 @@ struct Wave {
     // applyAnnotateRangeOp): refSeq = currentSeq, seq = UnassignedSequenceNumber, the local view; no
     // window asserts, no seq update.  The first one names the document's editing client.
     MT_DEV void apply_local(const mt_op_rec& op, const uint8_t* payload) {
-        const int np = MT_OP_NPAIRS(op.flags);
+        const int np = MT_OP_NPAIRS(op);
         const int C = op.client;
         if (s.lc.own < 0) {
             sync();
@@ -1513,7 +1513,7 @@ struct Wave {
         if (ev && s.evn > (int)evcap) fail(MT_DERR_EVENTS, -1);
     }
     MT_DEV void apply_ack(const mt_op_rec& op, const uint8_t* payload) {
-        const int np = MT_OP_NPAIRS(op.flags);
+        const int np = MT_OP_NPAIRS(op);
         const int32_t S = op.seq;
         s.evseq = S;
         if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                                  // client.ts:824
@@ -1527,7 +1527,7 @@ struct Wave {
     }
 
     MT_DEV void apply(const mt_op_rec& op, const uint8_t* payload) {
-        const int np = MT_OP_NPAIRS(op.flags);
+        const int np = MT_OP_NPAIRS(op);
         const int32_t S = op.seq;
         const int type = MT_OP_TYPE(op);
         const bool wop = (op.type & MT_OP_WIDE) != 0;

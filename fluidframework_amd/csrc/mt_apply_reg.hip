@@ -54,6 +54,14 @@ constexpr uint32_t F_NLQ = 1u << 21;
 constexpr uint32_t kEmptyCf = 0xFFu;     // padding: client 255 never matches (and the slot is dead)
 constexpr uint16_t kDead = 0xFFFFu;
 
+// The document arrays are read and written through global-address-space pointers (global_load /
+// global_store: vmcnt only), not generic ones (flat_*: both counters, so every wait drains LDS too)
+#define MT_GLOB __attribute__((address_space(1)))
+#define MT_KARG __attribute__((address_space(4)))
+template <class T>
+MT_DEV MT_GLOB T* gp(T* p) { return (MT_GLOB T*)p; }
+typedef const MT_KARG mt_gstate KGState;
+
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 MT_DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 // lane l <- lane l-1 (lane 0 <- fill)
@@ -113,9 +121,9 @@ struct RLds {
     int32_t nb[MT_MAXLEV];  // blocks per interior level (leaf blocks are counted by BS bits)
     // scour scratch: the live children by rank, one array per field (separate 4-byte stores: no
     // 4-register tuple built per slot, which cost ~20 VGPRs at the scour's register peak)
-    int32_t zsq[kMaxNodes];  // the removal seq of a removed child, else its seq
-    uint32_t zli[kMaxNodes], zcf[kMaxNodes];
-    int32_t zsl[kMaxNodes];  // its slot
+    // zr[q]: the removal seq of a removed child q, else its seq; zr[8 + q] its li, zr[16 + q] its cf,
+    // zr[24 + q] its slot
+    uint32_t zr[4 * kMaxNodes];
 };
 
 struct Elem {
@@ -594,6 +602,7 @@ struct RWave {
         PROF_BEGIN(tb2, P_B_TXT);
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
         const uint32_t id = id_of(e.li);
+        const uint64_t pid = s.props[id];  // (issued with the toff read: one LDS round trip)
         const uint32_t to = uniu(s.toff[id]);
 #ifdef MT_NO_NLQ
         uint8_t last = 0;  // a segment without any "\n" needs no text read
@@ -603,7 +612,7 @@ struct RWave {
         }
 #endif
         if (lane == 0) {
-            s.props[t] = s.props[id];
+            s.props[t] = pid;
             s.toff[t] = (uint16_t)(to + (uint32_t)off);
             s.tln[id] = (uint32_t)off;
             s.tln[t] = len - (uint32_t)off;
@@ -781,22 +790,24 @@ struct RWave {
         if (cnt > kMaxNodes) return fail(MT_DERR_CAPACITY, cur_seq), cnt;
         // the live children, rank by rank, through LDS scratch (one 16-byte record each: the
         // removal seq of a removed child, else its seq -- the only one the decisions read)
+        // (every lane stores every slot: a slot that is no live child of the block goes to the
+        // lane's dummy words in `scr`, dead during the op -- no per-slot branch)
+        uint32_t* const dum = reinterpret_cast<uint32_t*>(s.scr) + lane;
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            if ((lb >> j) & 1u) {
-                const int q = rbase + __popc(lb & ((1u << j) - 1u));
-                s.zsq[q] = (cf[j] & F_RM) ? rseq[j] : seq[j];
-                s.zli[q] = li[j];
-                s.zcf[q] = cf[j];
-                s.zsl[q] = idx(j);
-            }
+            const int q = rbase + __popc(lb & ((1u << j) - 1u));
+            uint32_t* const z = ((lb >> j) & 1u) ? &s.zr[q] : dum;
+            z[0] = (uint32_t)((cf[j] & F_RM) ? rseq[j] : seq[j]);
+            z[kMaxNodes] = li[j];
+            z[2 * kMaxNodes] = cf[j];
+            z[3 * kMaxNodes] = (uint32_t)idx(j);
         }
         wave_sync();
         const bool mine = lane < cnt;
-        const int32_t vsq = mine ? s.zsq[lane] : 0;
-        const uint32_t vli = mine ? s.zli[lane] : 0u;
-        uint32_t vcf = mine ? s.zcf[lane] : 0u;
-        const int vslot = mine ? s.zsl[lane] : 0;
+        const int32_t vsq = mine ? (int32_t)s.zr[lane] : 0;
+        const uint32_t vli = mine ? s.zr[kMaxNodes + lane] : 0u;
+        uint32_t vcf = mine ? s.zr[2 * kMaxNodes + lane] : 0u;
+        const int vslot = mine ? (int)s.zr[3 * kMaxNodes + lane] : 0;
         const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
         if (__ballot(mine && (vcf & F_NLQ))) {  // the children's pending ENDS_WITH_NEWLINE, in one load
             arena_sync();
@@ -1103,26 +1114,53 @@ struct RWave {
 #pragma unroll
             for (int j = 0; j < K; j++) {
                 const int ce = cum[j];
-                const bool touched = ce > cs && cs < end && ce > start;
-                tm |= touched ? (1u << j) : 0u;
-                // branch-free register updates (a store per branch would merge into a
-                // pointer phi and push the state arrays to scratch)
+                tm |= (ce > cs && cs < end && ce > start) ? (1u << j) : 0u;
+                cs = ce;
+            }
+        }
+        if (is_remove) {
+            // branch-free register updates (a store per branch would merge into a pointer phi and
+            // push the state arrays to scratch)
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                const bool touched = (tm >> j) & 1u;
                 const uint32_t f = cf[j];
                 const bool was_rm = (f & F_RM) != 0;
-                const bool mark = touched && is_remove && !was_rm;  // first remover wins
-                const bool overlap = touched && is_remove && was_rm;  // addOverlappingClient
-                const bool annot = touched && !is_remove;
+                const bool mark = touched && !was_rm;    // first remover wins
+                const bool overlap = touched && was_rm;  // addOverlappingClient
                 ov[j] = (overlap && !hic) ? (ov[j] | cbit) : ov[j];
                 if constexpr (W) oh[j] = (overlap && hic) ? (oh[j] | cbit) : oh[j];
                 rseq[j] = mark ? S : rseq[j];
-                cf[j] = mark ? ((f & ~0xFF00u) | F_RM | ((uint32_t)C << 8)) : (annot ? (f | F_PDEF) : f);
-                if (annot) {  // SegmentPropertiesManager.addProperties (remote, no combining op)
-                    const uint32_t id = id_of(li[j]);
-                    const uint64_t p = ((f & F_PDEF) && !rewrite) ? s.props[id] : 0;
-                    s.props[id] = (p & ~pclr) | pset;
-                }
-                cs = ce;
+                cf[j] = mark ? ((f & ~0xFF00u) | F_RM | ((uint32_t)C << 8)) : f;
             }
+        } else {
+            // SegmentPropertiesManager.addProperties (remote, no combining op) on the touched slots'
+            // property sets, four slots per LDS round trip: every lane reads and writes
+            // unconditionally, an untouched slot through the lane's dummy word in `scr` (dead during
+            // the op), so there is no per-slot branch and no per-slot wait
+            uint64_t* const dum = reinterpret_cast<uint64_t*>(s.scr) + lane;
+#pragma unroll
+            for (int j0 = 0; j0 < K; j0 += 4) {
+                constexpr int Q = 4;
+                uint64_t* pa[Q];
+                uint64_t pv[Q];
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    if (j0 + q < K) {
+                        pa[q] = ((tm >> (j0 + q)) & 1u) ? &s.props[id_of(li[j0 + q])] : dum;
+                        pv[q] = *pa[q];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    if (j0 + q < K) {
+                        const uint64_t p = ((cf[j0 + q] & F_PDEF) && !rewrite) ? pv[q] : 0ull;
+                        *pa[q] = (p & ~pclr) | pset;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < K; j++) cf[j] = ((tm >> j) & 1u) ? (cf[j] | F_PDEF) : cf[j];
         }
         // addToLRUSet for the touched segments in document order: one push per leaf block
         // (its first touched child) whose needsScour is not already true
@@ -1139,7 +1177,7 @@ struct RWave {
     // (client.ts:821-828, MergeTree.setMinSeq mergeTree.ts:1718-1736).  Every register-heavy
     // routine has exactly one call site.
     MT_DEV void apply(const mt_op_rec op, const uint8_t* payload) {
-        const int np = MT_OP_NPAIRS(op.flags);
+        const int np = MT_OP_NPAIRS(op);
         const int32_t S = op.seq;
         if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
         const uint8_t* pay = payload + op.payload_off;
@@ -1226,7 +1264,7 @@ struct RWave {
 
     // ------------------------------------------------------------ load / store
     // K consecutive u32 of one lane (16-byte aligned when K % 4 == 0, 8-byte when K is even)
-    MT_DEV VU ld_u32(const uint32_t* p) const {
+    MT_DEV VU ld_u32(const MT_GLOB uint32_t* p) const {
         VU v;
         if constexpr (K % 2 == 1) {
 #pragma unroll
@@ -1234,7 +1272,7 @@ struct RWave {
         } else if constexpr (K % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < K / 4; c++) {
-                const U4 x = reinterpret_cast<const U4*>(p)[c];
+                const U4 x = reinterpret_cast<const MT_GLOB U4*>(p)[c];
                 v[4 * c] = x[0];
                 v[4 * c + 1] = x[1];
                 v[4 * c + 2] = x[2];
@@ -1243,7 +1281,7 @@ struct RWave {
         } else {
 #pragma unroll
             for (int c = 0; c < K / 2; c++) {
-                const U2 x = reinterpret_cast<const U2*>(p)[c];
+                const U2 x = reinterpret_cast<const MT_GLOB U2*>(p)[c];
                 v[2 * c] = x[0];
                 v[2 * c + 1] = x[1];
             }
@@ -1273,8 +1311,51 @@ struct RWave {
         return v;
     }
 
-    MT_DEV void load(const mt_gstate& g, uint32_t d) {
-        const mt_doc_scalars& sc = g.sc[d];
+    // ---- raw rows of the load: every global read of a launch is issued before any of it is used
+    static constexpr int BW = (K % 2 == 1) ? K : (K % 4 == 0 ? K / 4 : K / 2);  // words per byte row
+    MT_DEV void ld8_raw(const MT_GLOB uint8_t* p, uint32_t (&w)[BW]) const {  // K consecutive bytes of one lane
+#pragma unroll
+        for (int c = 0; c < BW; c++) {
+            if constexpr (K % 2 == 1)
+                w[c] = p[c];
+            else if constexpr (K % 4 == 0)
+                w[c] = reinterpret_cast<const MT_GLOB uint32_t*>(p)[c];
+            else
+                w[c] = reinterpret_cast<const MT_GLOB uint16_t*>(p)[c];
+        }
+    }
+    MT_DEV static uint32_t byte_at(const uint32_t (&w)[BW], int j) {
+        if constexpr (K % 2 == 1) return w[j] & 0xFFu;
+        else if constexpr (K % 4 == 0) return (w[j / 4] >> (8 * (j % 4))) & 0xFFu;
+        else return (w[j / 2] >> (8 * (j % 2))) & 0xFFu;
+    }
+    MT_DEV void ld64_raw(const MT_GLOB uint64_t* p, uint32_t (&w)[2 * K]) const {  // K consecutive u64: (lo, hi) pairs
+        if constexpr (K % 2 == 1) {
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                const U2 x = reinterpret_cast<const MT_GLOB U2*>(p)[j];
+                w[2 * j] = x[0];
+                w[2 * j + 1] = x[1];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < K / 2; c++) {
+                const U4 x = reinterpret_cast<const MT_GLOB U4*>(p)[c];
+                w[4 * c] = x[0];
+                w[4 * c + 1] = x[1];
+                w[4 * c + 2] = x[2];
+                w[4 * c + 3] = x[3];
+            }
+        }
+    }
+
+    // The document's state into the wave: every global read is issued first (the per-segment rows
+    // blocked by lane, K consecutive entries each, like the register state; the leaf-block, heap and
+    // interior-level rows by chunks of 64) and waited for once, then the LDS images and the register
+    // state are built from the registers.  (Before: a loop per array with a dependent load per
+    // iteration, ~20 serialized memory round trips per launch.)
+    MT_DEV void load(KGState& g, uint32_t d) {
+        const MT_GLOB mt_doc_scalars& sc = gp(g.sc)[d];
         const int n = uni(sc.nseg);
         nlev = uni(sc.nlev);
         heap_n = uni(sc.heap_n);
@@ -1289,114 +1370,121 @@ struct RWave {
         nlive = n;
         ns = n;
         const size_t so = (size_t)d * g.segcap;
-#pragma clang loop unroll(disable) vectorize(disable)
-        for (int i = lane; i < n; i += 64) {
-            s.props[i] = g.props[so + i];
-            s.toff[i] = (uint16_t)g.toff[so + i];
-            s.tln[i] = g.len[so + i];
-            s.scr[i] = 0;
-        }
-        for (int Lv = 1; Lv < nlev; Lv++) {
-            const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv - 1)) * g.ibcap;
-            const int nbl_ = uni(sc.nb[Lv]);
-#pragma clang loop unroll(disable) vectorize(disable)
-            for (int i = lane; i < nbl_; i += 64) s.ibcnt[Lv - 1][i] = g.ibcnt[io + i];
-        }
+        const size_t lo = (size_t)d * g.lbcap;
         const size_t ho = (size_t)d * g.hcap;
+        const int i0 = lane * K;
+        const bool mine = i0 < n;
+        // ---- 1. the reads, straight-line (no branch, so nothing is waited for before the last is
+        // issued): rows are read whole (segcap >= CAP keeps them inside the document); a lane past
+        // the document's n segments, and a chunk past its blocks or heap, re-reads the first one
+        // (the same lines: no extra traffic) and its values are never used
+        const int ir = mine ? i0 : 0;
+        VU vsq, vrs, vln, vto;
+        uint32_t pw[2 * K], ow[2 * K], bcw[BW], brw[BW], bfw[BW];
+        vsq = ld_u32(reinterpret_cast<const MT_GLOB uint32_t*>(gp(g.seq) + so + ir));
+        vrs = ld_u32(reinterpret_cast<const MT_GLOB uint32_t*>(gp(g.rseq) + so + ir));
+        vln = ld_u32(gp(g.len) + so + ir);
+        vto = ld_u32(gp(g.toff) + so + ir);
+        ld64_raw(gp(g.props) + so + ir, pw);
+        ld64_raw(gp(g.ovl) + so + ir, ow);
+        ld8_raw(gp(g.client) + so + ir, bcw);
+        ld8_raw(gp(g.rclient) + so + ir, brw);
+        ld8_raw(gp(g.flags) + so + ir, bfw);
+        constexpr int LBC = (L::LB + 63) / 64;  // leaf-block chunks (nb0 <= LB <= lbcap)
+        uint32_t lbc_[LBC], lbs_[LBC];
+#pragma unroll
+        for (int c = 0; c < LBC; c++) {
+            const size_t b = lo + (c * 64 < nb0 ? c * 64 + lane : 0);
+            lbc_[c] = gp(g.lbcnt)[b];
+            lbs_[c] = gp(g.lbscour)[b];
+        }
+        constexpr int HC = (L::H + 63) / 64;  // heap chunks (entries 1..heap_n, hcap >= H)
+        int32_t hq[HC];
+        uint32_t hs[HC];
+#pragma unroll
+        for (int c = 0; c < HC; c++) {
+            const size_t i = ho + 1 + (c * 64 < heap_n ? c * 64 + lane : 0);
+            hq[c] = gp(g.hseq)[i];
+            hs[c] = gp(g.hslot)[i];  // position at store == id at load
+        }
+        constexpr int IBL = MT_MAXLEV - 1;  // interior levels, two chunks each (the rest: below)
+        uint32_t ibw[IBL][2];
+#pragma unroll
+        for (int Lv = 1; Lv <= IBL; Lv++) {
+            const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv < nlev ? Lv - 1 : 0)) * g.ibcap;
+#pragma unroll
+            for (int c = 0; c < 2; c++) ibw[Lv - 1][c] = gp(g.ibcnt)[io + c * 64 + lane];  // (ibcap >= 264)
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- 2. the LDS images: cold fields by segment id (= position at load; ids >= n get
+        // garbage here and are written when allocated), leaf marks cleared, heap, interior levels
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            s.props[i0 + j] = (uint64_t)pw[2 * j] | ((uint64_t)pw[2 * j + 1] << 32);
+            s.toff[i0 + j] = (uint16_t)vto[j];
+            s.tln[i0 + j] = vln[j];
+            s.scr[i0 + j] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < HC; c++) {
+            const int i = 1 + c * 64 + lane;
+            if (c * 64 < heap_n && i <= heap_n) {
+                s.hseq[i] = hq[c];
+                s.hslot[i] = (uint16_t)hs[c];
+            }
+        }
+#pragma unroll
+        for (int Lv = 1; Lv <= IBL; Lv++) {
+            if (Lv < nlev) {
+                const int nbl_ = uni(sc.nb[Lv]);
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+                    if (c * 64 + lane < nbl_) s.ibcnt[Lv - 1][c * 64 + lane] = (uint8_t)ibw[Lv - 1][c];
+                if (nbl_ > 128) {  // (documents far past the register classes' typical shape)
+                    const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv - 1)) * g.ibcap;
 #pragma clang loop unroll(disable) vectorize(disable)
-        for (int i = 1 + lane; i <= heap_n; i += 64) {
-            s.hseq[i] = g.hseq[ho + i];
-            s.hslot[i] = g.hslot[ho + i];  // position at store == id at load
+                    for (int i = 128 + lane; i < nbl_; i += 64) s.ibcnt[Lv - 1][i] = gp(g.ibcnt)[io + i];
+                }
+            }
         }
         if (lane < MT_MAXLEV) s.nb[lane] = sc.nb[lane];
         wave_sync();
         // leaf blocks -> a mark (1 | needsScour << 1) at the first position of every non-empty block
-        const size_t lo = (size_t)d * g.lbcap;
         int nempty = 0;
         {
             int carry = 0;
-            for (int base = 0; base < nb0; base += 64) {
-                const int b = base + lane;
-                const int c = b < nb0 ? (int)g.lbcnt[lo + b] : 0;
-                const int scv = b < nb0 ? (int)g.lbscour[lo + b] : 0;
-                const int incl = wave_incl_scan(c) + carry;
-                if (b < nb0 && c > 0) s.scr[incl - c] = 1 | (scv << 1);
-                nempty += __popcll(wave_ballot(b < nb0 && c == 0));
-                carry = wave_last(incl);
+#pragma unroll
+            for (int cc = 0; cc < LBC; cc++) {
+                if (cc * 64 < nb0) {
+                    const int b = cc * 64 + lane;
+                    const int c = b < nb0 ? (int)lbc_[cc] : 0;
+                    const int scv = (int)lbs_[cc];
+                    const int incl = wave_incl_scan(c) + carry;
+                    if (b < nb0 && c > 0) s.scr[incl - c] = 1 | (scv << 1);
+                    nempty += __popcll(wave_ballot(b < nb0 && c == 0));
+                    carry = wave_last(incl);
+                }
             }
         }
         wave_sync();
-        // the register state, one field at a time
-        const int i0 = lane * K;
+        // ---- 3. the register state (padding past n: dead, length 0, client 255)
         bsm = lvm = sc0 = sc1 = 0u;
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            seq[j] = 0x7fffffff;
-            rseq[j] = 0;
-            li[j] = kEmptyLi;
-            cf[j] = kEmptyCf;
-            ov[j] = 0;
-            if constexpr (W) oh[j] = 0;
+            const bool in = i0 + j < n;
+            const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
+            seq[j] = in ? (int32_t)vsq[j] : 0x7fffffff;
+            rseq[j] = in ? (int32_t)vrs[j] : 0;
+            li[j] = in ? (vln[j] | ((uint32_t)(i0 + j) << kLenBits)) : kEmptyLi;
+            ov[j] = in ? ((ow[2 * j] >> 1) | (ow[2 * j + 1] << 31)) : 0u;
+            if constexpr (W) oh[j] = in ? (ow[2 * j + 1] >> 1) : 0u;
+            cf[j] = in ? (byte_at(bcw, j) | (byte_at(brw, j) << 8) | ((byte_at(bfw, j) & 0x1Fu) << 16)) : kEmptyCf;
             cum[j] = 0;
-        }
-        if (i0 < n) {
-            // rows are read whole (segcap >= CAP keeps them inside the document); only li and
-            // cf need the padding values past n: padding is dead and has length 0
-            {
-                const VU v = ld_u32(reinterpret_cast<const uint32_t*>(g.seq + so + i0));
-#pragma unroll
-                for (int j = 0; j < K; j++) seq[j] = (int32_t)v[j];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                const VU v = ld_u32(reinterpret_cast<const uint32_t*>(g.rseq + so + i0));
-#pragma unroll
-                for (int j = 0; j < K; j++) rseq[j] = (int32_t)v[j];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                const VU v = ld_u32(g.len + so + i0);
-#pragma unroll
-                for (int j = 0; j < K; j++) li[j] = i0 + j < n ? (v[j] | ((uint32_t)(i0 + j) << kLenBits)) : kEmptyLi;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (K % 2 == 1) {
-#pragma unroll
-                for (int j = 0; j < K; j++) {
-                    ov[j] = (uint32_t)(g.ovl[so + i0 + j] >> 1);
-                    if constexpr (W) oh[j] = (uint32_t)(g.ovl[so + i0 + j] >> 33);
-                }
-            } else {
-                const uint32_t* op = reinterpret_cast<const uint32_t*>(g.ovl + so + i0);
-#pragma unroll
-                for (int c = 0; c < K / 2; c++) {
-                    const U4 x = reinterpret_cast<const U4*>(op)[c];  // two u64: (lo, hi), (lo, hi)
-                    ov[2 * c] = (x[0] >> 1) | (x[1] << 31);
-                    ov[2 * c + 1] = (x[2] >> 1) | (x[3] << 31);
-                    if constexpr (W) {
-                        oh[2 * c] = x[1] >> 1;
-                        oh[2 * c + 1] = x[3] >> 1;
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                const VU bc = ld_u8(g.client + so + i0);
-                const VU br = ld_u8(g.rclient + so + i0);
-                const VU bf = ld_u8(g.flags + so + i0);
-#pragma unroll
-                for (int j = 0; j < K; j++) {
-                    const int mk = s.scr[i0 + j];  // scr[i] for i >= n is harmless (selected away)
-                    const bool in = i0 + j < n;
-                    cf[j] = in ? (bc[j] | (br[j] << 8) | ((bf[j] & 0x1Fu) << 16)) : kEmptyCf;
-                    const uint32_t bit = in ? (1u << j) : 0u;
-                    lvm |= bit;
-                    bsm |= (mk & 1) ? bit : 0u;
-                    sc0 |= (mk & 2) ? bit : 0u;
-                    sc1 |= (mk & 4) ? bit : 0u;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t bit = in ? (1u << j) : 0u;
+            lvm |= bit;
+            bsm |= (mk & 1) ? bit : 0u;
+            sc0 |= (mk & 2) ? bit : 0u;
+            sc1 |= (mk & 4) ? bit : 0u;
         }
         // empty leaf blocks (rare): a dead slot holds each one's place and marks
         if (nempty) {
@@ -1406,8 +1494,8 @@ struct RWave {
                 int carry = 0, placed = 0;
                 for (int base = 0; base < nb0; base += 64) {
                     const int b = base + lane;
-                    const int c = b < nb0 ? (int)g.lbcnt[lo + b] : 0;
-                    const int scv = b < nb0 ? (int)g.lbscour[lo + b] : 0;
+                    const int c = b < nb0 ? (int)gp(g.lbcnt)[lo + b] : 0;
+                    const int scv = b < nb0 ? (int)gp(g.lbscour)[lo + b] : 0;
                     const int incl = wave_incl_scan(c) + carry;
                     uint64_t em = wave_ballot(b < nb0 && c == 0);
                     while (em) {
@@ -1435,16 +1523,26 @@ struct RWave {
     // coalesced HBM stores; no per-slot 64-bit addresses kept live)
     template <class T, class F>
     MT_DEV void store_field(const T& v, uint32_t lb, int pbase, int nn, F&& put) {
+        // (a dead slot goes to the lane's dummy word in `tln`, dead at store time: no per-slot branch)
+        int32_t* const dum = reinterpret_cast<int32_t*>(s.tln) + lane;
 #pragma unroll
         for (int j = 0; j < K; j++)
-            if ((lb >> j) & 1u) s.scr[pbase + __popc(lb & ((1u << j) - 1u))] = (int32_t)v[j];
+            *(((lb >> j) & 1u) ? &s.scr[pbase + __popc(lb & ((1u << j) - 1u))] : dum) = (int32_t)v[j];
         wave_sync();
+        // four rows per LDS round trip (scr holds CAP + 1 entries: the reads past nn are clamped)
 #pragma clang loop unroll(disable) vectorize(disable)
-        for (int i = lane; i < nn; i += 64) put(i, (uint32_t)s.scr[i]);
+        for (int base = 0; base < nn; base += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) v[q] = (uint32_t)s.scr[min(base + 64 * q + lane, CAP)];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (base + 64 * q + lane < nn) put(base + 64 * q + lane, v[q]);
+        }
         wave_sync();
     }
 
-    MT_DEV void store(const mt_gstate& g, uint32_t d) {
+    MT_DEV void store(KGState& g, uint32_t d) {
         const size_t so = (size_t)d * g.segcap;
         // live slots -> positions (dead slots are squeezed out here)
         const uint32_t lb = live_bits();
@@ -1458,30 +1556,37 @@ struct RWave {
             for (int j = 0; j < K; j++) q |= ((cf[j] & F_NLQ) && ((lb >> j) & 1u)) ? (1u << j) : 0u;
             if (__ballot(q != 0)) {
                 arena_sync();
+                // every slot's offset, then every slot's byte: one LDS and one memory round trip
+                uint32_t at[K];
 #pragma unroll
                 for (int j = 0; j < K; j++) {
-                    if ((q >> j) & 1u) {
-                        const uint8_t ch = arena()[(uint32_t)s.toff[id_of(li[j])] + len_of(li[j]) - 1];
-                        cf[j] = (cf[j] & ~(F_NL | F_NLQ)) | (ch == '\n' ? F_NL : 0u);
-                    }
+                    const bool on = (q >> j) & 1u;
+                    const uint32_t to = s.toff[on ? id_of(li[j]) : 0u];
+                    at[j] = on ? to + len_of(li[j]) - 1 : 0u;
                 }
+                uint32_t ch[K];
+#pragma unroll
+                for (int j = 0; j < K; j++) ch[j] = arena()[at[j]];
+#pragma unroll
+                for (int j = 0; j < K; j++)
+                    if ((q >> j) & 1u) cf[j] = (cf[j] & ~(F_NL | F_NLQ)) | (ch[j] == '\n' ? F_NL : 0u);
             }
         }
-        store_field(seq, lb, pbase, nn, [&](int i, uint32_t v) { g.seq[so + i] = (int32_t)v; });
-        store_field(rseq, lb, pbase, nn, [&](int i, uint32_t v) { g.rseq[so + i] = (int32_t)v; });
-        store_field(ov, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] = (uint64_t)v << 1; });
+        store_field(seq, lb, pbase, nn, [&](int i, uint32_t v) { gp(g.seq)[so + i] = (int32_t)v; });
+        store_field(rseq, lb, pbase, nn, [&](int i, uint32_t v) { gp(g.rseq)[so + i] = (int32_t)v; });
+        store_field(ov, lb, pbase, nn, [&](int i, uint32_t v) { gp(g.ovl)[so + i] = (uint64_t)v << 1; });
         if constexpr (W)  // (after the low half: the same rows, read back and completed)
-            store_field(oh, lb, pbase, nn, [&](int i, uint32_t v) { g.ovl[so + i] |= (uint64_t)v << 33; });
+            store_field(oh, lb, pbase, nn, [&](int i, uint32_t v) { gp(g.ovl)[so + i] |= (uint64_t)v << 33; });
         store_field(cf, lb, pbase, nn, [&](int i, uint32_t v) {
-            g.client[so + i] = (uint8_t)(v & 0xFFu);
-            g.rclient[so + i] = (uint8_t)((v >> 8) & 0xFFu);
-            g.flags[so + i] = (uint8_t)((v >> 16) & 0x1Fu);
+            gp(g.client)[so + i] = (uint8_t)(v & 0xFFu);
+            gp(g.rclient)[so + i] = (uint8_t)((v >> 8) & 0xFFu);
+            gp(g.flags)[so + i] = (uint8_t)((v >> 16) & 0x1Fu);
         });
         store_field(li, lb, pbase, nn, [&](int i, uint32_t v) {
             const uint32_t id = id_of(v);
-            g.len[so + i] = len_of(v);
-            g.toff[so + i] = s.toff[id];
-            g.props[so + i] = s.props[id];
+            gp(g.len)[so + i] = len_of(v);
+            gp(g.toff)[so + i] = s.toff[id];
+            gp(g.props)[so + i] = s.props[id];
         });
         // leaf blocks: live children and needsScour, in block order
         const uint32_t bm = bs_bits();
@@ -1502,8 +1607,8 @@ struct RWave {
 #pragma clang loop unroll(disable) vectorize(disable)
         for (int b = lane; b < nb0; b += 64) {
             const int cnt = s.scr[b + 1] - s.scr[b];
-            g.lbcnt[lo + b] = (uint8_t)cnt;
-            g.lbscour[lo + b] = s.lbsc[b];
+            gp(g.lbcnt)[lo + b] = (uint8_t)cnt;
+            gp(g.lbscour)[lo + b] = s.lbsc[b];
             nempty += cnt == 0 ? 1 : 0;
         }
         nempty = wave_total(nempty);
@@ -1519,19 +1624,19 @@ struct RWave {
             const size_t io = ((size_t)d * (MT_MAXLEV - 1) + (Lv - 1)) * g.ibcap;
             const int nbl_ = min(nbl(Lv), (int)g.ibcap);
 #pragma clang loop unroll(disable) vectorize(disable)
-            for (int i = lane; i < nbl_; i += 64) g.ibcnt[io + i] = s.ibcnt[Lv - 1][i];
+            for (int i = lane; i < nbl_; i += 64) gp(g.ibcnt)[io + i] = s.ibcnt[Lv - 1][i];
         }
         if (heap_n >= (int)g.hcap) fail(MT_DERR_CAPACITY, cur_seq);
         const size_t ho = (size_t)d * g.hcap;
         const int hn = min(heap_n, (int)g.hcap - 1);
 #pragma clang loop unroll(disable) vectorize(disable)
         for (int i = 1 + lane; i <= hn; i += 64) {
-            g.hseq[ho + i] = s.hseq[i];
+            gp(g.hseq)[ho + i] = s.hseq[i];
             const uint16_t id = s.hslot[i];
-            g.hslot[ho + i] = id == kDead ? kDead : s.toff[id];
+            gp(g.hslot)[ho + i] = id == kDead ? kDead : s.toff[id];
         }
         if (lane == 0) {
-            mt_doc_scalars& sc = g.sc[d];
+            MT_GLOB mt_doc_scalars& sc = gp(g.sc)[d];
             sc.nseg = nn;
             sc.nlev = nlev;
             sc.heap_n = heap_n;
@@ -1544,20 +1649,22 @@ struct RWave {
             sc.n_empty = (uint32_t)nempty;
             sc.nb[0] = nb0;
         }
-        if (lane >= 1 && lane < MT_MAXLEV) g.sc[d].nb[lane] = s.nb[lane];
+        if (lane >= 1 && lane < MT_MAXLEV) gp(g.sc)[d].nb[lane] = s.nb[lane];
     }
 };
 
-// Two waves per SIMD for the big classes: the state is register-resident, so occupancy is what
-// hides the latency of each op's dependent steps (a few spills at K = 16 are cheaper than one
-// wave per SIMD).
 // Op records in blocks of 8 (256 B: lane l holds dword l % 8 of record base + l / 8), double-
-// buffered: a record's fields are readlanes of a register loaded 7..15 ops earlier, so the op loop
-// never waits on the memory latency of the record it is about to apply (scalar loads would: the
-// LDS waits of the apply share their lgkm counter).
+// buffered: a record's fields are readlanes of a register loaded 1..15 ops earlier.  Both loads are
+// unconditional (the record index and the payload byte are clamped into the batch), so no exec-masked
+// branch hides their position from the compiler's vmcnt bookkeeping.
 MT_DEV uint32_t load_op_block(const mt_op_rec* ops, uint32_t base, uint32_t end, int lane) {
-    const uint32_t r = base + (uint32_t)(lane >> 3);
-    return r < end ? reinterpret_cast<const uint32_t*>(ops + r)[lane & 7] : 0u;
+    const uint32_t r = min(base + (uint32_t)(lane >> 3), end - 1u);  // (end > base's first record)
+    return reinterpret_cast<const uint32_t*>(ops + r)[lane & 7];
+}
+// lane i <- payload byte i of a record (i < 64; lanes past the payload hold a copy of its last byte,
+// never read); the payload buffer holds at least one byte
+MT_DEV uint32_t load_payload(const uint8_t* payload, uint32_t poff, uint32_t plen, int lane) {
+    return payload[plen ? poff + min((uint32_t)lane, plen - 1u) : 0u];
 }
 MT_DEV mt_op_rec op_from_block(uint32_t blk, uint32_t j) {
     const int l = (int)(j * 8);
@@ -1580,8 +1687,8 @@ MT_DEV mt_op_rec op_from_block(uint32_t blk, uint32_t j) {
 // through a pointer to the kernel's own argument block that the compiler cannot see through, so
 // the ~40 SGPRs of pointers are not held live across the op loop (where they were spilled into
 // VGPR lanes and reloaded in the hot phases).  g is the kernel's first argument: offset 0.
-MT_DEV const mt_gstate& kernarg_gstate() {
-    const mt_gstate* p = (const mt_gstate*)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+MT_DEV KGState& kernarg_gstate() {
+    KGState* p = (KGState*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
     return *p;
 }
@@ -1616,38 +1723,48 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
     PROF_BEGIN(tl, P_LOAD);
     wv.load(kernarg_gstate(), d);
     PROF_END(wv.prof, P_LOAD, tl);
-    // software pipeline: the records of the next 7..15 ops and the payload of op i+1 are in flight
-    // while op i is applied
+    // software pipeline: op i's payload was loaded at the end of op i-1's apply and op i+1's is
+    // issued at the end of op i's, so every wait for a prefetch finds it a whole op old (a prefetch
+    // issued at the top of the loop was waited for at once: the copy into the current-op register,
+    // and any arena read of the op, drain vmcnt to 0)
     uint32_t blk0 = load_op_block(ops, a, b, wv.lane);
     uint32_t blk1 = load_op_block(ops, a + 8, b, wv.lane);
-    uint32_t pb0;
-    {
-        const uint32_t poff = (uint32_t)__builtin_amdgcn_readlane((int)blk0, 6);
-        const uint32_t plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, 7);
-        pb0 = wv.lane < (int)plen ? payload[poff + wv.lane] : 0u;
-    }
+    uint32_t pb = load_payload(payload, (uint32_t)__builtin_amdgcn_readlane((int)blk0, 6),
+                               (uint32_t)__builtin_amdgcn_readlane((int)blk0, 7), wv.lane);
+    uint32_t pbn = 0;
+    if (a + 1 < b)
+        pbn = load_payload(payload, (uint32_t)__builtin_amdgcn_readlane((int)blk0, 14),
+                           (uint32_t)__builtin_amdgcn_readlane((int)blk0, 15), wv.lane);
     for (uint32_t i = a; i < b; i++) {
         if (wv.err) break;
         // op i's fields are taken from its block here (not carried over from the previous
         // iteration: ten fewer scalars live across the apply)
         const mt_op_rec op = op_from_block(blk0, (i - a) & 7u);
-        wv.pb = pb0;
-        const uint32_t j = (i + 1 - a) & 7u;  // op i+1's record in its block
-        if (j == 0) {
-            blk0 = blk1;
-            blk1 = load_op_block(ops, i + 9, b, wv.lane);
-        }
-        if (i + 1 < b) {  // payload prefetch of op i+1
-            const uint32_t poff = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j * 8 + 6));
-            const uint32_t plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j * 8 + 7));
-            pb0 = wv.lane < (int)plen ? payload[poff + wv.lane] : 0u;
-        }
+        wv.pb = pb;
         PROF_BEGIN(top, P_OP);
         wv.apply(op, payload);
         PROF_END(wv.prof, P_OP, top);
 #ifdef MT_PROF
         wv.prof[P_OPS]++;
 #endif
+        pb = pbn;
+        const uint32_t jn = (i + 1 - a) & 7u;  // op i+1's record in its block
+        if (jn == 0) {
+            blk0 = blk1;
+            blk1 = load_op_block(ops, i + 9, b, wv.lane);
+        }
+        if (i + 2 < b) {  // op i+2's payload: in blk1 when it starts the next block
+            const uint32_t j2 = (i + 2 - a) & 7u;
+            uint32_t poff, plen;
+            if (j2 == 0) {
+                poff = (uint32_t)__builtin_amdgcn_readlane((int)blk1, 6);
+                plen = (uint32_t)__builtin_amdgcn_readlane((int)blk1, 7);
+            } else {
+                poff = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j2 * 8 + 6));
+                plen = (uint32_t)__builtin_amdgcn_readlane((int)blk0, (int)(j2 * 8 + 7));
+            }
+            pbn = load_payload(payload, poff, plen, wv.lane);
+        }
     }
     PROF_BEGIN(tt, P_STORE);
     wv.store(kernarg_gstate(), d);

@@ -121,9 +121,12 @@ mt_status mt_comm_barrier(mt_comm* c) {
     return MT_OK;
 }
 
-// A rank that cannot take part (no device memory for its row) aborts the communicator, so the
-// other ranks' ncclGather returns an error instead of blocking forever; a rank whose checksums
-// fail still takes part with a poisoned row (count = ~0), which rank 0 reports as MT_ERR_COMM.
+// Every rank enters the gather: a rank whose own part fails after the argument checks (engine
+// query, more documents than the agreed bound, the checksum kernel) takes part with a poisoned row
+// (count = ~0), which rank 0 reports as MT_ERR_COMM -- so no peer is left blocked in ncclGather.
+// Only a rank that cannot take part at all (no device, no memory for its row) aborts the
+// communicator; that is best effort: RCCL gives intra-node peers no failure detection, so an
+// in-flight collective on another rank may still wait.
 static mt_status comm_abort(mt_comm* c, mt_status st) {
     fprintf(stderr, "libmtgpu: rank %d cannot join the checksum gather: aborting the communicator\n", c->rank);
     if (c->nc) (void)ncclCommAbort(c->nc);
@@ -135,11 +138,18 @@ mt_status mt_comm_gather_checksums(mt_comm* c, mt_engine* eng, uint32_t max_docs
                                    uint32_t* counts) {
     if (!c || !eng || !c->nc) return MT_ERR_ARG;
     if (c->rank == 0 && (!out || !counts)) return MT_ERR_ARG;
+    mt_status fail = MT_OK;  // this rank's own failure: its row goes out poisoned
     uint32_t n_docs = 0;
-    mt_status st = mt_engine_info(eng, &n_docs, nullptr);
-    if (st) return st;
-    if (n_docs > max_docs_per_rank) return MT_ERR_ARG;  // (every rank is given the same bound)
-    CM_HIP(hipSetDevice(c->device));
+    if (mt_engine_info(eng, &n_docs, nullptr) != MT_OK) {
+        fail = MT_ERR_ARG;
+        n_docs = 0;
+    } else if (n_docs > max_docs_per_rank) {  // (the bound must be agreed; a rank past it still joins)
+        fprintf(stderr, "libmtgpu: rank %d holds %u documents, past the gather's bound %u\n", c->rank, n_docs,
+                max_docs_per_rank);
+        fail = MT_ERR_ARG;
+        n_docs = 0;
+    }
+    if (hipSetDevice(c->device) != hipSuccess) return comm_abort(c, MT_ERR_HIP);
     // [0] = this rank's document count, [1 .. max] = its checksums (zero padded): one gather
     const size_t row = (size_t)max_docs_per_rank + 1;
     uint64_t *d_send = nullptr, *d_recv = nullptr;
@@ -152,7 +162,8 @@ mt_status mt_comm_gather_checksums(mt_comm* c, mt_engine* eng, uint32_t max_docs
     bool ok = hipMemsetAsync(d_send, 0, row * sizeof(uint64_t), c->stream) == hipSuccess &&
               hipStreamSynchronize(c->stream) == hipSuccess;
     if (ok && n_docs) ok = mt_checksums_device(eng, d_send + 1, n_docs) == MT_OK;
-    const bool local_ok = ok;
+    if (!ok && !fail) fail = MT_ERR_HIP;
+    const bool local_ok = !fail;
     if (!local_ok) cnt = ~0ull;  // poisoned row: this rank's checksums are not valid
     ok = hipMemcpyAsync(d_send, &cnt, sizeof cnt, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
          hipStreamSynchronize(c->stream) == hipSuccess;
@@ -180,7 +191,7 @@ mt_status mt_comm_gather_checksums(mt_comm* c, mt_engine* eng, uint32_t max_docs
         fprintf(stderr, "libmtgpu: ncclGather failed: %s\n", ncclGetErrorString(r));
         return MT_ERR_COMM;
     }
-    if (!local_ok) return MT_ERR_HIP;
+    if (!local_ok) return fail;
     if (poisoned) {
         fprintf(stderr, "libmtgpu: a rank's checksums failed: the gather is incomplete\n");
         return MT_ERR_COMM;

@@ -28,7 +28,7 @@ import json
 import numpy as np
 
 from .engine import _check, _ptr, lib
-from .oplog import F_MARKER, F_PROPS, NPAIRS_SHIFT, OP_DTYPE, OP_WIDE, OpBatch, encode_text
+from .oplog import F_MARKER, F_PROPS, OP_DTYPE, OP_WIDE, OpBatch, encode_text, pack_npairs
 
 MT_OP_LOAD = 4
 NONCOLLAB = 0xFE            # MT_CLIENT_NONCOLLAB: NonCollabClient (constants.ts:15)
@@ -215,16 +215,17 @@ def build_load(docs, interners=None):
                 batch_pos = None
             local += 0 if rseq >= 0 else n
             pairs = b''
-            flags = 0
+            flags = tbits = 0
             if pdef:
                 for k in sorted(pv):
                     pairs += bytes([k, pv[k] & 0xFF, pv[k] >> 8]) if wide else bytes([k, pv[k]])
-                flags = F_PROPS | (len(pv) << NPAIRS_SHIFT)
+                fbits, tbits = pack_npairs(len(pv), wide)
+                flags = F_PROPS | fbits
             if mk:
                 flags |= F_MARKER
             data = tb + pairs
             recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8),
-                         MT_OP_LOAD | (OP_WIDE if wide else 0), flags, pos, rseq, len(payload), len(data)))
+                         MT_OP_LOAD | (OP_WIDE if wide else 0) | tbits, flags, pos, rseq, len(payload), len(data)))
             payload += data
         body_rp.append(len(recs))
     segs_a = np.array(segs, dtype=LOAD_SEG_DTYPE) if segs else np.zeros(0, dtype=LOAD_SEG_DTYPE)

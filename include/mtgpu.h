@@ -47,8 +47,11 @@ enum mt_op_flags {
                                   Simple/Tile/NestBegin/NestEnd/RangeBegin/RangeEnd/Slide/Stay); the
                                   segment has length 1 and never appends (Marker.canAppend) */
 };
-#define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload */
-#define MT_OP_NPAIRS(flags) (((flags) >> MT_F_NPAIRS_SHIFT) & 0xF)
+#define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload, mod 16 */
+/* A record may carry 16 pairs (one per wide key, MT_MAX_KEYS_WIDE): the count's bit 4 is type bit 6
+ * (MT_OP_NP16), set only on wide records.  MT_OP_NPAIRS takes the record. */
+#define MT_OP_NP16 0x40u
+#define MT_OP_NPAIRS(o) ((((o).flags >> MT_F_NPAIRS_SHIFT) & 0xF) | (((o).type & MT_OP_NP16) ? 16 : 0))
 /* Wide payload (type bit 7): the op's text is UTF-16 code units (2 bytes each, little endian:
  * cachedLength = text.length, textSegment.ts:45 -- any string, surrogate halves included) and each
  * property pair is 3 bytes (key u8 < MT_MAX_KEYS_WIDE, value id u16 LE).  The host sets it on every
@@ -56,9 +59,9 @@ enum mt_op_flags {
  * A document that receives a wide op, or a client id >= MT_MAX_CLIENTS, becomes a WIDE document for
  * good (see "limits" below); narrow-form ops apply to wide documents unchanged. */
 #define MT_OP_WIDE 0x80u
-#define MT_OP_TYPE(o) ((o).type & 0x7Fu)
+#define MT_OP_TYPE(o) ((o).type & 0x3Fu)
 #define MT_OP_PAIR_BYTES(o) (((o).type & MT_OP_WIDE) ? 3u : 2u)
-#define MT_OP_PAIRS_LEN(o) (MT_OP_PAIR_BYTES(o) * MT_OP_NPAIRS((o).flags))
+#define MT_OP_PAIRS_LEN(o) (MT_OP_PAIR_BYTES(o) * MT_OP_NPAIRS(o))
 /* An insert whose segment spec is the empty string is dropped by Client.applyInsertOp before it
  * touches the tree (`if (op.seg)`, client.ts:403-407: no boundary split, no completeAndLogOp
  * asserts, no callback); only updateSeqNumbers runs.  Such a record (text insert, no props, no
@@ -478,7 +481,10 @@ mt_status mt_comm_create(int32_t device, int32_t rank, int32_t n_ranks, const ui
 mt_status mt_comm_destroy(mt_comm* comm);
 /* Gather every rank's per-document checksums (mt_checksums of `eng`) to rank 0: ncclGather from
  * HBM.  Rank 0: out[r * max_docs_per_rank + i] = rank r's document i, counts[r] = rank r's
- * n_docs (other ranks may pass NULL). */
+ * n_docs (other ranks may pass NULL).  Every rank that passes the argument checks enters the
+ * gather: one whose own part fails (more documents than max_docs_per_rank, the checksum kernel)
+ * sends a poisoned row and returns its error, and rank 0 returns MT_ERR_COMM; a rank that cannot
+ * allocate its row aborts the communicator (best effort). */
 mt_status mt_comm_gather_checksums(mt_comm* comm, mt_engine* eng, uint32_t max_docs_per_rank, uint64_t* out,
                                    uint32_t* counts);
 /* max over ranks (the job's clock), and a barrier (all-reduce + device synchronize) */

@@ -25,6 +25,7 @@ const native = require(path.join(__dirname, "mtgpu.node"));
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
 const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const OP_WIDE = 0x80;  // MT_OP_WIDE: UTF-16 text, (key u8, value u16) pairs
+const OP_NP16 = 0x40;  // MT_OP_NP16: property pair count bit 4 (wide records)
 // include/mtgpu.h "limits": the wide form's (a document goes wide with its first op beyond the narrow
 // ones: client id >= 64, key >= 8, value id >= 256 or a code unit above U+00FF)
 const MAX_CLIENTS = 254, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
@@ -96,8 +97,11 @@ class BatchEngine {
             for (const r of c.queue) {
                 const o = i * REC;
                 ops.writeInt32LE(r.seq, o); ops.writeInt32LE(r.ref, o + 4); ops.writeInt32LE(r.msn, o + 8);
-                ops.writeUInt16LE(r.client, o + 12); ops.writeUInt8(r.type, o + 14);
-                ops.writeUInt8(r.flags | (r.npairs << 3), o + 15);
+                ops.writeUInt16LE(r.client, o + 12);
+                // 16 pairs (wide only): the count's bit 4 is type bit 6 (include/mtgpu.h MT_OP_NP16)
+                if (r.npairs > 16) throw new Error("BatchClient: more than 16 property pairs in one op");
+                ops.writeUInt8(r.type | ((r.npairs & 16) ? OP_NP16 : 0), o + 14);
+                ops.writeUInt8(r.flags | ((r.npairs & 15) << 3), o + 15);
                 ops.writeInt32LE(r.pos1, o + 16); ops.writeInt32LE(r.pos2, o + 20);
                 ops.writeUInt32LE(off, o + 24); ops.writeUInt32LE(r.payload.length, o + 28);
                 r.payload.copy(payload, off);

@@ -17,7 +17,7 @@
 // specToSegment (snapshotLoader.ts:85-117): without merge info a segment is (seq 0, NonCollabClient).
 const native = require("./mtgpu.node");
 
-const MT_OP_LOAD = 4, F_PROPS = 2, F_MARKER = 128, OP_WIDE = 0x80;
+const MT_OP_LOAD = 4, F_PROPS = 2, F_MARKER = 128, OP_WIDE = 0x80;  // (npairs: BatchClient's encoder)
 const NONCOLLAB = 0xfe, UNIVERSAL_SEQ = 0, SF_PDEF = 2, SF_MARKER = 16, LSF_U16 = 64, LOAD_SEG = 64;
 
 function blobs(tree) {

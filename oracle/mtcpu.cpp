@@ -113,7 +113,7 @@ struct Pay {
 int keyLimit(const mt_op_rec& op) { return (op.type & MT_OP_WIDE) ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS; }
 Pay decodePay(const mt_op_rec& op, const uint8_t* payload) {
     Pay p;
-    p.np = MT_OP_NPAIRS(op.flags);
+    p.np = MT_OP_NPAIRS(op);
     const uint32_t pl = MT_OP_PAIRS_LEN(op);
     if (op.payload_len < pl) return p;
     const uint8_t* b = payload + op.payload_off;

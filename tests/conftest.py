@@ -20,6 +20,26 @@ GOLDEN_SETS = ['scenarios', 'markers', 'synth_c1', 'synth_c2', 'synth_c3', 'synt
 WIDE_SETS = ['wide', 'wide_synth']
 
 
+# reference pins at the benchmark configs' full shape (tests/golden/make_fullshape.py): the logs are
+# regenerated from the recorded config and seed, their bytes checked against the recorded SHA-256
+FULLSHAPE_SETS = ['full_c3', 'full_c4', 'fuzz_1k']
+
+
+def load_fullshape(name):
+    """(batch, fixture) of a full-shape set: the regenerated log, proven to be the bytes the
+    reference replayed, and the reference's per-document results."""
+    import json
+    from oracle import oracle
+    sys.path.insert(0, GOLDEN)
+    from make_fullshape import log_sha256
+    with open(os.path.join(GOLDEN, name + '.json')) as f:
+        fx = json.load(f)
+    oracle.build()
+    batch = oracle.generate(fx['n_docs'], seed=fx['seed'], **fx['cfg'])
+    assert log_sha256(batch) == fx['log_sha256'], f'{name}: the generator no longer produces the pinned log'
+    return batch, fx
+
+
 def load_golden(name):
     import json
     from fluidframework_amd.oplog import OpBatch

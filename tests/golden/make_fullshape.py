@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Reference pins at the benchmark configs' FULL shape (VERDICT r3 "What's missing" #4): the
+transpiled reference merge-tree (oracle/_tsref, built from /root/reference by
+oracle/tsref/build_ref.py) replays every document of
+
+  full_c3   256 documents x 1024 ops x 32 clients: annotates (8 keys x 16 values, nulls, rewrites),
+            props on inserts, half the removes aimed at a concurrent remove (BASELINE configs[2])
+  full_c4   256 documents x 1024 ops x 8 clients: refSeq lag up to 256, one client stalling for
+            200-op stretches (BASELINE configs[3]: heavy zamboni when the msn jumps)
+  fuzz_1k   1,000 documents x 1024 ops, a fixed-seed high-conflict mix: 24 clients, lag up to 96,
+            70 % of removes overlapping, 20 % null annotates, 5 % rewrites, props on 30 % of
+            inserts, 4 % markers (client.conflictFarm.spec.ts:238-278 in spirit: many clients,
+            wide windows, every op kind)
+
+through one observer `Client` per document (oracle/tsref/replay_ref.js `state`), and records, per
+document, the checksum of the reference's canonical state (the checksum is our pure
+function of the reference's output), its error, its length and segment count, plus the full
+canonical state of the first documents.  The op logs themselves are not committed: they are the
+deterministic output of the synthetic generator (oracle.generate == the device generator, byte for
+byte) at the recorded config and seed, and the fixture holds the SHA-256 of the exact bytes the
+reference replayed, so a test that regenerates them proves it feeds the same log.
+
+    python tests/golden/make_fullshape.py            # writes tests/golden/full_*.json
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from fluidframework_amd.oplog import CONFIGS  # noqa: E402
+from oracle import canon, oracle  # noqa: E402
+
+FUZZ = dict(n_clients=24, ops_per_doc=1024, max_lag=96, n_keys=8, n_values=12, p_insert=0.45, p_remove=0.33,
+            p_overlap=0.7, p_null=0.2, p_rewrite=0.05, p_insert_props=0.3, p_marker=0.04)
+
+
+def sets():
+    c3 = dict(CONFIGS['C3'])
+    c3.pop('n_docs')
+    c4 = dict(CONFIGS['C4'])
+    c4.pop('n_docs')
+    return {
+        'full_c3': dict(n_docs=256, seed=20261017, cfg=c3),
+        'full_c4': dict(n_docs=256, seed=20261017, cfg=c4),
+        'fuzz_1k': dict(n_docs=1000, seed=4417, cfg=FUZZ),
+    }
+
+
+def log_sha256(batch):
+    h = hashlib.sha256()
+    for a in (batch.ops, batch.payload, batch.row_ptr):
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def generate(spec):
+    return oracle.generate(spec['n_docs'], seed=spec['seed'], **spec['cfg'])
+
+
+def replay(path, n_docs, jobs=8):
+    """The reference's per-document result lines for docs [0, n_docs), jobs node processes."""
+    replay_js = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
+    step = (n_docs + jobs - 1) // jobs
+
+    def run(d0):
+        res = subprocess.run(['node', '--max-old-space-size=4096', replay_js, 'state', path, str(d0),
+                              str(min(n_docs, d0 + step))], check=True, capture_output=True, text=True)
+        return [json.loads(x) for x in res.stdout.strip().split('\n') if x.strip()]
+
+    out = []
+    with ThreadPoolExecutor(jobs) as ex:
+        for part in ex.map(run, range(0, n_docs, step)):
+            out += part
+    assert [r['doc'] for r in out] == list(range(n_docs))
+    return out
+
+
+def main():
+    subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
+    oracle.build()
+    only = [a.split('=', 1)[1] for a in sys.argv if a.startswith('--only=')]
+    for name, spec in sets().items():
+        if only and name not in only[0].split(','):
+            continue
+        batch = generate(spec)
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, name + '.mtlog')
+            batch.save(path)
+            rows = replay(path, spec['n_docs'])
+        fx = dict(name=name, n_docs=spec['n_docs'], seed=spec['seed'], cfg=spec['cfg'], n_ops=int(batch.n_ops),
+                  log_sha256=log_sha256(batch),
+                  checksum=['%016x' % canon.checksum(r['state']) for r in rows],
+                  err=[r['err'] for r in rows],
+                  length=[len(r['text']) for r in rows],
+                  nsegs=[len(r['state']['segs']) for r in rows],
+                  states={str(r['doc']): r['state'] for r in rows[:3]})
+        with open(os.path.join(HERE, name + '.json'), 'w') as f:
+            json.dump(fx, f, separators=(',', ':'))
+        print(name, spec['n_docs'], 'docs', batch.n_ops, 'ops, max segments', max(fx['nsegs']),
+              'errors', sum(1 for e in fx['err'] if e), os.path.getsize(os.path.join(HERE, name + '.json')), 'B')
+
+
+if __name__ == '__main__':
+    main()

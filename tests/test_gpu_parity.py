@@ -4,7 +4,7 @@ synthetic logs.  Run on the GPU box:  python -m pytest tests -m gpu"""
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_SETS, WIDE_SETS, load_golden
+from conftest import FULLSHAPE_SETS, GOLDEN_SETS, WIDE_SETS, load_fullshape, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -36,6 +36,25 @@ def test_golden_bit_exact(name, b):
         assert st == r['state'], f'{name} doc {d} b={b}: {_diff(st, r["state"])}'
         assert eng.text(d) == r['text']
         assert '%016x' % cs[d] == r['checksum']
+
+
+@pytest.mark.parametrize('b', [0, 32, 5])
+@pytest.mark.parametrize('name', FULLSHAPE_SETS)
+def test_fullshape_bit_exact(name, b):
+    """The engine against the reference itself at the benchmark configs' full shape (C3, C4: 256
+    documents x 1024 ops) and on a fixed-seed 1,000-document x 1024-op high-conflict fuzz
+    (tests/golden/make_fullshape.py): every document's checksum of the reference's canonical state,
+    and the first documents' states whole, at launch sizes 0 (one launch), 32 and 5."""
+    from fluidframework_amd.engine import MergeEngine
+    batch, fx = load_fullshape(name)
+    eng = MergeEngine(batch.n_docs, ops_per_launch=b)
+    eng.apply(batch)
+    got = ['%016x' % c for c in eng.checksums()]
+    bad = [d for d in range(batch.n_docs) if got[d] != fx['checksum'][d]]
+    assert not bad, f'{name} b={b}: {len(bad)} documents differ, first {bad[:5]}: {eng.error(bad[0])}'
+    for d, st in fx['states'].items():
+        assert eng.state(int(d)) == st, f'{name} doc {d} b={b}: {_diff(eng.state(int(d)), st)}'
+    assert all(eng.error(d) == (0, 0) for d in range(0, batch.n_docs, 7))
 
 
 @pytest.mark.parametrize('cfg_name', ['C2', 'C3', 'C4'])

@@ -50,3 +50,28 @@ def test_bench_with_a_one_rank_rccl_communicator():
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().split('\n')[-1])
     assert line['config']['comm'] == 'RcclComm' and line['n_gpus'] == 1 and line['value'] > 0
+
+
+def test_rank_past_the_gather_bound_still_joins_and_reports():
+    """A rank holding more documents than the agreed bound sends a poisoned row instead of skipping
+    the collective (a skipped ncclGather leaves the peers blocked): the call returns the
+    rank's error, and the communicator stays usable for the next gather."""
+    from fluidframework_amd import shard
+    from fluidframework_amd.engine import MergeEngine, MtError
+    from fluidframework_amd.oplog import CONFIGS
+    cfg = dict(CONFIGS['C3'])
+    cfg.pop('n_docs')
+    cfg['ops_per_doc'] = 64
+    n = 256
+    eng = MergeEngine(n, ops_per_launch=32)
+    dev = eng.synthesize(seed=9, **cfg)
+    eng.reset()
+    eng.apply_staged(dev)
+    comm = shard.RcclComm(0, 1, 0, rendezvous=shard.FileRendezvous(key='test_' + uuid.uuid4().hex))
+    try:
+        with pytest.raises(MtError):
+            comm.gather_checksums(eng, n - 1)
+        parts = comm.gather_checksums(eng, n)
+        assert np.array_equal(parts[0], eng.checksums())
+    finally:
+        comm.close()

@@ -113,10 +113,11 @@ def _bench(*args, timeout=600):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('config', ['C3', 'C5'])
+@pytest.mark.parametrize('config', ['C3', 'C4', 'C5'])
 def test_bench_two_ranks_match_one(config, oracle_lib):
     """bench.py --gpus 2 (spawned ranks, hash-routed shards, gather) == bench.py on one GPU over
-    the same 1,200-document universe, and == the oracle's digest of that universe (C3)."""
+    the same 1,200-document universe, and == the oracle's digest of that universe (C3, C4: the
+    config quoted at 1/2/4 GPUs)."""
     from fluidframework_amd import shard
     from fluidframework_amd.oplog import CONFIGS
     two = _bench('--config', config, '--gpus', '2', '--comm', 'gloo', '--devices', '0,0')
@@ -125,8 +126,8 @@ def test_bench_two_ranks_match_one(config, oracle_lib):
     assert two['config']['docs_total'] == one['config']['docs_total'] == 1200
     assert two['checksum_digest'] == one['checksum_digest']
     assert two['doc_errors_sampled'] == 0
-    if config == 'C3':
-        cfg = dict(CONFIGS['C3'])
+    if config in ('C3', 'C4'):
+        cfg = dict(CONFIGS[config])
         cfg.pop('n_docs')
         cfg['ops_per_doc'] = 160
         whole = oracle_lib.generate(1200, d0=0, seed=20261015, **cfg)

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_SETS, REPO, WIDE_SETS, load_golden
+from conftest import FULLSHAPE_SETS, GOLDEN_SETS, REPO, WIDE_SETS, load_fullshape, load_golden
 
 
 @pytest.mark.parametrize('name', GOLDEN_SETS + WIDE_SETS)
@@ -31,6 +31,21 @@ def test_oracle_matches_reference_golden(oracle_lib, name):
         assert o.text(d) == r['text']
         assert '%016x' % cs[d] == r['checksum']
         assert canon.checksum(st) == int(r['checksum'], 16)
+
+
+@pytest.mark.parametrize('name', FULLSHAPE_SETS)
+def test_oracle_matches_reference_at_full_shape(oracle_lib, name):
+    """The oracle against the reference at C3 / C4's full shape (256 documents x 1024 ops) and a
+    fixed-seed 1,000-document x 1024-op high-conflict fuzz: every document's checksum (and so its
+    whole canonical state), and the whole canonical state of the first three."""
+    batch, fx = load_fullshape(name)
+    o = oracle_lib.Oracle(batch.n_docs).apply(batch, threads=8)
+    got = ['%016x' % c for c in o.checksums()]
+    bad = [d for d in range(batch.n_docs) if got[d] != fx['checksum'][d]]
+    assert not bad, f'{name}: {len(bad)} documents differ, first {bad[:5]}'
+    assert all(not e for e in fx['err'])
+    for d, st in fx['states'].items():
+        assert o.state(int(d)) == st
 
 
 def test_generator_is_deterministic(oracle_lib):

@@ -46,7 +46,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
 PMC_ROUND = 'r03'
-CAL_ROUND = 'r02'  # profiles/<round>_js_calibration.json: r of the JS baseline (oracle/tsref/calibrate.py)
+CAL_ROUND = 'r04'  # profiles/<round>_js_calibration_<config>.json: r of the JS baseline (oracle/tsref/calibrate.py)
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
                 'C5': 'BASELINE.json configs[4], per-GPU share of 1M docs',
@@ -618,7 +618,8 @@ def js_baseline(dev, n_docs, threads, config='C3', docs=1536):
     finally:
         os.unlink(path)
     cal, cal_src = {}, None
-    for name in (f'r03_js_calibration_{config}.json', f'{CAL_ROUND}_js_calibration.json'):
+    for name in (f'{CAL_ROUND}_js_calibration_{config}.json', f'r03_js_calibration_{config}.json',
+                 'r02_js_calibration.json'):
         try:
             with open(os.path.join(PROFILES, name)) as f:
                 c = json.load(f)

@@ -53,6 +53,25 @@ struct LocState {
     uint32_t rgn, rgpn;
 };
 
+// An editing document's per-segment rows in HBM: its big-pool row once it has one, else its
+// MT_LOC_CAP-slot row (mt_state.h)
+struct LocRow {
+    uint64_t* gm;
+    uint64_t* pk;
+    uint32_t* ct;
+    uint64_t* lsq;
+    int cap;
+};
+MT_DEV LocRow loc_row(const mt_gstate& g, uint32_t d) {
+    const uint32_t r = g.locbig[d];
+    if (r != MT_NO_ROW) {
+        const size_t o = (size_t)r * MT_LOC_BIGCAP;
+        return {g.gmb + o, g.pkb + o, g.ctb + o, g.lsqb + o, MT_LOC_BIGCAP};
+    }
+    const size_t o = (size_t)d * MT_LOC_CAP;
+    return {g.gm + o, g.pk + o, g.ct + o, g.lsq + o, MT_LOC_CAP};
+}
+
 // W: a wide document (include/mtgpu.h "limits"): per slot also the overlap ids >= 64 (ovx) and the
 // property words ph / pxl / pxh (u16 value ids, keys 8..15); UTF-16 text.  GW: (LOC) group-mask
 // words per slot, 64 GW pending edits at most (GW > 1: MT_WIDE_GROUPS documents, HBM workspace only)
@@ -1804,17 +1823,19 @@ struct Wave {
             }
             // (a document that has not edited yet has never stored these arrays)
             const bool has = g.loc[d].own >= 0;
-            const size_t lo2 = (size_t)d * g.locstride;
+            const LocRow lr = loc_row(g, d);
             if constexpr (GW == 1) {
                 s.lc.gt[lane] = g.loc[d].gt[lane];
                 s.lc.gls[lane] = g.loc[d].gls[lane];
-                for (int i = lane; i < n; i += 64) s.gm[i] = has ? g.gm[lo2 + i] : 0ull;
+                for (int i = lane; i < n; i += 64) s.gm[i] = has ? lr.gm[i] : 0ull;
             } else if (g.sc[d].wide & MT_WIDE_GROUPS) {
+                const uint32_t gx = g.locgx[d];
                 for (uint32_t j = lane; j < GN; j += 64) {
-                    s.lc.gt[j] = g.locx[d].gt[j];
-                    s.lc.gls[j] = g.locx[d].gls[j];
+                    s.lc.gt[j] = g.locx[gx].gt[j];
+                    s.lc.gls[j] = g.locx[gx].gls[j];
                 }
-                for (int i = lane; i < n * GW; i += 64) s.gm[i] = g.gmx[lo2 * GW + i];
+                const uint64_t* gmx = g.gmx + (size_t)gx * MT_LOC_BIGCAP * GW;
+                for (int i = lane; i < n * GW; i += 64) s.gm[i] = gmx[i];
             } else {
                 // entering the wide-group form: ordinal N moves from bit / index N % 64 to N % GN
                 // (at most 64 pending, so N % 64 names one ordinal of [glo, ghi))
@@ -1828,7 +1849,7 @@ struct Wave {
                 }
                 for (int i = lane; i < n; i += 64) {
                     for (int w = 0; w < GW; w++) s.gm[i * GW + w] = 0ull;
-                    uint64_t m = has ? g.gm[lo2 + i] : 0ull;
+                    uint64_t m = has ? lr.gm[i] : 0ull;
                     while (m) {
                         const uint32_t b = (uint32_t)__builtin_ctzll(m);
                         m &= m - 1;
@@ -1837,9 +1858,9 @@ struct Wave {
                 }
             }
             for (int i = lane; i < n; i += 64) {
-                s.pk[i] = has ? g.pk[lo2 + i] : 0ull;
-                s.ct[i] = has ? g.ct[lo2 + i] : 0u;
-                s.lsq[i] = has ? g.lsq[lo2 + i] : 0ull;
+                s.pk[i] = has ? lr.pk[i] : 0ull;
+                s.ct[i] = has ? lr.ct[i] : 0u;
+                s.lsq[i] = has ? lr.lsq[i] : 0ull;
             }
         }
         sync();
@@ -1956,17 +1977,18 @@ struct Wave {
         }
         if constexpr (LOC) {
             if (s.lc.own >= 0) {
-                const size_t lo2 = (size_t)d * g.locstride;
-                for (int i = lane; i < min(nn, (int)g.locstride); i += 64) {
+                const LocRow lr = loc_row(g, d);  // (loc_admit: nn <= CAP <= lr.cap)
+                uint64_t* gmx = GW > 1 ? g.gmx + (size_t)g.locgx[d] * MT_LOC_BIGCAP * GW : nullptr;
+                for (int i = lane; i < min(nn, lr.cap); i += 64) {
                     const int sl = s.order[i];
                     if constexpr (GW == 1) {
-                        g.gm[lo2 + i] = s.gm[sl];
+                        lr.gm[i] = s.gm[sl];
                     } else {
-                        for (int w = 0; w < GW; w++) g.gmx[(lo2 + i) * GW + w] = s.gm[sl * GW + w];
+                        for (int w = 0; w < GW; w++) gmx[i * GW + w] = s.gm[sl * GW + w];
                     }
-                    g.pk[lo2 + i] = s.pk[sl];
-                    g.ct[lo2 + i] = s.ct[sl];
-                    g.lsq[lo2 + i] = s.lsq[sl];
+                    lr.pk[i] = s.pk[sl];
+                    lr.ct[i] = s.ct[sl];
+                    lr.lsq[i] = s.lsq[sl];
                 }
                 if (lane == 0) {
                     g.loc[d].own = s.lc.own;
@@ -1981,9 +2003,10 @@ struct Wave {
                     g.loc[d].gt[lane] = s.lc.gt[lane];
                     g.loc[d].gls[lane] = s.lc.gls[lane];
                 } else {
+                    const uint32_t gx = g.locgx[d];
                     for (uint32_t j = lane; j < GN; j += 64) {
-                        g.locx[d].gt[j] = s.lc.gt[j];
-                        g.locx[d].gls[j] = s.lc.gls[j];
+                        g.locx[gx].gt[j] = s.lc.gt[j];
+                        g.locx[gx].gls[j] = s.lc.gls[j];
                     }
                 }
             }
@@ -2004,7 +2027,8 @@ struct GenArgs {
 // An editing document enters the editing form at CAP slots only if this launch's ops cannot outgrow
 // it (the form cannot move a document between capacities mid-launch); otherwise it halts with
 // MT_DERR_CAPACITY, and a wide document with MT_DERR_LIMITS (no local edits in the wide form).
-template <int CAP>
+// MT_DERR_CAPACITY too when the engine could not give the document the pool rows its form needs.
+template <int CAP, int GW = 1>
 MT_DEV bool loc_admit(const mt_gstate& g, const mt_op_rec* ops, uint32_t d, uint32_t a, uint32_t b) {
     using LS = Lds<CAP, true>;
     const mt_doc_scalars& sc = g.sc[d];
@@ -2019,7 +2043,8 @@ MT_DEV bool loc_admit(const mt_gstate& g, const mt_op_rec* ops, uint32_t d, uint
     int ib_need = 0;
     for (int L = 1; L < sc.nlev; L++) ib_need = max(ib_need, sc.nb[L]);
     if (!(sc.nseg + 2 * nops + (int)sc.n_empty + 1 <= CAP && sc.nb[0] + 2 * nops + 1 <= LS::LB &&
-          ib_need + nops + 1 <= LS::IB && sc.heap_n + 4 * nops + 16 <= LS::H && CAP <= (int)g.locstride)) {
+          ib_need + nops + 1 <= LS::IB && sc.heap_n + 4 * nops + 16 <= LS::H && CAP <= loc_row(g, d).cap &&
+          (GW == 1 || g.locgx[d] != MT_NO_ROW))) {
         if (threadIdx.x == 0 && !sc.err) {
             g.sc[d].err = MT_DERR_CAPACITY;
             g.sc[d].err_seq = ops[a].seq;
@@ -2111,8 +2136,7 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
-    if (LOC && !loc_admit<CAP>(g, ops, d, a, b)) return;
-    if (GW > 1 && !(g.gmx && g.locx)) return;  // (the engine allocates them before such a launch)
+    if (LOC && !loc_admit<CAP, GW>(g, ops, d, a, b)) return;
     wv.load(g, d);
     if (LOC) {
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;

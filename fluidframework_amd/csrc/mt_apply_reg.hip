@@ -61,6 +61,16 @@ constexpr uint16_t kDead = 0xFFFFu;
 template <class T>
 MT_DEV MT_GLOB T* gp(T* p) { return (MT_GLOB T*)p; }
 typedef const MT_KARG mt_gstate KGState;
+typedef uint32_t EvWords __attribute__((ext_vector_type(4)));
+// one 64-byte event row through a global pointer: four 16-byte stores
+MT_DEV void put_event(MT_GLOB mt_event* p, const mt_event& e) {
+    static_assert(sizeof(mt_event) == 64, "mt_event");
+    EvWords w[4];
+    __builtin_memcpy(w, &e, sizeof w);
+    MT_GLOB EvWords* q = reinterpret_cast<MT_GLOB EvWords*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; i++) q[i] = w[i];
+}
 
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 MT_DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -131,10 +141,17 @@ struct Elem {
     uint32_t li, cf, ov, oh;
     int32_t cum;
 };
+// A boundary split of the segment at slot k: the two parts' lengths / ids (li), the left part's
+// flags and cumulative end (insert_at applies it: the right part enters at k + 1)
+struct Cut {
+    uint32_t lli, lcf, rli;
+    int32_t pos;
+};
 
 // W: documents with client ids above 32 (any up to 63): the overlap set takes a second register
-// per slot (oh), otherwise the same engine
-template <int K, bool W = false>
+// per slot (oh), otherwise the same engine.  EV: delta / maintenance events are recorded
+// (mt_events_enable): the reference's callbacks in firing order, as mt_event rows
+template <int K, bool W = false, bool EV = false>
 struct RWave {
     using L = RLds<K>;
     static constexpr int CAP = L::CAP;
@@ -163,6 +180,11 @@ struct RWave {
     // per-lane K-bit masks over this lane's slots: starts a leaf block (bsm), live (lvm), and the
     // needsScour state (MT_SC_*) of the block a start slot begins: bit 0 in sc0, bit 1 in sc1
     uint32_t bsm, lvm, sc0, sc1;
+    // (EV) the document's event rows, their capacity, the rows recorded so far, the op's seq
+    MT_GLOB mt_event* evp = nullptr;
+    uint32_t evcap = 0;
+    int evn = 0;
+    int32_t evseq = 0;
 #ifdef MT_PROF
     uint64_t prof[P_NSLOT] = {};
 #endif
@@ -286,6 +308,104 @@ struct RWave {
             r -= c;
         }
         return -1;
+    }
+
+    // ------------------------------------------------------------ delta events (EV)
+    // One callback record (mt_event, include/mtgpu.h) written by lane 0 in firing order (the
+    // reference's mergeTreeDeltaCallback / mergeTreeMaintenanceCallback, mergeTreeDeltaCallback.ts).
+    // Segments are named by their leaf ordinal among the linked segments (live slots) and, for op
+    // callbacks, their local-view position; rows past the capacity are counted, not written (the
+    // document then halts with MT_DERR_EVENTS after the op).
+    MT_DEV void emit(int op, unsigned flags, int leaf, int pos, uint32_t len) {
+        if (lane == 0 && evn < (int)evcap) {
+            mt_event e{};
+            e.seq = evseq;
+            e.op = (int8_t)op;
+            e.flags = (uint8_t)flags;
+            e.leaf = leaf;
+            e.pos = pos;
+            e.len = len;
+            put_event(evp + evn, e);
+        }
+        evn = evn + 1;
+    }
+    MT_DEV int live_before(int k) const { return uni(wave_total(__popc(lvm & below(k)))); }
+    // characters of the unremoved linked segments before slot k: the local view's position
+    MT_DEV int local_before(int k) const {
+        const uint32_t m = lvm & below(k);
+        int t = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) t += (((m >> j) & 1u) && !(cf[j] & F_RM)) ? (int)len_of(li[j]) : 0;
+        return uni(wave_total(t));
+    }
+    // The REMOVE / ANNOTATE callback (mergeTree.ts:2705-2712 / 2592-2600): its delta segments in
+    // document order, lane-parallel (each lane writes the rows of its own slots, placed by a prefix
+    // count).  REMOVE runs after the edits (the segments this op removed: rseq == S by C; positions
+    // with the removal applied), ANNOTATE before them (propertyDeltas need the previous values:
+    // SegmentPropertiesManager.addProperties' deltas, segmentPropertiesManager.ts:60-108 -- a
+    // rewrite records each key it deletes with its old value, every key of the op the value before
+    // it is set, null for a rewrite's null-valued key).  tm: the op's touched slots.
+    MT_DEV void emit_range(bool is_remove, int32_t S, int C, uint32_t tm, uint64_t pclr, uint64_t pset, bool rewrite) {
+        uint32_t hm = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const uint32_t f = cf[j];
+            const bool hit = ((tm >> j) & 1u) &&
+                             (!is_remove || ((f & F_RM) && rseq[j] == S && ((f >> 8) & 0xFFu) == (uint32_t)C));
+            hm |= hit ? (1u << j) : 0u;
+        }
+        const int hc = __popc(hm);
+        const int hinc = wave_incl_scan(hc);
+        const int total = wave_last(hinc);
+        if (total == 0) return emit(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE, MT_EVF_FIRST | MT_EVF_EMPTY, -1, -1, 0);
+        int ll = 0, lc = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            ll += (((lvm >> j) & 1u) && !(cf[j] & F_RM)) ? (int)len_of(li[j]) : 0;
+            lc += (lvm >> j) & 1u;
+        }
+        int pos = wave_incl_scan(ll) - ll, leaf = wave_incl_scan(lc) - lc, idx = evn + hinc - hc;
+        // the op's keys (bit k), and those it sets to a value (not null)
+        uint32_t okeys = 0, onz = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            okeys |= ((pclr >> (8 * k)) & 0xFFu) ? (1u << k) : 0u;
+            onz |= ((pset >> (8 * k)) & 0xFFu) ? (1u << k) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const bool live = (lvm >> j) & 1u;
+            if ((hm >> j) & 1u) {
+                if (idx < (int)evcap) {
+                    mt_event e{};
+                    e.seq = evseq;
+                    e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
+                    e.flags = (uint8_t)(idx == evn ? MT_EVF_FIRST : 0u);
+                    e.leaf = leaf;
+                    e.pos = pos;
+                    e.len = len_of(li[j]);
+                    if (!is_remove) {
+                        const uint64_t old = (cf[j] & F_PDEF) ? s.props[id_of(li[j])] : 0ull;
+                        uint32_t oldnz = 0;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) oldnz |= ((old >> (8 * k)) & 0xFFu) ? (1u << k) : 0u;
+                        const uint32_t pm = okeys | (rewrite ? (oldnz & ~onz) : 0u);
+                        e.pmask = (uint16_t)pm;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            const uint32_t ov = (uint32_t)(old >> (8 * k)) & 0xFFu;
+                            const bool nulled = rewrite && ((okeys >> k) & 1u) && !((onz >> k) & 1u);
+                            e.pvals[k] = ((pm >> k) & 1u) && !nulled ? (uint16_t)ov : (uint16_t)0;
+                        }
+                    }
+                    put_event(evp + idx, e);
+                }
+                idx++;
+            }
+            pos += (live && !(cf[j] & F_RM)) ? (int)len_of(li[j]) : 0;
+            leaf += live ? 1 : 0;
+        }
+        evn = evn + total;
     }
 
     // ------------------------------------------------------------ element access
@@ -488,11 +608,22 @@ struct RWave {
 
     // insert e at slot k (a <= k <= en) of the leaf block of slots [a, en) (insertingWalk's child
     // insert, mergeTree.ts:2446-2470)
-    MT_DEV bool insert_at(int k, int a, int en, Elem e, int32_t sq) {
+    // (cut: a boundary split's right part, a copy of slot k - 1 patched after the shift; k > a)
+    MT_DEV bool insert_at(int k, int a, int en, const Elem& e, int32_t sq, const Cut& cut, bool dup) {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
         const bool front = k == a;  // new first child: it takes over the block's marks
         PROF_BEGIN(ti0, P_B_INS);
-        shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
+        if (dup) {
+            // (fetching slot k - 1 and shifting it in measured faster than an in-register duplicate:
+            // profiles/r04_ab_split_htop_C3.log)
+            Elem r = get(k - 1);
+            r.li = cut.rli;
+            set_li_cf(k - 1, cut.lli, cut.lcf);
+            set_cum(k - 1, cut.pos);
+            shift_in<true>(k, r, false, 0, true);
+        } else {
+            shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
+        }
         if (front) {
             set_bs(k + 1, false);
             set_sc(k + 1, MT_SC_UNDEF);
@@ -570,10 +701,11 @@ struct RWave {
         return false;
     }
 
-    // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245), first half: find the segment
-    // visible to the op's view that strictly contains pos, cut it (left part in place, cum kept
-    // valid for the view) and return its right part r, to be inserted at slot k1 of leaf block b.
-    MT_DEV bool split_prep(int pos, int32_t sq, Elem& r, int& k1, int& ba, int& be) {
+    // ensureIntervalBoundary(pos) (mergeTree.ts:2241-2245), first half: find the segment visible to
+    // the op's view that strictly contains pos and describe its cut (left part in place, cum kept
+    // valid for the view; right part entering at slot k1 of the leaf block [ba, be)).  Nothing in
+    // the registers changes here: insert_at applies the cut.
+    MT_DEV bool split_prep(int pos, int32_t sq, Cut& c, int& k1, int& ba, int& be) {
         PROF_BEGIN(ts0, P_B_SRCH);
         int cs = cs0();
         int hitj = -1;
@@ -588,11 +720,14 @@ struct RWave {
         PROF_CNT(P_N_SPLIT, 1);
         PROF_BEGIN(tb0, P_B_GET);
         const int lk = first_lane(m);
-        const int k = lk * K + __builtin_amdgcn_readlane(hitj, lk);
-        const Elem e = get(k);
+        const int jk = uni(__builtin_amdgcn_readlane(hitj, lk));
+        const int k = lk * K + jk;
+        const uint32_t eli = (uint32_t)__builtin_amdgcn_readlane((int)li[jk], lk);
+        const uint32_t ecf = (uint32_t)__builtin_amdgcn_readlane((int)cf[jk], lk);
+        const int32_t ecum = __builtin_amdgcn_readlane(cum[jk], lk);
         PROF_END(prof, P_B_GET, tb0);
-        const uint32_t len = len_of(e.li);
-        const int off = pos - (e.cum - (int)len);
+        const uint32_t len = len_of(eli);
+        const int off = pos - (ecum - (int)len);
         const int t = alloc_id(sq);
         if (t < 0) return false;
         PROF_BEGIN(tb1, P_B_BLK);
@@ -601,34 +736,28 @@ struct RWave {
         PROF_END(prof, P_B_BLK, tb1);
         PROF_BEGIN(tb2, P_B_TXT);
         // BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTree.ts:524-568)
-        const uint32_t id = id_of(e.li);
+        const uint32_t id = id_of(eli);
         const uint64_t pid = s.props[id];  // (issued with the toff read: one LDS round trip)
         const uint32_t to = uniu(s.toff[id]);
-#ifdef MT_NO_NLQ
-        uint8_t last = 0;  // a segment without any "\n" needs no text read
-        if (e.cf & F_HASNL) {
-            arena_sync();
-            last = arena()[to + (uint32_t)off - 1];
-        }
-#endif
         if (lane == 0) {
             s.props[t] = pid;
             s.toff[t] = (uint16_t)(to + (uint32_t)off);
             s.tln[id] = (uint32_t)off;
             s.tln[t] = len - (uint32_t)off;
         }
-        r = e;
-        r.li = (len - (uint32_t)off) | ((uint32_t)t << kLenBits);
-        r.cf = e.cf;
-#ifdef MT_NO_NLQ
-        set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & ~F_NL) | (last == '\n' ? F_NL : 0u));
-#else
-        // the left part ends in "\n" only if the segment has one: otherwise known now
-        set_li_cf(k, (uint32_t)off | (id << kLenBits), (e.cf & F_HASNL) ? ((e.cf & ~F_NL) | F_NLQ) : (e.cf & ~(F_NL | F_NLQ)));
-#endif
-        set_cum(k, pos);
+        c.lli = (uint32_t)off | (id << kLenBits);
+        // the left part ends in "\n" only if the segment has one: otherwise known now (F_NLQ: the
+        // character is read where the flag is needed -- scour, store)
+        c.lcf = (ecf & F_HASNL) ? ((ecf & ~F_NL) | F_NLQ) : (ecf & ~(F_NL | F_NLQ));
+        c.rli = (len - (uint32_t)off) | ((uint32_t)t << kLenBits);
+        c.pos = pos;
         wave_sync();
         PROF_END(prof, P_B_TXT, tb2);
+        if constexpr (EV) {  // MergeTreeMaintenanceType.SPLIT (mergeTree.ts:2231-2236): the right part is not linked yet
+            const int lf = live_before(k);
+            emit(MT_EV_SPLIT, MT_EVF_FIRST, lf, -1, (uint32_t)off);
+            emit(MT_EV_SPLIT, 0u, lf + 1, -1, len - (uint32_t)off);
+        }
         k1 = k + 1;
         return true;
     }
@@ -665,44 +794,49 @@ struct RWave {
     // Pop (collections.ts:240-263): the last entry x replaces the root and sinks along the
     // smaller-child path (the left child unless the right one is strictly smaller) while
     // `x - child > 0`.  Lane t < 62 holds the node t + 2 of the five-level subtree below k in
-    // heap order (relative index r at lane r - 2).
+    // heap order (relative index r at lane r - 2); the path is decided from two ballots -- "the
+    // right sibling is strictly smaller" at every left child, "x - node <= 0" at every node -- by
+    // bit walks on the scalar unit, with no readlane per level, and the path's nodes move up one
+    // level in one masked LDS store.  (The first window's read also fetches the root's segment and
+    // the last entry, in lanes 62 and 63: one LDS round trip per window.)
     MT_DEV int heap_pop() {
-        const int id = uni(s.hslot[1]);
         const int cnt = heap_n - 1;
-        const int32_t x = uni(s.hseq[heap_n]);
-        const uint32_t xs = uniu(s.hslot[heap_n]);
-        int k = 1;
-        for (bool more = (k << 1) <= cnt; more;) {
-            const int r = lane + 2;
-            const int dep = 31 - __builtin_clz((uint32_t)r);
+        int k = 1, id = 0;
+        int32_t x = 0;
+        uint32_t xs = 0;
+        const int r = lane + 2;
+        const int dep = 31 - __builtin_clz((uint32_t)r);
+        for (bool first = true, more = true; more; first = false) {
             const int node = (k << dep) + (r - (1 << dep));
             const bool ok = lane < 62 && node <= cnt;
-            const int32_t v = ok ? s.hseq[node] : 0;
-            const uint32_t sl = ok ? (uint32_t)s.hslot[node] : 0u;
+            const int at = lane < 62 ? (ok ? node : 0) : (lane == 62 ? heap_n : 1);
+            const int32_t v = (ok || (first && lane >= 62)) ? s.hseq[at] : 0;
+            const uint32_t sl = (ok || (first && lane >= 62)) ? (uint32_t)s.hslot[at] : 0u;
+            if (first) {
+                id = uni(__builtin_amdgcn_readlane((int)sl, 63));
+                x = uni(__builtin_amdgcn_readlane(v, 62));
+                xs = uniu((uint32_t)__builtin_amdgcn_readlane((int)sl, 62));
+            }
+            const int32_t vr = shl1(v, 0);
+            const bool rok = shl1(ok ? 1 : 0, 0) != 0;  // the right sibling exists
+            const uint64_t pick = wave_ballot((r & 1) == 0 && ok && rok && v - vr > 0);
+            const uint64_t stop = wave_ballot(ok && x - v <= 0);
             wave_sync();
+            uint64_t path = 0;
             int rr = 1;
             more = false;
             for (int lv = 0; lv < 5; lv++) {
                 if ((k << 1) > cnt) break;
-                int j = k << 1, jr = rr << 1;
-                int32_t vj = __builtin_amdgcn_readlane(v, jr - 2);
-                if (j < cnt) {
-                    const int32_t v1 = __builtin_amdgcn_readlane(v, jr - 1);
-                    if (vj - v1 > 0) {
-                        j++;
-                        jr++;
-                        vj = v1;
-                    }
-                }
-                if (x - vj <= 0) break;
-                const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)sl, jr - 2);
-                if (lane == 0) {  // the child moves up into k
-                    s.hseq[k] = vj;
-                    s.hslot[k] = (uint16_t)sj;
-                }
-                k = j;
+                const int jr = (rr << 1) + (int)((pick >> ((rr << 1) - 2)) & 1u);
+                if ((stop >> (jr - 2)) & 1u) break;
+                path |= 1ull << (jr - 2);
+                k = (k << 1) + (jr & 1);
                 rr = jr;
                 more = lv == 4 && (k << 1) <= cnt;
+            }
+            if ((path >> lane) & 1u) {  // the path's children move up into their parents
+                s.hseq[node >> 1] = v;
+                s.hslot[node >> 1] = (uint16_t)sl;
             }
             wave_sync();
         }
@@ -856,6 +990,54 @@ struct RWave {
         // lane q appended: the child of the run's head, the last child before q not appended
         const uint32_t heads = ~appm & ((1u << (lane & 31)) - 1u);
         const int vtgt = (lane < 32 && ((appm >> lane) & 1u)) ? 31 - __builtin_clz(heads) : -1;
+        if constexpr (EV) {
+            // UNLINK (mergeTree.ts:1310-1315) and APPEND (:1335-1340) callbacks in child order: child q
+            // is named by the block's first ordinal plus the children kept before it (the earlier ones
+            // are gone by then); an APPEND pair names the run's head with its grown length, then q
+            const bool app = vtgt >= 0;
+            const bool tomb = mine && ((unlink >> lane) & 1u) && !app;
+            const int kb = lane - __popc(unlink & (lane < 32 ? ((1u << lane) - 1u) : 0xFFFFFFFFu));
+            const int nrec = tomb ? 1 : (app ? 2 : 0);
+            const int rinc = wave_incl_scan(nrec);
+            const int rtot = wave_last(rinc);
+            if (rtot) {
+                const int st = live_before(a);
+                const int ainc = wave_incl_scan(app ? (int)ql : 0);
+                const int hp = app ? vtgt : lane;
+                const int kbp = __shfl(kb, hp, 64), aincp = __shfl(ainc, hp, 64);
+                const uint32_t lenp = (uint32_t)__shfl((int)ql, hp, 64);
+                const int o = evn + rinc - nrec;
+                if (tomb && o < (int)evcap) {
+                    mt_event ev{};
+                    ev.seq = evseq;
+                    ev.op = (int8_t)MT_EV_UNLINK;
+                    ev.flags = (uint8_t)MT_EVF_FIRST;
+                    ev.leaf = st + kb;
+                    ev.pos = -1;
+                    ev.len = ql;
+                    put_event(evp + o, ev);
+                }
+                if (app) {
+                    mt_event ev{};
+                    ev.seq = evseq;
+                    ev.op = (int8_t)MT_EV_APPEND;
+                    ev.pos = -1;
+                    if (o < (int)evcap) {
+                        ev.flags = (uint8_t)MT_EVF_FIRST;
+                        ev.leaf = st + kbp;
+                        ev.len = lenp + (uint32_t)(ainc - aincp);
+                        put_event(evp + o, ev);
+                    }
+                    if (o + 1 < (int)evcap) {
+                        ev.flags = 0;
+                        ev.leaf = st + kb;
+                        ev.len = ql;
+                        put_event(evp + o + 1, ev);
+                    }
+                }
+                evn = evn + rtot;
+            }
+        }
         PROF_CNT(P_N_UNLINK, __popc(unlink));
         uint64_t runs = __ballot(vtgt >= 0);
         while (runs) {
@@ -1011,10 +1193,20 @@ struct RWave {
     // blockInsert (mergeTree.ts:2141-2224) of a text segment at pos, after the boundary split:
     // choose its slot k in leaf block b, write its text and cold fields, build its element.
     // Returns its id (< 0 on error) and its child index inside block b before a possible split.
+    // kl >= 0: the boundary split at pos just cut the segment at slot kl (its right part is at kl + 1).
+    // Then the walk needs no search: the first block whose cumulative end >= pos is kl's block (every
+    // earlier block ends at or before kl's start, < pos), and in it the first child with pos < end is
+    // the right part -- or, when the split's leaf split moved the right part into the next block,
+    // kl's block ends at kl and the segment goes at its end: slot kl + 1 either way.
     MT_DEV int place_prep(const mt_op_rec op, const uint8_t* pay, int tlen, int np, Elem& en,
-                          int& k, int& ba, int& be) {
+                          int& k, int& ba, int& be, int kl) {
         const int32_t S = op.seq, R = op.ref_seq;
         const int C = op.client, pos = op.pos1;
+        if (kl >= 0) {
+            k = kl + 1;
+            ba = block_start(kl);
+            be = next_start(kl);
+        } else {
         // insertingWalk descends into the first block whose cumulative visible end >= pos
         // (breakTie is true for blocks, :2248-2277): that leaf block's last slot is the first
         // block-ending slot with cum >= pos
@@ -1050,6 +1242,7 @@ struct RWave {
         }
         best = first_hit(best);
         k = best != 0x7fffffff ? best : e;
+        }
         const int t = alloc_id(S);
         if (t < 0) return -1;
         if (!arena_reserve((uint32_t)tlen, S, t)) return -1;  // (t's text is not written yet)
@@ -1118,6 +1311,7 @@ struct RWave {
                 cs = ce;
             }
         }
+        if (EV && !is_remove) emit_range(false, S, C, tm, pclr, pset, rewrite);
         if (is_remove) {
             // branch-free register updates (a store per branch would merge into a pointer phi and
             // push the state arrays to scratch)
@@ -1162,6 +1356,7 @@ struct RWave {
 #pragma unroll
             for (int j = 0; j < K; j++) cf[j] = ((tm >> j) & 1u) ? (cf[j] | F_PDEF) : cf[j];
         }
+        if (EV && is_remove) emit_range(true, S, C, tm, 0, 0, false);
         // addToLRUSet for the touched segments in document order: one push per leaf block
         // (its first touched child) whose needsScour is not already true
         int from = 0;
@@ -1183,6 +1378,7 @@ struct RWave {
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
+        if constexpr (EV) evseq = S;
         if (!noop) {
             if (op.client == 0 || op.client > (W ? kC64Clients : kNarrowClients)) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
@@ -1203,18 +1399,21 @@ struct RWave {
             // insertion steps: the boundary splits (ensureIntervalBoundary), then for an insert
             // the new segment; every step ends in the one insert_at call site
             const int nsteps = ins ? (tlen > 0 ? 2 : 1) : 2;
+            int kl = -1;  // (an insert) the slot of the segment the boundary split at pos cut
             for (int step = 0; step < nsteps; step++) {
                 PROF_BEGIN2(t1, P_BOUND, P_INSERT);
                 const bool placing = ins && step == 1;
-                Elem e;
+                Elem e{};
+                Cut cut{};
                 int k = 0, ba = 0, be = 0, t = -1;
                 if (!placing) {
-                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, e, k, ba, be)) {
+                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, cut, k, ba, be)) {
                         if (err) return;
                         continue;
                     }
+                    kl = k - 1;
                 } else {
-                    t = place_prep(op, pay, tlen, np, e, k, ba, be);
+                    t = place_prep(op, pay, tlen, np, e, k, ba, be, uni(kl));
                     if (t < 0) return;
                 }
                 // (uniform by construction; the phi that merges the two prep paths is not
@@ -1223,7 +1422,7 @@ struct RWave {
                 ba = uni(ba);
                 be = uni(be);
                 t = uni(t);
-                const bool ok = insert_at(k, ba, be, e, S);
+                const bool ok = insert_at(k, ba, be, e, S, cut, !placing);
                 if (placing) {
                     PROF_END(prof, P_INSERT, t1);
                 } else {
@@ -1234,7 +1433,10 @@ struct RWave {
                     // the new segment's block after a possible split: the one holding slot k
                     if (!add_lru(block_start(k), t, S)) return;
                 }
+                if (EV && placing)  // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988)
+                    emit(MT_EV_INSERT, MT_EVF_FIRST, live_before(k), local_before(k), (uint32_t)tlen);
             }
+            if (EV && ins && tlen == 0) emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
             if (!ins) {
                 PROF_BEGIN(t2, P_RANGE);
                 range_action(op, pay, tlen, np);
@@ -1260,6 +1462,7 @@ struct RWave {
             PROF_END(prof, P_ZAMBONI, t3);
             if (err) return;
         }
+        if (EV && evn > (int)evcap) fail(MT_DERR_EVENTS, S);  // halt rather than drop callbacks
     }
 
     // ------------------------------------------------------------ load / store
@@ -1369,6 +1572,12 @@ struct RWave {
         next_id = n;
         nlive = n;
         ns = n;
+        if constexpr (EV) {
+            evp = gp(g.ev) + (size_t)d * g.evcap;
+            evcap = g.evcap;
+            evn = uni((int)gp(g.evn)[d]);
+            evseq = cur_seq;
+        }
         const size_t so = (size_t)d * g.segcap;
         const size_t lo = (size_t)d * g.lbcap;
         const size_t ho = (size_t)d * g.hcap;
@@ -1650,6 +1859,8 @@ struct RWave {
             sc.nb[0] = nb0;
         }
         if (lane >= 1 && lane < MT_MAXLEV) gp(g.sc)[d].nb[lane] = s.nb[lane];
+        if constexpr (EV)
+            if (lane == 0) gp(g.evn)[d] = (uint32_t)evn;
     }
 };
 
@@ -1706,7 +1917,7 @@ constexpr int wpe_default(int K) { return K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 
 #endif
 constexpr int wpe_ov[17] = MT_WPE_OV;
 constexpr int wpe(int K) { return K < 17 && wpe_ov[K] > 0 ? wpe_ov[K] : wpe_default(K); }
-template <int K, bool W>
+template <int K, bool W, bool EV>
 MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restrict__ ops,
                       const uint8_t* __restrict__ payload, const uint32_t* __restrict__ row_ptr,
                       const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt) {
@@ -1715,7 +1926,7 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     RLds<K>& lds = *reinterpret_cast<RLds<K>*>(smem);
-    RWave<K, W> wv(lds, text + (size_t)d * 2 * textcap, textcap);
+    RWave<K, W, EV> wv(lds, text + (size_t)d * 2 * textcap, textcap);
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -1792,19 +2003,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) vo
     mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
     const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
     uint32_t op_cnt) {
-    reg_apply<K, false>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
+    reg_apply<K, false, false>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
+}
+// ... and with delta / maintenance events recorded (mt_events_enable): the same engine, its event
+// rows written from the split, insert, range and scour steps (the kernel without EV carries no event
+// code; C64 documents record on the LDS engine)
+template <int K>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel_ev(
+    mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
+    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
+    uint32_t op_cnt) {
+    reg_apply<K, false, true>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
 }
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe_c64(K)))) void reg_apply_kernel_c64(
     mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
     const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
     uint32_t op_cnt) {
-    reg_apply<K, true>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
+    reg_apply<K, true, false>(g.text, g.textcap, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);
 }
 
 }  // namespace mtr
 
-extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstate* g, const mt_op_rec* ops,
+// form: 0 = the narrow register engine, 1 = its C64 form, 2 = the narrow form recording events
+extern "C" hipError_t mt_launch_apply_reg(int cap_class, int form, const mt_gstate* g, const mt_op_rec* ops,
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
@@ -1812,8 +2034,11 @@ extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstat
 #define MTR_LAUNCH(CAPV)                                                                                     \
     case CAPV: {                                                                                             \
         constexpr int K = CAPV / 64;                                                                         \
-        if (c64)                                                                                             \
+        if (form == 1)                                                                                       \
             hipLaunchKernelGGL((mtr::reg_apply_kernel_c64<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g, \
+                               ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
+        else if (form == 2)                                                                                  \
+            hipLaunchKernelGGL((mtr::reg_apply_kernel_ev<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g,  \
                                ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
         else                                                                                                 \
             hipLaunchKernelGGL((mtr::reg_apply_kernel<K>), grid, block, sizeof(mtr::RLds<K>), stream, *g,     \

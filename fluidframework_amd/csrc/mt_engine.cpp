@@ -23,7 +23,7 @@
 extern "C" hipError_t mt_launch_apply(int cap_class, const mt_gstate* g, const mt_op_rec* ops, const uint8_t* payload,
                                       const uint32_t* row_ptr, const uint32_t* doc_ids, uint32_t n_docs,
                                       uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
-extern "C" hipError_t mt_launch_apply_reg(int cap_class, int c64, const mt_gstate* g, const mt_op_rec* ops,
+extern "C" hipError_t mt_launch_apply_reg(int cap_class, int form, const mt_gstate* g, const mt_op_rec* ops,
                                           const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream);
 extern "C" size_t mt_lds_bytes(int cap_class);
@@ -58,6 +58,10 @@ extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* 
                                        mt_stack_item* items, uint32_t* depth, hipStream_t st);
 extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q, uint32_t n, mt_tile_result* out,
                                       hipStream_t st);
+extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, mt_pos_result* out,
+                                        hipStream_t st);
+extern "C" hipError_t mt_launch_seginfo(const mt_gstate* g, const uint32_t* docs, const int32_t* ords, uint32_t n,
+                                        mt_seg_info* out, hipStream_t st);
 extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
                                             hipStream_t st);
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
@@ -162,6 +166,9 @@ struct mt_engine {
     hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
     uint64_t gen = 0;  // bumped by every call that can change document state (snap_cache's key)
     std::vector<uint16_t> lkeys;  // per document: its declared label keys (mt_set_label_keys), host copy
+    // the editing documents' pool rows (mt_state.h locbig / locgx): host copies, rows in use, rows held
+    std::vector<uint32_t> h_locbig, h_locgx, h_bucket;
+    uint32_t nbig = 0, bigcap = 0, ngx = 0, gxcap = 0;
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
         uint64_t gen = 0;
@@ -206,52 +213,102 @@ static mt_status ensure_wide(mt_engine* e) {
     }
     return MT_OK;
 }
-// The editing documents' per-segment state (gm / pk / ct / lsq) holds MT_LOC_CAP slots per document
-// until a document's editing form needs a larger class (mt_launch_apply_loc_big): then every
-// document's rows are re-laid at that stride (nothing runs on the engine's streams meanwhile)
-template <class T>
-static mt_status relay_rows(mt_engine* e, T** p, uint32_t from, uint32_t to) {
-    const size_t D = e->cfg.max_docs;
-    T* q = nullptr;
-    if (hipMalloc(&q, D * to * sizeof(T)) != hipSuccess) return MT_ERR_NOMEM;
-    if (hipMemset(q, 0, D * to * sizeof(T)) != hipSuccess ||
-        hipMemcpy2D(q, to * sizeof(T), *p, from * sizeof(T), from * sizeof(T), D, hipMemcpyDeviceToDevice) !=
-            hipSuccess) {
-        (void)hipFree(q);
-        return MT_ERR_HIP;
-    }
-    for (auto& a : e->allocs)
-        if (a == (void*)*p) a = q;
-    HIP_OK(hipFree(*p));
-    *p = q;
-    return MT_OK;
+// The editing documents' pools (mt_state.h): a document whose editing form needs more than
+// MT_LOC_CAP slots gets a big-pool row, one past 64 pending edits a group-pool row, when it first
+// reaches such a form; the pools grow geometrically (a grow re-allocates and copies the rows in use;
+// nothing runs on the engine's streams meanwhile).  Memory scales with the documents that reach
+// those forms, not with max_docs.
+static bool pool_alloc(void** out, size_t bytes) {
+    *out = nullptr;
+    return hipMalloc(out, bytes) == hipSuccess;
 }
-static mt_status ensure_locstride(mt_engine* e, uint32_t cap) {
+static bool grow_big(mt_engine* e, uint32_t rows) {
     mt_gstate& g = e->g;
-    if (g.locstride >= cap) return MT_OK;
+    const size_t C = MT_LOC_BIGCAP, n = (size_t)rows * C, u = (size_t)e->nbig * C;
+    void *gm = nullptr, *pk = nullptr, *ct = nullptr, *lsq = nullptr;
+    if (!pool_alloc(&gm, n * 8) || !pool_alloc(&pk, n * 8) || !pool_alloc(&ct, n * 4) || !pool_alloc(&lsq, n * 8)) {
+        for (void* q : {gm, pk, ct, lsq})
+            if (q) (void)hipFree(q);
+        return false;
+    }
+    if (u && (hipMemcpy(gm, g.gmb, u * 8, hipMemcpyDeviceToDevice) != hipSuccess ||
+              hipMemcpy(pk, g.pkb, u * 8, hipMemcpyDeviceToDevice) != hipSuccess ||
+              hipMemcpy(ct, g.ctb, u * 4, hipMemcpyDeviceToDevice) != hipSuccess ||
+              hipMemcpy(lsq, g.lsqb, u * 8, hipMemcpyDeviceToDevice) != hipSuccess)) {
+        for (void* q : {gm, pk, ct, lsq}) (void)hipFree(q);
+        return false;
+    }
+    for (void* q : {(void*)g.gmb, (void*)g.pkb, (void*)g.ctb, (void*)g.lsqb})
+        if (q) (void)hipFree(q);
+    g.gmb = (uint64_t*)gm;
+    g.pkb = (uint64_t*)pk;
+    g.ctb = (uint32_t*)ct;
+    g.lsqb = (uint64_t*)lsq;
+    e->bigcap = rows;
+    return true;
+}
+static bool grow_gx(mt_engine* e, uint32_t rows) {
+    mt_gstate& g = e->g;
+    const size_t n = (size_t)rows * MT_LOC_BIGCAP * 4, u = (size_t)e->ngx * MT_LOC_BIGCAP * 4;
+    void *gm = nullptr, *lx = nullptr;
+    if (!pool_alloc(&gm, n * 8) || !pool_alloc(&lx, (size_t)rows * sizeof(mt_locx))) {
+        for (void* q : {gm, lx})
+            if (q) (void)hipFree(q);
+        return false;
+    }
+    if (u && (hipMemcpy(gm, g.gmx, u * 8, hipMemcpyDeviceToDevice) != hipSuccess ||
+              hipMemcpy(lx, g.locx, (size_t)e->ngx * sizeof(mt_locx), hipMemcpyDeviceToDevice) != hipSuccess)) {
+        (void)hipFree(gm);
+        (void)hipFree(lx);
+        return false;
+    }
+    if (g.gmx) (void)hipFree(g.gmx);
+    if (g.locx) (void)hipFree(g.locx);
+    g.gmx = (uint64_t*)gm;
+    g.locx = (mt_locx*)lx;
+    e->gxcap = rows;
+    return true;
+}
+// rows for `want` more documents: double the pool (at least 16 rows), else exactly what is needed;
+// returns how many of them got rows
+template <class Grow>
+static uint32_t pool_reserve(uint32_t used, uint32_t cap, uint32_t want, Grow grow) {
+    if (used + want <= cap) return want;
+    const uint32_t need = used + want;
+    if (grow(std::max<uint32_t>({need, 2 * cap, 16u}))) return want;
+    if (grow(need)) return want;
+    return cap > used ? cap - used : 0;
+}
+// Assigns the rows of one tick's editing buckets (bk: the bucket's index in d_ids); the documents that
+// get no row halt in the kernel with MT_DERR_CAPACITY (mt_apply.hip loc_admit)
+static mt_status assign_loc_rows(mt_engine* e, const uint32_t* ids, uint32_t cnt, bool big, bool gx) {
+    mt_gstate& g = e->g;
+    e->h_bucket.resize(cnt);
+    HIP_OK(hipMemcpy(e->h_bucket.data(), ids, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> nb, ng;
+    for (uint32_t d : e->h_bucket) {
+        if (big && e->h_locbig[d] == MT_NO_ROW) nb.push_back(d);
+        if (gx && e->h_locgx[d] == MT_NO_ROW) ng.push_back(d);
+    }
+    if (nb.empty() && ng.empty()) return MT_OK;
     HIP_OK(hipDeviceSynchronize());
-    mt_status st = MT_OK;
-    if ((st = relay_rows(e, &g.gm, g.locstride, cap)) || (st = relay_rows(e, &g.pk, g.locstride, cap)) ||
-        (st = relay_rows(e, &g.ct, g.locstride, cap)) || (st = relay_rows(e, &g.lsq, g.locstride, cap)) ||
-        (g.gmx && (st = relay_rows(e, &g.gmx, 4 * g.locstride, 4 * cap))))
-        return st;  // (a failed relay leaves the arrays it did at the new stride: the engine is unusable)
-    g.locstride = cap;
-    return MT_OK;
-}
-
-// The MT_WIDE_GROUPS documents' group masks (4 words per segment) and group stamps, allocated the
-// first time a document passes 64 pending edits
-static mt_status ensure_groups(mt_engine* e) {
-    mt_gstate& g = e->g;
-    if (g.gmx) return MT_OK;
-    const size_t D = e->cfg.max_docs;
-    mt_status st = MT_OK;
-    if ((st = dalloc(e, &g.locx, D)) || (st = dalloc(e, &g.gmx, D * 4 * g.locstride))) {
-        g.gmx = nullptr;
-        return st;
+    const uint32_t kb = pool_reserve(e->nbig, e->bigcap, (uint32_t)nb.size(), [&](uint32_t r) { return grow_big(e, r); });
+    for (uint32_t i = 0; i < kb; i++) {
+        const uint32_t d = nb[i], r = e->nbig++;
+        const size_t o = (size_t)r * MT_LOC_BIGCAP, s = (size_t)d * MT_LOC_CAP;
+        HIP_OK(hipMemcpy(g.gmb + o, g.gm + s, MT_LOC_CAP * 8, hipMemcpyDeviceToDevice));
+        HIP_OK(hipMemcpy(g.pkb + o, g.pk + s, MT_LOC_CAP * 8, hipMemcpyDeviceToDevice));
+        HIP_OK(hipMemcpy(g.ctb + o, g.ct + s, MT_LOC_CAP * 4, hipMemcpyDeviceToDevice));
+        HIP_OK(hipMemcpy(g.lsqb + o, g.lsq + s, MT_LOC_CAP * 8, hipMemcpyDeviceToDevice));
+        e->h_locbig[d] = r;
+        HIP_OK(hipMemcpy(g.locbig + d, &r, 4, hipMemcpyHostToDevice));
     }
-    HIP_OK(hipMemset(g.locx, 0, D * sizeof(mt_locx)));
-    HIP_OK(hipMemset(g.gmx, 0, D * 4 * g.locstride * sizeof(uint64_t)));
+    const uint32_t kg = pool_reserve(e->ngx, e->gxcap, (uint32_t)ng.size(), [&](uint32_t r) { return grow_gx(e, r); });
+    for (uint32_t i = 0; i < kg; i++) {
+        const uint32_t d = ng[i], r = e->ngx++;
+        e->h_locgx[d] = r;
+        HIP_OK(hipMemcpy(g.locgx + d, &r, 4, hipMemcpyHostToDevice));
+    }
     return MT_OK;
 }
 
@@ -298,7 +355,6 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
     g.ibcap = g.segcap / 8 + 8;
     g.hcap = e->cfg.heap_capacity;
     g.textcap = e->cfg.text_capacity;
-    g.locstride = MT_LOC_CAP;
     mt_status st = MT_OK;
     const size_t S = D * g.segcap;
     if ((st = dalloc(e, &g.seq, S)) || (st = dalloc(e, &g.rseq, S)) || (st = dalloc(e, &g.len, S)) ||
@@ -311,7 +367,8 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.gm, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pk, D * MT_LOC_CAP)) ||
         (st = dalloc(e, &g.ct, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
         (st = dalloc(e, &g.lsq, D * MT_LOC_CAP)) || (st = dalloc(e, &g.rg, D * MT_RG_RECS)) ||
-        (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) ||
+        (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) || (st = dalloc(e, &g.locbig, D)) ||
+        (st = dalloc(e, &g.locgx, D)) ||
         // (the editing documents' and the wide documents' buckets after the capacity classes)
         (st = dalloc(e, &e->d_counts, kBuckets)) || (st = dalloc(e, &e->d_acc, kBuckets)) ||
         (st = dalloc(e, &e->d_ids, D * kBuckets))) {
@@ -325,6 +382,10 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         return MT_ERR_HIP;
     }
     HIP_OK(hipMemcpy(e->d_classes, kClassParams, sizeof(kClassParams), hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(g.locbig, 0xFF, D * sizeof(uint32_t)));  // MT_NO_ROW
+    HIP_OK(hipMemset(g.locgx, 0xFF, D * sizeof(uint32_t)));
+    e->h_locbig.assign(D, MT_NO_ROW);
+    e->h_locgx.assign(D, MT_NO_ROW);
     {
         const char* v = getenv("MTGPU_ENGINE");
         // the register engine keeps text offsets in 16 bits (textcap <= 64 KiB)
@@ -357,6 +418,9 @@ mt_status mt_engine_destroy(mt_engine* e) {
     if (e->g.ev) (void)hipFree(e->g.ev);
     if (e->g.evn) (void)hipFree(e->g.evn);
     if (e->ws) (void)hipFree(e->ws);
+    for (void* p : {(void*)e->g.gmb, (void*)e->g.pkb, (void*)e->g.ctb, (void*)e->g.lsqb, (void*)e->g.gmx,
+                    (void*)e->g.locx})
+        if (p) (void)hipFree(p);
     if (e->h_counts) hipHostFree(e->h_counts);
     for (auto ev : e->kev) (void)hipEventDestroy(ev);
     if (e->ev0) hipEventDestroy(e->ev0);
@@ -503,6 +567,75 @@ mt_status mt_find_tiles(mt_engine* e, const mt_tile_query* q, uint32_t n, mt_til
     return r == hipSuccess ? MT_OK : MT_ERR_HIP;
 }
 
+mt_status mt_resolve_positions(mt_engine* e, const mt_pos_query* q, uint32_t n, mt_pos_result* out) {
+    static_assert(sizeof(mt_pos_query) == 16 && sizeof(mt_pos_result) == 16, "mt_pos_query / result are 16 bytes");
+    if (!e || (n && (!q || !out))) return MT_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if (q[i].doc >= e->n_docs || q[i].kind > MT_POS_OF_ORDINAL) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    void* buf = nullptr;
+    const size_t qb = (size_t)n * sizeof(mt_pos_query), rb = (size_t)n * sizeof(mt_pos_result);
+    if (hipMalloc(&buf, qb + rb) != hipSuccess) return MT_ERR_NOMEM;
+    auto* dq = static_cast<mt_pos_query*>(buf);
+    auto* dr = reinterpret_cast<mt_pos_result*>(static_cast<uint8_t*>(buf) + qb);
+    hipError_t r = hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = mt_launch_resolve(&e->g, dq, n, dr, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(out, dr, rb, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    return r == hipSuccess ? MT_OK : MT_ERR_HIP;
+}
+
+mt_status mt_resolve_positions_device(mt_engine* e, const mt_pos_query* d_q, uint32_t n, mt_pos_result* d_out) {
+    if (!e || (n && (!d_q || !d_out))) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    HIP_OK(mt_launch_resolve(&e->g, d_q, n, d_out, e->stream));
+    return MT_OK;
+}
+
+mt_status mt_segment_infos(mt_engine* e, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out) {
+    static_assert(sizeof(mt_seg_info) == 80, "mt_seg_info is 80 bytes");
+    if (!e || (n && (!docs || !ordinals || !out))) return MT_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if (docs[i] >= e->n_docs) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    void* buf = nullptr;
+    const size_t db = (size_t)n * 4, ob = (size_t)n * sizeof(mt_seg_info);
+    if (hipMalloc(&buf, 2 * db + ob) != hipSuccess) return MT_ERR_NOMEM;
+    auto* dd = static_cast<uint32_t*>(buf);
+    auto* dor = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(buf) + db);
+    auto* dout = reinterpret_cast<mt_seg_info*>(static_cast<uint8_t*>(buf) + 2 * db);
+    hipError_t r = hipMemcpyAsync(dd, docs, db, hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(dor, ordinals, db, hipMemcpyHostToDevice, e->stream);
+    if (r == hipSuccess) r = mt_launch_seginfo(&e->g, dd, dor, n, dout, e->stream);
+    if (r == hipSuccess) r = hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    return r == hipSuccess ? MT_OK : MT_ERR_HIP;
+}
+
+mt_status mt_segment_text(mt_engine* e, uint32_t doc, uint32_t toff, uint32_t len, uint16_t* out) {
+    if (!e || doc >= e->n_docs || (len && !out)) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    mt_doc_scalars sc;
+    HIP_OK(hipMemcpyAsync(&sc, e->g.sc + doc, sizeof sc, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if ((uint64_t)toff + len > sc.text_top) return MT_ERR_ARG;
+    if (!len) return MT_OK;
+    const size_t base = ((size_t)doc * 2 + sc.text_half) * e->g.textcap;
+    if (sc.wide & MT_WIDE_DOC) {
+        HIP_OK(hipMemcpy(out, e->g.text + base + (size_t)toff * 2, (size_t)len * 2, hipMemcpyDeviceToHost));
+        return MT_OK;
+    }
+    std::vector<uint8_t> b(len);
+    HIP_OK(hipMemcpy(b.data(), e->g.text + base + toff, len, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < len; i++) out[i] = b[i];
+    return MT_OK;
+}
+
 mt_status mt_regen_drain(mt_engine* e, uint32_t doc, mt_op_rec* recs, uint32_t cap, uint8_t* payload, uint32_t pcap,
                          uint32_t* n, uint32_t* pn) {
     if (!e || doc >= e->n_docs || !n || !pn) return MT_ERR_ARG;
@@ -556,8 +689,10 @@ mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
     e->g.ev = nullptr;
     e->g.evn = nullptr;
     e->g.evcap = 0;
-    // the register engine's hot loop records nothing: every class runs on the LDS engine meanwhile
-    e->use_reg = per_doc ? false : e->reg_default;
+    // the register engine records events in its own kernels (mtr::reg_apply_kernel_ev; its C64
+    // documents on the LDS engine); MTGPU_EV_ENGINE=lds keeps every class on the LDS engine instead
+    const char* evw = getenv("MTGPU_EV_ENGINE");
+    e->use_reg = (per_doc && evw && strcmp(evw, "lds") == 0) ? false : e->reg_default;
     e->first_lds = e->use_reg ? kFirstLds : 0;
     if (!per_doc) return MT_OK;
     const size_t D = e->cfg.max_docs;
@@ -724,8 +859,8 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         for (int q = 0; q < kLocForms; q++) {
             const uint32_t cnt = e->h_counts[lds_base + 2 * e->first_lds + q];
             if ((kLocCaps[q] <= MT_LOC_CAP && kLocGW[q] == 1) || !cnt) continue;
-            mt_status ls = ensure_locstride(e, (uint32_t)std::max(kLocCaps[q], MT_LOC_CAP));
-            if (!ls && kLocGW[q] > 1) ls = ensure_groups(e);
+            const mt_status ls = assign_loc_rows(e, e->d_ids + (size_t)(lds_base + 2 * e->first_lds + q) * b->n_docs,
+                                                 cnt, kLocCaps[q] > MT_LOC_CAP, kLocGW[q] > 1);
             if (ls) return ls;
             lws_off[q] = need;
             need += (size_t)cnt * mt_lds_bytes_loc(kLocCaps[q], kLocGW[q]);
@@ -756,7 +891,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], st));
             if (e->use_reg && kClasses[c] <= kRegMaxCap)
-                HIP_OK(mt_launch_apply_reg(kClasses[c], 0, &e->g, b->ops, b->payload, b->row_ptr,
+                HIP_OK(mt_launch_apply_reg(kClasses[c], e->g.ev ? 2 : 0, &e->g, b->ops, b->payload, b->row_ptr,
                                            e->d_ids + (size_t)c * b->n_docs, cnt, lo, per, st));
             else if (c >= kLdsClasses)
                 HIP_OK(mt_launch_apply_big(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
@@ -789,7 +924,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], st));
-            if (c64)
+            if (c64 && !e->g.ev)
                 HIP_OK(mt_launch_apply_reg(kClasses[c], 1, &e->g, b->ops, b->payload, b->row_ptr,
                                            e->d_ids + (size_t)(lds_base + q) * b->n_docs, cnt, lo, per, st));
             else
@@ -1078,12 +1213,14 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 1>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if ((capacity & MT_CLASS_C64) && e->g.ev)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_C64)));
     else if (capacity & MT_CLASS_C64)
         snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel_c64<%u>", (capacity & ~(uint32_t)MT_CLASS_C64) / 64);
     else if (capacity & MT_CLASS_LDS)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_LDS)));
     else if (e->use_reg && capacity <= (uint32_t)kRegMaxCap)
-        snprintf(tmp, sizeof tmp, "mtr::reg_apply_kernel<%u>", capacity / 64);
+        snprintf(tmp, sizeof tmp, e->g.ev ? "mtr::reg_apply_kernel_ev<%u>" : "mtr::reg_apply_kernel<%u>", capacity / 64);
     else if (capacity > 2048)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u>", capacity);
     else

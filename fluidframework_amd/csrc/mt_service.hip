@@ -609,6 +609,101 @@ extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q
     return hipGetLastError();
 }
 
+// mt_resolve_positions: MergeTree.getContainingSegment / getPosition for a batch of queries, one wave
+// per query over the document's compact state in HBM (include/mtgpu.h).  The B-tree walk of
+// searchBlock (mergeTree.ts:1797-1829) descends into the first child whose length in the view exceeds
+// what is left of pos; over the leaves in order that is the first leaf whose inclusive view prefix
+// exceeds pos -- a wave prefix sum per 64 leaves, stopping at the chunk that holds it.  getPosition
+// (mergeTree.ts:1585-1602) sums the local view's lengths before the leaf.
+__global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_pos_query* __restrict__ q, uint32_t nq,
+                                                        mt_pos_result* __restrict__ out) {
+    const uint32_t w = blockIdx.x;
+    if (w >= nq) return;
+    const int lane = lane_id();
+    const mt_pos_query qq = q[w];
+    const uint32_t d = qq.doc;
+    const mt_doc_scalars sc = g.sc[d];
+    const int n = sc.nseg;
+    const size_t so = (size_t)d * g.segcap;
+    const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+    const bool local = qq.ref_seq == MT_POS_LOCAL;
+    const int32_t R = qq.ref_seq;
+    const uint32_t C = qq.client;
+    auto view_len = [&](int i) -> int {  // nodeLength's leaf branch (mergeTree.ts:1659-1697)
+        const bool rm = (g.flags[so + i] & MT_SF_REMOVED) != 0;
+        if (local) return rm ? 0 : (int)g.len[so + i];
+        const bool seen = g.client[so + i] == C || g.seq[so + i] <= R;
+        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0 : (wdoc && mt_ovx_has(g.ovx[so + i], C));
+        const bool hid = rm && (g.rclient[so + i] == C || ov || g.rseq[so + i] <= R);
+        return (seen && !hid) ? (int)g.len[so + i] : 0;
+    };
+    mt_pos_result r{-1, 0, 0, 0};
+    int vcarry = 0, lcarry = 0;
+    const bool by_ord = qq.kind == MT_POS_OF_ORDINAL;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        const int vl = i < n ? view_len(i) : 0;
+        const int ll = (i < n && !(g.flags[so + i] & MT_SF_REMOVED)) ? (int)g.len[so + i] : 0;
+        const int vincl = vcarry + wave_incl_scan(vl);
+        const int lincl = lcarry + wave_incl_scan(ll);
+        const uint64_t m = wave_ballot(i < n && (by_ord ? i == qq.pos : qq.pos < vincl));
+        if (m) {
+            const int l = first_lane(m);
+            r.ordinal = base + l;
+            r.offset = qq.pos - __builtin_amdgcn_readlane(vincl - vl, l);
+            r.position = __builtin_amdgcn_readlane(lincl - ll, l);
+            r.length = g.len[so + base + l];
+            if (by_ord) r.offset = 0;
+            break;
+        }
+        vcarry = __builtin_amdgcn_readlane(vincl, 63);
+        lcarry = __builtin_amdgcn_readlane(lincl, 63);
+    }
+    if (r.ordinal < 0) {  // none: offset = pos minus the view's length, position = the local length
+        r.offset = qq.pos - vcarry;
+        r.position = lcarry;
+    }
+    if (lane == 0) out[w] = r;
+}
+
+// mt_segment_infos: one thread per (document, ordinal) pair gathers the segment's fields
+__global__ void mt_seginfo_kernel(mt_gstate g, const uint32_t* __restrict__ docs, const int32_t* __restrict__ ords,
+                                  uint32_t n, mt_seg_info* __restrict__ out) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n) return;
+    const uint32_t d = docs[w];
+    const int32_t i = ords[w];
+    const mt_doc_scalars sc = g.sc[d];
+    mt_seg_info r{};
+    r.seq = INT32_MIN;
+    if (i >= 0 && i < sc.nseg) {
+        const size_t so = (size_t)d * g.segcap + i;
+        const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0 && g.ovx;
+        const uint8_t f = g.flags[so];
+        const bool rm = (f & MT_SF_REMOVED) != 0;
+        r.seq = g.seq[so];
+        r.rseq = rm ? g.rseq[so] : -1;
+        r.client = mt_canon_client(g.client[so]);
+        r.rclient = rm ? (int32_t)g.rclient[so] : -1;
+        r.len = g.len[so];
+        r.flags = f & (MT_SF_REMOVED | MT_SF_PDEF | MT_SF_MARKER);
+        r.toff = g.toff[so];
+        r.wide = wdoc ? 1u : 0u;
+        r.overlap = g.ovl[so];
+        r.overlap_hi = wdoc ? g.ovx[so] : 0ull;
+        const uint64_t p = g.props[so];
+        for (int k = 0; k < 8; k++) {
+            uint32_t v = (uint32_t)(p >> (8 * k)) & 0xFFu;
+            if (wdoc) v |= ((uint32_t)(g.ph[so] >> (8 * k)) & 0xFFu) << 8;
+            r.props[k] = (uint16_t)v;
+            if (wdoc)
+                r.props[8 + k] = (uint16_t)(((uint32_t)(g.pxl[so] >> (8 * k)) & 0xFFu) |
+                                            (((uint32_t)(g.pxh[so] >> (8 * k)) & 0xFFu) << 8));
+        }
+    }
+    out[w] = r;
+}
+
 // mt_range_stacks: Client.getStackContext for a batch of (document, position, label) queries, one wave
 // per query (include/mtgpu.h; mergeTree.ts:1750-1760, 953-994, 246-261).  The stack is always its
 // unmatched ends followed by its unmatched begins (an end is pushed only when the top is not a
@@ -783,5 +878,18 @@ extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32
                                          uint32_t* specs, uint32_t* counts, hipStream_t st) {
     if (n_docs == 0) return hipSuccess;
     hipLaunchKernelGGL(mt_snapshot_kernel, dim3(n_docs), dim3(64), 0, st, *g, d0, n_docs, cap, specs, counts);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, mt_pos_result* out,
+                                        hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_resolve_kernel, dim3(n), dim3(64), 0, st, *g, q, n, out);
+    return hipGetLastError();
+}
+extern "C" hipError_t mt_launch_seginfo(const mt_gstate* g, const uint32_t* docs, const int32_t* ords, uint32_t n,
+                                        mt_seg_info* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mt_seginfo_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *g, docs, ords, n, out);
     return hipGetLastError();
 }

@@ -79,6 +79,8 @@ struct mt_locx {
 #define MT_RG_RECS 256       // regenerated op records per document between drains
 #define MT_RG_BYTES 4096     // and their payload bytes
 #define MT_LOC_CAP 1024      // the editing form's largest LDS capacity (above: its HBM-workspace form)
+#define MT_LOC_BIGCAP 4096   // the editing form's largest class: the slots of a big-pool row
+#define MT_NO_ROW 0xFFFFFFFFu
 // pending property counts per segment (SegmentPropertiesManager, segmentPropertiesManager.ts:11-12):
 // 7 bits per key id 0..7 at bit 7k, the pending rewrite count in bits 56..63
 #define MT_PK_KEY(pk, k) ((uint32_t)((pk) >> (7 * (k))) & 0x7Fu)
@@ -116,19 +118,26 @@ struct mt_gstate {
     uint8_t* text;     // [doc][2][textcap]  text arena, double-buffered for in-kernel compaction
     struct mt_event* ev;  // [doc][evcap] delta / maintenance events (mt_events_enable), or null
     uint32_t* evn;     // [doc] events recorded since the last drain (may exceed evcap: halted)
-    // editing documents, [doc][locstride]: MT_LOC_CAP slots per document until a document's editing
-    // form needs a larger class (its HBM-workspace form), then the engine re-lays them at that class
+    // editing documents, [doc][MT_LOC_CAP]: MT_LOC_CAP slots per document (mt_loc_row)
     uint64_t* gm;      // pending group mask per segment
     uint64_t* pk;      // pending property counts (MT_PK_*)
     uint32_t* ct;      // creation stamp
     uint64_t* lsq;     // localSeq (low 32 bits) / localRemovedSeq (high), 0: undefined
     mt_loc* loc;       // [doc]
-    // MT_WIDE_GROUPS documents (allocated on first need, else null): the group masks, 4 words per
-    // segment ([doc][locstride][4]), and the groups' stamps / localSeqs
+    // an editing document whose form needs more than MT_LOC_CAP slots (its HBM-workspace form) gets a
+    // row of MT_LOC_BIGCAP slots in the big pool ([row][MT_LOC_BIGCAP], grown by the engine as
+    // documents need rows) and keeps its state there from then on: locbig[doc] = that row, or MT_NO_ROW
+    uint64_t* gmb;
+    uint64_t* pkb;
+    uint32_t* ctb;
+    uint64_t* lsqb;
+    uint32_t* locbig;  // [doc]
+    // MT_WIDE_GROUPS documents: a row of the group pool (locgx[doc], or MT_NO_ROW), the group masks,
+    // 4 words per segment ([row][MT_LOC_BIGCAP][4]), and the groups' stamps / localSeqs ([row])
     uint64_t* gmx;
-    mt_locx* locx;     // [doc]
+    mt_locx* locx;
+    uint32_t* locgx;   // [doc]
     struct mt_op_rec* rg;  // [doc][MT_RG_RECS] regenerated ops (seq = the resetting record's index)
     uint8_t* rgp;      // [doc][MT_RG_BYTES] their payload
     uint32_t segcap, lbcap, ibcap, hcap, textcap, evcap;
-    uint32_t locstride;  // slots per document of gm / pk / ct / lsq
 };

@@ -32,6 +32,11 @@ DOC_ERRORS = {0: None,
 TILE_QUERY_DTYPE = np.dtype([('doc', '<u4'), ('pos', '<i4'), ('key', 'u1'), ('preceding', 'u1'), ('pad0', 'u1'),
                              ('pad1', 'u1'), ('vmask', '<u4', (8,)), ('pad2', '<u4')])
 TILE_RESULT_DTYPE = np.dtype([('pos', '<i4'), ('ordinal', '<i4')])
+# mt_pos_query / mt_pos_result (include/mtgpu.h): getContainingSegment / getPosition queries
+POS_QUERY_DTYPE = np.dtype([('doc', '<u4'), ('pos', '<i4'), ('ref_seq', '<i4'), ('client', '<u2'), ('kind', '<u2')])
+POS_RESULT_DTYPE = np.dtype([('ordinal', '<i4'), ('offset', '<i4'), ('position', '<i4'), ('length', '<u4')])
+POS_CONTAINING, POS_OF_ORDINAL, POS_LOCAL = 0, 1, -2**31
+assert POS_QUERY_DTYPE.itemsize == 16 and POS_RESULT_DTYPE.itemsize == 16
 assert TILE_QUERY_DTYPE.itemsize == 48
 # mt_stack_item (include/mtgpu.h "range stacks")
 STACK_ITEM_DTYPE = np.dtype([('pos', '<i4'), ('ordinal', '<i4'), ('ref_type', '<u4')])
@@ -94,6 +99,10 @@ def lib():
         L.mt_get_snapshots.argtypes = [vp, u32, u32, u32, ctypes.POINTER(ctypes.c_char_p), u32, ctypes.c_char_p, u64,
                                        vp]
         L.mt_find_tiles.argtypes = [vp, vp, u32, vp]
+        for name in ('mt_resolve_positions', 'mt_resolve_positions_device'):  # (absent from older A/B builds)
+            if hasattr(L, name):
+                getattr(L, name).argtypes = [vp, vp, u32, vp]
+                getattr(L, name).restype = ctypes.c_int
         L.mt_range_stacks.argtypes = [vp, vp, u32, u32, vp, vp]
         L.mt_regen_drain.argtypes = [vp, u32, vp, u32, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.mt_events_enable.argtypes = [vp, u32]
@@ -105,6 +114,7 @@ def lib():
                      'mt_checksums', 'mt_doc_error', 'mt_last_apply_stats', 'mt_seg_counts', 'mt_synth_generate',
                      'mt_batch_copy_docs', 'mt_batch_info', 'mt_last_apply_class_stats', 'mt_class_kernel_name',
                      'mt_get_snapshot', 'mt_get_snapshots', 'mt_snapshot_extract', 'mt_find_tiles', 'mt_range_stacks', 'mt_regen_drain', 'mt_set_concurrent_classes',
+
                      'mt_events_enable', 'mt_events_drain', 'mt_set_label_keys'):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -266,6 +276,14 @@ class MergeEngine:
         q = np.ascontiguousarray(queries, dtype=TILE_QUERY_DTYPE)
         out = np.zeros(len(q), dtype=TILE_RESULT_DTYPE)
         _check(lib().mt_find_tiles(self.h, _ptr(q), len(q), _ptr(out)), 'mt_find_tiles')
+        return out
+
+    def resolve_positions(self, queries):
+        """MergeTree.getContainingSegment / getPosition for a batch of POS_QUERY_DTYPE rows
+        (mt_resolve_positions): POS_RESULT_DTYPE rows (ordinal -1: none)."""
+        q = np.ascontiguousarray(queries, dtype=POS_QUERY_DTYPE)
+        out = np.zeros(len(q), dtype=POS_RESULT_DTYPE)
+        _check(lib().mt_resolve_positions(self.h, _ptr(q), len(q), _ptr(out)), 'mt_resolve_positions')
         return out
 
     def regen_drain(self, doc):

@@ -335,6 +335,61 @@ typedef struct mt_tile_result {
  * refuses the query, so a label never goes unmatched silently) */
 mt_status mt_find_tiles(mt_engine* eng, const mt_tile_query* q, uint32_t n, mt_tile_result* out);
 
+/* ---- position queries (SURVEY.md §8(b) read surface) -------------------------------------------
+ * MergeTree.getContainingSegment(pos, refSeq, clientId) (mergeTree.ts:1623-1634 through searchBlock,
+ * :1797-1829; Client.getContainingSegment client.ts:1004-1007 uses the local view) and
+ * MergeTree.getPosition(segment, currentSeq, own client) (mergeTree.ts:1585-1602; Client.getPosition
+ * client.ts:290-292) for a batch of queries, one wave per query over the document's state in HBM:
+ *   MT_POS_CONTAINING: the first segment whose view length exceeds what is left of pos (pos minus the
+ *     view lengths of the segments before it) -- for pos < 0 the first segment, for pos past the
+ *     view's length none (ordinal -1); offset = pos minus the view length before it;
+ *   MT_POS_OF_ORDINAL: the segment of ordinal `pos` (its index among the linked segments).
+ * With no such segment: ordinal -1, offset = pos minus the view's whole length, position = the
+ * local view's whole length (resolveRemoteClientPosition's end-of-view case, mergeTree.ts:2105-2127). 
+ * The view is (ref_seq, client) -- nodeLength's leaf branch, mergeTree.ts:1659-1697 -- or, with
+ * ref_seq = MT_POS_LOCAL, the local view (a removed segment has length 0; an editing client's
+ * pending inserts count): Client's own reads.  position is always the local view's (getPosition). */
+#define MT_POS_CONTAINING 0u
+#define MT_POS_OF_ORDINAL 1u
+#define MT_POS_LOCAL INT32_MIN
+typedef struct mt_pos_query {   /* 16 bytes */
+    uint32_t doc;
+    int32_t pos;                /* a position in the view, or an ordinal (MT_POS_OF_ORDINAL) */
+    int32_t ref_seq;            /* the view's refSeq, or MT_POS_LOCAL */
+    uint16_t client;            /* the view's short client id (ignored for MT_POS_LOCAL) */
+    uint16_t kind;              /* MT_POS_CONTAINING / MT_POS_OF_ORDINAL */
+} mt_pos_query;
+typedef struct mt_pos_result {  /* 16 bytes */
+    int32_t ordinal;            /* the segment's index among the linked segments, -1: none */
+    int32_t offset;             /* MT_POS_CONTAINING: pos relative to the segment's start in the view */
+    int32_t position;           /* the segment's local-view position (getPosition) */
+    uint32_t length;            /* its cachedLength */
+} mt_pos_result;
+mt_status mt_resolve_positions(mt_engine* eng, const mt_pos_query* q, uint32_t n, mt_pos_result* out);
+/* the same with device-resident queries and results (no copies, no synchronisation beyond the stream) */
+mt_status mt_resolve_positions_device(mt_engine* eng, const mt_pos_query* d_q, uint32_t n, mt_pos_result* d_out);
+
+/* One segment's fields, by ordinal, for a batch of (document, ordinal) pairs (a reader that holds a
+ * segment found by mt_resolve_positions, e.g. Client.getPropertiesAtPosition client.ts:1009-1023):
+ * one small gather kernel and one copy, not a whole-document read.  ordinal past the document's
+ * segments: seq = INT32_MIN.  Text: mt_segment_text. */
+typedef struct mt_seg_info {    /* 80 bytes */
+    int32_t seq;                /* INT32_MIN: no such segment */
+    int32_t rseq;               /* removedSeq, -1: not removed */
+    int32_t client;             /* short client id; -2 = NonCollabClient (constants.ts:15) */
+    int32_t rclient;            /* removedClientId, -1: not removed */
+    uint32_t len;               /* cachedLength (UTF-16 code units) */
+    uint32_t flags;             /* MT_SF_* of mt_state.h: 1 removed, 2 properties defined, 16 marker */
+    uint32_t toff;              /* its text in the document's arena (code units) */
+    uint32_t wide;              /* 1: a wide document (UTF-16 arena) */
+    uint64_t overlap;           /* removedClientOverlap: bit c for ids c < 64 */
+    uint64_t overlap_hi;        /* a wide document's overlapping removers >= 64: up to 8 ids, one per byte */
+    uint16_t props[16];         /* value id per key (0: absent) */
+} mt_seg_info;
+mt_status mt_segment_infos(mt_engine* eng, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out);
+/* a segment's text: `len` code units of document doc's arena at `toff` (from mt_seg_info) */
+mt_status mt_segment_text(mt_engine* eng, uint32_t doc, uint32_t toff, uint32_t len, uint16_t* out);
+
 /* The ops document `doc` regenerated at its MT_SEQ_REGEN records since the last drain (at most 256
  * records / 4 KiB of payload between drains, else MT_DERR_CAPACITY): per regenerated op one
  * MT_OP_NOOP header record whose seq is the index of the resetting record within the document's

@@ -26,6 +26,8 @@ const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
 const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const OP_WIDE = 0x80;  // MT_OP_WIDE: UTF-16 text, (key u8, value u16) pairs
 const OP_NP16 = 0x40;  // MT_OP_NP16: property pair count bit 4 (wide records)
+// mt_pos_query (include/mtgpu.h): kinds, and the local view's refSeq
+const POS_CONTAINING = 0, POS_OF_ORDINAL = 1, POS_LOCAL = -2147483648;
 // include/mtgpu.h "limits": the wide form's (a document goes wide with its first op beyond the narrow
 // ones: client id >= 64, key >= 8, value id >= 256 or a code unit above U+00FF)
 const MAX_CLIENTS = 254, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
@@ -549,16 +551,66 @@ class BatchClient {
             (d.removedSeq !== -1 && d.removedSeq <= refSeq))) return 0;
         return d.cachedLength;
     }
-    _containing(segs, pos, refSeq, clientId, local) {  // MergeTree.getContainingSegment (mergeTree.ts:1623-1634)
-        for (const d of segs) {
-            const len = BatchClient._viewLength(d, refSeq, clientId, local);
-            if (pos < len) return { segment: d, offset: pos };
-            pos -= len;
+    // ---- device queries (include/mtgpu.h mt_resolve_positions / mt_segment_infos): one wave per
+    // query over the document's state in HBM, no whole-document read.  A descriptor from them carries
+    // {ordinal, position, cachedLength} at once; its other fields are read from the device on first
+    // access (one segment's row), so it too is valid until the document next changes.
+    _resolve(kind, pos, refSeq, clientId) {
+        this.engine.flush();
+        this._checkError();
+        const q = Buffer.alloc(16);
+        q.writeUInt32LE(this.doc, 0);
+        q.writeInt32LE(pos, 4);
+        q.writeInt32LE(refSeq === undefined ? POS_LOCAL : refSeq, 8);
+        q.writeUInt16LE(clientId || 0, 12);
+        q.writeUInt16LE(kind, 14);
+        const r = native.resolvePositions(this.engine.handle, q);
+        return { ordinal: r.readInt32LE(0), offset: r.readInt32LE(4), position: r.readInt32LE(8), length: r.readUInt32LE(12) };
+    }
+    _descriptor(ordinal, position, cachedLength) {
+        const self = this;
+        let info;
+        const load = () => {
+            if (info) return info;
+            const docs = Buffer.alloc(4), ords = Buffer.alloc(4);
+            docs.writeUInt32LE(self.doc, 0);
+            ords.writeInt32LE(ordinal, 0);
+            const b = native.segmentInfos(self.engine.handle, docs, ords);
+            const flags = b.readUInt32LE(20), removed = (flags & 1) !== 0;
+            const overlap = [];
+            const lo = b.readUInt32LE(32), hi = b.readUInt32LE(36);
+            for (let c = 0; c < 32; c++) if ((lo >>> c) & 1) overlap.push(c);
+            for (let c = 0; c < 32; c++) if ((hi >>> c) & 1) overlap.push(32 + c);
+            for (let k = 0; k < 8; k++) { const c = b.readUInt8(40 + k); if (c) overlap.push(c); }
+            let properties;
+            if (flags & 2) {
+                properties = {};
+                for (let kid = 0; kid < 16; kid++) {
+                    const vid = b.readUInt16LE(48 + 2 * kid);
+                    if (vid) properties[self.keys[kid]] = self.values[kid][vid];
+                }
+            }
+            info = { seq: b.readInt32LE(0), clientId: b.readInt32LE(8),
+                removedSeq: removed ? b.readInt32LE(4) : undefined, removedClientId: removed ? b.readInt32LE(12) : undefined,
+                removedClientOverlap: overlap.length ? overlap : undefined, properties,
+                marker: (flags & 16) !== 0, toff: b.readUInt32LE(24), len: b.readUInt32LE(16) };
+            return info;
+        };
+        const text = () => native.segmentText(self.engine.handle, self.doc, load().toff, load().len);
+        const d = { ordinal, position, cachedLength };
+        for (const k of ["seq", "clientId", "removedSeq", "removedClientId", "removedClientOverlap", "properties"]) {
+            Object.defineProperty(d, k, { get: () => load()[k], enumerable: true });
         }
-        return { segment: undefined, offset: undefined };
+        Object.defineProperty(d, "text", { get: () => (load().marker ? undefined : text()), enumerable: true });
+        Object.defineProperty(d, "refType", { get: () => (load().marker ? text().charCodeAt(0) : undefined), enumerable: true });
+        return d;
     }
     /** Client.getContainingSegment (client.ts:1004-1007): {segment, offset} in the local view. */
-    getContainingSegment(pos) { return this._containing(this._segments(), pos, 0, 0, true); }
+    getContainingSegment(pos) {
+        const r = this._resolve(POS_CONTAINING, pos);
+        if (r.ordinal < 0) return { segment: undefined, offset: undefined };
+        return { segment: this._descriptor(r.ordinal, r.position, r.length), offset: r.offset };
+    }
     /** Client.getPropertiesAtPosition (client.ts:1009-1023). */
     getPropertiesAtPosition(pos) {
         const seg = this.getContainingSegment(pos).segment;
@@ -566,15 +618,14 @@ class BatchClient {
     }
     /** Client.getRangeExtentsOfPosition (client.ts:1024-1040). */
     getRangeExtentsOfPosition(pos) {
-        const seg = this.getContainingSegment(pos).segment;
-        return seg ? { posStart: seg.position, posAfterEnd: seg.position + seg.cachedLength }
+        const r = this._resolve(POS_CONTAINING, pos);
+        return r.ordinal >= 0 ? { posStart: r.position, posAfterEnd: r.position + r.length }
             : { posStart: undefined, posAfterEnd: undefined };
     }
     /** Client.getPosition (client.ts:290-292): the local-view position of the segment (by ordinal). */
     getPosition(segment) {
-        const segs = this._segments();
-        const d = segs[segment.ordinal];
-        return d ? d.position : 0;
+        const r = this._resolve(POS_OF_ORDINAL, segment.ordinal);
+        return r.ordinal >= 0 ? r.position : 0;
     }
     /**
      * Client.walkSegments (client.ts:275-284, MergeTree.mapRange / nodeMap mergeTree.ts:2903-2960):
@@ -620,11 +671,9 @@ class BatchClient {
     resolveRemoteClientPosition(remoteClientPosition, remoteClientRefSeq, remoteClientId) {
         const cid = this._shortId(remoteClientId);
         const local = cid === this._shortId(this.longClientId);  // (nodeLength: the own client sees the local view)
-        const segs = this._segments();
-        const r = this._containing(segs, remoteClientPosition, remoteClientRefSeq, cid, local);
-        if (r.segment) return r.segment.position + r.offset;
-        const rlen = segs.reduce((a, d) => a + BatchClient._viewLength(d, remoteClientRefSeq, cid, local), 0);
-        if (remoteClientPosition === rlen) return segs.reduce((a, d) => a + BatchClient._viewLength(d, 0, 0, true), 0);
+        const r = this._resolve(POS_CONTAINING, remoteClientPosition, local ? undefined : remoteClientRefSeq, cid);
+        if (r.ordinal >= 0) return r.position + r.offset;
+        if (r.offset === 0) return r.position;  // at the end of the remote view: the local length
         return undefined;
     }
 

@@ -367,6 +367,78 @@ static napi_value find_tiles(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* resolvePositions(engine, queries (16-byte mt_pos_query rows)) -> Buffer of 16-byte mt_pos_result rows */
+static napi_value resolve_positions(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 2 ? get_box(env, argv[0]) : NULL;
+    size_t nq = 0;
+    const void* q = b ? buffer_data(env, argv[1], &nq) : NULL;
+    if (!b || nq % sizeof(mt_pos_query)) {
+        napi_throw_type_error(env, NULL, "resolvePositions(engine, queries)");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(nq / sizeof(mt_pos_query));
+    void* data = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(mt_pos_result) : 1, &data, &out));
+    enter(b);
+    mt_status st = mt_resolve_positions(b->e, (const mt_pos_query*)q, n, (mt_pos_result*)data);
+    leave(b);
+    if (st) return throw_status(env, "mt_resolve_positions", st);
+    return out;
+}
+
+/* segmentInfos(engine, docs (uint32 rows), ordinals (int32 rows)) -> Buffer of 80-byte mt_seg_info rows */
+static napi_value segment_infos(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 3 ? get_box(env, argv[0]) : NULL;
+    size_t nd = 0, no = 0;
+    const void* docs = b ? buffer_data(env, argv[1], &nd) : NULL;
+    const void* ords = b ? buffer_data(env, argv[2], &no) : NULL;
+    if (!b || nd % 4 || nd != no) {
+        napi_throw_type_error(env, NULL, "segmentInfos(engine, docs, ordinals)");
+        return NULL;
+    }
+    const uint32_t n = (uint32_t)(nd / 4);
+    void* data = NULL;
+    NAPI_CALL(env, napi_create_buffer(env, n ? n * sizeof(mt_seg_info) : 1, &data, &out));
+    enter(b);
+    mt_status st = mt_segment_infos(b->e, (const uint32_t*)docs, (const int32_t*)ords, n, (mt_seg_info*)data);
+    leave(b);
+    if (st) return throw_status(env, "mt_segment_infos", st);
+    return out;
+}
+
+/* segmentText(engine, doc, toff, len) -> string of `len` UTF-16 code units */
+static napi_value segment_text(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4], out;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    engine_box* b = argc == 4 ? get_box(env, argv[0]) : NULL;
+    uint32_t doc = 0, toff = 0, len = 0;
+    if (!b || napi_get_value_uint32(env, argv[1], &doc) != napi_ok || napi_get_value_uint32(env, argv[2], &toff) != napi_ok ||
+        napi_get_value_uint32(env, argv[3], &len) != napi_ok) {
+        napi_throw_type_error(env, NULL, "segmentText(engine, doc, toff, len)");
+        return NULL;
+    }
+    uint16_t* u = (uint16_t*)malloc((len ? len : 1) * sizeof(uint16_t));
+    if (!u) return throw_status(env, "segmentText", MT_ERR_NOMEM);
+    enter(b);
+    mt_status st = mt_segment_text(b->e, doc, toff, len, u);
+    leave(b);
+    if (st) {
+        free(u);
+        return throw_status(env, "mt_segment_text", st);
+    }
+    const napi_status ns = napi_create_string_utf16(env, (const char16_t*)u, len, &out);
+    free(u);
+    if (ns != napi_ok) return throw_status(env, "segmentText", MT_ERR_NOMEM);
+    return out;
+}
+
 /* rangeStacks(engine, queries (48-byte mt_tile_query rows), cap) -> [Buffer of n*cap 12-byte mt_stack_item
  * rows, Buffer of n uint32 depth words (MT_STACK_TOUCHED | depth)] */
 static napi_value range_stacks(napi_env env, napi_callback_info info) {
@@ -614,6 +686,9 @@ static napi_value init(napi_env env, napi_value exports) {
         {"findTiles", NULL, find_tiles, NULL, NULL, NULL, napi_default, NULL},
         {"setLabelKeys", NULL, set_label_keys, NULL, NULL, NULL, napi_default, NULL},
         {"rangeStacks", NULL, range_stacks, NULL, NULL, NULL, napi_default, NULL},
+        {"resolvePositions", NULL, resolve_positions, NULL, NULL, NULL, napi_default, NULL},
+        {"segmentInfos", NULL, segment_infos, NULL, NULL, NULL, napi_default, NULL},
+        {"segmentText", NULL, segment_text, NULL, NULL, NULL, napi_default, NULL},
         {"regenDrain", NULL, regen_drain, NULL, NULL, NULL, napi_default, NULL},
         {"eventsDrain", NULL, events_drain, NULL, NULL, NULL, napi_default, NULL},
         {"createDeli", NULL, create_deli, NULL, NULL, NULL, napi_default, NULL},

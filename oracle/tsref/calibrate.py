@@ -34,7 +34,7 @@ def main():
     ap.add_argument('--docs', type=int, default=1536)
     ap.add_argument('--threads', type=int, default=os.cpu_count())
     ap.add_argument('--reps', type=int, default=3)
-    ap.add_argument('--out', default=os.path.join(REPO, 'profiles', 'r02_js_calibration.json'))
+    ap.add_argument('--out', default=None, help='default: profiles/r04_js_calibration_<config>[_t<threads>].json')
     a = ap.parse_args()
     subprocess.check_call([sys.executable, os.path.join(HERE, 'build_ref.py')], stdout=subprocess.DEVNULL)
     cfg = dict(CONFIGS[a.config])
@@ -51,7 +51,9 @@ def main():
            'r': statistics.median(ref) / statistics.median(js), 'reps': {'reference': ref, 'restatement': js},
            'how': 'apply-only rate (max over workers of time inside the apply loops), messages pre-built, '
                   'docs round-robin over worker_threads (replayMultipleFiles.ts:123-190 pattern)'}
-    with open(a.out, 'w') as f:
+    out = a.out or os.path.join(REPO, 'profiles', f'r04_js_calibration_{a.config}' +
+                                ('' if a.threads == os.cpu_count() else f'_t{a.threads}') + '.json')
+    with open(out, 'w') as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
 

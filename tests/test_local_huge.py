@@ -153,3 +153,45 @@ def test_engine_editing_form_past_64_pending_edits_events_match_reference():
         assert len(ev) == g['n'] and hashlib.sha256(json.dumps(ev, separators=(',', ':')).encode()).hexdigest() == \
             g['sha256'], d
     eng.close()
+
+
+@pytest.mark.gpu
+def test_editing_pool_rows_scale_with_the_documents_that_need_them():
+    """Two of 100,000 documents pass 1024 editing segments: only they get rows of the editing form's
+    big pool (mt_state.h locbig, MT_LOC_BIGCAP slots), so the engine's device memory grows by far
+    less than 100 MB (a re-lay of every document's editing rows at 4096 slots would take ~11 GB),
+    and both end in the reference's final states."""
+    import ctypes
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.hipmem import hip
+    from fluidframework_amd.oplog import OpBatch
+    src = OpBatch.load(os.path.join(GOLDEN, NAME + '.mtlog'))
+    rows = load_rows()
+    D = 100_000
+    place = {r['doc']: D // 2 + i * (D // 2 - 1) for i, r in enumerate(rows)}  # docs 50000 and 99999
+    cnt = np.zeros(D, dtype=np.int64)
+    idx = []
+    for d in sorted(place, key=place.get):
+        a, b = int(src.row_ptr[d]), int(src.row_ptr[d + 1])
+        idx.append(np.arange(a, b))
+        cnt[place[d]] = b - a
+    rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
+    batch = OpBatch(src.ops[np.concatenate(idx)].copy(), src.payload, rp)
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    eng = MergeEngine(D, ops_per_launch=32)
+    before = free_bytes()
+    eng.apply(batch)
+    grown = before - free_bytes()
+    used = {cap: n for cap, _, n, _ in eng.last_class_stats() if n}
+    for r in rows:
+        k = place[r['doc']]
+        assert eng.error(k) == (0, 0), (r['doc'], eng.error(k))
+        assert eng.state(k) == r['states'][-1][1], r['doc']
+    assert used.get(0x40000000 | 2048, 0) > 0, used
+    assert grown < 100 << 20, f'device memory grew by {grown >> 20} MiB'
+    eng.close()

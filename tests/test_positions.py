@@ -1,0 +1,128 @@
+"""Device position queries (include/mtgpu.h mt_resolve_positions; SURVEY.md §8(b) read surface):
+MergeTree.getContainingSegment(pos, refSeq, clientId) (mergeTree.ts:1623-1634 through searchBlock,
+:1797-1829) and getPosition (mergeTree.ts:1585-1602) answered by one wave per query over the state in
+HBM, checked against the same questions asked of the reference's own final states
+(tests/golden/*.expected.jsonl, produced by the transpiled reference): every position of the local
+view and of remote clients' views at two refSeqs, past-the-end and negative positions, and every
+ordinal.  The restatement here is searchBlock's walk flattened over the leaves in order (a block is
+entered iff the first leaf that holds pos is inside it)."""
+import numpy as np
+import pytest
+
+from conftest import WIDE_SETS, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _units(text):
+    """cachedLength: UTF-16 code units (textSegment.ts:45); a marker is 1"""
+    return 1 if isinstance(text, dict) else len(text.encode('utf-16-le', 'surrogatepass')) // 2
+
+
+def _view_len(seg, ref_seq, client):
+    """nodeLength's leaf branch (mergeTree.ts:1659-1697) over a canonical segment row; ref_seq None:
+    the local view."""
+    text, seq, cl, rseq, rcl, ovl = seg[0], seg[1], seg[2], seg[3], seg[4], seg[5]
+    ln = _units(text)
+    removed = rcl != -1 or rseq != -1
+    if ref_seq is None:
+        return 0 if removed else ln
+    if not (cl == client or (seq != -1 and seq <= ref_seq)):
+        return 0
+    if removed and (rcl == client or client in ovl or (rseq != -1 and rseq <= ref_seq)):
+        return 0
+    return ln
+
+
+def _expected(state, pos, ref_seq, client):
+    segs = state['segs']
+    left = pos
+    for i, s in enumerate(segs):
+        vl = _view_len(s, ref_seq, client)
+        if left < vl:
+            lpos = sum(_view_len(x, None, 0) for x in segs[:i])
+            return i, left, lpos, _units(s[0])
+        left -= vl
+    return -1, left, sum(_view_len(x, None, 0) for x in segs), 0
+
+
+@pytest.mark.parametrize('name', ['scenarios', 'markers', 'synth_c3', 'synth_c4', 'synth_tiny'] + WIDE_SETS)
+def test_resolve_positions_match_reference_states(name):
+    from fluidframework_amd.engine import POS_CONTAINING, POS_LOCAL, POS_OF_ORDINAL, POS_QUERY_DTYPE, MergeEngine
+    batch, exp = load_golden(name)
+    eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.apply(batch)
+    rows, want = [], []
+    for r in exp:
+        d, st = r['doc'], r['state']
+        if eng.error(d) != (0, 0):
+            continue
+        clients = sorted({s[2] for s in st['segs'] if s[2] > 0})[:3]
+        views = [(None, 0)] + [(rs, c) for c in clients for rs in (st['msn'], st['seq'])]
+        for ref_seq, client in views:
+            vlen = sum(_view_len(s, ref_seq, client) for s in st['segs'])
+            stride = max(1, (vlen + 2) // 24)
+            for p in sorted(set(list(range(-1, vlen + 2, stride)) + [vlen, vlen + 1])):
+                rows.append((d, p, POS_LOCAL if ref_seq is None else ref_seq, client, POS_CONTAINING))
+                want.append(_expected(st, p, ref_seq, client))
+        n = len(st['segs'])
+        lp = 0
+        for i, s in enumerate(st['segs']):
+            rows.append((d, i, POS_LOCAL, 0, POS_OF_ORDINAL))
+            want.append((i, 0, lp, _units(s[0])))
+            lp += _view_len(s, None, 0)
+        rows.append((d, n, POS_LOCAL, 0, POS_OF_ORDINAL))
+        want.append((-1, None, None, None))
+    q = np.array(rows, dtype=POS_QUERY_DTYPE)
+    got = eng.resolve_positions(q)
+    for k, (g, w) in enumerate(zip(got, want)):
+        if w[1] is None:  # an ordinal past the end: none
+            ok = int(g['ordinal']) == -1
+        elif w[0] < 0:  # past the view: none, with the view's overshoot and the local length
+            ok = int(g['ordinal']) == -1 and int(g['offset']) == w[1] and int(g['position']) == w[2]
+        else:
+            ok = (int(g['ordinal']), int(g['offset']), int(g['position']), int(g['length'])) == w
+        if not ok:
+            pytest.fail(f'{name}: query {rows[k]} -> {tuple(int(x) for x in g)}, reference state gives {w}')
+    assert len(rows) > 100
+
+
+def test_resolve_positions_on_editing_documents():
+    """The local view of an editing client counts its pending inserts and hides its pending
+    removals: getContainingSegment over every position of the local_rounds / local_lag documents at
+    their final states (the reference's canonical states, tests/golden/local.expected.jsonl)."""
+    import json
+    import os
+
+    from conftest import GOLDEN
+    from fluidframework_amd.engine import POS_CONTAINING, POS_LOCAL, POS_QUERY_DTYPE, MergeEngine
+    from fluidframework_amd.oplog import OpBatch
+    with open(os.path.join(GOLDEN, 'local.expected.jsonl')) as f:
+        exp = [json.loads(x) for x in f if x.strip()]
+    checked = 0
+    for log in ('local_rounds', 'local_lag'):
+        src = OpBatch.load(os.path.join(GOLDEN, log + '.mtlog'))
+        last = {r['doc']: r['states'][-1] for r in exp if r['log'] == log and r['states'] and not r['err']}
+        docs = sorted(last)
+        # each document's records up to its last checkpoint: the engine ends in that state
+        idx = np.concatenate([np.arange(int(src.row_ptr[d]), int(src.row_ptr[d]) + last[d][0]) for d in docs])
+        rp = np.concatenate([[0], np.cumsum([last[d][0] for d in docs])]).astype(np.uint32)
+        batch = OpBatch(src.ops[idx].copy(), src.payload, rp)
+        eng = MergeEngine(len(docs), ops_per_launch=32)
+        eng.apply(batch)
+        rows, want = [], []
+        for k, d in enumerate(docs):
+            st = last[d][1]
+            assert eng.state(k) == st, (log, d)
+            n = sum(_view_len(s, None, 0) for s in st['segs'])
+            for p in range(0, n + 2, max(1, n // 16)):
+                rows.append((k, p, POS_LOCAL, 0, POS_CONTAINING))
+                want.append(_expected(st, p, None, 0))
+        got = eng.resolve_positions(np.array(rows, dtype=POS_QUERY_DTYPE))
+        for k, (g, w) in enumerate(zip(got, want)):
+            if w[0] < 0:
+                assert int(g['ordinal']) == -1, (log, rows[k])
+            else:
+                assert (int(g['ordinal']), int(g['offset']), int(g['position']), int(g['length'])) == w, (log, rows[k])
+        checked += len(rows)
+    assert checked > 100

@@ -5,8 +5,10 @@ sources (fluidframework_amd/build/*.o, from a normal build).  Output: ablib/libm
 tools/ab.py on the GPU box.
     python tools/build_variants.py base= new=-DMT_FOO 'both=-DMT_FOO -DMT_BAR'"""
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 from concurrent.futures import ThreadPoolExecutor
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -16,12 +18,20 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-u
          '-Wno-unused-value']
 
 
+# the sources are snapshotted first: hipcc reads the file once per compilation pass (device, then
+# host), so an edit made while a variant builds would otherwise split one object between two versions
+SNAP = tempfile.mkdtemp(prefix='mtgpu_variants_')
+shutil.copytree(os.path.join(PKG, 'csrc'), os.path.join(SNAP, 'fluidframework_amd', 'csrc'))
+shutil.copytree(os.path.join(REPO, 'include'), os.path.join(SNAP, 'include'))
+
+
 def build_one(spec):
     name, _, defs = spec.partition('=')
     out = os.path.join(REPO, 'ablib')
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, f'mt_apply_reg_{name}.o')
-    subprocess.check_call([HIPCC] + FLAGS + defs.split() + ['-c', os.path.join(PKG, 'csrc', 'mt_apply_reg.hip'), '-o', obj])
+    src = os.path.join(SNAP, 'fluidframework_amd', 'csrc', 'mt_apply_reg.hip')
+    subprocess.check_call([HIPCC] + FLAGS + defs.split() + ['-c', src, '-o', obj])
     others = [os.path.join(PKG, 'build', f + '.o') for f in
               ('mt_apply.hip', 'mt_service.hip', 'mt_deli.hip', 'mt_engine.cpp', 'mt_comm.cpp')]
     lib = os.path.join(out, f'libmtgpu_{name}.so')

@@ -22,10 +22,10 @@ def main():
     print('# mt_apply_reg.hip, hipcc -O3 --offload-arch=gfx950 -Rpass-analysis=kernel-resource-usage')
     print('# %-8s %6s %6s %14s %10s' % ('kernel', 'VGPR', 'SGPR', 'scratch B/lane', 'waves/SIMD'))
     for b in re.split(r'remark: [^\n]*Function Name: ', r.stderr)[1:]:
-        m = re.search(r'reg_apply_kernel(_c64)?ILi(\d+)E', b.split('\n')[0])
+        m = re.search(r'reg_apply_kernel(_c64|_ev)?ILi(\d+)E', b.split('\n')[0])
         if not m:
             continue
-        kname = ('c64 K=' if m.group(1) else 'K=') + m.group(2)
+        kname = {'_c64': 'c64 K=', '_ev': 'ev K='}.get(m.group(1), 'K=') + m.group(2)
 
         def g(k):
             x = re.search(k + r': (\S+)', b)

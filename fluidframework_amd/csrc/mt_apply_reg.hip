@@ -121,10 +121,17 @@ struct RLds {
     static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
     static constexpr int H = CAP / 2 + 64;  // heap entries (1-based)
     uint64_t props[CAP];    // by segment id: 8 keys x u8 value id
-    int32_t scr[CAP + 1];   // scratch by slot / position / leaf block (load, store, compaction)
+    // scr: scratch by slot / position / leaf block (load, store); tln: by segment id, the text length
+    // while linked, 0 once unlinked (the op loop's compaction).  They share their words, as neither
+    // is live while the other is (load writes tln after its last scr read; store runs after the op
+    // loop): 4 B per slot less LDS, which lifts the waves per CU that LDS allows at K = 7, 9, 10
+    // and 14-16 to what the registers allow (K = 9: 11 -> 12, K = 10: 11 -> 12)
+    union {
+        int32_t scr[CAP + 1];
+        uint32_t tln[CAP + 1];
+    };
     int32_t hseq[H];
     uint16_t toff[CAP];     // by segment id: text view offset (at store: id -> position)
-    uint32_t tln[CAP];      // by segment id: text length while linked, 0 once unlinked (compaction)
     uint16_t hslot[H];      // heap entry -> segment id
     uint8_t ibcnt[MT_MAXLEV - 1][IB];  // interior levels: level L's child counts in ibcnt[L - 1]
     uint8_t lbsc[LB + 1];   // store staging: needsScour per leaf block
@@ -134,6 +141,9 @@ struct RLds {
     // zr[q]: the removal seq of a removed child q, else its seq; zr[8 + q] its li, zr[16 + q] its cf,
     // zr[24 + q] its slot
     uint32_t zr[4 * kMaxNodes];
+    // the lanes' discard words of the branch-free LDS stores (a lane with nothing to store writes
+    // here; never read)
+    uint64_t dum[64];
 };
 
 struct Elem {
@@ -925,8 +935,8 @@ struct RWave {
         // the live children, rank by rank, through LDS scratch (one 16-byte record each: the
         // removal seq of a removed child, else its seq -- the only one the decisions read)
         // (every lane stores every slot: a slot that is no live child of the block goes to the
-        // lane's dummy words in `scr`, dead during the op -- no per-slot branch)
-        uint32_t* const dum = reinterpret_cast<uint32_t*>(s.scr) + lane;
+        // lane's discard words -- no per-slot branch)
+        uint32_t* const dum = reinterpret_cast<uint32_t*>(s.dum) + lane;  // (z[0 .. 3 kMaxNodes])
 #pragma unroll
         for (int j = 0; j < K; j++) {
             const int q = rbase + __popc(lb & ((1u << j) - 1u));
@@ -1330,9 +1340,9 @@ struct RWave {
         } else {
             // SegmentPropertiesManager.addProperties (remote, no combining op) on the touched slots'
             // property sets, four slots per LDS round trip: every lane reads and writes
-            // unconditionally, an untouched slot through the lane's dummy word in `scr` (dead during
-            // the op), so there is no per-slot branch and no per-slot wait
-            uint64_t* const dum = reinterpret_cast<uint64_t*>(s.scr) + lane;
+            // unconditionally, an untouched slot through the lane's discard word, so there is no
+            // per-slot branch and no per-slot wait
+            uint64_t* const dum = s.dum + lane;
 #pragma unroll
             for (int j0 = 0; j0 < K; j0 += 4) {
                 constexpr int Q = 4;
@@ -1631,7 +1641,6 @@ struct RWave {
         for (int j = 0; j < K; j++) {
             s.props[i0 + j] = (uint64_t)pw[2 * j] | ((uint64_t)pw[2 * j + 1] << 32);
             s.toff[i0 + j] = (uint16_t)vto[j];
-            s.tln[i0 + j] = vln[j];
             s.scr[i0 + j] = 0;
         }
 #pragma unroll
@@ -1695,6 +1704,9 @@ struct RWave {
             sc0 |= (mk & 2) ? bit : 0u;
             sc1 |= (mk & 4) ? bit : 0u;
         }
+        wave_sync();  // (tln shares scr's words: the marks are read)
+#pragma unroll
+        for (int j = 0; j < K; j++) s.tln[i0 + j] = vln[j];
         // empty leaf blocks (rare): a dead slot holds each one's place and marks
         if (nempty) {
             if (ns + nempty > CAP) {
@@ -1732,8 +1744,8 @@ struct RWave {
     // coalesced HBM stores; no per-slot 64-bit addresses kept live)
     template <class T, class F>
     MT_DEV void store_field(const T& v, uint32_t lb, int pbase, int nn, F&& put) {
-        // (a dead slot goes to the lane's dummy word in `tln`, dead at store time: no per-slot branch)
-        int32_t* const dum = reinterpret_cast<int32_t*>(s.tln) + lane;
+        // (a dead slot goes to the lane's discard word: no per-slot branch)
+        int32_t* const dum = reinterpret_cast<int32_t*>(s.dum) + lane;
 #pragma unroll
         for (int j = 0; j < K; j++)
             *(((lb >> j) & 1u) ? &s.scr[pbase + __popc(lb & ((1u << j) - 1u))] : dum) = (int32_t)v[j];
@@ -2008,8 +2020,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) vo
 // ... and with delta / maintenance events recorded (mt_events_enable): the same engine, its event
 // rows written from the split, insert, range and scour steps (the kernel without EV carries no event
 // code; C64 documents record on the LDS engine)
+// The event-recording kernels need ~35 VGPRs more (the event rows' placement and property deltas):
+// at the plain kernels' occupancy they would spill 180-560 B per lane from K = 2 on, so they run one
+// or two waves lower, spill-free up to K = 9 (K = 10 / 11: 100 / 180 B at two waves).
+// MT_WPE_EV_OV overrides them like MT_WPE_OV.
+constexpr int wpe_ev_default(int K) { return K <= 2 ? 4 : K <= 5 ? 3 : 2; }
+#ifndef MT_WPE_EV_OV
+#define MT_WPE_EV_OV {0}
+#endif
+constexpr int wpe_ev_ov[17] = MT_WPE_EV_OV;
+constexpr int wpe_ev(int K) { return K < 17 && wpe_ev_ov[K] > 0 ? wpe_ev_ov[K] : wpe_ev_default(K); }
 template <int K>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel_ev(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe_ev(K)))) void reg_apply_kernel_ev(
     mt_gstate g, const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
     const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ doc_ids, uint32_t n_docs, uint32_t op_lo,
     uint32_t op_cnt) {

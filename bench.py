@@ -45,7 +45,7 @@ METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofli
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
-PMC_ROUND = 'r03'
+PMC_ROUND = 'r04'
 CAL_ROUND = 'r04'  # profiles/<round>_js_calibration_<config>.json: r of the JS baseline (oracle/tsref/calibrate.py)
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
@@ -87,8 +87,8 @@ def parse():
     p.add_argument('--no-h2d', action='store_true', help='skip the extra step whose op log is uploaded from '
                                                          'host memory inside the timed region (value_with_h2d)')
     p.add_argument('--no-slow-paths', action='store_true',
-                   help='skip the N=1 side lines for the LDS-engine paths (C3 with delta events recorded, C3 '
-                        'with 48 clients, the editing-client farm at 100K documents)')
+                   help='skip the N=1 side lines for the paths off the narrow register engine (C3 with delta '
+                        'events recorded, C3 with 48 clients, the editing-client farm at 100K documents)')
     return p.parse_args()
 
 
@@ -224,6 +224,14 @@ def main():
 
     cs = eng.checksums()
     errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 64)) if eng.error(d)[0])
+    # SURVEY.md §8(d)'s b = infinity figure (the minimal traffic of the job): every op record and its
+    # payload read once, each document's state read once (empty after the reset: its 80-byte scalar
+    # header) and written once (35 B per final segment + the header); the mean payload per op from
+    # the first 512 documents' logs
+    samp = dev.to_host(0, min(n_docs, 512))
+    ops_b = n_ops * 32 + float(samp.ops['payload_len'].astype(np.float64).sum()) * n_ops / max(1, samp.n_ops)
+    min_bytes = ops_b + 35.0 * float(eng.seg_counts().astype(np.float64).sum()) + 2 * 80.0 * n_docs
+    del samp
     if deli is None:
         assert np.array_equal(cs, gen_cs), 'replay does not reproduce the generation state'
     else:
@@ -304,6 +312,10 @@ def main():
                                if rcls is not cls else 'the timed steps (classes serialized)',
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
                 'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
+                'b_infinity': {'bytes_per_step_rank0': int(min_bytes),
+                               'frac': round(min_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
+                               'note': 'SURVEY.md 8(d): state read + written once per step, every op once; '
+                                       'the step time of the timed steps'},
                 'all_apply_kernels': {'launches': launches, 'kernel_ms': round(kern_ms, 2),
                                       'achieved_GBps': round(all_achieved, 1),
                                       'apply_wall_ms': round(wall_ms, 2),
@@ -329,14 +341,20 @@ def main():
 
 
 MT_CLASS_EDITING = 0x40000000  # include/mtgpu.h: the editing documents' bucket in the class stats
-MT_CLASS_LDS = 0x20000000      # the LDS engine inside a register class (client ids above 32, label keys)
+MT_CLASS_LDS = 0x20000000      # the LDS engine inside a register class (declared label keys)
+MT_CLASS_C64 = 0x10000000      # the register engine's C64 form (client ids 33..63)
+MT_CLASS_GROUPS = 0x08000000   # with MT_CLASS_EDITING: the form for more than 64 pending edits
 
 
 def class_label(cap):
     if cap & MT_CLASS_EDITING:
+        if cap & MT_CLASS_GROUPS:
+            return f'editing_groups{cap & ~(MT_CLASS_EDITING | MT_CLASS_GROUPS)}'
         return f'editing{cap & ~MT_CLASS_EDITING}'
     if cap & MT_CLASS_LDS:
         return f'lds{cap & ~MT_CLASS_LDS}'
+    if cap & MT_CLASS_C64:
+        return f'c64_{cap & ~MT_CLASS_C64}'
     return str(cap)
 
 
@@ -349,7 +367,9 @@ def roofline_of(eng, rcls):
     per = b / max(1, n)
     ach = per / (avg * 1e-3) / 1e9 if n and avg else 0.0
     return {'bound': 'hbm', 'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(ach / HBM_PEAK_GBS, 4), 'traffic': None, 'kernel': eng.class_kernel(dom), 'launches': n,
+            'frac': round(ach / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(eng.class_kernel(dom), 'C3'),
+            'traffic_source': os.path.relpath(pmc_path('C3'), HERE) + ' (the PMC passes of the full C3 bench, side lines '
+                              'included; bytes per launch)', 'kernel': eng.class_kernel(dom), 'launches': n,
             'avg_launch_ms': round(avg, 4), 'alg_bytes_per_launch': int(per),
             'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]}}
 
@@ -384,7 +404,8 @@ def timed_side_step(eng, dbatch, warmup=1, after=None):
 
 def slow_paths(device, n_docs, seed):
     """N = 1 side lines for the paths off the register engine's narrow form: C3 with
-    the delta callbacks recorded (any SharedString with a sequenceDelta listener: LDS engine), C3
+    the delta callbacks recorded (any SharedString with a sequenceDelta listener: the register
+    engine's event-recording kernels, reg_apply_kernel_ev), C3
     with 48 clients (overlap sets past 32 bits: the register engine's C64 form), and the
     editing-client farm (local edits + remote ops + acks: the LDS engine's editing form) tiled over
     100K documents.  Each is a full replay of HBM-resident logs, checked against the generation
@@ -412,7 +433,7 @@ def slow_paths(device, n_docs, seed):
     ok = bool(np.array_equal(eng.checksums(), gen_cs))
     errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 256)) if eng.error(d)[0])
     out['C3_events'] = {'workload': f'C3 ({n_docs} docs x 32 clients x 1024 ops) with every delta callback recorded '
-                                    '(mt_events_enable; LDS engine)',
+                                    '(mt_events_enable; register engine, reg_apply_kernel_ev)',
                         'value': round(ops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
                         'events_per_step': n_ev, 'drain_s': round(drain_s, 3),
                         'note': 'the drain (CSR gather of every callback record + D2H) follows the timed replay',
@@ -420,7 +441,7 @@ def slow_paths(device, n_docs, seed):
     dev.free()
     eng.close()
 
-    # C3 with 48 clients: client ids past 32 (the register engine's overlap set) -> LDS engine
+    # C3 with 48 clients: client ids past 32 (the register engine's overlap set) -> its C64 form
     cfg48 = dict(CONFIGS['C3W'])
     cfg48.pop('n_docs')
     eng = MergeEngine(n_docs, device=device, ops_per_launch=32)

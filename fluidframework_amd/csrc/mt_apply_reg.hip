@@ -1343,9 +1343,9 @@ struct RWave {
             // unconditionally, an untouched slot through the lane's discard word, so there is no
             // per-slot branch and no per-slot wait
             uint64_t* const dum = s.dum + lane;
+            constexpr int Q = 4;
 #pragma unroll
-            for (int j0 = 0; j0 < K; j0 += 4) {
-                constexpr int Q = 4;
+            for (int j0 = 0; j0 < K; j0 += Q) {
                 uint64_t* pa[Q];
                 uint64_t pv[Q];
 #pragma unroll
@@ -2008,7 +2008,10 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
 constexpr int wpe_c64_ov[17] = MT_WPE_C64_OV;
 // The C64 form carries K more VGPRs of state; same rule (A/B on C3W in profiles/r03_ab_occupancy.log:
 // K = 3..6 one wave up, K = 8, 9 at 3 with <= 100 B of scratch; K = 7 at 4 would spill ~200 B).
-constexpr int wpe_c64_default(int K) { return K <= 4 ? 5 : K <= 6 ? 4 : K <= 9 ? 3 : 2; }
+// K >= 13 runs one wave per SIMD: at two it spilled 590-660 B per lane in round 4's code, at one the
+// excess lives in AGPRs (C3W 137.3 -> 184.5 M ops/s, profiles/r04_ab_c64_occupancy_C3W.log).  (The
+// event kernels measured the other way: one wave at K >= 11 0.89x, r04_ab_events_onewave_C3.jsonl.)
+constexpr int wpe_c64_default(int K) { return K <= 4 ? 5 : K <= 6 ? 4 : K <= 9 ? 3 : K <= 12 ? 2 : 1; }
 constexpr int wpe_c64(int K) { return K < 17 && wpe_c64_ov[K] > 0 ? wpe_c64_ov[K] : wpe_c64_default(K); }
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(

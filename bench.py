@@ -464,6 +464,39 @@ def slow_paths(device, n_docs, seed):
     dev.free()
     eng.close()
 
+    # C3 with client ids past 255: the wide form (u16 short ids, UTF-16 arena, structure in an HBM
+    # workspace; include/mtgpu.h "limits").  The device generator keeps ids below 64, so the C3 logs
+    # of n_docs / 5 documents are generated, copied out, every client id shifted by 300 and staged
+    # again: the same edits by clients 301..332
+    n_w = max(1, n_docs // 5)
+    eng = MergeEngine(n_w, device=device, ops_per_launch=32)
+    dev = eng.synthesize(seed=seed, **cfg)
+    host = dev.to_host(0, n_w)
+    dev.free()
+    eng.close()
+    host.ops['client'] = np.where(host.ops['client'] > 0, host.ops['client'] + 300, 0).astype(host.ops['client'].dtype)
+    eng = MergeEngine(n_w, device=device, ops_per_launch=32)
+    dev = eng.stage(host)
+    el, rf, _ = timed_side_step(eng, dev)
+    cs = eng.checksums()
+    par = {'doc_errors_sampled': sum(1 for d in range(0, n_w, max(1, n_w // 256)) if eng.error(d)[0])}
+    try:
+        from oracle import oracle
+        k = 256
+        sub = dev.to_host(0, k)
+        o = oracle.Oracle(k).apply(sub, threads=int(os.environ.get('OMP_NUM_THREADS') or 8))
+        par.update(docs_checked=k, mismatches=int(np.count_nonzero(o.checksums() != cs[:k])), against='oracle/mtcpu.cpp')
+    except Exception as ex:
+        par['oracle'] = f'unavailable: {ex}'
+    wops = n_w * cfg['ops_per_doc']
+    out['C3_wide_ids'] = {'workload': f'C3 with client ids 301..332 ({n_w} docs x 1024 ops; the wide form: u16 '
+                                      'short ids, UTF-16 arena, HBM workspace)',
+                          'value': round(wops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
+                          'roofline': rf, 'parity': par}
+    dev.free()
+    eng.close()
+    del host
+
     # the editing-client farm (tests/golden/local_big: reference clients' logs as one of them sees
     # them) tiled over n_docs documents
     src = OpBatch.load(os.path.join(HERE, 'tests', 'golden', 'local_big.mtlog'))

@@ -92,8 +92,9 @@ struct Lds {
     uint16_t hslot[H];
     uint16_t order[CAP];    // document order -> slot
     uint16_t freel[CAP];
-    uint8_t client[CAP];
-    uint8_t rclient[CAP];
+    // short client ids: u8 in the narrow form, u16 in the wide one (ids up to 65534)
+    typename std::conditional<W, uint16_t, uint8_t>::type client[CAP];
+    typename std::conditional<W, uint16_t, uint8_t>::type rclient[CAP];
     uint8_t flags[CAP];
     uint8_t lbcnt[LB];
     uint8_t lbscour[LB];
@@ -112,7 +113,7 @@ struct Lds {
     uint64_t pk[LOC ? CAP : 1];
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
-    uint64_t ovx[W ? CAP : 1];
+    uint64_t ovx[W ? MT_OVX_WORDS * CAP : 1];  // (W) overlapping removers >= 64: u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
     uint64_t pxh[W ? CAP : 1];
@@ -130,6 +131,7 @@ struct Lds {
 template <int CAP, bool G = false, bool LOC = false, bool W = false, int GW = 1>
 struct Wave {
     using L = Lds<CAP, LOC, W, GW>;
+    using CT = typename std::conditional<W, uint16_t, uint8_t>::type;  // a short client id (Lds::client)
     // (LOC) pending-group masks: GW words per slot; pending edit ordinal N is bit N % GN
     static constexpr uint32_t GN = 64u * GW;
     MT_DEV uint64_t& gmw(int sl, uint32_t N) { return s.gm[sl * GW + (int)((N % GN) >> 6)]; }
@@ -177,7 +179,7 @@ struct Wave {
     // removedClientOverlap holds client C (ids < 64: the bitmask; a wide document's others: ovx)
     MT_DEV bool ovl_has(int slot, int C) const {
         if (C < 64) return C >= 0 && ((s.ovl[slot] >> C) & 1ull);
-        if constexpr (W) return mt_ovx_has(s.ovx[slot], (uint32_t)C);
+        if constexpr (W) return mt_ovx_has(&s.ovx[MT_OVX_WORDS * slot], (uint32_t)C);
         return false;
     }
     // addOverlappingClient (mergeTree.ts:2544-2552); false: a wide segment's ovx list is full
@@ -187,23 +189,27 @@ struct Wave {
             return true;
         }
         if constexpr (W) {
-            const uint64_t x = s.ovx[slot];
+            uint64_t* x = &s.ovx[MT_OVX_WORDS * slot];
             if (mt_ovx_has(x, (uint32_t)C)) return true;
-            if (x >> 56) return false;
-            uint64_t out = 0;  // insert C into the ascending byte list
+            if (mt_ovx_id(x, MT_OVX_IDS - 1)) return false;  // full: MT_DERR_LIMITS
+            uint64_t out[MT_OVX_WORDS] = {0, 0, 0, 0};  // insert C into the ascending u16 list
             int j = 0;
             bool done = false;
-            for (int b = 0; b < 8; b++) {
-                const uint32_t v = (uint32_t)(x >> (8 * b)) & 0xFFu;
+            auto put = [&](uint32_t v) {
+                out[j >> 2] |= (uint64_t)v << (16 * (j & 3));
+                j++;
+            };
+            for (int q = 0; q < MT_OVX_IDS; q++) {
+                const uint32_t v = mt_ovx_id(x, q);
                 if (!v) break;
                 if (!done && (uint32_t)C < v) {
-                    out |= (uint64_t)C << (8 * j++);
+                    put((uint32_t)C);
                     done = true;
                 }
-                out |= (uint64_t)v << (8 * j++);
+                put(v);
             }
-            if (!done) out |= (uint64_t)C << (8 * j);
-            s.ovx[slot] = out;
+            if (!done) put((uint32_t)C);
+            for (int w = 0; w < MT_OVX_WORDS; w++) x[w] = out[w];
             return true;
         }
         return false;
@@ -694,7 +700,8 @@ struct Wave {
             s.rseq[t] = s.rseq[sl];
             s.rclient[t] = s.rclient[sl];
             s.ovl[t] = s.ovl[sl];
-            if constexpr (W) s.ovx[t] = s.ovx[sl];
+            if constexpr (W)
+                for (int q = 0; q < MT_OVX_WORDS; q++) s.ovx[MT_OVX_WORDS * t + q] = s.ovx[MT_OVX_WORDS * sl + q];
             pcopy(t, sl);
             s.flags[t] = s.flags[sl];
             s.len[t] = s.len[sl] - (uint32_t)off;
@@ -983,7 +990,8 @@ struct Wave {
     // -------------------------------------------------------------------- ops
     MT_DEV void op_insert(const mt_op_rec& op, const uint8_t* pay, int tlen, const Pairs& pr) {
         const int32_t S = op.seq, R = op.ref_seq;
-        const int C = op.client & 0xFF, pos = op.pos1;  // (MT_OP_LOAD: removedClient in the high byte)
+        const bool ld = MT_OP_TYPE(op) == MT_OP_LOAD;
+        const int C = ld ? (int)MT_LOAD_CLIENT(op) : (int)op.client, pos = op.pos1;
         if (!boundary(pos, R, C, S)) return;  // cum: apply() scanned for (R, C)
         if (tlen > 0) {  // blockInsert (mergeTree.ts:2141-2224)
             block_starts();
@@ -1072,11 +1080,12 @@ struct Wave {
                 // snapshotLoader.ts:101-106): MT_OP_LOAD carries removedSeq in pos2
                 const bool lrm = MT_OP_TYPE(op) == MT_OP_LOAD && op.pos2 >= 0;
                 s.seq[t] = S;
-                s.client[t] = (uint8_t)C;
+                s.client[t] = (CT)C;
                 s.rseq[t] = lrm ? op.pos2 : 0;
-                s.rclient[t] = lrm ? (uint8_t)(op.client >> 8) : 0;
+                s.rclient[t] = lrm ? (CT)MT_LOAD_RCLIENT(op) : 0;
                 s.ovl[t] = 0;
-                if constexpr (W) s.ovx[t] = 0;
+                if constexpr (W)
+                    for (int q = 0; q < MT_OVX_WORDS; q++) s.ovx[MT_OVX_WORDS * t + q] = 0;
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
                 // a Marker (MT_F_MARKER): length 1, its arena byte is its ReferenceType
@@ -1164,7 +1173,7 @@ struct Wave {
                         if constexpr (LOC) pend_rm = (s.flags[sl] & MT_SF_REMOVED) && s.rseq[sl] == -1;
                         if (pend_rm) {  // a pending local removal: this one replaces it (mergeTree.ts:2621-2627)
                             s.rseq[sl] = S;
-                            s.rclient[sl] = (uint8_t)C;
+                            s.rclient[sl] = (CT)C;
                             s.flags[sl] |= MT_SF_OVW;  // (not among this op's removedSegments)
                             if constexpr (LOC) s.lsq[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
                         } else if (s.flags[sl] & MT_SF_REMOVED) {
@@ -1172,7 +1181,7 @@ struct Wave {
                         } else {
                             s.flags[sl] |= MT_SF_REMOVED;
                             s.rseq[sl] = S;
-                            s.rclient[sl] = (uint8_t)C;
+                            s.rclient[sl] = (CT)C;
                             if constexpr (LOC) {  // localRemovedSeq (mergeTree.ts:2637)
                                 s.lsq[sl] = (s.lsq[sl] & 0xFFFFFFFFull) | ((uint64_t)(local ? s.lc.lseq : 0u) << 32);
                             }
@@ -1564,16 +1573,19 @@ struct Wave {
         // no Client around it: no window asserts and no updateSeqNumbers
         const bool load = type == MT_OP_LOAD;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
-        const int C = op.client & 0xFF;
+        // (a short id >= 256 only in the wide form; 254 is NonCollabClient's, never a remote client's)
+        const int C = load ? (int)MT_LOAD_CLIENT(op) : (int)op.client;
         const uint32_t plen = MT_OP_PAIRS_LEN(op);
         s.evseq = S;
         if (load) {
+            const int RC = (int)MT_LOAD_RCLIENT(op);
             const bool ok = (C == MT_CLIENT_NONCOLLAB || (C >= 1 && C < kClients)) &&
-                            (op.pos2 < 0 || ((op.client >> 8) >= 1 && (op.client >> 8) < kClients));
+                            (op.pos2 < 0 || (RC >= 1 && RC < kClients && RC != MT_CLIENT_NONCOLLAB));
             if (!ok) return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u))) return fail(MT_DERR_BAD_OP, S);
         } else if (!noop) {
-            if (op.client == 0 || op.client >= kClients) return fail(MT_DERR_LIMITS, S);
+            if (op.client == 0 || op.client >= kClients || op.client == MT_CLIENT_NONCOLLAB)
+                return fail(MT_DERR_LIMITS, S);
             if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u))) return fail(MT_DERR_BAD_OP, S);
         } else {  // every assert of the message before any edit: the document halts before it
             if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);  // client.ts:824
@@ -1787,7 +1799,12 @@ struct Wave {
         const bool was_wide = (sc.wide & MT_WIDE_DOC) != 0;
         if constexpr (W) {
             for (int i = lane; i < n; i += 64) {
-                s.ovx[i] = was_wide ? g.ovx[so + i] : 0ull;
+                for (int q = 0; q < MT_OVX_WORDS; q++)
+                    s.ovx[MT_OVX_WORDS * i + q] = was_wide ? g.ovx[MT_OVX_WORDS * (so + i) + q] : 0ull;
+                // (the short ids' high bytes; a narrow document's ids are below 64)
+                const uint32_t hi = was_wide ? g.chi[so + i] : 0u;
+                s.client[i] = (CT)(s.client[i] | ((hi & 0xFFu) << 8));
+                s.rclient[i] = (CT)(s.rclient[i] | ((hi >> 8) << 8));
                 s.ph[i] = was_wide ? g.ph[so + i] : 0ull;
                 s.pxl[i] = was_wide ? g.pxl[so + i] : 0ull;
                 s.pxh[i] = was_wide ? g.pxh[so + i] : 0ull;
@@ -1924,8 +1941,8 @@ struct Wave {
             g.toff[so + i] = s.toff[sl];
             g.ovl[so + i] = s.ovl[sl];
             g.props[so + i] = s.props[sl];
-            g.client[so + i] = s.client[sl];
-            g.rclient[so + i] = s.rclient[sl];
+            g.client[so + i] = (uint8_t)s.client[sl];
+            g.rclient[so + i] = (uint8_t)s.rclient[sl];
             g.flags[so + i] = s.flags[sl];
             if (track()) g.slab[so + i] = LOC ? xslab[sl] : s.slab[sl];
             s.cum[sl] = i;  // slot -> position for the heap remap
@@ -1969,7 +1986,8 @@ struct Wave {
         if constexpr (W) {
             for (int i = lane; i < nn; i += 64) {
                 const int sl = s.order[i];
-                g.ovx[so + i] = s.ovx[sl];
+                for (int q = 0; q < MT_OVX_WORDS; q++) g.ovx[MT_OVX_WORDS * (so + i) + q] = s.ovx[MT_OVX_WORDS * sl + q];
+                g.chi[so + i] = (uint16_t)(((uint32_t)s.client[sl] >> 8) | (((uint32_t)s.rclient[sl] >> 8) << 8));
                 g.ph[so + i] = s.ph[sl];
                 g.pxl[so + i] = s.pxl[sl];
                 g.pxh[so + i] = s.pxh[sl];

@@ -24,8 +24,9 @@ MT_HD static inline uint64_t mt_seg_hash(uint64_t idx, uint64_t text_hash, int32
     h = mt_mix64(h ^ props_lo ^ ((uint64_t)props_defined << 63));
     return h;
 }
-// The overlap term: the ids < 64 as a bitmask; a wide document's ids >= 64 (ovx: ascending from the
-// low byte, 0 = none) hashed in.  The props term: the low bytes of the value ids of keys 0..7 (the
+// The overlap term: the ids < 64 as a bitmask; a wide document's ids >= 64 hashed in (mt_ovx_hash:
+// up to eight ids below 256 as their ascending byte list -- round 3's form, so earlier fixtures keep
+// their checksums -- any other list folded id by id).  The props term: the low bytes of the value ids of keys 0..7 (the
 // narrow u64); a wide document's high bytes (hi) and keys 8..15 (xlo, xhi) hashed in.  Both are the
 // narrow word itself whenever the wide part is empty.
 MT_HD static inline uint64_t mt_ovl_term(uint64_t mask, uint64_t ovx) {
@@ -64,13 +65,43 @@ MT_HD static inline bool mt_gprops_eq(const mt_gstate& g, bool wide, size_t a, s
 MT_HD static inline uint64_t mt_gprops_term(const mt_gstate& g, bool wide, size_t i) {
     return wide ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i]) : g.props[i];
 }
-MT_HD static inline uint64_t mt_govl_term(const mt_gstate& g, bool wide, size_t i) {
-    return wide ? mt_ovl_term(g.ovl[i], g.ovx[i]) : g.ovl[i];
+// A wide segment's overlapping removers >= 64: up to MT_OVX_IDS (16) u16 ids, ascending from the low
+// half-word of x[0], 0 = none (mt_state.h ovx, four words per segment)
+#define MT_OVX_WORDS 4
+MT_HD static inline uint32_t mt_ovx_id(const uint64_t* x, int q) {
+    return (uint32_t)(x[q >> 2] >> (16 * (q & 3))) & 0xFFFFu;
 }
-// a wide document's overlap list (ascending bytes, 0 = none) holds client c
-MT_HD static inline bool mt_ovx_has(uint64_t x, uint32_t c) {
-    const uint64_t t = x ^ (0x0101010101010101ull * (uint64_t)(c & 0xFFu));
-    return ((t - 0x0101010101010101ull) & ~t & 0x8080808080808080ull) != 0;
+MT_HD static inline bool mt_ovx_has(const uint64_t* x, uint32_t c) {
+    for (int q = 0; q < 4 * MT_OVX_WORDS; q++) {
+        const uint32_t v = mt_ovx_id(x, q);
+        if (!v) return false;
+        if (v == c) return true;
+    }
+    return false;
+}
+MT_HD static inline uint64_t mt_ovx_hash(const uint64_t* x) {
+    uint64_t packed = 0, h = 0x9E3779B97F4A7C15ull;
+    bool small = true;
+    int n = 0;
+    for (; n < 4 * MT_OVX_WORDS; n++) {
+        const uint32_t v = mt_ovx_id(x, n);
+        if (!v) break;
+        if (v > 255u || n >= 8) small = false;
+        else packed |= (uint64_t)v << (8 * n);
+        h = mt_mix64(h ^ v);
+    }
+    if (!n) return 0;
+    return small ? packed : (h ? h : 1ull);
+}
+// the short client ids of the segment at HBM index i (a wide document's ids >= 256 via chi)
+MT_HD static inline uint32_t mt_gclient(const mt_gstate& g, bool wide, size_t i) {
+    return (uint32_t)g.client[i] | (wide && g.chi ? (uint32_t)(g.chi[i] & 0xFFu) << 8 : 0u);
+}
+MT_HD static inline uint32_t mt_grclient(const mt_gstate& g, bool wide, size_t i) {
+    return (uint32_t)g.rclient[i] | (wide && g.chi ? (uint32_t)(g.chi[i] >> 8) << 8 : 0u);
+}
+MT_HD static inline uint64_t mt_govl_term(const mt_gstate& g, bool wide, size_t i) {
+    return wide ? mt_ovl_term(g.ovl[i], mt_ovx_hash(g.ovx + MT_OVX_WORDS * i)) : g.ovl[i];
 }
 // code unit q of the text at arena unit offset `off` of document d (its current half)
 MT_HD static inline uint32_t mt_gtext(const mt_gstate& g, uint32_t d, const mt_doc_scalars& sc, uint32_t off) {

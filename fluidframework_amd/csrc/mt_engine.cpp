@@ -207,7 +207,7 @@ static mt_status ensure_wide(mt_engine* e) {
     mt_gstate& g = e->g;
     mt_status st = MT_OK;
     if ((st = dalloc(e, &g.ph, S)) || (st = dalloc(e, &g.pxl, S)) || (st = dalloc(e, &g.pxh, S)) ||
-        (st = dalloc(e, &g.ovx, S))) {
+        (st = dalloc(e, &g.chi, S)) || (st = dalloc(e, &g.ovx, S * MT_OVX_WORDS))) {
         g.ovx = nullptr;  // (the kernels test ovx; the others are freed with the engine)
         return st;
     }
@@ -316,14 +316,16 @@ static mt_status assign_loc_rows(mt_engine* e, const uint32_t* ids, uint32_t cnt
 static bool wide_rec(const mt_op_rec& o) {
     if (o.type & MT_OP_WIDE) return true;
     if (MT_OP_TYPE(o) == MT_OP_LOAD) {
-        const uint32_t c0 = o.client & 0xFFu, c1 = o.client >> 8;
+        const uint32_t c0 = MT_LOAD_CLIENT(o), c1 = MT_LOAD_RCLIENT(o);
         return (c0 != MT_CLIENT_NONCOLLAB && c0 >= MT_MAX_CLIENTS) || (o.pos2 >= 0 && c1 >= MT_MAX_CLIENTS);
     }
     return !MT_OP_IS_NOOP(o) && o.client >= MT_MAX_CLIENTS;
 }
+static uint32_t seg_client(const mt_load_seg& sg) { return sg.client | ((uint32_t)sg.client_hi << 8); }
+static uint32_t seg_rclient(const mt_load_seg& sg) { return sg.rclient | ((uint32_t)sg.rclient_hi << 8); }
 static bool wide_load_seg(const mt_load_seg& sg) {
-    if ((sg.flags & MT_LSF_U16) || (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) ||
-        (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS))
+    if ((sg.flags & MT_LSF_U16) || (seg_client(sg) >= MT_MAX_CLIENTS && seg_client(sg) != MT_CLIENT_NONCOLLAB) ||
+        (sg.rseq >= 0 && seg_rclient(sg) >= MT_MAX_CLIENTS))
         return true;
     for (int k = 0; k < 16; k++)
         if ((sg.flags & MT_SF_PDEF) && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255)) return true;
@@ -507,8 +509,9 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
         const mt_load_seg& sg = segs[seg_row_ptr[0] + k];
         const uint64_t tb = (uint64_t)sg.text_len * ((sg.flags & MT_LSF_U16) ? 2u : 1u);
         if ((uint64_t)sg.text_off + tb > text_bytes) return MT_ERR_ARG;
-        if (sg.client >= MT_MAX_CLIENTS_WIDE && sg.client != MT_CLIENT_NONCOLLAB) return MT_ERR_ARG;
-        if (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS_WIDE) return MT_ERR_ARG;
+        if (seg_client(sg) >= MT_MAX_CLIENTS_WIDE) return MT_ERR_ARG;
+        if (sg.rseq >= 0 && (seg_rclient(sg) >= MT_MAX_CLIENTS_WIDE || seg_rclient(sg) == MT_CLIENT_NONCOLLAB))
+            return MT_ERR_ARG;
         wide = wide || wide_load_seg(sg);
     }
     HIP_OK(hipSetDevice(e->cfg.device));
@@ -596,7 +599,7 @@ mt_status mt_resolve_positions_device(mt_engine* e, const mt_pos_query* d_q, uin
 }
 
 mt_status mt_segment_infos(mt_engine* e, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out) {
-    static_assert(sizeof(mt_seg_info) == 80, "mt_seg_info is 80 bytes");
+    static_assert(sizeof(mt_seg_info) == 104, "mt_seg_info is 104 bytes");
     if (!e || (n && (!docs || !ordinals || !out))) return MT_ERR_ARG;
     for (uint32_t i = 0; i < n; i++)
         if (docs[i] >= e->n_docs) return MT_ERR_ARG;
@@ -1286,6 +1289,7 @@ struct HostDoc {
     std::vector<uint32_t> len, toff;
     std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
     std::vector<uint8_t> client, rclient, flags;
+    std::vector<uint16_t> chi;                 // (wide) the short ids' high bytes
     std::vector<uint16_t> text;                // the arena's current half, in code units
     std::vector<std::vector<uint8_t>> levels;  // per level child counts (level 0 = leaf blocks)
     uint32_t prop(int i, int k) const {
@@ -1299,10 +1303,13 @@ struct HostDoc {
         for (int c = 0; c < 64; c++)
             if ((ovl[i] >> c) & 1) v.push_back(c);
         if (wide)
-            for (int b = 0; b < 8; b++)
-                if (const int c = (int)((ovx[i] >> (8 * b)) & 0xFF)) v.push_back(c);
+            for (int q = 0; q < MT_OVX_IDS; q++)
+                if (const int c = (int)mt_ovx_id(ovx.data() + (size_t)MT_OVX_WORDS * i, q)) v.push_back(c);
+                else break;
         return v;
     }
+    uint32_t client_of(int i) const { return client[i] | (wide ? (uint32_t)(chi[i] & 0xFF) << 8 : 0u); }
+    uint32_t rclient_of(int i) const { return rclient[i] | (wide ? (uint32_t)(chi[i] >> 8) << 8 : 0u); }
     const uint16_t* units(int i) const { return text.data() + toff[i]; }
 };
 
@@ -1344,7 +1351,8 @@ mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
     HIP_OK(fetch(h.ovl, g.ovl, so, n, e->stream));
     HIP_OK(fetch(h.props, g.props, so, n, e->stream));
     if (h.wide) {
-        HIP_OK(fetch(h.ovx, g.ovx, so, n, e->stream));
+        HIP_OK(fetch(h.ovx, g.ovx, so * MT_OVX_WORDS, n * MT_OVX_WORDS, e->stream));
+        HIP_OK(fetch(h.chi, g.chi, so, n, e->stream));
         HIP_OK(fetch(h.ph, g.ph, so, n, e->stream));
         HIP_OK(fetch(h.pxl, g.pxl, so, n, e->stream));
         HIP_OK(fetch(h.pxh, g.pxh, so, n, e->stream));
@@ -1399,8 +1407,8 @@ std::string state_json(const HostDoc& h) {
         else
             json_units(o, h.units(i), h.len[i]);
         const bool rm = h.flags[i] & MT_SF_REMOVED;
-        o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(mt_canon_client(h.client[i])) + ',';
-        o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient[i]) : "-1") + ",[";
+        o += ',' + std::to_string(h.seq[i]) + ',' + std::to_string(mt_canon_client(h.client_of(i))) + ',';
+        o += (rm ? std::to_string(h.rseq[i]) : "-1") + ',' + (rm ? std::to_string(h.rclient_of(i)) : "-1") + ",[";
         bool f = true;
         for (int c : h.overlap(i)) {
             if (!f) o += ',';
@@ -1505,11 +1513,11 @@ std::string snapshot_json(const HostDoc& h, const std::vector<uint32_t>& sp, uin
         o += "{\"json\":";
         seg_json(o, h, pos, text);
         if (h.seq[pos] > h.sc.min_seq)
-            o += ",\"seq\":" + std::to_string(h.seq[pos]) + ",\"client\":\"" + client_name(names, n_names, h.client[pos]) +
+            o += ",\"seq\":" + std::to_string(h.seq[pos]) + ",\"client\":\"" + client_name(names, n_names, h.client_of(pos)) +
                  "\"";
         if (h.flags[pos] & MT_SF_REMOVED)
             o += ",\"removedSeq\":" + std::to_string(h.rseq[pos]) + ",\"removedClient\":\"" +
-                 client_name(names, n_names, h.rclient[pos]) + "\"";
+                 client_name(names, n_names, h.rclient_of(pos)) + "\"";
         o += '}';
     }
     // getSeqLengthSegs (:57-79): chunks of >= `chunk` characters
@@ -1558,6 +1566,7 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
     std::vector<uint32_t> len, toff;
     std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
     std::vector<uint8_t> client, rclient, flags, lb, ib;
+    std::vector<uint16_t> chi;
     bool any_wide = false;
     for (uint32_t i = 0; i < n; i++) any_wide = any_wide || ((sc[i].wide & MT_WIDE_DOC) && g.ovx);
     HIP_OK(fetch(seq, g.seq, so, S, e->stream));
@@ -1567,7 +1576,8 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
     HIP_OK(fetch(ovl, g.ovl, so, S, e->stream));
     HIP_OK(fetch(props, g.props, so, S, e->stream));
     if (any_wide) {
-        HIP_OK(fetch(ovx, g.ovx, so, S, e->stream));
+        HIP_OK(fetch(ovx, g.ovx, so * MT_OVX_WORDS, S * MT_OVX_WORDS, e->stream));
+        HIP_OK(fetch(chi, g.chi, so, S, e->stream));
         HIP_OK(fetch(ph, g.ph, so, S, e->stream));
         HIP_OK(fetch(pxl, g.pxl, so, S, e->stream));
         HIP_OK(fetch(pxh, g.pxh, so, S, e->stream));
@@ -1593,7 +1603,8 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
         h.ovl.assign(ovl.begin() + a, ovl.begin() + a + m);
         h.props.assign(props.begin() + a, props.begin() + a + m);
         if (h.wide) {
-            h.ovx.assign(ovx.begin() + a, ovx.begin() + a + m);
+            h.ovx.assign(ovx.begin() + a * MT_OVX_WORDS, ovx.begin() + (a + m) * MT_OVX_WORDS);
+            h.chi.assign(chi.begin() + a, chi.begin() + a + m);
             h.ph.assign(ph.begin() + a, ph.begin() + a + m);
             h.pxl.assign(pxl.begin() + a, pxl.begin() + a + m);
             h.pxh.assign(pxh.begin() + a, pxh.begin() + a + m);

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
     const size_t so = (size_t)d * g.segcap;
     uint8_t* arena = g.text + (size_t)d * 2 * g.textcap;  // half 0
     // a document with any segment beyond the narrow limits loads in the wide form (UTF-16 text,
-    // u16 value ids, keys < 16, client ids < 254; include/mtgpu.h "limits")
+    // u16 value ids, keys < 16, client ids >= 64; include/mtgpu.h "limits")
     bool wdoc = false, lds = false;
     for (int base = 0; base < ns; base += 64) {
         const int i = base + lane;
@@ -91,10 +91,11 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
         if (i < ns) {
             const mt_load_seg& sg = segs[r0 + i];
             const bool pdef = sg.flags & MT_SF_PDEF;
-            w = (sg.flags & MT_LSF_U16) || (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) ||
-                (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS);
+            const uint32_t c = sg.client | ((uint32_t)sg.client_hi << 8), rc = sg.rclient | ((uint32_t)sg.rclient_hi << 8);
+            w = (sg.flags & MT_LSF_U16) || (c >= MT_MAX_CLIENTS && c != MT_CLIENT_NONCOLLAB) ||
+                (sg.rseq >= 0 && rc >= MT_MAX_CLIENTS);
             for (int k = 0; k < 16; k++) w = w || (pdef && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255));
-            l32 = (sg.client > 32 && sg.client != MT_CLIENT_NONCOLLAB) || (sg.rseq >= 0 && sg.rclient > 32);
+            l32 = (c > 32 && c != MT_CLIENT_NONCOLLAB) || (sg.rseq >= 0 && rc > 32);
         }
         wdoc = wdoc || wave_ballot(w) != 0;
         lds = lds || wave_ballot(l32) != 0;
@@ -143,7 +144,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             g.ovl[so + i] = 0;  // removedClientOverlap is not part of a snapshot
             g.props[so + i] = w4[0];
             if (wdoc) {
-                g.ovx[so + i] = 0;
+                for (int q = 0; q < MT_OVX_WORDS; q++) g.ovx[(so + i) * MT_OVX_WORDS + q] = 0;
+                g.chi[so + i] = (uint16_t)(sg.client_hi | ((rm ? sg.rclient_hi : 0u) << 8));
                 g.ph[so + i] = w4[1];
                 g.pxl[so + i] = w4[2];
                 g.pxh[so + i] = w4[3];
@@ -248,7 +250,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 if (!wdoc0) {
                     const uint32_t c = o.client;
                     const bool load = ty == MT_OP_LOAD;
-                    const uint32_t c0 = load ? (c & 0xFFu) : c, c1 = load ? (c >> 8) : 0u;
+                    const uint32_t c0 = load ? MT_LOAD_CLIENT(o) : c, c1 = load ? MT_LOAD_RCLIENT(o) : 0u;
                     const bool has0 = !load || c0 != MT_CLIENT_NONCOLLAB, has1 = load && o.pos2 >= 0;
                     c64 = c64 || (has0 && c0 > 32) || (has1 && c1 > 32);
                     wdoc = wdoc || (o.type & MT_OP_WIDE) ||
@@ -387,9 +389,11 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     int64_t len = 0;
     for (int i = 0; i < sc.nseg; i++) {  // nodeLength leaf branch (mergeTree.ts:1667-1697)
-        const bool seen = g.client[so + i] == C || g.seq[so + i] <= R;
-        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0 : (wdoc && mt_ovx_has(g.ovx[so + i], C));
-        const bool hid = (g.flags[so + i] & MT_SF_REMOVED) && (g.rclient[so + i] == C || ov || g.rseq[so + i] <= R);
+        const bool seen = mt_gclient(g, wdoc, so + i) == C || g.seq[so + i] <= R;
+        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
+                               : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
+        const bool hid = (g.flags[so + i] & MT_SF_REMOVED) &&
+                         (mt_grclient(g, wdoc, so + i) == C || ov || g.rseq[so + i] <= R);
         if (seen && !hid) len += g.len[so + i];
     }
     if ((int64_t)o.pos1 > len) g.sc[d].err = MT_DERR_INSERT_FAILED;
@@ -411,8 +415,9 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
         const uint8_t f = g.flags[so + i];
         if (f & MT_SF_MARKER) h ^= MT_MARKER_TAG;  // a Marker: its ReferenceType byte, tagged
         const bool rm = f & MT_SF_REMOVED;
-        seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(g.client[so + i]), rm ? g.rseq[so + i] : -1,
-                               rm ? (int32_t)g.rclient[so + i] : -1, mt_govl_term(g, wdoc, so + i),
+        seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(mt_gclient(g, wdoc, so + i)),
+                               rm ? g.rseq[so + i] : -1, rm ? (int32_t)mt_grclient(g, wdoc, so + i) : -1,
+                               mt_govl_term(g, wdoc, so + i),
                                mt_gprops_term(g, wdoc, so + i), (f & MT_SF_PDEF) ? 1u : 0u);
     }
     uint64_t tree_sum = 0;
@@ -632,9 +637,10 @@ __global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_po
     auto view_len = [&](int i) -> int {  // nodeLength's leaf branch (mergeTree.ts:1659-1697)
         const bool rm = (g.flags[so + i] & MT_SF_REMOVED) != 0;
         if (local) return rm ? 0 : (int)g.len[so + i];
-        const bool seen = g.client[so + i] == C || g.seq[so + i] <= R;
-        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0 : (wdoc && mt_ovx_has(g.ovx[so + i], C));
-        const bool hid = rm && (g.rclient[so + i] == C || ov || g.rseq[so + i] <= R);
+        const bool seen = mt_gclient(g, wdoc, so + i) == C || g.seq[so + i] <= R;
+        const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
+                               : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
+        const bool hid = rm && (mt_grclient(g, wdoc, so + i) == C || ov || g.rseq[so + i] <= R);
         return (seen && !hid) ? (int)g.len[so + i] : 0;
     };
     mt_pos_result r{-1, 0, 0, 0};
@@ -683,14 +689,14 @@ __global__ void mt_seginfo_kernel(mt_gstate g, const uint32_t* __restrict__ docs
         const bool rm = (f & MT_SF_REMOVED) != 0;
         r.seq = g.seq[so];
         r.rseq = rm ? g.rseq[so] : -1;
-        r.client = mt_canon_client(g.client[so]);
-        r.rclient = rm ? (int32_t)g.rclient[so] : -1;
+        r.client = mt_canon_client(mt_gclient(g, wdoc, so));
+        r.rclient = rm ? (int32_t)mt_grclient(g, wdoc, so) : -1;
         r.len = g.len[so];
         r.flags = f & (MT_SF_REMOVED | MT_SF_PDEF | MT_SF_MARKER);
         r.toff = g.toff[so];
         r.wide = wdoc ? 1u : 0u;
         r.overlap = g.ovl[so];
-        r.overlap_hi = wdoc ? g.ovx[so] : 0ull;
+        for (int q = 0; q < MT_OVX_IDS; q++) r.overlap_hi[q] = wdoc ? (uint16_t)mt_ovx_id(g.ovx + MT_OVX_WORDS * so, q) : 0;
         const uint64_t p = g.props[so];
         for (int k = 0; k < 8; k++) {
             uint32_t v = (uint32_t)(p >> (8 * k)) & 0xFFu;

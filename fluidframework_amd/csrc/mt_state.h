@@ -95,10 +95,13 @@ struct mt_gstate {
     uint64_t* ovl;     // removedClientOverlap as a bitmask over short client ids < 64
     uint64_t* props;   // 8 keys x u8 value id (a wide document: the low bytes of keys 0..7's u16 ids)
     // a wide document's extra state (MT_WIDE_DOC; [doc][segcap], allocated on first need, else null):
-    // ovx = its overlapping removers >= 64 (up to MT_OVX_IDS ids, ascending from the low byte, 0 =
-    // none); ph = the high bytes of keys 0..7's value ids; pxl / pxh = keys 8..15, low / high bytes.
+    // ovx = its overlapping removers >= 64 ([doc][segcap][4]: up to MT_OVX_IDS u16 ids ascending from
+    // the low half-word of word 0, 0 = none); chi = the high bytes of its short client ids (client's
+    // in bits 0..7, removedClient's in 8..15); ph = the high bytes of keys 0..7's value ids; pxl / pxh
+    // = keys 8..15, low / high bytes.
     // Its text arena holds UTF-16 code units (2 bytes each; toff / len / text_top in units).
     uint64_t* ovx;
+    uint16_t* chi;
     uint64_t* ph;
     uint64_t* pxl;
     uint64_t* pxh;

@@ -38,7 +38,8 @@ SF_MARKER = 16
 LSF_U16 = 64                # MT_LSF_U16: the segment's text is UTF-16 code units
 
 LOAD_SEG_DTYPE = np.dtype([('seq', '<i4'), ('rseq', '<i4'), ('client', 'u1'), ('rclient', 'u1'), ('flags', 'u1'),
-                           ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('pad2', '<u4'),
+                           ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('client_hi', 'u1'),
+                           ('rclient_hi', 'u1'), ('pad2', '<u2'),
                            ('props', '<u2', (16,)), ('pad3', '<u8')])
 assert LOAD_SEG_DTYPE.itemsize == 64
 
@@ -60,13 +61,31 @@ class Interner:
         return self.ids[k]
 
 
+class ClientInterner(Interner):
+    """Short client ids 1..65534 in first-appearance order, skipping 254 (NonCollabClient's:
+    include/mtgpu.h MT_CLIENT_NONCOLLAB; ids from 64 on make the document wide)."""
+
+    def __init__(self):
+        super().__init__(1, 65535)
+
+    def __call__(self, key):
+        k = json.dumps(key, sort_keys=True)
+        if k not in self.ids:
+            n = self.first + len(self.ids)
+            n += 1 if n >= NONCOLLAB else 0
+            if n >= self.limit:
+                raise ValueError(f'more than {self.limit - 2} distinct client ids in one document')
+            self.ids[k] = n
+        return self.ids[k]
+
+
 class DocInterners:
-    """Per-document id spaces: long client ids -> short ids (1..253), property keys -> 0..15, and
-    per key its values -> 1..65535 (0 = absent; ids are opaque, only equality matters,
+    """Per-document id spaces: long client ids -> short ids (1..65534 but 254), property keys ->
+    0..15, and per key its values -> 1..65535 (0 = absent; ids are opaque, only equality matters,
     properties.ts:62-93)."""
 
     def __init__(self):
-        self.client = Interner(1, 254)
+        self.client = ClientInterner()
         self.key = Interner(0, 16)
         self.values = {}
 
@@ -189,9 +208,10 @@ def build_load(docs, interners=None):
             tb, wide_text = encode_text(t)
             n = len(tb) // 2 if wide_text else len(tb)
             props = [pv.get(k, 0) for k in range(16)]
-            segs.append((seq, rseq, client, rclient,
+            rc = rclient if rseq >= 0 else 0
+            segs.append((seq, rseq, client & 0xFF, rc & 0xFF,
                          (SF_PDEF if pdef else 0) | (SF_MARKER if mk else 0) | (LSF_U16 if wide_text else 0), 0,
-                         len(text), n, 0, props, 0))
+                         len(text), n, client >> 8, rc >> 8, 0, props, 0))
             text += tb
             local += 0 if rseq >= 0 else n
         row_ptr.append(len(segs))
@@ -224,7 +244,9 @@ def build_load(docs, interners=None):
             if mk:
                 flags |= F_MARKER
             data = tb + pairs
-            recs.append((seq, UNIVERSAL_SEQ, 0, client | ((rclient if rseq >= 0 else 0) << 8),
+            rc = rclient if rseq >= 0 else 0
+            # (MT_OP_LOAD: the ids' low bytes in `client`, their high bytes in `msn`)
+            recs.append((seq, UNIVERSAL_SEQ, (client >> 8) | ((rc >> 8) << 8), (client & 0xFF) | ((rc & 0xFF) << 8),
                          MT_OP_LOAD | (OP_WIDE if wide else 0) | tbits, flags, pos, rseq, len(payload), len(data)))
             payload += data
         body_rp.append(len(recs))

@@ -35,7 +35,9 @@ enum mt_op_type {
                            client, seq) as SnapshotLoader.loadBody appends it (snapshotLoader.ts:
                            192-224) -- no collab-window asserts, no updateSeqNumbers.  The segment
                            may arrive removed: pos2 = its removedSeq (-1: not removed) and the
-                           high byte of `client` its removedClient.  See mt_docs_load. */
+                           high byte of `client` the low byte of its removedClient; `msn` holds the
+                           high bytes of both short ids (client's in bits 0..7, removedClient's in
+                           8..15: 0 below 256).  See mt_docs_load. */
 };
 enum mt_op_flags {
     MT_F_REWRITE = 1u << 0,    /* annotate with combiningOp {name:"rewrite"} (properties.ts:118-124) */
@@ -52,6 +54,9 @@ enum mt_op_flags {
  * (MT_OP_NP16), set only on wide records.  MT_OP_NPAIRS takes the record. */
 #define MT_OP_NP16 0x40u
 #define MT_OP_NPAIRS(o) ((((o).flags >> MT_F_NPAIRS_SHIFT) & 0xF) | (((o).type & MT_OP_NP16) ? 16 : 0))
+/* an MT_OP_LOAD record's segment client and removedClient (short ids; see MT_OP_LOAD) */
+#define MT_LOAD_CLIENT(o) (((uint32_t)(o).client & 0xFFu) | (((uint32_t)(o).msn & 0xFFu) << 8))
+#define MT_LOAD_RCLIENT(o) (((uint32_t)(o).client >> 8) | ((((uint32_t)(o).msn >> 8) & 0xFFu) << 8))
 /* Wide payload (type bit 7): the op's text is UTF-16 code units (2 bytes each, little endian:
  * cachedLength = text.length, textSegment.ts:45 -- any string, surrogate halves included) and each
  * property pair is 3 bytes (key u8 < MT_MAX_KEYS_WIDE, value id u16 LE).  The host sets it on every
@@ -119,19 +124,20 @@ typedef struct mt_op_rec {
  * A NARROW document (every document starts narrow) holds short client ids < 64 (overlap sets as a
  * u64 bitmask), keys < 8 with u8 value ids and one byte per text code unit (Latin-1): the register
  * engine's and the LDS engine's fast forms.  A WIDE document (promoted for good by its first wide
- * op, client id >= 64 or wide snapshot segment) holds client ids < 254 (u8; 0xFE is NonCollabClient),
- * keys < 16 with u16 value ids, UTF-16 text (2 bytes per code unit in the same arena: half the
- * units), and overlap sets of the ids < 64 plus at most MT_OVX_IDS ids >= 64 per segment.  Wide
+ * op, client id >= 64 or wide snapshot segment) holds client ids < 65535 (u16; 254 = 0xFE is
+ * NonCollabClient, so a host interning more than 253 clients skips it), keys < 16 with u16 value
+ * ids, UTF-16 text (2 bytes per code unit in the same arena: half the units), and overlap sets of
+ * the ids < 64 plus up to MT_OVX_IDS ids >= 64 per segment.  Wide
  * documents run on the LDS engine's wide form (its structure in an HBM workspace); their extra
  * per-segment state (32 B) is allocated by the engine on first need.  Value ids are opaque
  * (equality only) and may be interned per key. */
 #define MT_MAX_CLIENTS 64      /* narrow: short client ids 0..63 (overlap set is a u64 bitmask)  */
 #define MT_MAX_KEYS 8          /* narrow: property keys per document (u8 value id per key)      */
 #define MT_MAX_VALUES 255      /* narrow: property value ids 1..255 (0 = absent/null)           */
-#define MT_MAX_CLIENTS_WIDE 254 /* wide: short client ids 0..253                                */
+#define MT_MAX_CLIENTS_WIDE 65535 /* wide: short client ids 1..65534, except 254 (NonCollabClient) */
 #define MT_MAX_KEYS_WIDE 16    /* wide: property keys 0..15                                      */
 #define MT_MAX_VALUES_WIDE 65535 /* wide: property value ids 1..65535 per key                    */
-#define MT_OVX_IDS 8           /* wide: overlapping removers with ids >= 64 per segment          */
+#define MT_OVX_IDS 16          /* wide: overlapping removers with ids >= 64 per segment          */
 #define MT_MAX_TEXTCAP (512u * 1024u) /* text arena bytes per document half (mt_cfg.text_capacity) */
 
 typedef enum mt_status {
@@ -199,7 +205,9 @@ typedef struct mt_load_seg {  /* 64 bytes */
     uint8_t pad;
     uint32_t text_off;    /* the segment's text: byte offset in the batch's text bytes              */
     uint32_t text_len;    /* code units (= bytes without MT_LSF_U16)                                */
-    uint32_t pad2;
+    uint8_t client_hi;    /* high bytes of the short ids (a wide document's ids >= 256)             */
+    uint8_t rclient_hi;
+    uint16_t pad2;
     uint16_t props[16];   /* value id per key (0 = absent)                                           */
     uint64_t pad3;
 } mt_load_seg;
@@ -373,7 +381,7 @@ mt_status mt_resolve_positions_device(mt_engine* eng, const mt_pos_query* d_q, u
  * segment found by mt_resolve_positions, e.g. Client.getPropertiesAtPosition client.ts:1009-1023):
  * one small gather kernel and one copy, not a whole-document read.  ordinal past the document's
  * segments: seq = INT32_MIN.  Text: mt_segment_text. */
-typedef struct mt_seg_info {    /* 80 bytes */
+typedef struct mt_seg_info {    /* 104 bytes */
     int32_t seq;                /* INT32_MIN: no such segment */
     int32_t rseq;               /* removedSeq, -1: not removed */
     int32_t client;             /* short client id; -2 = NonCollabClient (constants.ts:15) */
@@ -383,8 +391,8 @@ typedef struct mt_seg_info {    /* 80 bytes */
     uint32_t toff;              /* its text in the document's arena (code units) */
     uint32_t wide;              /* 1: a wide document (UTF-16 arena) */
     uint64_t overlap;           /* removedClientOverlap: bit c for ids c < 64 */
-    uint64_t overlap_hi;        /* a wide document's overlapping removers >= 64: up to 8 ids, one per byte */
     uint16_t props[16];         /* value id per key (0: absent) */
+    uint16_t overlap_hi[MT_OVX_IDS]; /* a wide document's overlapping removers >= 64, ascending (0: none) */
 } mt_seg_info;
 mt_status mt_segment_infos(mt_engine* eng, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out);
 /* a segment's text: `len` code units of document doc's arena at `toff` (from mt_seg_info) */

@@ -30,7 +30,7 @@ const OP_NP16 = 0x40;  // MT_OP_NP16: property pair count bit 4 (wide records)
 const POS_CONTAINING = 0, POS_OF_ORDINAL = 1, POS_LOCAL = -2147483648;
 // include/mtgpu.h "limits": the wide form's (a document goes wide with its first op beyond the narrow
 // ones: client id >= 64, key >= 8, value id >= 256 or a code unit above U+00FF)
-const MAX_CLIENTS = 254, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
+const MAX_CLIENTS = 65535, NONCOLLAB_ID = 0xfe, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
 const REC = 32, EVREC = 64;
 
 function canonicalJson(v) {
@@ -201,8 +201,10 @@ class BatchClient {
     _shortId(longId) {
         let id = this.shortIds.get(longId);
         if (id === undefined) {
+            // (short id 254 is NonCollabClient's, include/mtgpu.h: never a client's)
+            if (this.longIds.length === NONCOLLAB_ID) this.longIds.push(undefined);
             id = this.longIds.length;
-            if (id >= MAX_CLIENTS) throw new Error(`BatchClient: more than ${MAX_CLIENTS} client ids in one document`);
+            if (id >= MAX_CLIENTS) throw new Error(`BatchClient: more than ${MAX_CLIENTS - 2} client ids in one document`);
             this.shortIds.set(longId, id);
             this.longIds.push(longId);
         }
@@ -581,12 +583,12 @@ class BatchClient {
             const lo = b.readUInt32LE(32), hi = b.readUInt32LE(36);
             for (let c = 0; c < 32; c++) if ((lo >>> c) & 1) overlap.push(c);
             for (let c = 0; c < 32; c++) if ((hi >>> c) & 1) overlap.push(32 + c);
-            for (let k = 0; k < 8; k++) { const c = b.readUInt8(40 + k); if (c) overlap.push(c); }
+            for (let q = 0; q < 16; q++) { const c = b.readUInt16LE(72 + 2 * q); if (!c) break; overlap.push(c); }
             let properties;
             if (flags & 2) {
                 properties = {};
                 for (let kid = 0; kid < 16; kid++) {
-                    const vid = b.readUInt16LE(48 + 2 * kid);
+                    const vid = b.readUInt16LE(40 + 2 * kid);
                     if (vid) properties[self.keys[kid]] = self.values[kid][vid];
                 }
             }

@@ -389,7 +389,7 @@ static napi_value resolve_positions(napi_env env, napi_callback_info info) {
     return out;
 }
 
-/* segmentInfos(engine, docs (uint32 rows), ordinals (int32 rows)) -> Buffer of 80-byte mt_seg_info rows */
+/* segmentInfos(engine, docs (uint32 rows), ordinals (int32 rows)) -> Buffer of 104-byte mt_seg_info rows */
 static napi_value segment_infos(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3], out;

@@ -130,7 +130,9 @@ function loadSnapshots(engine, entries) {
             const x = spec(client, s);
             const row = Buffer.alloc(LOAD_SEG);  // mt_load_seg (include/mtgpu.h)
             row.writeInt32LE(x.seq, 0); row.writeInt32LE(x.rseq, 4);
-            row.writeUInt8(x.client, 8); row.writeUInt8(x.rclient, 9);
+            const rc = x.rseq >= 0 ? x.rclient : 0;
+            row.writeUInt8(x.client & 0xff, 8); row.writeUInt8(rc & 0xff, 9);
+            row.writeUInt8(x.client >> 8, 20); row.writeUInt8(rc >> 8, 21);  // client_hi, rclient_hi
             row.writeUInt8((x.pdef ? SF_PDEF : 0) | (x.marker ? SF_MARKER : 0) | (x.u16 ? LSF_U16 : 0), 10);
             row.writeUInt32LE(textOff, 12); row.writeUInt32LE(x.units, 16);
             for (let q = 0; q < x.pairs.length; q += 2) row.writeUInt16LE(x.pairs[q + 1], 24 + 2 * x.pairs[q]);
@@ -162,8 +164,10 @@ function loadSnapshots(engine, entries) {
             sorted.forEach(([k, v], q) => {
                 if (x.wide) { pb.writeUInt8(k, 3 * q); pb.writeUInt16LE(v, 3 * q + 1); } else { pb.writeUInt8(k, 2 * q); pb.writeUInt8(v, 2 * q + 1); }
             });
-            client.queue.push({ seq: x.seq, ref: UNIVERSAL_SEQ, msn: 0,
-                client: x.client | ((x.rseq >= 0 ? x.rclient : 0) << 8), type: MT_OP_LOAD | (x.wide ? OP_WIDE : 0),
+            // (MT_OP_LOAD: the short ids' low bytes in `client`, their high bytes in `msn`)
+            const rc = x.rseq >= 0 ? x.rclient : 0;
+            client.queue.push({ seq: x.seq, ref: UNIVERSAL_SEQ, msn: (x.client >> 8) | ((rc >> 8) << 8),
+                client: (x.client & 0xff) | ((rc & 0xff) << 8), type: MT_OP_LOAD | (x.wide ? OP_WIDE : 0),
                 flags: (x.pdef ? F_PROPS : 0) | (x.marker ? F_MARKER : 0), npairs: sorted.length, pos1: pos,
                 pos2: x.rseq, payload: Buffer.concat([x.bytes, pb]) });
             engine.pending++;

@@ -33,8 +33,21 @@ def seg_hash(idx, text_hash, seq, client, rseq, rclient, overlap, props_lo, prop
 
 
 def ovl_term(mask, ovx):
-    """the overlap term: ids < 64 as a bitmask, ids >= 64 (ascending bytes from the low one) hashed in"""
+    """the overlap term: ids < 64 as a bitmask, ids >= 64 hashed in (ovx_hash)"""
     return mask ^ mix64(ovx ^ 0x4F56584944530000) if ovx else mask
+
+
+def ovx_hash(ids):
+    """the ids >= 64, ascending: up to eight below 256 as their byte list, any other list folded id by
+    id (mt_checksum.h mt_ovx_hash)"""
+    if not ids:
+        return 0
+    if len(ids) <= 8 and max(ids) <= 255:
+        return sum(o << (8 * q) for q, o in enumerate(ids))
+    h = 0x9E3779B97F4A7C15
+    for o in ids:
+        h = mix64(h ^ o)
+    return h or 1
 
 
 def props_term(lo, hi, xlo, xhi):
@@ -55,13 +68,8 @@ def checksum(state):
     """state: canonical JSON dict {"seq","msn","segs":[[text,seq,client,rseq,rclient,[ov],props]],"tree"}"""
     seg_sum = 0
     for i, (text, seq, client, rseq, rclient, ov, props) in enumerate(state['segs']):
-        mask, ovx, nx = 0, 0, 0
-        for o in sorted(ov):
-            if o < 64:
-                mask |= 1 << o
-            else:
-                ovx |= o << (8 * nx)
-                nx += 1
+        mask = sum(1 << o for o in set(ov) if o < 64)
+        ovx = ovx_hash(sorted(o for o in set(ov) if o >= 64))
         w = [0, 0, 0, 0]
         if props is not None:
             for k, v in props.items():

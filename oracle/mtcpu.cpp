@@ -75,7 +75,8 @@ struct Seg : Node {
     int32_t seq = 0, client = 0;
     bool removed = false;
     int32_t rseq = 0, rclient = 0;
-    uint64_t overlap[4] = {0, 0, 0, 0};  // removedClientOverlap as a set of client ids 0..255
+    uint64_t overlap = 0;             // removedClientOverlap: the client ids < 64 as a bitmask ...
+    std::vector<uint16_t> ovx;        // ... and the ids >= 64, ascending
     bool props_defined = false;
     uint16_t props[kMaxKeys] = {0};   // value id per key (0 = absent)
     bool marker = false;              // a Marker (mergeTree.ts:630-798): text = its one refType byte
@@ -87,15 +88,22 @@ struct Seg : Node {
     int32_t lseq = 0, lrseq = 0;      // localSeq / localRemovedSeq (0: undefined; mergeTree.ts:91-92)
     Seg() : Node(true) {}
     int len() const { return (int)text.size(); }
-    bool ovHas(int32_t c) const { return c >= 0 && c < 256 && ((overlap[c >> 6] >> (c & 63)) & 1); }
+    bool ovHas(int32_t c) const {
+        if (c < 0) return false;
+        if (c < 64) return (overlap >> c) & 1;
+        return std::binary_search(ovx.begin(), ovx.end(), (uint16_t)c);
+    }
     // addOverlappingClient; false when the device's wide form could not hold it (more than
     // MT_OVX_IDS overlapping removers with ids >= 64: MT_DERR_LIMITS, as the engine reports)
     bool ovAdd(int32_t c) {
-        if (c < 0 || c >= 256) return false;
-        if (c >= 64 && !ovHas(c) && __builtin_popcountll(overlap[1]) + __builtin_popcountll(overlap[2]) +
-                                            __builtin_popcountll(overlap[3]) >= MT_OVX_IDS)
-            return false;
-        overlap[c >> 6] |= 1ull << (c & 63);
+        if (c < 0 || c >= MT_MAX_CLIENTS_WIDE) return false;
+        if (c < 64) {
+            overlap |= 1ull << c;
+            return true;
+        }
+        if (ovHas(c)) return true;
+        if (ovx.size() >= MT_OVX_IDS) return false;
+        ovx.insert(std::upper_bound(ovx.begin(), ovx.end(), (uint16_t)c), (uint16_t)c);
         return true;
     }
 };
@@ -376,7 +384,8 @@ struct Doc {
         r->rclient = s->rclient;
         r->seq = s->seq;
         r->client = s->client;
-        std::memcpy(r->overlap, s->overlap, sizeof(r->overlap));
+        r->overlap = s->overlap;
+        r->ovx = s->ovx;
         r->marker = s->marker;
         // segmentGroups.copyTo and the property manager's pending counts (mergeTree.ts:555-560,
         // segmentPropertiesManager.ts:113-127)
@@ -644,15 +653,16 @@ struct Doc {
             for (uint32_t q = 0; q < sg.text_len; q++)
                 sx->text.push_back((sg.flags & MT_LSF_U16) ? (char16_t)(t[2 * q] | (t[2 * q + 1] << 8)) : (char16_t)t[q]);
             sx->seq = sg.seq;
-            sx->client = sg.client == MT_CLIENT_NONCOLLAB ? -2 : sg.client;
+            const int c = sg.client | (sg.client_hi << 8), rc = sg.rclient | (sg.rclient_hi << 8);
+            sx->client = c == MT_CLIENT_NONCOLLAB ? -2 : c;
             if (sg.rseq >= 0) {
                 sx->removed = true;
                 sx->rseq = sg.rseq;
-                sx->rclient = sg.rclient;
+                sx->rclient = rc;
             }
             sx->marker = (sg.flags & 16u) != 0;  // MT_SF_MARKER
-            wide = wide || (sg.flags & MT_LSF_U16) || (sg.client >= MT_MAX_CLIENTS && sg.client != MT_CLIENT_NONCOLLAB) ||
-                   (sg.rseq >= 0 && sg.rclient >= MT_MAX_CLIENTS);
+            wide = wide || (sg.flags & MT_LSF_U16) || (c >= MT_MAX_CLIENTS && c != MT_CLIENT_NONCOLLAB) ||
+                   (sg.rseq >= 0 && rc >= MT_MAX_CLIENTS);
             for (int k = 0; k < kMaxKeys; k++) wide = wide || ((sg.flags & 2u) && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255));
             if (sg.flags & 2u) {  // MT_SF_PDEF
                 sx->props_defined = true;
@@ -961,7 +971,8 @@ struct Doc {
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
         const Pay p = decodePay(op, payload);
         if (!noop) {
-            if (op.client >= MT_MAX_CLIENTS_WIDE || op.client == 0) return fail(MT_DERR_LIMITS, S);
+            if (op.client >= MT_MAX_CLIENTS_WIDE || op.client == 0 || op.client == MT_CLIENT_NONCOLLAB)
+                return fail(MT_DERR_LIMITS, S);
             if (!p.ok) return fail(MT_DERR_BAD_OP, S);
             int wc = 0;
             if (!(currentSeq < S)) wc = MT_DERR_SEQ_ORDER;              // completeAndLogOp, client.ts:461-462
@@ -1070,10 +1081,10 @@ struct Doc {
     void loadInsert(const mt_op_rec& op, const uint8_t* payload) {
         const int32_t S = op.seq, R = op.ref_seq;
         evSeq = S;
-        const int c = op.client & 0xFF, rc = op.client >> 8;
+        const int c = (int)MT_LOAD_CLIENT(op), rc = (int)MT_LOAD_RCLIENT(op);
         const int32_t C = c == MT_CLIENT_NONCOLLAB ? -2 : c;
         if (!(c == MT_CLIENT_NONCOLLAB || (c >= 1 && c < MT_MAX_CLIENTS_WIDE)) ||
-            (op.pos2 >= 0 && !(rc >= 1 && rc < MT_MAX_CLIENTS_WIDE)))
+            (op.pos2 >= 0 && !(rc >= 1 && rc < MT_MAX_CLIENTS_WIDE && rc != MT_CLIENT_NONCOLLAB)))
             return fail(MT_DERR_LIMITS, S);
         const Pay p = decodePay(op, payload);
         if (!p.ok || op.pos1 < 0) return fail(MT_DERR_BAD_OP, S);
@@ -1345,14 +1356,20 @@ uint64_t doc_checksum(const Doc& doc) {
             w[(k >> 3) * 2] |= (uint64_t)(s->props[k] & 0xFF) << (8 * (k & 7));
             w[(k >> 3) * 2 + 1] |= (uint64_t)(s->props[k] >> 8) << (8 * (k & 7));
         }
-        uint64_t ovx = 0;
-        int nx = 0;
-        for (int c = 64; c < 256; c++)
-            if (s->ovHas(c)) ovx |= (uint64_t)c << (8 * nx++);
+        // (mt_ovx_hash: up to eight ids below 256 as their byte list, any other list folded)
+        uint64_t ovx = 0, fold = 0x9E3779B97F4A7C15ull;
+        bool small = true;
+        for (size_t q = 0; q < s->ovx.size(); q++) {
+            const uint32_t v = s->ovx[q];
+            if (v > 255u || q >= 8) small = false;
+            else ovx |= (uint64_t)v << (8 * q);
+            fold = mix64(fold ^ v);
+        }
+        if (!small) ovx = fold ? fold : 1ull;
         const uint64_t th = fnv1a(s->text) ^ (s->marker ? 0x4D41524B45520000ull : 0ull);
         d.seg_sum += mto_seg_hash(idx++, th, s->seq, s->client,
                                   s->removed ? s->rseq : -1, s->removed ? s->rclient : -1,
-                                  mt_ovl_term(s->overlap[0], ovx), mt_props_term(w[0], w[1], w[2], w[3]),
+                                  mt_ovl_term(s->overlap, ovx), mt_props_term(w[0], w[1], w[2], w[3]),
                                   s->props_defined);
     });
     d.nsegs = (uint32_t)idx;
@@ -1408,12 +1425,14 @@ std::string doc_state_json(const Doc& doc) {
         o += (s->removed ? std::to_string(s->rseq) : "-1") + ',';
         o += (s->removed ? std::to_string(s->rclient) : "-1") + ",[";
         bool f2 = true;
-        for (int c = 0; c < 256; c++)
-            if (s->ovHas(c)) {
-                if (!f2) o += ',';
-                f2 = false;
-                o += std::to_string(c);
-            }
+        auto put = [&](int c) {
+            if (!f2) o += ',';
+            f2 = false;
+            o += std::to_string(c);
+        };
+        for (int c = 0; c < 64; c++)
+            if ((s->overlap >> c) & 1) put(c);
+        for (uint16_t c : s->ovx) put(c);
         o += "],";
         if (!s->props_defined) {
             o += "null";

@@ -50,7 +50,10 @@ function main() {
             let msn = seq;  // the least refSeq any active client may still send: here the window's lower end
             for (let c = 1; c <= nClients; c++) msn = Math.min(msn, Math.max(lastRef[c], seq - maxLag));
             msn = Math.max(0, Math.min(msn, R));
-            const shortId = obs.getOrAddShortClientId("c" + C);
+            // the log's short id: client C, past 253 one up (254 is NonCollabClient's in the engine's
+            // log form, include/mtgpu.h)
+            const id = C < 254 ? C : C + 1;
+            const shortId = obs.getOrAddShortClientId("c" + id);
             const L = obs.mergeTree.getLength(R, shortId);
             const t = r();
             let rec;
@@ -63,20 +66,20 @@ function main() {
                     props = {};
                     props[u(0, 11)] = u(1, 1200);
                 }
-                rec = [S, R, msn, C, 0, u(0, L), 0, text, props, 0];
+                rec = [S, R, msn, id, 0, u(0, L), 0, text, props, 0];
             } else {
                 const a = u(0, L - 1), b = Math.min(L, a + u(1, 8));
                 if (t < 0.78) {
-                    rec = [S, R, msn, C, 1, a, b, null, null, 0];
+                    rec = [S, R, msn, id, 1, a, b, null, null, 0];
                 } else {
                     const props = {};
                     props[u(0, 11)] = r() < 0.1 ? null : u(1, 1500);
                     if (r() < 0.4) props[u(0, 15)] = u(1, 400);
-                    rec = [S, R, msn, C, 2, a, b, null, props, r() < 0.05 ? 1 : 0];
+                    rec = [S, R, msn, id, 2, a, b, null, props, r() < 0.05 ? 1 : 0];
                 }
             }
             const op = toOp(rec);
-            obs.applyMsg({ clientId: "c" + C, clientSequenceNumber: 1, contents: op, metadata: undefined,
+            obs.applyMsg({ clientId: "c" + id, clientSequenceNumber: 1, contents: op, metadata: undefined,
                 minimumSequenceNumber: msn, origin: undefined, referenceSequenceNumber: R, sequenceNumber: S,
                 timestamp: 0, term: 1, traces: [], type: "op" });
             seq = S;

@@ -31,7 +31,8 @@ from make_golden import I, R, build_log  # noqa: E402
 REF_SNAP = '/root/reference/packages/dds/sequence/src/test/snapshots'
 # (set, message index k, mergeTreeSnapshotChunkSize (0 = default))
 LOG_SETS = [('synth_tiny', 384, 0), ('synth_c3', 256, 300), ('synth_c4', 512, 0), ('scenarios', 3, 0),
-            ('synth_c1', 1024, 400), ('markers', 4, 0), ('synth_markers', 320, 250)]
+            ('synth_c1', 1024, 400), ('markers', 4, 0), ('synth_markers', 320, 250),
+            ('wide_many', 330, 200)]
 # every data file snapshotVersion.spec.ts loads (sequence/src/test/snapshots/{v1,legacy,legacyWithCatchUp}/*)
 REF_FILES = [f'{v}/{k}' for v in ('v1', 'legacy', 'legacyWithCatchUp')
              for k in ('headerOnly', 'headerAndBody', 'largeBody', 'withAnnotations', 'withMarkers')]
@@ -58,7 +59,10 @@ def followup(length, seq0=0):
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
+    only = sys.argv[1:]  # (regenerate just these sets)
     for name, k, chunk in LOG_SETS:
+        if only and name not in only:
+            continue
         args = ['node', replay, 'load', os.path.join(HERE, name + '.mtlog'), str(k)] + ([str(chunk)] if chunk else [])
         res = subprocess.run(args, check=True, capture_output=True, text=True)
         out = os.path.join(HERE, f'load_{name}.jsonl')
@@ -68,6 +72,8 @@ def main():
                 r['k'] = k
                 f.write(json.dumps(r, separators=(',', ':')) + '\n')
         print(os.path.basename(out), os.path.getsize(out), 'B')
+    if only:
+        return
     dst = os.path.join(HERE, 'ref_snapshots')
     os.makedirs(dst, exist_ok=True)
     lines = []

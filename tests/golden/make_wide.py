@@ -10,7 +10,10 @@ is stored as the expected output (the make_golden.py pattern).
     a narrow document promoted mid-life by a wide op and by a client id >= 64, markers with wide props;
   * wide_synth.mtlog / .expected.jsonl -- observer-driven logs over the reference
     (oracle/tsref/wide_log.js): 120 clients per document, UTF-16 text with CJK and surrogate pairs,
-    value ids past 255, keys past 7.
+    value ids past 255, keys past 7;
+  * wide_many.mtlog / .expected.jsonl -- short client ids past 255 (320 clients per document) and
+    sixteen overlapping removers >= 64 on one segment (hand-made), plus wide_log.js documents with
+    320 clients.
 Fixtures are data only (inputs and reference outputs).
 """
 import json
@@ -75,7 +78,52 @@ def scenarios():
     return build_log(docs)
 
 
-def synth(n_docs, seed, ops, clients, lag=8):
+def many():
+    """More client ids than a byte holds and a full overlap list of high ids:
+    include/mtgpu.h MT_MAX_CLIENTS_WIDE / MT_OVX_IDS.  Short ids skip 254 (NonCollabClient's)."""
+    ids = [k for k in range(1, 330) if k != 254]
+    docs = []
+    # 0: 320 clients insert once each; then 14 clients with ids >= 256 and two in 64..255 remove one
+    #    range concurrently -- sixteen overlapping removers >= 64, the device list full -- plus a
+    #    narrow one; later ops by ids past 300 see the removal, an annotate by one splits the range
+    d, s = [], 0
+    for k in ids[:320]:
+        s += 1
+        d.append(I(s, s - 1, 0, k, 0, chr(ord('a') + k % 26)))
+    base = s
+    removers = [100, 300, 256, 257, 258, 259, 260, 261, 262, 263, 264, 265, 266, 267, 268, 200, 40]
+    for j, k in enumerate(removers):
+        s += 1
+        d.append(R(s, base, 0, k, 10, 20 + j % 4))
+    s += 1
+    d.append(I(s, s - 1, 0, 310, 5, 'after'))
+    s += 1
+    d.append(A(s, s - 1, 0, 305, 3, 12, {2: 7}))
+    for _ in range(3):  # (the msn stays below the removals: the overlap sets survive in the final state)
+        s += 1
+        d.append(N(s, base - 4))
+    docs.append(d)
+    # 1: overlapping removes by ids 255..301 interleaved with ids below 256, then the msn passes
+    #    everything: zamboni unlinks the removed segments and packs the rest
+    d, s = [], 0
+    for k in ids[:300]:
+        s += 1
+        d.append(I(s, s - 1, 0, k, min(s % 7, 2 * (s - 1)), 'xy'))
+    base = s
+    for j, k in enumerate([255, 70, 299, 301, 280, 65, 290]):
+        s += 1
+        d.append(R(s, base, 0, k, 20 + j, 40 + j))
+    s += 1
+    d.append(I(s, base, 0, 302, 30, 'mid'))
+    for _ in range(4):
+        s += 1
+        d.append(N(s, s - 1))
+    docs.append(d)
+    docs += synth_docs(6, 2029, 900, 320, 12)
+    return build_log(docs)
+
+
+def synth_docs(n_docs, seed, ops, clients, lag=8):
     res = subprocess.run(['node', os.path.join(REPO, 'oracle/tsref/wide_log.js'), str(n_docs), str(seed), str(ops),
                           str(clients), str(lag)], check=True, capture_output=True, text=True)
     docs = json.loads(res.stdout)['docs']
@@ -86,13 +134,20 @@ def synth(n_docs, seed, ops, clients, lag=8):
             props = None if props is None else {int(k): v for k, v in props.items()}
             recs.append((seq, ref, msn, c, typ, p1, p2, text, props, flags))
         out.append(recs)
-    return build_log(out)
+    return out
+
+
+def synth(n_docs, seed, ops, clients, lag=8):
+    return build_log(synth_docs(n_docs, seed, ops, clients, lag))
 
 
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
-    for name, batch in (('wide', scenarios()), ('wide_synth', synth(12, 2027, 700, 120))):
+    sets = (('wide', scenarios()), ('wide_synth', synth(12, 2027, 700, 120)), ('wide_many', many()))
+    for name, batch in sets:
+        if len(sys.argv) > 1 and name not in sys.argv[1:]:
+            continue
         path = os.path.join(HERE, name + '.mtlog')
         batch.save(path)
         res = subprocess.run(['node', replay, 'state', path], check=True, capture_output=True, text=True)

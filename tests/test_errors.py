@@ -147,7 +147,7 @@ def _device_limit_batch(oracle_lib, faulty=True):
                 int(o['pos2']), data, int(o['flags']))
         if not faulty:
             continue
-        if d == 1:   # client id 254 (short ids < 254 -- 0xFE is NonCollabClient: MT_DERR_LIMITS)
+        if d == 1:   # client id 254 (NonCollabClient's short id 0xFE, never a client's: MT_DERR_LIMITS)
             rec(201, 200, m, 254, INSERT, 0, 0, b'x')
         if d == 3:   # unknown op type (MT_DERR_BAD_OP)
             rec(201, 200, m, 1, 9)

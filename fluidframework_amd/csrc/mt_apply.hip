@@ -1516,7 +1516,7 @@ struct Wave {
         // (the editing client may be short id 0, the reference's own id, client.ts:1057-1062; its
         // document stays narrow: the editing form has no wide state)
         if (C != s.lc.own || C >= MT_MAX_CLIENTS || (op.type & MT_OP_WIDE)) return fail(MT_DERR_LIMITS, -1);
-        if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, -1);
+        if (op.payload_len < (uint32_t)(2 * np) || !MT_OP_NO_TEXT_OK(op)) return fail(MT_DERR_BAD_OP, -1);
         if (s.lc.ghi - s.lc.glo >= GN) return fail(MT_DERR_CAPACITY, -1);
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
@@ -1547,7 +1547,7 @@ struct Wave {
         if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                                  // client.ts:824
         if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);           // :826
         if (op.type & MT_OP_WIDE) return fail(MT_DERR_LIMITS, S);
-        if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+        if (op.payload_len < (uint32_t)(2 * np) || !MT_OP_NO_TEXT_OK(op)) return fail(MT_DERR_BAD_OP, S);
         op_ack(op, payload + op.payload_off + (op.payload_len - 2 * np), np);
         if (s.err) return;
         if (!(op.flags & MT_F_GROUP_MORE)) update_seq(op.msn, S);
@@ -1586,7 +1586,8 @@ struct Wave {
         } else if (!noop) {
             if (op.client == 0 || op.client >= kClients || op.client == MT_CLIENT_NONCOLLAB)
                 return fail(MT_DERR_LIMITS, S);
-            if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u))) return fail(MT_DERR_BAD_OP, S);
+            if (op.payload_len < plen || (wop && ((op.payload_len - plen) & 1u)) || !MT_OP_NO_TEXT_OK(op))
+                return fail(MT_DERR_BAD_OP, S);
         } else {  // every assert of the message before any edit: the document halts before it
             if (!(s.cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);  // client.ts:824
             if (!(op.msn <= S) || !(s.min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722

@@ -1391,7 +1391,7 @@ struct RWave {
         if constexpr (EV) evseq = S;
         if (!noop) {
             if (op.client == 0 || op.client > (W ? kC64Clients : kNarrowClients)) return fail(MT_DERR_LIMITS, S);
-            if (op.payload_len < (uint32_t)(2 * np)) return fail(MT_DERR_BAD_OP, S);
+            if (op.payload_len < (uint32_t)(2 * np) || !MT_OP_NO_TEXT_OK(op)) return fail(MT_DERR_BAD_OP, S);
             for (int q = 0; q < np; q++)
                 if (pbyte(pay, tlen + 2 * q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
             const bool ins = op.type == MT_OP_INSERT;

@@ -67,6 +67,9 @@ enum mt_op_flags {
 #define MT_OP_TYPE(o) ((o).type & 0x3Fu)
 #define MT_OP_PAIR_BYTES(o) (((o).type & MT_OP_WIDE) ? 3u : 2u)
 #define MT_OP_PAIRS_LEN(o) (MT_OP_PAIR_BYTES(o) * MT_OP_NPAIRS(o))
+/* a remove or annotate record carries no text: its payload is exactly its pairs (else MT_DERR_BAD_OP) */
+#define MT_OP_NO_TEXT_OK(o) ((MT_OP_TYPE(o) != MT_OP_REMOVE && MT_OP_TYPE(o) != MT_OP_ANNOTATE) || \
+                             (o).payload_len == MT_OP_PAIRS_LEN(o))
 /* An insert whose segment spec is the empty string is dropped by Client.applyInsertOp before it
  * touches the tree (`if (op.seg)`, client.ts:403-407: no boundary split, no completeAndLogOp
  * asserts, no callback); only updateSeqNumbers runs.  Such a record (text insert, no props, no

@@ -123,7 +123,7 @@ Pay decodePay(const mt_op_rec& op, const uint8_t* payload) {
     Pay p;
     p.np = MT_OP_NPAIRS(op);
     const uint32_t pl = MT_OP_PAIRS_LEN(op);
-    if (op.payload_len < pl) return p;
+    if (op.payload_len < pl || !MT_OP_NO_TEXT_OK(op)) return p;
     const uint8_t* b = payload + op.payload_off;
     const uint32_t tb = op.payload_len - pl;
     const bool wide = (op.type & MT_OP_WIDE) != 0;

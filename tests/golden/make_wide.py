@@ -119,6 +119,12 @@ def many():
         s += 1
         d.append(N(s, s - 1))
     docs.append(d)
+    # 2: records carrying all sixteen keys (a 16-pair record: MT_OP_NP16): an insert with sixteen
+    #    props, an annotate setting all sixteen, a rewrite with sixteen (four of them null)
+    docs.append([I(1, 0, 0, 1, 0, 'sixteen keys here', {k: 300 + k for k in range(16)}),
+                 A(2, 1, 0, 2, 2, 9, {k: 1000 + k for k in range(16)}),
+                 A(3, 2, 0, 300, 5, 14, {k: (None if k % 4 == 0 else 2000 + k) for k in range(16)}, flags=1),
+                 I(4, 3, 1, 256, 3, 'x', {15: 9}), N(5, 4), N(6, 5)])
     docs += synth_docs(6, 2029, 900, 320, 12)
     return build_log(docs)
 

@@ -105,3 +105,34 @@ def test_engine_overlap_list_limit(oracle_lib, n_high):
             if o.error(d) == (0, 0):
                 assert eng.state(d) == o.state(d), (b, d)
         eng.close()
+
+
+def _text_on_remove_batch():
+    """a remove or annotate record whose payload holds more than its pairs is malformed
+    (MT_OP_NO_TEXT_OK): document 0's remove carries two stray bytes, document 1's annotate one."""
+    from fluidframework_amd.oplog import ANNOTATE, INSERT, OP_DTYPE, REMOVE, OpBatch
+    recs, payload = [], bytearray()
+
+    def rec(seq, ref, client, typ, p1, p2, data, flags=0):
+        recs.append((seq, ref, 0, client, typ, flags, p1, p2, len(payload), len(data)))
+        payload.extend(data)
+    rec(1, 0, 1, INSERT, 0, 0, b'hello')
+    rec(2, 1, 2, REMOVE, 1, 3, b'xy')
+    rec(1, 0, 1, INSERT, 0, 0, b'hello')
+    rec(2, 1, 2, ANNOTATE, 1, 3, b'z' + bytes([1, 5]), 1 << 3)
+    return OpBatch(np.array(recs, dtype=OP_DTYPE), np.frombuffer(bytes(payload), np.uint8),
+                   np.array([0, 2, 4], dtype=np.uint32))
+
+
+def test_oracle_rejects_text_on_remove_and_annotate(oracle_lib):
+    o = oracle_lib.Oracle(2).apply(_text_on_remove_batch())
+    assert o.error(0) == (7, 2) and o.error(1) == (7, 2)
+
+
+@pytest.mark.gpu
+def test_engine_rejects_text_on_remove_and_annotate():
+    from fluidframework_amd.engine import MergeEngine
+    eng = MergeEngine(2, ops_per_launch=32)
+    eng.apply(_text_on_remove_batch())
+    assert eng.error(0) == (7, 2) and eng.error(1) == (7, 2)
+    eng.close()

@@ -56,3 +56,21 @@ def test_register_engine_hands_over_to_the_big_classes(oracle_lib):
     used = {cap: k for cap, ms, k, b in eng.last_class_stats() if k}
     assert 4096 in used and 1024 in used, used
     _check(eng, o, n, range(0, n, 5))
+
+
+def test_documents_grow_past_16k_segments(oracle_lib):
+    """The 32768-segment class (the largest the LDS engine's u16 slot indices allow) and a 4 MiB
+    text arena (include/mtgpu.h MT_MAX_TEXTCAP): one document x 26,000 ops (98 % inserts) ends above
+    16,384 segments, bit-exact against the oracle."""
+    from fluidframework_amd.engine import MergeEngine
+    n = 2
+    cfg = dict(GROW, p_insert=0.98, p_remove=0.01)
+    batch = oracle_lib.generate(n, seed=77, ops_per_doc=26000, **cfg)
+    o = oracle_lib.Oracle(n).apply(batch, threads=2)
+    segs = [o.nsegs(d) for d in range(n)]
+    assert max(segs) > 16384, segs
+    eng = MergeEngine(n, seg_capacity=32768, text_capacity=4 << 20, ops_per_launch=32)
+    eng.apply(batch)
+    assert list(eng.seg_counts()) == segs
+    _check(eng, o, n, range(n))
+    assert eng.class_kernel(32768) == 'mt::apply_kernel_g<32768>'

@@ -402,6 +402,37 @@ def timed_side_step(eng, dbatch, warmup=1, after=None):
     return el, roofline_of(eng, rcls), res
 
 
+def widen_payloads(batch):
+    """Every record of `batch` in the wide form (include/mtgpu.h MT_OP_WIDE): its text as UTF-16 code
+    units -- "a" as U+4E2D, so the documents hold non-Latin-1 text -- and (key u8, value u16) pairs."""
+    from fluidframework_amd.oplog import OpBatch
+    ops, pay = batch.ops.copy(), batch.payload
+    npairs = ((ops['flags'].astype(np.int64) >> 3) & 0xF) | np.where(ops['type'] & 0x40, 16, 0)
+    tl = ops['payload_len'].astype(np.int64) - 2 * npairs
+    new_len = 2 * tl + 3 * npairs
+    new_off = np.concatenate([[0], np.cumsum(new_len)[:-1]]).astype(np.int64)
+    out = np.zeros(int(new_len.sum()), dtype=np.uint8)
+    src_off = ops['payload_off'].astype(np.int64)
+
+    def ranks(counts):  # 0..c-1 for every op, concatenated
+        return np.arange(int(counts.sum())) - np.repeat(np.cumsum(counts) - counts, counts)
+    k = ranks(tl)
+    b = pay[np.repeat(src_off, tl) + k]
+    d = np.repeat(new_off, tl) + 2 * k
+    cjk = b == ord('a')
+    out[d] = np.where(cjk, 0x2D, b)
+    out[d + 1] = np.where(cjk, 0x4E, 0)
+    q = ranks(npairs)
+    s0 = np.repeat(src_off + tl, npairs) + 2 * q
+    d0 = np.repeat(new_off + 2 * tl, npairs) + 3 * q
+    out[d0] = pay[s0]
+    out[d0 + 1] = pay[s0 + 1]
+    ops['type'] = ops['type'] | 0x80
+    ops['payload_off'] = new_off.astype(np.uint32)
+    ops['payload_len'] = new_len.astype(np.uint32)
+    return OpBatch(ops, out, batch.row_ptr)
+
+
 def slow_paths(device, n_docs, seed):
     """N = 1 side lines for the paths off the register engine's narrow form: C3 with
     the delta callbacks recorded (any SharedString with a sequenceDelta listener: the register
@@ -475,6 +506,7 @@ def slow_paths(device, n_docs, seed):
     dev.free()
     eng.close()
     host.ops['client'] = np.where(host.ops['client'] > 0, host.ops['client'] + 300, 0).astype(host.ops['client'].dtype)
+    host = widen_payloads(host)
     eng = MergeEngine(n_w, device=device, ops_per_launch=32)
     dev = eng.stage(host)
     el, rf, _ = timed_side_step(eng, dev)
@@ -489,8 +521,9 @@ def slow_paths(device, n_docs, seed):
     except Exception as ex:
         par['oracle'] = f'unavailable: {ex}'
     wops = n_w * cfg['ops_per_doc']
-    out['C3_wide_ids'] = {'workload': f'C3 with client ids 301..332 ({n_w} docs x 1024 ops; the wide form: u16 '
-                                      'short ids, UTF-16 arena, HBM workspace)',
+    out['C3_wide_ids'] = {'workload': f'C3 with client ids 301..332 and UTF-16 text ({n_w} docs x 1024 ops, every '
+                                      'record wide, "a" as U+4E2D; the wide form: u16 short ids, UTF-16 arena, '
+                                      'HBM workspace)',
                           'value': round(wops / el, 1), 'unit': 'ops/s', 'ms_per_step': round(el * 1e3, 2),
                           'roofline': rf, 'parity': par}
     dev.free()

@@ -2322,6 +2322,8 @@ extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gs
     MT_LAUNCH_LOCB(4096, 1)
     MT_LAUNCH_LOCB(1024, 4)
     MT_LAUNCH_LOCB(4096, 4)
+    MT_LAUNCH_LOCB(8192, 1)
+    MT_LAUNCH_LOCB(8192, 4)
 #undef MT_LAUNCH_LOCB
     return hipErrorInvalidValue;
 }
@@ -2331,6 +2333,8 @@ extern "C" size_t mt_lds_bytes_loc(int cap_class, int gw) {
     if (gw == 1 && cap_class == 4096) return sizeof(mt::Lds<4096, true>);
     if (gw == 4 && cap_class == 1024) return sizeof(mt::Lds<1024, true, false, 4>);
     if (gw == 4 && cap_class == 4096) return sizeof(mt::Lds<4096, true, false, 4>);
+    if (gw == 1 && cap_class == 8192) return sizeof(mt::Lds<8192, true>);
+    if (gw == 4 && cap_class == 8192) return sizeof(mt::Lds<8192, true, false, 4>);
     return 0;
 }
 

@@ -93,10 +93,11 @@ constexpr int kWideClasses = kNumClasses - kFirstWide;
 // above 32, run by the register engine's C64 form (mt_bin_kernel)
 // (then the editing documents that fit 256 / 512 slots: the editing form at that size; then those
 // above MT_LOC_CAP = 1024: its HBM-workspace form at 2048 / 4096; then those past 64 pending edits
-// (MT_WIDE_GROUPS): the HBM-workspace form with 4 group-mask words per slot at 1024 / 4096)
-constexpr int kLocForms = 6;
-const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096, 1024, 4096};
-const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, 4, 4};
+// (MT_WIDE_GROUPS): the HBM-workspace form with 4 group-mask words per slot at 1024 / 4096; then
+// both forms at 8192)
+constexpr int kLocForms = 8;
+const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096, 1024, 4096, 8192, 8192};
+const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, 4, 4, 1, 4};
 constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
 // the register engine's C64 form per class, the other editing forms

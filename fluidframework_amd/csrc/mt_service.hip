@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 // the LDS engine at that class's capacity, not at first_lds's; then one per such class for the
 // documents that only need 64-bit overlap sets (a client id above 32): the register engine's C64 form;
 // then the editing documents' 256 / 512-slot forms, their 2048 / 4096-slot HBM-workspace forms and
-// the wide-group forms (MT_WIDE_GROUPS: 256 pending edits) at 1024 / 4096 slots.
+// the wide-group forms (MT_WIDE_GROUPS: 256 pending edits) at 1024 / 4096 slots, then both at 8192.
 // Binning is wave-aggregated: one atomic per (wave, bucket).
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
@@ -329,17 +329,19 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             if (editing) {
                 // the editing documents' buckets (mt_launch_apply_loc): the 1024-slot form at n_classes,
                 // the 256 / 512-slot forms after the C64 buckets (when the chosen class fits them), then
-                // the HBM-workspace forms at 2048 / 4096 slots (mt_launch_apply_loc_big)
+                // the HBM-workspace forms at 2048 / 4096 / 8192 slots (mt_launch_apply_loc_big)
                 const int cap = classes[4 * cls];
                 const int ebase = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds;
                 c = cap <= 256    ? ebase
                     : cap <= 512  ? ebase + 1
                     : cap <= 1024 ? n_classes
                     : cap <= 2048 ? ebase + 2
-                                  : ebase + 3;
+                    : cap <= 4096 ? ebase + 3
+                                  : ebase + 6;
                 // past 64 pending edits (or close: each local edit and each reconnect's op adds a
-                // group): the form with 256 group slots, at 1024 / 4096 slots, for good
-                if ((sc.wide & MT_WIDE_GROUPS) || pend + nloc + 4u * nregen > 48u) c = cap <= 1024 ? ebase + 4 : ebase + 5;
+                // group): the form with 256 group slots, at 1024 / 4096 / 8192 slots, for good
+                if ((sc.wide & MT_WIDE_GROUPS) || pend + nloc + 4u * nregen > 48u)
+                    c = cap <= 1024 ? ebase + 4 : cap <= 4096 ? ebase + 5 : ebase + 7;
             }
             if (acc) {
                 // algorithmic bytes of this document's share of the launch (DESIGN.md "Roofline
@@ -353,7 +355,7 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 6;
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 8;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;

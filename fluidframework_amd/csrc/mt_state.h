@@ -79,7 +79,7 @@ struct mt_locx {
 #define MT_RG_RECS 256       // regenerated op records per document between drains
 #define MT_RG_BYTES 4096     // and their payload bytes
 #define MT_LOC_CAP 1024      // the editing form's largest LDS capacity (above: its HBM-workspace form)
-#define MT_LOC_BIGCAP 4096   // the editing form's largest class: the slots of a big-pool row
+#define MT_LOC_BIGCAP 8192   // the editing form's largest class: the slots of a big-pool row
 #define MT_NO_ROW 0xFFFFFFFFu
 // pending property counts per segment (SegmentPropertiesManager, segmentPropertiesManager.ts:11-12):
 // 7 bits per key id 0..7 at bit 7k, the pending rewrite count in bits 56..63

@@ -89,8 +89,8 @@ enum mt_op_flags {
  * Remote ops see the pending segments as the reference does (nodeLength, breakTie,
  * blockInsert's continuePredicate, pending property keys).  Such a document runs on the LDS
  * engine's editing form (in LDS up to MT_LOC_CAP = 1024 segments, then with its structure in an HBM
- * workspace at 2048 / 4096; past 64 pending edits at once the workspace form with 256 pending-edit
- * slots, for good; at most 4096 segments and 256 pending edits; beyond:
+ * workspace at 2048 / 4096 / 8192; past 64 pending edits at once the workspace form with 256
+ * pending-edit slots, for good; at most 8192 segments and 256 pending edits; beyond:
  * MT_DERR_CAPACITY); its delta events include the local edits' callbacks (seq -1). */
 #define MT_SEQ_LOCAL (-1)
 /* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =

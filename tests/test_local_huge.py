@@ -195,3 +195,51 @@ def test_editing_pool_rows_scale_with_the_documents_that_need_them():
     assert used.get(0x40000000 | 2048, 0) > 0, used
     assert grown < 100 << 20, f'device memory grew by {grown >> 20} MiB'
     eng.close()
+
+
+def _editing_grow_batch(n_local):
+    """One editing document that grows past 4096 segments: client 1's local inserts (seq -1), each
+    acked by its sequenced echo at once, and every tenth a remote insert by client 2; the msn stays
+    0 (no zamboni), and each insert carries its own property value, so segments never merge."""
+    from fluidframework_amd.oplog import F_PROPS, INSERT, OP_DTYPE, OpBatch
+    recs, payload = [], bytearray()
+
+    def rec(seq, ref, client, pos, data):
+        recs.append((seq, ref, 0, client, INSERT, F_PROPS | (1 << 3), pos, 0, len(payload), len(data)))
+        payload.extend(data)
+    s = length = 0
+    for i in range(n_local):
+        pos = (i * 7919) % (length + 1)
+        data = b'ab'[i % 2:i % 2 + 1] + bytes([0, 1 + i % 250])
+        rec(-1, s, 1, pos, data)     # the local edit (MT_SEQ_LOCAL) ...
+        rec(s + 1, s, 1, pos, data)  # ... and its ack
+        s += 1
+        length += 1
+        if i % 10 == 9:
+            rec(s + 1, s, 2, (i * 31) % (length + 1), b'z' + bytes([1, 1 + i % 200]))
+            s += 1
+            length += 1
+    return OpBatch(np.array(recs, dtype=OP_DTYPE), np.frombuffer(bytes(payload), np.uint8),
+                   np.array([0, len(recs)], dtype=np.uint32))
+
+
+def test_oracle_editing_document_grows_past_4096_segments(oracle_lib):
+    b = _editing_grow_batch(4500)
+    o = oracle_lib.Oracle(1).apply(b)
+    assert o.error(0) == (0, 0) and 4096 < o.nsegs(0) < 8192, o.nsegs(0)
+
+
+@pytest.mark.gpu
+def test_engine_editing_form_past_4096_segments():
+    """The editing form's 8192-slot HBM-workspace class (apply_kernel_g<8192, false, true, 1>, a big-pool
+    row of MT_LOC_BIGCAP = 8192 slots): the device ends in the oracle's state."""
+    import oracle.oracle as oracle_lib
+    from fluidframework_amd.engine import MergeEngine
+    b = _editing_grow_batch(4500)
+    o = oracle_lib.Oracle(1).apply(b)
+    eng = MergeEngine(1, seg_capacity=8192, ops_per_launch=32)
+    eng.apply(b)
+    assert eng.error(0) == (0, 0), eng.error(0)
+    assert eng.state(0) == o.state(0)
+    assert eng.class_kernel(0x40000000 | 8192) == 'mt::apply_kernel_g<8192, false, true, 1>'
+    eng.close()

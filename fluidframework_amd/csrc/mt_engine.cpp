@@ -101,7 +101,8 @@ const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, 4, 4, 1, 4};
 constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
 // the register engine's C64 form per class, the other editing forms
-constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocForms;
+constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocForms + kWideClasses;
+constexpr int kStatWide = kNumClasses + 1 + 2 * kFirstLds + kLocForms;  // the wide form's entries
 // {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
 const int32_t kClassParams[kNumClasses * 4] = {
     128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
@@ -981,7 +982,7 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             HIP_OK(mt_launch_apply_wide(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
                                         e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
-            e->kev_cls.push_back(c);
+            e->kev_cls.push_back(kStatWide + (c - kFirstWide));
             nk++;
         }
     }
@@ -1003,7 +1004,6 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     HIP_OK(hipEventElapsedTime(&e->last_wall_ms, e->ev0, e->ev1));
     unsigned long long acc[kBuckets];
     HIP_OK(hipMemcpy(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost));
-    for (int c = kFirstWide; c < e->n_classes; c++) acc[c] += acc[e->n_classes + 1 + (c - kFirstWide)];
     e->last_ms = kms;
     e->last_launches = nk;
     e->last_bytes = 0;
@@ -1022,6 +1022,11 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     for (int q = 0; q < kLocForms; q++) {
         e->cls_bytes[kNumClasses + 1 + 2 * kFirstLds + q] = acc[lds_base + 2 * e->first_lds + q];
         e->last_bytes += acc[lds_base + 2 * e->first_lds + q];
+    }
+    for (int c = kFirstWide; c < kNumClasses; c++) {
+        const uint64_t v = c < e->n_classes ? acc[e->n_classes + 1 + (c - kFirstWide)] : 0;
+        e->cls_bytes[kStatWide + (c - kFirstWide)] = v;
+        e->last_bytes += v;
     }
     return MT_OK;
 }
@@ -1167,6 +1172,113 @@ mt_status mt_submit(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const ui
     return st;
 }
 
+// mt_submit with the upload overlapped: the documents are cut into n_chunks ranges of about equal op
+// counts; every range's records, payload bytes and its own row pointers (zero-length rows outside the
+// range: the same batch layout, so no kernel changes) go over PCIe on a copy stream, queued at once,
+// and the engine applies range k as soon as its copy has landed, while the DMA engine moves range
+// k + 1.  Documents are independent, so applying them range by range ends in the same states.
+mt_status mt_submit_pipelined(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
+                              uint64_t payload_bytes, const uint32_t* doc_row_ptr, uint32_t n_chunks) {
+    if (!e || !doc_row_ptr || n_chunks == 0) return MT_ERR_ARG;
+    const uint32_t D = e->n_docs;
+    if (doc_row_ptr[D] != n_ops) return MT_ERR_ARG;
+    for (uint32_t d = 0; d < D; d++)
+        if (doc_row_ptr[d + 1] < doc_row_ptr[d]) return MT_ERR_ARG;
+    n_chunks = std::min<uint32_t>(n_chunks, std::max<uint32_t>(1, D));
+    HIP_OK(hipSetDevice(e->cfg.device));
+    // the records' checks, as mt_batch_upload makes them (bit 0: a payload out of bounds, bit 1: wide)
+    auto scan_range = [&](uint64_t lo, uint64_t hi) {
+        bool bad = false, wide = false;
+        for (uint64_t i = lo; i < hi; i++) {
+            bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
+            wide |= wide_rec(ops[i]);
+        }
+        return (bad ? 1 : 0) | (wide ? 2 : 0);
+    };
+    int flags = 0;
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    if (n_ops < (1u << 20) || nt == 1) {
+        flags = scan_range(0, n_ops);
+    } else {
+        std::vector<std::thread> th;
+        std::vector<int> res(nt, 0);
+        for (unsigned t = 0; t < nt; t++)
+            th.emplace_back([&, t] { res[t] = scan_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
+        for (auto& x : th) x.join();
+        for (int r : res) flags |= r;
+    }
+    if (flags & 1) return MT_ERR_ARG;
+    // document ranges [cut[k], cut[k+1]) of about n_ops / n_chunks records each
+    std::vector<uint32_t> cut(n_chunks + 1, D);
+    cut[0] = 0;
+    for (uint32_t k = 1, d = 0; k < n_chunks; k++) {
+        const uint64_t want = n_ops * k / n_chunks;
+        while (d < D && doc_row_ptr[d] < want) d++;
+        cut[k] = std::max(cut[k - 1], d);
+    }
+    std::vector<mt_batch> bs(n_chunks);
+    std::vector<uint32_t> rp((size_t)n_chunks * (D + 1));
+    mt_op_rec* d_ops = nullptr;
+    uint8_t* d_pay = nullptr;
+    uint32_t* d_rp = nullptr;
+    std::vector<hipEvent_t> evs(n_chunks, nullptr);
+    mt_status st = MT_OK;
+    hipStream_t cs = nullptr;
+    auto cleanup = [&]() {
+        if (cs) (void)hipStreamSynchronize(cs);
+        (void)hipStreamSynchronize(e->stream);
+        for (auto ev : evs)
+            if (ev) (void)hipEventDestroy(ev);
+        if (cs) (void)hipStreamDestroy(cs);
+        if (d_ops) (void)hipFree(d_ops);
+        if (d_pay) (void)hipFree(d_pay);
+        if (d_rp) (void)hipFree(d_rp);
+    };
+    if (hipMalloc(&d_ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
+        hipMalloc(&d_pay, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||
+        hipMalloc(&d_rp, rp.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
+        cleanup();
+        return MT_ERR_NOMEM;
+    }
+    for (uint32_t k = 0; k < n_chunks && !st; k++) {
+        const uint32_t a = cut[k], b = cut[k + 1];
+        uint32_t* r = rp.data() + (size_t)k * (D + 1);
+        uint32_t mx = 0;
+        for (uint32_t d = 0; d <= D; d++) r[d] = doc_row_ptr[std::min(std::max(d, a), b)];
+        for (uint32_t d = a; d < b; d++) mx = std::max(mx, doc_row_ptr[d + 1] - doc_row_ptr[d]);
+        const uint64_t o0 = doc_row_ptr[a], o1 = doc_row_ptr[b];
+        uint64_t p0 = payload_bytes, p1 = 0;  // the range's payload bytes (offsets may interleave)
+        for (uint64_t i = o0; i < o1; i++) {
+            p0 = std::min<uint64_t>(p0, ops[i].payload_off);
+            p1 = std::max<uint64_t>(p1, (uint64_t)ops[i].payload_off + ops[i].payload_len);
+        }
+        if (hipEventCreateWithFlags(&evs[k], hipEventDisableTiming) != hipSuccess ||
+            (o1 > o0 && hipMemcpyAsync(d_ops + o0, ops + o0, (o1 - o0) * sizeof(mt_op_rec), hipMemcpyHostToDevice,
+                                       cs) != hipSuccess) ||
+            (p1 > p0 && hipMemcpyAsync(d_pay + p0, payload + p0, p1 - p0, hipMemcpyHostToDevice, cs) != hipSuccess) ||
+            hipMemcpyAsync(d_rp + (size_t)k * (D + 1), r, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, cs) !=
+                hipSuccess ||
+            hipEventRecord(evs[k], cs) != hipSuccess)
+            st = MT_ERR_HIP;
+        bs[k].ops = d_ops;
+        bs[k].payload = d_pay;
+        bs[k].row_ptr = d_rp + (size_t)k * (D + 1);
+        bs[k].n_ops = o1 - o0;
+        bs[k].payload_bytes = payload_bytes;
+        bs[k].n_docs = D;
+        bs[k].max_ops_per_doc = mx;
+        bs[k].wide = (flags & 2) != 0;
+    }
+    for (uint32_t k = 0; k < n_chunks && !st; k++) {
+        if (hipStreamWaitEvent(e->stream, evs[k], 0) != hipSuccess) st = MT_ERR_HIP;
+        else st = mt_batch_apply(e, &bs[k]);
+    }
+    cleanup();
+    for (auto& b : bs) b.ops = nullptr, b.payload = nullptr, b.row_ptr = nullptr;  // (freed above)
+    return st;
+}
+
 mt_status mt_sync(mt_engine* e) {
     if (!e) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
@@ -1194,7 +1306,8 @@ mt_status mt_last_apply_class_stats(mt_engine* e, uint32_t cls, uint32_t* capaci
     if (!e || cls >= (uint32_t)kStatClasses) return MT_ERR_ARG;
     if (capacity) {
         const uint32_t q = cls - kNumClasses - 1;  // (past the editing bucket)
-        *capacity = cls < (uint32_t)kNumClasses         ? (uint32_t)kClasses[cls]
+        *capacity = cls >= (uint32_t)kStatWide          ? (MT_CLASS_WIDE | (uint32_t)kClasses[kFirstWide + cls - kStatWide])
+                    : cls < (uint32_t)kNumClasses       ? (uint32_t)kClasses[cls]
                     : cls == (uint32_t)kNumClasses      ? (MT_CLASS_EDITING | MT_LOC_CAP)
                     : q < (uint32_t)kFirstLds           ? (MT_CLASS_LDS | (uint32_t)kClasses[q])
                     : q < (uint32_t)(2 * kFirstLds)     ? (MT_CLASS_C64 | (uint32_t)kClasses[q - kFirstLds])
@@ -1217,6 +1330,8 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 1>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if (capacity & MT_CLASS_WIDE)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, true>", capacity & ~(uint32_t)MT_CLASS_WIDE);
     else if ((capacity & MT_CLASS_C64) && e->g.ev)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_C64)));
     else if (capacity & MT_CLASS_C64)

@@ -71,6 +71,8 @@ def lib():
         L.mt_batch_apply.argtypes = [vp, vp]
         L.mt_batch_free.argtypes = [vp, vp]
         L.mt_submit.argtypes = [vp, vp, u64, vp, u64, vp]
+        if hasattr(L, 'mt_submit_pipelined'):  # (absent from older builds kept for A/Bs)
+            L.mt_submit_pipelined.argtypes = [vp, vp, u64, vp, u64, vp, u32]
         L.mt_sync.argtypes = [vp]
         L.mt_get_length.argtypes = [vp, u32, ctypes.POINTER(u32)]
         L.mt_get_text.argtypes = [vp, u32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
@@ -203,6 +205,15 @@ class MergeEngine:
                                _ptr(batch.row_ptr)), 'mt_submit')
         return self
 
+    def apply_pipelined(self, batch: OpBatch, chunks=4):
+        """apply() with the upload overlapped (mt_submit_pipelined): document ranges copied on a
+        stream of their own while the previous range applies; the same states.  The batch's arrays
+        should be page-locked (hipmem.PinnedArray) for the copies to run asynchronously."""
+        assert batch.n_docs == self.n_docs, 'a batch covers every document of the engine'
+        _check(lib().mt_submit_pipelined(self.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload),
+                                         len(batch.payload), _ptr(batch.row_ptr), chunks), 'mt_submit_pipelined')
+        return self
+
     def stage(self, batch: OpBatch):
         assert batch.n_docs == self.n_docs
         return DeviceBatch(self, batch)
@@ -249,7 +260,7 @@ class MergeEngine:
         editing bucket, MT_CLASS_EDITING | 1024, and the LDS engine inside each register class,
         MT_CLASS_LDS | capacity: include/mtgpu.h)."""
         out = []
-        for c in range(64):  # classes 0.. until the library reports MT_ERR_ARG
+        for c in range(256):  # classes 0.. until the library reports MT_ERR_ARG
             cap, ms, n, nb = ctypes.c_uint32(), ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
             if lib().mt_last_apply_class_stats(self.h, c, ctypes.byref(cap), ctypes.byref(ms), ctypes.byref(n),
                                                ctypes.byref(nb)) != 0:

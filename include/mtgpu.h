@@ -243,6 +243,11 @@ mt_status mt_batch_free(mt_engine* eng, mt_batch* batch);
 /* upload + apply + free (the synchronous drop-in for a loop of applyMsg calls) */
 mt_status mt_submit(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops,
                     const uint8_t* payload, uint64_t payload_bytes, const uint32_t* doc_row_ptr);
+/* mt_submit with the upload overlapped with the apply (from page-locked host memory): the documents
+ * are cut into n_chunks ranges of about equal op counts, every range is copied on a stream of its
+ * own, and range k is applied while range k + 1 is in flight.  The same states as mt_submit. */
+mt_status mt_submit_pipelined(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
+                              uint64_t payload_bytes, const uint32_t* doc_row_ptr, uint32_t n_chunks);
 mt_status mt_sync(mt_engine* eng);
 
 /* Readout (synchronises).  Text = MergeTreeTextHelper.getText for the observer, as UTF-16 code
@@ -276,12 +281,14 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
  * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),
  * reading MT_CLASS_C64 | capacity, then the editing form's other sizes, MT_CLASS_EDITING | 256 / 512
  * (LDS) and | 2048 / 4096 (HBM workspace), then MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024 / 4096 (the
- * HBM-workspace form with 256 pending-edit slots); MT_ERR_ARG past the last): each class is one kernel
- * instantiation (see mt_class_kernel_name). */
+ * HBM-workspace form with 256 pending-edit slots), then the wide form per class from 2048 on,
+ * MT_CLASS_WIDE | capacity; MT_ERR_ARG past the last): each class is one kernel instantiation (see
+ * mt_class_kernel_name). */
 #define MT_CLASS_EDITING 0x40000000u
 #define MT_CLASS_GROUPS 0x08000000u  /* with MT_CLASS_EDITING: the form for more than 64 pending edits */
 #define MT_CLASS_LDS 0x20000000u
 #define MT_CLASS_C64 0x10000000u
+#define MT_CLASS_WIDE 0x04000000u  /* the wide form (include/mtgpu.h "limits"), HBM workspace */
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);
 /* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class

@@ -2170,6 +2170,35 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     wv.store(g, d);
 }
 
+// The wide form with the document staged in LDS (small wide documents: CAP <= 512, where its
+// ~112 B per slot still lets two or more waves share a CU)
+template <int CAP>
+__global__ __launch_bounds__(64) void apply_kernel_wl(mt_gstate g, const mt_op_rec* __restrict__ ops,
+                                                      const uint8_t* __restrict__ payload,
+                                                      const uint32_t* __restrict__ row_ptr,
+                                                      const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
+                                                      uint32_t op_lo, uint32_t op_cnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t w = blockIdx.x;
+    if (w >= n_docs) return;
+    const uint32_t d = doc_ids ? doc_ids[w] : w;
+    using LS = Lds<CAP, false, true>;
+    LS& st = *reinterpret_cast<LS*>(smem);
+    Wave<CAP, false, false, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
+                                     g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
+    const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
+    const uint32_t a = min(r1, r0 + op_lo);
+    const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
+    if (a >= b) return;
+    wv.load(g, d);
+    for (uint32_t i = a; i < b; i++) {
+        if (st.err) break;
+        const mt_op_rec op = ops[i];
+        wv.apply(op, payload);
+    }
+    wv.store(g, d);
+}
+
 }  // namespace mt
 
 // ------------------------------------------------------------------------------------------
@@ -2245,19 +2274,33 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
 #undef MT_LAUNCH_BIG
 }
 
-// wide documents (mt_bin_kernel's wide buckets; workspace: n_docs * mt_lds_bytes_wide(cap_class))
+// wide documents (mt_bin_kernel's wide buckets; workspace: n_docs * mt_lds_bytes_wide(cap_class)):
+// up to 512 segments staged in LDS, above that in the HBM workspace (1024 for the classes up to it)
 extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
                                            const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                            uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
                                            hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     dim3 grid(n_docs), block(64);
+    if (cap_class <= 512) {
+#define MT_LAUNCH_WL(CAPV)                                                                                   \
+        hipLaunchKernelGGL((mt::apply_kernel_wl<CAPV>), grid, block, sizeof(mt::Lds<CAPV, false, true>), stream, \
+                           *g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
+        return hipGetLastError();
+        if (cap_class <= 256) {
+            MT_LAUNCH_WL(256)
+        }
+        MT_LAUNCH_WL(512)
+#undef MT_LAUNCH_WL
+    }
+    if (cap_class <= 1024) cap_class = 1024;
 #define MT_LAUNCH_WIDE(CAPV)                                                                                 \
     case CAPV:                                                                                               \
         hipLaunchKernelGGL((mt::apply_kernel_g<CAPV, true>), grid, block, 0, stream, *g, ops, payload, row_ptr, \
                            doc_ids, n_docs, op_lo, op_cnt, ws);                                              \
         return hipGetLastError();
     switch (cap_class) {
+        MT_LAUNCH_WIDE(1024)
         MT_LAUNCH_WIDE(2048)
         MT_LAUNCH_WIDE(4096)
         MT_LAUNCH_WIDE(8192)
@@ -2270,6 +2313,8 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
 }
 
 extern "C" size_t mt_lds_bytes_wide(int cap_class) {
+    if (cap_class <= 512) return 0;  // (staged in LDS: no workspace)
+    if (cap_class <= 1024) return sizeof(mt::Lds<1024, false, true>);
     switch (cap_class) {
         case 2048: return sizeof(mt::Lds<2048, false, true>);
         case 4096: return sizeof(mt::Lds<4096, false, true>);

@@ -86,7 +86,9 @@ constexpr int kFirstLds = 15;    // index of the 2048 class: the first the regis
 constexpr int kMaxSegCap = 32768;  // (the LDS engine's slot indices are u16: Lds::order / hslot)
 // bins of a tick (mt_bin_kernel): the classes, the editing documents, and the wide documents of the
 // classes from 2048 up (the LDS engine's wide form, include/mtgpu.h "limits")
-constexpr int kFirstWide = kFirstLds;
+// the wide form serves the classes from 256 segments on: up to 512 staged in LDS, above in the HBM
+// workspace (mt_launch_apply_wide)
+constexpr int kFirstWide = 2;
 constexpr int kWideClasses = kNumClasses - kFirstWide;
 // ... and, after those, per register class: the documents that need the LDS engine there (declared
 // label keys), run by the LDS engine at that class's capacity, then the documents with client ids
@@ -939,6 +941,30 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
             e->kev_cls.push_back(kNumClasses + 1 + (c64 ? kFirstLds : 0) + c);
             nk++;
         }
+        // wide documents: the LDS engine's wide form, per class, on the class's stream (disjoint
+        // documents, their own workspace regions)
+        for (int c = kFirstWide; c < e->n_classes; c++) {
+            const int k = e->n_classes + 1 + (c - kFirstWide);
+            const uint32_t cnt = e->h_counts[k];
+            if (!cnt) continue;
+            hipStream_t st = e->stream;
+            if (e->concurrent) {
+                st = e->side[c];
+                if (!joined[c]) HIP_OK(hipStreamWaitEvent(st, e->fork_ev, 0));
+                joined[c] = true;
+            }
+            while (e->kev.size() < 2 * (nk + 1)) {
+                hipEvent_t ev;
+                HIP_OK(hipEventCreate(&ev));
+                e->kev.push_back(ev);
+            }
+            HIP_OK(hipEventRecord(e->kev[2 * nk], st));
+            HIP_OK(mt_launch_apply_wide(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
+                                        e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], st));
+            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], st));
+            e->kev_cls.push_back(kStatWide + (c - kFirstWide));
+            nk++;
+        }
         for (int c = 0; c < kNumClasses; c++) {  // join: the next tick's binning sees every class done
             if (!joined[c]) continue;
             HIP_OK(hipEventRecord(e->join_ev[c], e->side[c]));
@@ -966,23 +992,6 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
                                            e->d_ids + (size_t)bk * b->n_docs, cnt, lo, per, e->stream));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
             e->kev_cls.push_back(q < 0 ? kNumClasses : kNumClasses + 1 + 2 * kFirstLds + q);
-            nk++;
-        }
-        // wide documents: the LDS engine's wide form, per class
-        for (int c = kFirstWide; c < e->n_classes; c++) {
-            const int k = e->n_classes + 1 + (c - kFirstWide);
-            const uint32_t cnt = e->h_counts[k];
-            if (!cnt) continue;
-            while (e->kev.size() < 2 * (nk + 1)) {
-                hipEvent_t ev;
-                HIP_OK(hipEventCreate(&ev));
-                e->kev.push_back(ev);
-            }
-            HIP_OK(hipEventRecord(e->kev[2 * nk], e->stream));
-            HIP_OK(mt_launch_apply_wide(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
-                                        e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], e->stream));
-            HIP_OK(hipEventRecord(e->kev[2 * nk + 1], e->stream));
-            e->kev_cls.push_back(kStatWide + (c - kFirstWide));
             nk++;
         }
     }
@@ -1330,8 +1339,11 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 1>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_EDITING)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%u, false, true>", capacity & ~(uint32_t)MT_CLASS_EDITING);
+    else if ((capacity & MT_CLASS_WIDE) && (capacity & ~(uint32_t)MT_CLASS_WIDE) <= 512)
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_wl<%u>", (capacity & ~(uint32_t)MT_CLASS_WIDE) <= 256 ? 256u : 512u);
     else if (capacity & MT_CLASS_WIDE)
-        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, true>", capacity & ~(uint32_t)MT_CLASS_WIDE);
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, true>",
+                 std::max<uint32_t>(1024u, capacity & ~(uint32_t)MT_CLASS_WIDE));
     else if ((capacity & MT_CLASS_C64) && e->g.ev)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel<%d, false>", lds_cap((int)(capacity & ~(uint32_t)MT_CLASS_C64)));
     else if (capacity & MT_CLASS_C64)

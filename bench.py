@@ -62,9 +62,15 @@ def pmc_traffic(kernel, config):
     from the committed PMC summary of the same bench command and config; None if not profiled."""
     try:
         with open(pmc_path(config)) as f:
-            k = json.load(f)['kernels'].get(kernel)
+            ks = json.load(f)['kernels']
     except (OSError, ValueError, KeyError):
         return None
+    k = ks.get(kernel)
+    if k is None and kernel.endswith('>'):
+        # the engine names a kernel without its defaulted template arguments; the trace spells them
+        # out ("mt::apply_kernel_g<1024, true>" -> "mt::apply_kernel_g<1024, true, false, 1>")
+        hit = [v for n, v in ks.items() if n.startswith(kernel[:-1] + ', ')]
+        k = hit[0] if len(hit) == 1 else None
     return int(k['hbm_bytes_per_launch']) if k else None
 
 

@@ -22,7 +22,7 @@ WIDE_SETS = ['wide', 'wide_synth', 'wide_many']
 
 # reference pins at the benchmark configs' full shape (tests/golden/make_fullshape.py): the logs are
 # regenerated from the recorded config and seed, their bytes checked against the recorded SHA-256
-FULLSHAPE_SETS = ['full_c3', 'full_c4', 'fuzz_1k']
+FULLSHAPE_SETS = ['full_c3', 'full_c4', 'full_c5', 'full_c3w', 'fuzz_1k']
 
 
 def load_fullshape(name):

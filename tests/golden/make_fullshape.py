@@ -7,6 +7,8 @@ oracle/tsref/build_ref.py) replays every document of
             props on inserts, half the removes aimed at a concurrent remove (BASELINE configs[2])
   full_c4   256 documents x 1024 ops x 8 clients: refSeq lag up to 256, one client stalling for
             200-op stretches (BASELINE configs[3]: heavy zamboni when the msn jumps)
+  full_c5   1,024 documents x 256 ops x 8 clients (BASELINE configs[4]'s apply);
+  full_c3w  256 documents x 1024 ops x 48 clients (C3 past 32 clients: the C64 register form);
   fuzz_1k   1,000 documents x 1024 ops, a fixed-seed high-conflict mix: 24 clients, lag up to 96,
             70 % of removes overlapping, 20 % null annotates, 5 % rewrites, props on 30 % of
             inserts, 4 % markers (client.conflictFarm.spec.ts:238-278 in spirit: many clients,
@@ -46,10 +48,18 @@ def sets():
     c3.pop('n_docs')
     c4 = dict(CONFIGS['C4'])
     c4.pop('n_docs')
+    c5 = dict(CONFIGS['C5'])
+    c5.pop('n_docs')
+    c3w = dict(CONFIGS['C3W'])
+    c3w.pop('n_docs')
     return {
         'full_c3': dict(n_docs=256, seed=20261017, cfg=c3),
         'full_c4': dict(n_docs=256, seed=20261017, cfg=c4),
         'fuzz_1k': dict(n_docs=1000, seed=4417, cfg=FUZZ),
+        # C5's apply (8 clients x 256 ops: the deli kernel assigns these logs' seq / msn) and C3 with
+        # 48 clients (the register engine's C64 form)
+        'full_c5': dict(n_docs=1024, seed=20261018, cfg=c5),
+        'full_c3w': dict(n_docs=256, seed=20261018, cfg=c3w),
     }
 
 

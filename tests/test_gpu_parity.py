@@ -42,7 +42,7 @@ def test_golden_bit_exact(name, b):
 @pytest.mark.parametrize('name', FULLSHAPE_SETS)
 def test_fullshape_bit_exact(name, b):
     """The engine against the reference itself at the benchmark configs' full shape (C3, C4: 256
-    documents x 1024 ops) and on a fixed-seed 1,000-document x 1024-op high-conflict fuzz
+    documents x 1024 ops; C5: 1,024 documents x 256 ops; C3 with 48 clients, the C64 form) and on a fixed-seed 1,000-document x 1024-op high-conflict fuzz
     (tests/golden/make_fullshape.py): every document's checksum of the reference's canonical state,
     and the first documents' states whole, at launch sizes 0 (one launch), 32 and 5."""
     from fluidframework_amd.engine import MergeEngine
@@ -55,6 +55,21 @@ def test_fullshape_bit_exact(name, b):
     for d, st in fx['states'].items():
         assert eng.state(int(d)) == st, f'{name} doc {d} b={b}: {_diff(eng.state(int(d)), st)}'
     assert all(eng.error(d) == (0, 0) for d in range(0, batch.n_docs, 7))
+
+
+@pytest.mark.parametrize('chunks', [1, 3, 8])
+@pytest.mark.parametrize('name', ['full_c4', 'fuzz_1k'])
+def test_pipelined_submit_equals_reference(name, chunks):
+    """mt_submit_pipelined (document ranges uploaded on a copy stream while the previous range
+    applies) ends in the reference's states, as mt_submit does, at 1, 3 and 8 ranges."""
+    from fluidframework_amd.engine import MergeEngine
+    batch, fx = load_fullshape(name)
+    eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.apply_pipelined(batch, chunks=chunks)
+    got = ['%016x' % c for c in eng.checksums()]
+    bad = [d for d in range(batch.n_docs) if got[d] != fx['checksum'][d]]
+    assert not bad, f'{name} chunks={chunks}: {len(bad)} documents differ, first {bad[:5]}'
+    eng.close()
 
 
 @pytest.mark.parametrize('cfg_name', ['C2', 'C3', 'C4'])

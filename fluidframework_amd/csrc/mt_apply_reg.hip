@@ -117,9 +117,13 @@ MT_DEV uint64_t prof_now() {
 template <int K>
 struct RLds {
     static constexpr int CAP = 64 * K;
-    static constexpr int LB = CAP / 2;      // leaf blocks        (same class limits as mt::Lds)
-    static constexpr int IB = CAP / 8 + 8;  // blocks per interior level
-    static constexpr int H = CAP / 2 + 64;  // heap entries (1-based)
+    // leaf blocks, blocks per interior level, heap entries (1-based): the class limits of mt::Lds at
+    // CAP, and at least those of the 256 class -- the launch's worst-case growth (mt_bin_kernel: 2 leaf
+    // blocks, 1 interior block and 4 heap entries per op) needs them for a b = 32 launch to fit the
+    // 192 class at all (mt_engine.cpp kClassParams)
+    static constexpr int LB = CAP / 2 > 128 ? CAP / 2 : 128;
+    static constexpr int IB = CAP / 8 + 8 > 40 ? CAP / 8 + 8 : 40;
+    static constexpr int H = CAP / 2 + 64 > 192 ? CAP / 2 + 64 : 192;
     uint64_t props[CAP];    // by segment id: 8 keys x u8 value id
     // scr: scratch by slot / position / leaf block (load, store); tln: by segment id, the text length
     // while linked, 0 once unlinked (the op loop's compaction).  They share their words, as neither

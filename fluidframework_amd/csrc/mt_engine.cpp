@@ -105,18 +105,20 @@ constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocFo
 // the register engine's C64 form per class, the other editing forms
 constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocForms + kWideClasses;
 constexpr int kStatWide = kNumClasses + 1 + 2 * kFirstLds + kLocForms;  // the wide form's entries
-// {CAP, LB, IB, H} per class: must match mt::Lds<CAP> / mtr::RLds<CAP/64>
+// {CAP, LB, IB, H} per class: at most mt::Lds<lds_cap(CAP)>'s and mtr::RLds<CAP/64>'s (the 128 and 192
+// classes take the 256 class's block and heap limits, which both hold: with CAP / 2 blocks and
+// CAP / 8 + 8 interior blocks no b = 32 launch fits them)
 const int32_t kClassParams[kNumClasses * 4] = {
-    128, 64, 24, 128, 192, 96, 32, 160, 256, 128, 40, 192, 320, 160, 48, 224,
+    128, 128, 40, 192, 192, 128, 40, 192, 256, 128, 40, 192, 320, 160, 48, 224,
     384, 192, 56, 256, 448, 224, 64, 288, 512, 256, 72, 320, 576, 288, 80, 352,
     640, 320, 88, 384, 704, 352, 96, 416, 768, 384, 104, 448, 832, 416, 112, 480,
     896, 448, 120, 512, 960, 480, 128, 544, 1024, 512, 136, 576, 2048, 1024, 264, 1088,
     4096, 2048, 520, 2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256, 32768, 16384, 4104, 16448};
-// the LDS engine is instantiated at 128 / 256 / 384 / 512 / 640 / 768 / 896 / 1024 / 2048 slots: the
+// the LDS engine serves the classes at 256 / 384 / 512 / 640 / 768 / 896 / 1024 / 2048 slots: the
 // next one up serves a class.  Its LDS (≈ 55 B per slot) sets the waves per CU: the steps between 512
 // and 1024 keep documents of 520-900 slots at 3-4 waves per CU instead of the 1024 form's 2.
 int lds_cap(int cap) {
-    static const int caps[] = {128, 256, 384, 512, 640, 768, 896, 1024};
+    static const int caps[] = {256, 384, 512, 640, 768, 896, 1024};  // (128: the 256 class's limits)
     for (int c : caps)
         if (cap <= c) return c;
     return cap;
@@ -1430,10 +1432,13 @@ struct HostDoc {
         std::vector<int> v;
         for (int c = 0; c < 64; c++)
             if ((ovl[i] >> c) & 1) v.push_back(c);
-        if (wide)
-            for (int q = 0; q < MT_OVX_IDS; q++)
-                if (const int c = (int)mt_ovx_id(ovx.data() + (size_t)MT_OVX_WORDS * i, q)) v.push_back(c);
-                else break;
+        if (wide) {
+            for (int q = 0; q < MT_OVX_IDS; q++) {
+                const int c = (int)mt_ovx_id(ovx.data() + (size_t)MT_OVX_WORDS * i, q);
+                if (!c) break;
+                v.push_back(c);
+            }
+        }
         return v;
     }
     uint32_t client_of(int i) const { return client[i] | (wide ? (uint32_t)(chi[i] & 0xFF) << 8 : 0u); }

@@ -1925,8 +1925,10 @@ MT_DEV KGState& kernarg_gstate() {
 // bound, so a class takes the highest occupancy whose spill stays small: K = 4 runs at 5 waves
 // (96 VGPRs, 8 B of scratch per lane), K = 6 and 7 at 4 (128 VGPRs, 8 / 56 B), K = 10 at 3 (48 B);
 // each measured faster than one wave fewer without scratch, while 200+ B of scratch (K = 8 at 4,
-// K = 11 / 12 at 3) measured 1.2-2.6x slower (profiles/r03_ab_occupancy.log).
-constexpr int wpe_default(int K) { return K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2; }
+// K = 11 / 12 at 3) measured 1.2-2.6x slower (profiles/r03_ab_occupancy.log).  The small classes
+// (documents up to ~125 segments, C5's) run at K = 2: 7 and K = 3: 6 waves, +3.3 % on C5 against 5 / 5
+// and +2.5 % against 8 / 7 (profiles/r04_ab_small_occupancy*_C5.log).
+constexpr int wpe_default(int K) { return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2; }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV
 #define MT_WPE_OV {0}

@@ -1610,6 +1610,9 @@ uint64_t mto_doc_text(mto_engine* e, uint32_t doc, char* buf, uint64_t cap) {
     return s.size() + 1;
 }
 
+// entries of the document's zamboni LRU heap (diagnostics: tools/class_bind.py)
+uint32_t mto_doc_heap(mto_engine* e, uint32_t doc) { return (uint32_t)(e->docs[doc].heap.size() - 1); }
+
 uint32_t mto_doc_nsegs(mto_engine* e, uint32_t doc) {
     uint32_t n = 0;
     Doc::walkSegs(e->docs[doc].root, [&](const Seg*) { n++; });

@@ -34,6 +34,7 @@ int mto_load(mto_engine* e, uint32_t doc, const mt_load_seg* segs, uint32_t n_se
 uint64_t mto_doc_state(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
 uint64_t mto_doc_text(mto_engine* e, uint32_t doc, char* buf, uint64_t cap);
 uint32_t mto_doc_nsegs(mto_engine* e, uint32_t doc);
+uint32_t mto_doc_heap(mto_engine* e, uint32_t doc);
 int mto_generate(const mt_synth_cfg* cfg, uint32_t d0, uint32_t n_docs, mt_op_rec* ops, uint8_t* payload,
                  uint32_t* row_ptr, uint64_t* pay_ptr, int n_threads);
 uint64_t mto_seg_hash(uint64_t idx, uint64_t text_hash, int32_t seq, int32_t client, int32_t rseq,

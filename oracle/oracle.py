@@ -51,6 +51,8 @@ def lib():
         L.mto_doc_text.argtypes = [vp, u32, ctypes.c_char_p, u64]
         L.mto_doc_nsegs.restype = u32
         L.mto_doc_nsegs.argtypes = [vp, u32]
+        L.mto_doc_heap.restype = u32
+        L.mto_doc_heap.argtypes = [vp, u32]
         L.mto_generate.restype = ctypes.c_int
         L.mto_generate.argtypes = [vp, u32, u32, vp, vp, vp, vp, ctypes.c_int]
         L.mto_load.restype = ctypes.c_int
@@ -179,3 +181,7 @@ class Oracle:
 
     def nsegs(self, doc):
         return lib().mto_doc_nsegs(self.h, doc)
+
+    def heap_size(self, doc):
+        """entries of the document's zamboni LRU heap (diagnostics)"""
+        return lib().mto_doc_heap(self.h, doc)

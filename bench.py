@@ -90,8 +90,6 @@ def parse():
                    help='rank exchange: RCCL over xGMI (default for N > 1; "rccl" also at N = 1, a one-rank '
                         'communicator), or gloo (ranks sharing one GPU, tests)')
     p.add_argument('--devices', default='', help='device of each local rank, e.g. "0,0" (default: rank i -> GPU i)')
-    p.add_argument('--no-h2d', action='store_true', help='skip the extra step whose op log is uploaded from '
-                                                         'host memory inside the timed region (value_with_h2d)')
     p.add_argument('--no-slow-paths', action='store_true',
                    help='skip the N=1 side lines for the paths off the narrow register engine (C3 with delta '
                         'events recorded, C3 with 48 clients, the editing-client farm at 100K documents)')
@@ -131,6 +129,7 @@ def main():
     from fluidframework_amd.hipmem import device_synchronize
     from fluidframework_amd.oplog import CONFIGS, DELI_CONFIGS
     from fluidframework_amd import shard
+    from fluidframework_amd.ticks import TickLog
 
     if world == 1 and args.comm != 'rccl':
         comm = shard.LocalComm()
@@ -183,40 +182,70 @@ def main():
         deli.sync()
     deli_ms = 0.0
 
+    # SURVEY.md §8(d) times the apply "from the first H2D of the op batch": the job's op log (and for
+    # C5 its raw client messages) starts in page-locked host memory, laid out tick-major -- the next
+    # b ops of every document per tick, what a serving node receives -- and mt_submit_ticks copies
+    # tick k + 1 on a copy stream while tick k applies.  Laying the log out is log generation (not
+    # timed); the upload, deli and the apply are.
+    t0 = time.time()
+    host = dev.to_host()
+    if deli is None:
+        log = TickLog.from_batch(host, args.ops_per_launch)
+    else:
+        log = TickLog.from_batch(host, args.ops_per_launch, msgs=d_msgs.download(RAW_DTYPE, n_msgs),
+                                 msg_row_ptr=d_mrow.download(np.uint32, n_docs + 1), tickets=True)
+    del host
+    layout_s = time.time() - t0
+
     def step():
-        nonlocal deli_ms
+        eng.reset()
         if deli is not None:
             deli.restore_all(seq=0, clients={})   # new documents (lambda.ts:124-167)
+        eng.apply_ticks(log, deli=deli)
+
+    def step_hbm():
+        # the same job with its op log already resident in HBM (generated there): reset + apply
+        nonlocal deli_ms
+        if deli is not None:
+            deli.restore_all(seq=0, clients={})
             deli.ticket_device(d_msgs.ptr, d_mrow.ptr, n_docs, d_tick.ptr, d_ops, n_ops)
             deli.sync()
             deli_ms += deli.last_ms()
         eng.reset()
         eng.apply_staged(dev)
 
+    def timed(fn):
+        kern_ms = wall_ms = 0.0
+        launches = alg_bytes = 0
+        cls = {}
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+            k, w, nl, nb = eng.last_stats()
+            kern_ms += k
+            wall_ms += w
+            launches += nl
+            alg_bytes += nb
+            for cap, ms, n, b in eng.last_class_stats():
+                a = cls.setdefault(cap, [0.0, 0, 0])
+                a[0] += ms
+                a[1] += n
+                a[2] += b
+        barrier()
+        return comm.max(time.perf_counter() - t0), kern_ms, wall_ms, launches, alg_bytes, cls
+
     for _ in range(args.warmup):
         step()
     ref_cs = eng.checksums() if deli is not None and args.warmup else None
-    deli_ms = 0.0
+    elapsed, kern_ms, wall_ms, launches, alg_bytes, cls = timed(step)
+    cs_fed = eng.checksums()
+    tk_ok = bool(np.all(log.tickets['status'] == 1)) if deli is not None else None
 
-    kern_ms = wall_ms = 0.0
-    launches = alg_bytes = 0
-    cls = {}
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        k, w, nl, nb = eng.last_stats()
-        kern_ms += k
-        wall_ms += w
-        launches += nl
-        alg_bytes += nb
-        for cap, ms, n, b in eng.last_class_stats():
-            a = cls.setdefault(cap, [0.0, 0, 0])
-            a[0] += ms
-            a[1] += n
-            a[2] += b
-    barrier()
-    elapsed = comm.max(time.perf_counter() - t0)
+    # the HBM-resident figure (side field): the same steps with the log generated in HBM
+    step_hbm()
+    deli_ms = 0.0
+    elapsed_hbm = timed(step_hbm)[0]
 
     # the dominant kernel's roofline: one more (untimed) step with the classes serialized, so each
     # class kernel has the GPU to itself and its launch duration is its own (in the timed steps the
@@ -224,7 +253,7 @@ def main():
     rcls = cls
     if os.environ.get('MTGPU_SERIAL') != '1':
         eng.set_concurrent_classes(False)
-        step()
+        step_hbm()
         eng.set_concurrent_classes(True)
         rcls = {cap: [ms, n, b] for cap, ms, n, b in eng.last_class_stats()}
 
@@ -232,12 +261,10 @@ def main():
     errs = sum(1 for d in range(0, n_docs, max(1, n_docs // 64)) if eng.error(d)[0])
     # SURVEY.md §8(d)'s b = infinity figure (the minimal traffic of the job): every op record and its
     # payload read once, each document's state read once (empty after the reset: its 80-byte scalar
-    # header) and written once (35 B per final segment + the header); the mean payload per op from
-    # the first 512 documents' logs
-    samp = dev.to_host(0, min(n_docs, 512))
-    ops_b = n_ops * 32 + float(samp.ops['payload_len'].astype(np.float64).sum()) * n_ops / max(1, samp.n_ops)
+    # header) and written once (35 B per final segment + the header)
+    ops_b = n_ops * 32 + float(log.tick_payload[-1])
     min_bytes = ops_b + 35.0 * float(eng.seg_counts().astype(np.float64).sum()) + 2 * 80.0 * n_docs
-    del samp
+    assert np.array_equal(cs_fed, cs), 'the host-fed tick steps differ from the HBM-resident replay'
     if deli is None:
         assert np.array_equal(cs, gen_cs), 'replay does not reproduce the generation state'
     else:
@@ -245,14 +272,12 @@ def main():
             assert np.array_equal(cs, ref_cs), 'deli + apply is not deterministic across steps'
         t = d_tick.download(TICKET_DTYPE)
         assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
-
-    value_h2d = None
-    if not args.no_h2d:
-        if deli is None:
-            value_h2d = h2d_step(eng, dev, n_total * ops_per_doc, barrier, comm)
-        else:
-            value_h2d = h2d_step_deli(eng, dev, deli, d_msgs, d_mrow, n_msgs, d_tick, n_total * ops_per_doc,
-                                      barrier, comm, cs)
+        assert tk_ok, 'a ticket of the host-fed steps is not SENT'
+    upload = {'bytes_per_step': log.upload_bytes(), 'ticks': log.n_ticks, 'layout_s': round(layout_s, 2),
+              'note': 'page-locked host memory, tick-major (mt_log_to_ticks), payload compacted per tick; '
+                      'copied on a copy stream into a ring of 3 device slots while the previous tick applies'
+                      + ('; tickets copied back per tick' if deli is not None else '')}
+    log.free()
 
     # final per-document checksum gather to rank 0 (RCCL ncclGather from HBM; the only collective)
     parts = comm.gather_checksums(eng, max_docs)
@@ -275,6 +300,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(dev, cs, n_docs, args.cpu_seconds, args.config)
 
+    kname_of = {c: eng.class_kernel(c) for c in rcls}
     slow = None
     if world == 1 and args.config == 'C3' and not args.no_slow_paths and not args.docs and not args.ops:
         # the main engine's HBM goes back before the side lines allocate theirs
@@ -297,7 +323,8 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'int32',
-            'data': 'synthetic (device-generated observer-driven op logs, mt_synth.h)',
+            'data': 'synthetic (device-generated observer-driven op logs, mt_synth.h), fed from page-locked host '
+                    'memory tick by tick inside the timed region (SURVEY.md 8(d): from the first H2D)',
             'config': {
                 'workload': f'{args.config}: {docs_per_gpu} docs/GPU x {cfg["n_clients"]} clients x {ops_per_doc} '
                             f'sequenced ops/doc ({CONFIG_NAMES.get(args.config, args.config)}), '
@@ -318,6 +345,7 @@ def main():
                                if rcls is not cls else 'the timed steps (classes serialized)',
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
                 'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
+                'classes': class_table(rcls, args.config, kname_of),
                 'b_infinity': {'bytes_per_step_rank0': int(min_bytes),
                                'frac': round(min_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
                                'note': 'SURVEY.md 8(d): state read + written once per step, every op once; '
@@ -333,8 +361,14 @@ def main():
                 'messages_per_step': n_msgs, 'joins_per_doc': n_join,
                 'kernel_ms_per_step': round(deli_ms / args.steps, 3),
                 'tickets_per_s_kernel': round(n_msgs / (deli_ms / args.steps * 1e-3), 1) if deli_ms else None,
-                'share_of_step': round(deli_ms / (elapsed * 1e3), 4)},
-            'value_with_h2d': value_h2d,
+                'share_of_step': round(deli_ms / (elapsed_hbm * 1e3), 4),
+                'note': 'kernel time from the HBM-resident steps (in the host-fed steps deli runs per tick on the '
+                        'engine stream)'},
+            'value_hbm_resident': {'value': round(total_ops / elapsed_hbm, 1), 'unit': 'ops/s',
+                                   'ms_per_step': round(elapsed_hbm / args.steps * 1e3, 3),
+                                   'note': 'the same steps with the op log already resident in HBM (generated '
+                                           'there): reset + apply' + (' (+ deli ticketing)' if deli is not None else '')},
+            'upload': upload,
             'slow_paths': slow,
             'cpu_baseline': cpu,
             'parity': parity,
@@ -365,6 +399,25 @@ def class_label(cap):
     if cap & MT_CLASS_WIDE:
         return f'wide{cap & ~MT_CLASS_WIDE}'
     return str(cap)
+
+
+def class_table(rcls, config, kname_of):
+    """Per capacity class of the serialized step: its kernel, device time, launches, algorithmic bytes
+    per launch and -- from the committed PMC passes of the same config -- the HBM bytes it actually
+    moved per launch and their ratio (every class's traffic ratio visible)."""
+    out = {}
+    tot = sum(v[0] for v in rcls.values()) or 1.0
+    for c, (ms, n, b) in sorted(rcls.items()):
+        if not n:
+            continue
+        k = kname_of[c]
+        alg = b / n
+        pmc = pmc_traffic(k, config)
+        out[class_label(c)] = {'kernel': k, 'ms': round(ms, 2), 'share': round(ms / tot, 3), 'launches': n,
+                               'avg_launch_ms': round(ms / n, 4), 'alg_bytes_per_launch': int(alg),
+                               'pmc_bytes_per_launch': pmc,
+                               'pmc_over_alg': round(pmc / alg, 2) if pmc and alg else None}
+    return out
 
 
 def roofline_of(eng, rcls):
@@ -571,100 +624,6 @@ def slow_paths(device, n_docs, seed):
     dev.free()
     eng.close()
     return out
-
-
-def h2d_step(eng, dev, job_ops, barrier, comm):
-    """One step whose op log starts in page-locked host memory ("from the first
-    H2D of the op batch"): mt_batch_upload (record validation + H2D over PCIe) and the apply,
-    timed together.  Returns the job's ops (every rank's documents) per second and the upload's
-    share."""
-    from fluidframework_amd.engine import DeviceBatch
-    from fluidframework_amd.hipmem import PinnedArray
-    from fluidframework_amd.oplog import OpBatch
-    host = dev.to_host()
-    pins = [PinnedArray(len(host.ops), host.ops.dtype), PinnedArray(len(host.payload), np.uint8),
-            PinnedArray(len(host.row_ptr), np.uint32)]
-    for p, a in zip(pins, (host.ops, host.payload, host.row_ptr)):
-        p.a[:] = a
-    pinned = OpBatch(pins[0].a, pins[1].a, pins[2].a)
-    del host
-    want = eng.checksums()
-    barrier()
-    t0 = time.perf_counter()
-    eng.reset()
-    staged = DeviceBatch(eng, pinned)
-    t1 = time.perf_counter()
-    eng.apply_staged(staged)
-    barrier()
-    el = comm.max(time.perf_counter() - t0)
-    up = comm.max(t1 - t0)
-    staged.free()
-    # the same with the upload overlapped (mt_submit_pipelined: document ranges copied while the
-    # previous range applies)
-    barrier()
-    t0 = time.perf_counter()
-    eng.reset()
-    eng.apply_pipelined(pinned, chunks=4)
-    barrier()
-    el_p = comm.max(time.perf_counter() - t0)
-    assert np.array_equal(eng.checksums(), want), 'the pipelined host-fed step differs from the HBM-resident one'
-    for p in pins:
-        p.free()
-    return {'value': round(job_ops / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3), 'step_s': round(el, 3),
-            'bytes_uploaded': int(len(pinned.ops) * 32 + len(pinned.payload)),
-            'pipelined': {'value': round(job_ops / el_p, 1), 'step_s': round(el_p, 3), 'chunks': 4},
-            'note': 'op log from page-locked host memory, validation + H2D + apply in the timed region: the '
-                    'whole log uploaded, then applied; pipelined: 4 document ranges, each uploaded while the '
-                    'previous one applies (mt_submit_pipelined)'}
-
-
-def h2d_step_deli(eng, dev, deli, d_msgs, d_mrow, n_msgs, d_tick, job_ops, barrier, comm, want_cs):
-    """C5's step with its inputs starting in page-locked host memory: the raw client messages
-    (joins + ops) and the op contents they carry are uploaded (validation + H2D), deli tickets the
-    messages and stamps seq / msn into the uploaded op records, then the apply; all timed.  The
-    result must equal the HBM-resident step's."""
-    from fluidframework_amd.deli import RAW_DTYPE
-    from fluidframework_amd.engine import DeviceBatch
-    from fluidframework_amd.hipmem import DeviceBuffer, PinnedArray
-    from fluidframework_amd.oplog import OpBatch
-    host = dev.to_host()
-    msgs = d_msgs.download(RAW_DTYPE, n_msgs)
-    mrow = d_mrow.download(np.uint32, eng.n_docs + 1)
-    pins = [PinnedArray(len(host.ops), host.ops.dtype), PinnedArray(len(host.payload), np.uint8),
-            PinnedArray(len(host.row_ptr), np.uint32), PinnedArray(len(msgs), RAW_DTYPE),
-            PinnedArray(len(mrow), np.uint32)]
-    for p, a in zip(pins, (host.ops, host.payload, host.row_ptr, msgs, mrow)):
-        p.a[:] = a
-    pinned = OpBatch(pins[0].a, pins[1].a, pins[2].a)
-    nbytes = int(len(host.ops) * 32 + len(host.payload) + msgs.nbytes + mrow.nbytes)
-    del host, msgs
-    d_m2, d_r2 = DeviceBuffer(pins[3].a.nbytes), DeviceBuffer(pins[4].a.nbytes)
-    barrier()
-    t0 = time.perf_counter()
-    eng.reset()
-    deli.restore_all(seq=0, clients={})
-    staged = DeviceBatch(eng, pinned)
-    d_m2.upload(pins[3].a)
-    d_r2.upload(pins[4].a)
-    t1 = time.perf_counter()
-    from fluidframework_amd.deli import batch_device_ptrs
-    d_ops2 = batch_device_ptrs(staged)[0]
-    deli.ticket_device(d_m2.ptr, d_r2.ptr, eng.n_docs, d_tick.ptr, d_ops2, staged.n_ops)
-    deli.sync()
-    eng.apply_staged(staged)
-    barrier()
-    el = comm.max(time.perf_counter() - t0)
-    up = comm.max(t1 - t0)
-    assert np.array_equal(eng.checksums(), want_cs), 'the host-fed C5 step differs from the HBM-resident one'
-    staged.free()
-    d_m2.free()
-    d_r2.free()
-    for p in pins:
-        p.free()
-    return {'value': round(job_ops / el, 1), 'unit': 'ops/s', 'upload_s': round(up, 3), 'step_s': round(el, 3),
-            'bytes_uploaded': nbytes,
-            'note': 'raw client messages + op contents from page-locked host memory: validation + H2D + deli '
-                    'ticketing + apply in the timed region'}
 
 
 def cpu_baseline(dev, gpu_cs, n_docs, budget_s, config='C3'):

@@ -33,12 +33,30 @@ def build(force=False, verbose=False, prof=False):
     flags = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
              '-Wno-unused-result', '-Wno-unused-value'] + os.environ.get('MTGPU_EXTRA_FLAGS', '').split()
 
+    stamp = ' '.join(flags + (['-DMT_PROF'] if prof else []))
+    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS if os.path.exists(os.path.join(CSRC, h)))
+
+    def fresh(f, obj):
+        # an object is reused when it is newer than its source and every header, and was built
+        # with the same flags (recorded next to it)
+        try:
+            t = os.path.getmtime(obj)
+            with open(obj + '.flags') as fh:
+                same = fh.read() == stamp
+        except OSError:
+            return False
+        return same and t > os.path.getmtime(os.path.join(CSRC, f)) and t > hdr_t
+
     def cc(f):
         obj = os.path.join(objdir, f + ('.prof.o' if prof else '.o'))
+        if not force and fresh(f, obj):
+            return obj
         cmd = [HIPCC] + flags + (['-DMT_PROF'] if prof else []) + ['-c', os.path.join(CSRC, f), '-o', obj]
         if verbose:
             print(' '.join(cmd))
         subprocess.check_call(cmd)
+        with open(obj + '.flags', 'w') as fh:
+            fh.write(stamp)
         return obj
 
     with ThreadPoolExecutor(max_workers=len(srcs)) as ex:

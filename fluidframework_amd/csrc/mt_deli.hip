@@ -489,6 +489,20 @@ mt_status mt_deli_ticket_device(mt_deli* dl, const mt_raw_msg* d_msgs, const uin
     return launch_ticket(dl, d_msgs, d_row_ptr, n_docs, d_out, d_ops, n_ops);
 }
 
+// (internal, mt_engine.cpp's mt_submit_ticks_deli) the ticket kernel on the apply engine's stream,
+// for the documents [0, n_docs) of a deli on `device`
+mt_status mt_deli_ticket_on_stream(mt_deli* dl, int32_t device, hipStream_t st, const mt_raw_msg* d_msgs,
+                                   const uint32_t* d_row_ptr, uint32_t n_docs, mt_ticket* d_out, mt_op_rec* d_ops,
+                                   uint64_t n_ops) {
+    if (!dl || dl->device != device || n_docs > dl->max_docs) return MT_ERR_ARG;
+    if (n_docs == 0) return MT_OK;
+    hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, st, dl->g,
+                       reinterpret_cast<const int4*>(d_msgs), d_row_ptr, n_docs, reinterpret_cast<int4*>(d_out), d_ops,
+                       n_ops);
+    DL_HIP(hipGetLastError());
+    return MT_OK;
+}
+
 mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
                                mt_raw_msg* d_msgs) {
     if (!dl || !d_ops || !d_row_ptr || !d_msgs) return MT_ERR_ARG;

@@ -58,7 +58,8 @@ extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* 
                                        mt_stack_item* items, uint32_t* depth, hipStream_t st);
 extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q, uint32_t n, mt_tile_result* out,
                                       hipStream_t st);
-extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, mt_pos_result* out,
+extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, uint32_t n_docs,
+                                        mt_pos_result* out,
                                         hipStream_t st);
 extern "C" hipError_t mt_launch_seginfo(const mt_gstate* g, const uint32_t* docs, const int32_t* ords, uint32_t n,
                                         mt_seg_info* out, hipStream_t st);
@@ -175,6 +176,21 @@ struct mt_engine {
     // the editing documents' pool rows (mt_state.h locbig / locgx): host copies, rows in use, rows held
     std::vector<uint32_t> h_locbig, h_locgx, h_bucket;
     uint32_t nbig = 0, bigcap = 0, ngx = 0, gxcap = 0;
+    std::vector<uint32_t> free_big, free_gx;  // rows given back by reloaded documents, reused first
+    // mt_submit_ticks: a ring of device slots; tick k is copied into slot k % kRing on the h2d
+    // stream while the ticks before it apply, and the slot is reused once its tick has applied (and
+    // its tickets have gone back on the d2h stream)
+    struct TickSlot {
+        mt_op_rec* ops = nullptr;
+        uint8_t* pay = nullptr;
+        uint32_t* rp = nullptr;
+        mt_raw_msg* msgs = nullptr;
+        uint32_t* mrp = nullptr;
+        mt_ticket* tk = nullptr;
+        uint64_t ops_cap = 0, pay_cap = 0, msg_cap = 0;
+        hipEvent_t ready = nullptr, applied = nullptr, drained = nullptr, ticketed = nullptr;
+    } ring[3];
+    hipStream_t h2d = nullptr, d2h = nullptr;
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
         uint64_t gen = 0;
@@ -298,9 +314,18 @@ static mt_status assign_loc_rows(mt_engine* e, const uint32_t* ids, uint32_t cnt
     }
     if (nb.empty() && ng.empty()) return MT_OK;
     HIP_OK(hipDeviceSynchronize());
-    const uint32_t kb = pool_reserve(e->nbig, e->bigcap, (uint32_t)nb.size(), [&](uint32_t r) { return grow_big(e, r); });
+    const uint32_t rb = std::min<uint32_t>((uint32_t)nb.size(), (uint32_t)e->free_big.size());
+    const uint32_t kb = rb + pool_reserve(e->nbig, e->bigcap, (uint32_t)nb.size() - rb,
+                                          [&](uint32_t r) { return grow_big(e, r); });
     for (uint32_t i = 0; i < kb; i++) {
-        const uint32_t d = nb[i], r = e->nbig++;
+        uint32_t r;
+        if (i < rb) {
+            r = e->free_big.back();
+            e->free_big.pop_back();
+        } else {
+            r = e->nbig++;
+        }
+        const uint32_t d = nb[i];
         const size_t o = (size_t)r * MT_LOC_BIGCAP, s = (size_t)d * MT_LOC_CAP;
         HIP_OK(hipMemcpy(g.gmb + o, g.gm + s, MT_LOC_CAP * 8, hipMemcpyDeviceToDevice));
         HIP_OK(hipMemcpy(g.pkb + o, g.pk + s, MT_LOC_CAP * 8, hipMemcpyDeviceToDevice));
@@ -309,11 +334,40 @@ static mt_status assign_loc_rows(mt_engine* e, const uint32_t* ids, uint32_t cnt
         e->h_locbig[d] = r;
         HIP_OK(hipMemcpy(g.locbig + d, &r, 4, hipMemcpyHostToDevice));
     }
-    const uint32_t kg = pool_reserve(e->ngx, e->gxcap, (uint32_t)ng.size(), [&](uint32_t r) { return grow_gx(e, r); });
+    const uint32_t rg = std::min<uint32_t>((uint32_t)ng.size(), (uint32_t)e->free_gx.size());
+    const uint32_t kg = rg + pool_reserve(e->ngx, e->gxcap, (uint32_t)ng.size() - rg,
+                                          [&](uint32_t r) { return grow_gx(e, r); });
     for (uint32_t i = 0; i < kg; i++) {
-        const uint32_t d = ng[i], r = e->ngx++;
+        uint32_t r;
+        if (i < rg) {
+            r = e->free_gx.back();
+            e->free_gx.pop_back();
+        } else {
+            r = e->ngx++;
+        }
+        const uint32_t d = ng[i];
         e->h_locgx[d] = r;
         HIP_OK(hipMemcpy(g.locgx + d, &r, 4, hipMemcpyHostToDevice));
+    }
+    return MT_OK;
+}
+
+// A document that starts over (mt_docs_load) gives its pool rows back: the next document that needs
+// such a form reuses them before the pools grow (its 1024-slot row is copied in then, as for a new row)
+static mt_status release_loc_rows(mt_engine* e, uint32_t d) {
+    if (d >= e->h_locbig.size()) return MT_OK;
+    const uint32_t none = MT_NO_ROW;
+    if (e->h_locbig[d] != MT_NO_ROW) {
+        e->free_big.push_back(e->h_locbig[d]);
+        e->h_locbig[d] = MT_NO_ROW;
+        HIP_OK(hipMemcpyAsync(e->g.locbig + d, &none, 4, hipMemcpyHostToDevice, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+    }
+    if (e->h_locgx[d] != MT_NO_ROW) {
+        e->free_gx.push_back(e->h_locgx[d]);
+        e->h_locgx[d] = MT_NO_ROW;
+        HIP_OK(hipMemcpyAsync(e->g.locgx + d, &none, 4, hipMemcpyHostToDevice, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
     }
     return MT_OK;
 }
@@ -326,6 +380,28 @@ static bool wide_rec(const mt_op_rec& o) {
         return (c0 != MT_CLIENT_NONCOLLAB && c0 >= MT_MAX_CLIENTS) || (o.pos2 >= 0 && c1 >= MT_MAX_CLIENTS);
     }
     return !MT_OP_IS_NOOP(o) && o.client >= MT_MAX_CLIENTS;
+}
+// Payload bounds (the kernels trust these) and whether any record needs the wide document form, in
+// one pass; a big batch is checked on all host cores.  Result bit 0: a payload out of bounds, bit 1:
+// wide.
+static int scan_records(const mt_op_rec* ops, uint64_t n_ops, uint64_t payload_bytes) {
+    auto scan_range = [&](uint64_t lo, uint64_t hi) {
+        bool bad = false, wide = false;
+        for (uint64_t i = lo; i < hi; i++) {
+            bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
+            wide |= wide_rec(ops[i]);
+        }
+        return (bad ? 1 : 0) | (wide ? 2 : 0);
+    };
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    if (n_ops < (1u << 20) || nt == 1) return scan_range(0, n_ops);
+    std::vector<std::thread> th;
+    std::vector<int> res(nt, 0);
+    for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { res[t] = scan_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
+    for (auto& x : th) x.join();
+    int flags = 0;
+    for (int r : res) flags |= r;
+    return flags;
 }
 static uint32_t seg_client(const mt_load_seg& sg) { return sg.client | ((uint32_t)sg.client_hi << 8); }
 static uint32_t seg_rclient(const mt_load_seg& sg) { return sg.rclient | ((uint32_t)sg.rclient_hi << 8); }
@@ -442,6 +518,17 @@ mt_status mt_engine_destroy(mt_engine* e) {
         if (e->join_ev[c]) (void)hipEventDestroy(e->join_ev[c]);
     }
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+    for (hipStream_t s : {e->h2d, e->d2h})
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (auto& s : e->ring) {
+        for (void* p : {(void*)s.ops, (void*)s.pay, (void*)s.rp, (void*)s.msgs, (void*)s.mrp, (void*)s.tk})
+            if (p) (void)hipFree(p);
+        for (hipEvent_t ev : {s.ready, s.applied, s.drained, s.ticketed})
+            if (ev) (void)hipEventDestroy(ev);
+    }
     delete e;
     return MT_OK;
 }
@@ -459,6 +546,17 @@ mt_status mt_docs_init(mt_engine* e, uint32_t n_docs) {
     e->n_docs = n_docs;
     e->gen++;
     e->lkeys.assign(e->cfg.max_docs, (uint16_t)MT_NO_LABEL_KEYS);
+    // every document starts over: the editing pools' rows are all free again
+    if (e->nbig || e->ngx) {
+        HIP_OK(hipStreamSynchronize(e->stream));
+        HIP_OK(hipMemset(e->g.locbig, 0xFF, e->cfg.max_docs * sizeof(uint32_t)));  // MT_NO_ROW
+        HIP_OK(hipMemset(e->g.locgx, 0xFF, e->cfg.max_docs * sizeof(uint32_t)));
+        e->h_locbig.assign(e->cfg.max_docs, MT_NO_ROW);
+        e->h_locgx.assign(e->cfg.max_docs, MT_NO_ROW);
+        e->nbig = e->ngx = 0;
+        e->free_big.clear();
+        e->free_gx.clear();
+    }
     HIP_OK(mt_launch_init(&e->g, n_docs, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return MT_OK;
@@ -519,6 +617,11 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
         if (sg.rseq >= 0 && (seg_rclient(sg) >= MT_MAX_CLIENTS_WIDE || seg_rclient(sg) == MT_CLIENT_NONCOLLAB))
             return MT_ERR_ARG;
         wide = wide || wide_load_seg(sg);
+    }
+    HIP_OK(hipSetDevice(e->cfg.device));
+    for (uint32_t i = 0; i < n; i++) {
+        const mt_status rs = release_loc_rows(e, doc_ids[i]);
+        if (rs) return rs;
     }
     HIP_OK(hipSetDevice(e->cfg.device));
     if (wide) {
@@ -589,7 +692,7 @@ mt_status mt_resolve_positions(mt_engine* e, const mt_pos_query* q, uint32_t n, 
     auto* dq = static_cast<mt_pos_query*>(buf);
     auto* dr = reinterpret_cast<mt_pos_result*>(static_cast<uint8_t*>(buf) + qb);
     hipError_t r = hipMemcpyAsync(dq, q, qb, hipMemcpyHostToDevice, e->stream);
-    if (r == hipSuccess) r = mt_launch_resolve(&e->g, dq, n, dr, e->stream);
+    if (r == hipSuccess) r = mt_launch_resolve(&e->g, dq, n, e->n_docs, dr, e->stream);
     if (r == hipSuccess) r = hipMemcpyAsync(out, dr, rb, hipMemcpyDeviceToHost, e->stream);
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
     (void)hipFree(buf);
@@ -600,7 +703,7 @@ mt_status mt_resolve_positions_device(mt_engine* e, const mt_pos_query* d_q, uin
     if (!e || (n && (!d_q || !d_out))) return MT_ERR_ARG;
     if (n == 0) return MT_OK;
     HIP_OK(hipSetDevice(e->cfg.device));
-    HIP_OK(mt_launch_resolve(&e->g, d_q, n, d_out, e->stream));
+    HIP_OK(mt_launch_resolve(&e->g, d_q, n, e->n_docs, d_out, e->stream));
     return MT_OK;
 }
 
@@ -775,28 +878,7 @@ mt_status mt_batch_upload(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, co
         }
         b->max_ops_per_doc = std::max(b->max_ops_per_doc, doc_row_ptr[d + 1] - doc_row_ptr[d]);
     }
-    // payload bounds (the kernels trust these) and whether any record needs the wide document
-    // form, in one pass; a big batch is checked on all host cores.  Result bit 0: bad, bit 1: wide.
-    auto scan_range = [&](uint64_t lo, uint64_t hi) {
-        bool bad = false, wide = false;
-        for (uint64_t i = lo; i < hi; i++) {
-            bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
-            wide |= wide_rec(ops[i]);
-        }
-        return (bad ? 1 : 0) | (wide ? 2 : 0);
-    };
-    int flags = 0;
-    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
-    if (n_ops < (1u << 20) || nt == 1) {
-        flags = scan_range(0, n_ops);
-    } else {
-        std::vector<std::thread> th;
-        std::vector<int> res(nt, 0);
-        for (unsigned t = 0; t < nt; t++)
-            th.emplace_back([&, t] { res[t] = scan_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
-        for (auto& x : th) x.join();
-        for (int r : res) flags |= r;
-    }
+    const int flags = scan_records(ops, n_ops, payload_bytes);
     if (flags & 1) {
         delete b;
         return MT_ERR_ARG;
@@ -828,10 +910,22 @@ mt_status mt_batch_free(mt_engine* e, mt_batch* b) {
     return MT_OK;
 }
 
-mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
-    if (!e || !b || b->n_docs != e->n_docs) return MT_ERR_ARG;
-    HIP_OK(hipSetDevice(e->cfg.device));
+}  // extern "C"
+
+// One apply call (mt_batch_apply, mt_submit_ticks) = apply_begin, the launches of one or more
+// batches (apply_launches), apply_end: the statistics of mt_last_apply_stats cover the whole call.
+static mt_status apply_begin(mt_engine* e) {
     e->gen++;
+    e->last_launches = 0;
+    HIP_OK(hipMemsetAsync(e->d_acc, 0, kBuckets * sizeof(unsigned long long), e->stream));
+    e->kev_cls.clear();
+    HIP_OK(hipEventRecord(e->ev0, e->stream));
+    return MT_OK;
+}
+
+// The launches of one staged batch on the engine stream, in launches of ops_per_launch ops per
+// document, then the window-assert fixup over the batch's records; nk counts the kernel events.
+static mt_status apply_launches(mt_engine* e, const mt_batch* b, uint32_t& nk) {
     if (b->wide) {
         const mt_status ws = ensure_wide(e);
         if (ws) return ws;
@@ -839,11 +933,6 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
     const uint32_t per = e->cfg.ops_per_launch ? e->cfg.ops_per_launch : std::max<uint32_t>(1, b->max_ops_per_doc);
     const uint32_t ticks = (b->max_ops_per_doc + per - 1) / per;
     const int lds_base = e->n_classes + 1 + (e->n_classes > kFirstWide ? e->n_classes - kFirstWide : 0);
-    e->last_launches = 0;
-    uint32_t nk = 0;
-    HIP_OK(hipMemsetAsync(e->d_acc, 0, kBuckets * sizeof(unsigned long long), e->stream));
-    e->kev_cls.clear();
-    HIP_OK(hipEventRecord(e->ev0, e->stream));
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
         HIP_OK(hipMemsetAsync(e->d_counts, 0, kBuckets * sizeof(uint32_t), e->stream));
@@ -998,6 +1087,11 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         }
     }
     HIP_OK(mt_launch_fixup(&e->g, b->ops, b->n_docs, e->stream));  // error precedence, see mt_service.hip
+    return MT_OK;
+}
+
+static mt_status apply_end(mt_engine* e, uint32_t nk) {
+    const int lds_base = e->n_classes + 1 + (e->n_classes > kFirstWide ? e->n_classes - kFirstWide : 0);
     HIP_OK(hipEventRecord(e->ev1, e->stream));
     HIP_OK(hipEventSynchronize(e->ev1));
     float kms = 0.f;
@@ -1040,6 +1134,312 @@ mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
         e->last_bytes += v;
     }
     return MT_OK;
+}
+
+extern "C" mt_status mt_deli_ticket_on_stream(mt_deli* dl, int32_t device, hipStream_t st, const mt_raw_msg* d_msgs,
+                                              const uint32_t* d_row_ptr, uint32_t n_docs, mt_ticket* d_out,
+                                              mt_op_rec* d_ops, uint64_t n_ops);
+
+namespace {
+constexpr int kRing = 3;  // device slots of mt_submit_ticks: two ticks in flight while one applies
+
+// slot buffers of at least the given sizes (called with nothing in flight on the engine)
+mt_status ring_reserve(mt_engine* e, uint64_t n_ops, uint64_t pay, uint64_t n_msgs) {
+    if (!e->h2d && hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking) != hipSuccess) return MT_ERR_HIP;
+    if (!e->d2h && hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking) != hipSuccess) return MT_ERR_HIP;
+    const size_t rp = ((size_t)e->cfg.max_docs + 1) * sizeof(uint32_t);
+    for (auto& s : e->ring) {
+        if (!s.ready) {
+            for (hipEvent_t* ev : {&s.ready, &s.applied, &s.drained, &s.ticketed})
+                if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return MT_ERR_HIP;
+            // (recorded once, so the first waits on them pass)
+            HIP_OK(hipEventRecord(s.applied, e->stream));
+            HIP_OK(hipEventRecord(s.drained, e->stream));
+            HIP_OK(hipMalloc(&s.rp, rp));
+            HIP_OK(hipMalloc(&s.mrp, rp));
+        }
+        if (s.ops_cap < n_ops) {
+            if (s.ops) HIP_OK(hipFree(s.ops));
+            s.ops = nullptr;
+            s.ops_cap = 0;
+            if (hipMalloc(&s.ops, n_ops * sizeof(mt_op_rec)) != hipSuccess) return MT_ERR_NOMEM;
+            s.ops_cap = n_ops;
+        }
+        if (s.pay_cap < pay) {
+            if (s.pay) HIP_OK(hipFree(s.pay));
+            s.pay = nullptr;
+            s.pay_cap = 0;
+            if (hipMalloc(&s.pay, pay) != hipSuccess) return MT_ERR_NOMEM;
+            s.pay_cap = pay;
+        }
+        if (s.msg_cap < n_msgs) {
+            if (s.msgs) HIP_OK(hipFree(s.msgs));
+            if (s.tk) HIP_OK(hipFree(s.tk));
+            s.msgs = nullptr;
+            s.tk = nullptr;
+            s.msg_cap = 0;
+            if (hipMalloc(&s.msgs, n_msgs * sizeof(mt_raw_msg)) != hipSuccess ||
+                hipMalloc(&s.tk, n_msgs * sizeof(mt_ticket)) != hipSuccess)
+                return MT_ERR_NOMEM;
+            s.msg_cap = n_msgs;
+        }
+    }
+    return MT_OK;
+}
+
+bool row_ptr_ok(const uint32_t* rp, uint32_t n_docs, uint64_t n, uint32_t* max_rows) {
+    if (!rp || rp[0] != 0 || rp[n_docs] != n) return false;
+    uint32_t mx = 0;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        if (rp[d + 1] < rp[d]) return false;
+        mx = std::max(mx, rp[d + 1] - rp[d]);
+    }
+    if (max_rows) *max_rows = mx;
+    return true;
+}
+
+mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t n) {
+    if (!e || (n && !ticks)) return MT_ERR_ARG;
+    const uint32_t D = e->n_docs;
+    uint64_t mo = 1, mp = 1, mm = 1;
+    for (uint32_t k = 0; k < n; k++) {
+        const mt_tick& t = ticks[k];
+        if (!t.doc_row_ptr || (t.n_ops && !t.ops) || (t.payload_bytes && !t.payload) || t.n_ops >= (1ull << 32) ||
+            (t.n_msgs && (!dl || !t.msgs || !t.msg_row_ptr)) || t.n_msgs >= (1ull << 32))
+            return MT_ERR_ARG;
+        mo = std::max(mo, t.n_ops);
+        mp = std::max(mp, t.payload_bytes);
+        mm = std::max(mm, t.n_msgs);
+    }
+    HIP_OK(hipSetDevice(e->cfg.device));
+    if (n == 0) return MT_OK;
+    HIP_OK(hipStreamSynchronize(e->stream));
+    mt_status st = ring_reserve(e, mo, mp, mm);
+    if (st) return st;
+    mt_batch bs[kRing];
+    // tick k: checked on the host, then copied into its slot once the slot's previous tick has
+    // applied and its tickets have gone back
+    auto stage = [&](uint32_t k) -> mt_status {
+        const mt_tick& t = ticks[k];
+        auto& s = e->ring[k % kRing];
+        mt_batch& b = bs[k % kRing];
+        uint32_t mx = 0;
+        if (!row_ptr_ok(t.doc_row_ptr, D, t.n_ops, &mx) || (t.n_msgs && !row_ptr_ok(t.msg_row_ptr, D, t.n_msgs, nullptr)))
+            return MT_ERR_ARG;
+        const int flags = scan_records(t.ops, t.n_ops, t.payload_bytes);
+        if (flags & 1) return MT_ERR_ARG;
+        b = mt_batch();
+        b.ops = s.ops;
+        b.payload = s.pay;
+        b.row_ptr = s.rp;
+        b.n_ops = t.n_ops;
+        b.payload_bytes = t.payload_bytes;
+        b.n_docs = D;
+        b.max_ops_per_doc = mx;
+        b.wide = (flags & 2) != 0;
+        HIP_OK(hipStreamWaitEvent(e->h2d, s.applied, 0));
+        HIP_OK(hipStreamWaitEvent(e->h2d, s.drained, 0));
+        if (t.n_ops) HIP_OK(hipMemcpyAsync(s.ops, t.ops, t.n_ops * sizeof(mt_op_rec), hipMemcpyHostToDevice, e->h2d));
+        if (t.payload_bytes) HIP_OK(hipMemcpyAsync(s.pay, t.payload, t.payload_bytes, hipMemcpyHostToDevice, e->h2d));
+        HIP_OK(hipMemcpyAsync(s.rp, t.doc_row_ptr, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->h2d));
+        if (t.n_msgs) {
+            HIP_OK(hipMemcpyAsync(s.msgs, t.msgs, t.n_msgs * sizeof(mt_raw_msg), hipMemcpyHostToDevice, e->h2d));
+            HIP_OK(hipMemcpyAsync(s.mrp, t.msg_row_ptr, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->h2d));
+        }
+        HIP_OK(hipEventRecord(s.ready, e->h2d));
+        return MT_OK;
+    };
+    if ((st = apply_begin(e))) return st;
+    uint32_t nk = 0;
+    // a tick that fails its checks ends the feed there: the ticks staged before it still apply
+    uint32_t limit = n;
+    mt_status refused = MT_OK;
+    auto stage_or_stop = [&](uint32_t k) {
+        if (k >= limit) return;
+        if ((refused = stage(k))) limit = k;
+    };
+    for (uint32_t k = 0; k + 1 < kRing; k++) stage_or_stop(k);
+    for (uint32_t k = 0; k < limit && !st; k++) {
+        stage_or_stop(k + kRing - 1);
+        if (k >= limit) break;
+        auto& s = e->ring[k % kRing];
+        const mt_tick& t = ticks[k];
+        HIP_OK(hipStreamWaitEvent(e->stream, s.ready, 0));
+        if (t.n_msgs) {
+            if ((st = mt_deli_ticket_on_stream(dl, e->cfg.device, e->stream, s.msgs, s.mrp, D, s.tk, s.ops, t.n_ops)))
+                break;
+            if (t.tickets) {
+                HIP_OK(hipEventRecord(s.ticketed, e->stream));
+                HIP_OK(hipStreamWaitEvent(e->d2h, s.ticketed, 0));
+                HIP_OK(hipMemcpyAsync(t.tickets, s.tk, t.n_msgs * sizeof(mt_ticket), hipMemcpyDeviceToHost, e->d2h));
+                HIP_OK(hipEventRecord(s.drained, e->d2h));
+            }
+        }
+        if ((st = apply_launches(e, &bs[k % kRing], nk))) break;
+        HIP_OK(hipEventRecord(s.applied, e->stream));
+    }
+    // (on an error the ticks in flight still land before the slots can be reused or freed)
+    const mt_status se = apply_end(e, nk);
+    HIP_OK(hipStreamSynchronize(e->h2d));
+    HIP_OK(hipStreamSynchronize(e->d2h));
+    return st ? st : se ? se : refused;
+}
+}  // namespace
+
+extern "C" {
+
+mt_status mt_batch_apply(mt_engine* e, const mt_batch* b) {
+    if (!e || !b || b->n_docs != e->n_docs) return MT_ERR_ARG;
+    HIP_OK(hipSetDevice(e->cfg.device));
+    mt_status st = apply_begin(e);
+    uint32_t nk = 0;
+    if (!st) st = apply_launches(e, b, nk);
+    const mt_status se = apply_end(e, nk);
+    return st ? st : se;
+}
+
+mt_status mt_submit_ticks(mt_engine* e, const mt_tick* ticks, uint32_t n_ticks) {
+    if (e && ticks)
+        for (uint32_t k = 0; k < n_ticks; k++)
+            if (ticks[k].n_msgs) return MT_ERR_ARG;  // (raw messages need mt_submit_ticks_deli)
+    return submit_ticks(e, nullptr, ticks, n_ticks);
+}
+
+mt_status mt_submit_ticks_deli(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t n_ticks) {
+    if (!dl) return MT_ERR_ARG;
+    return submit_ticks(e, dl, ticks, n_ticks);
+}
+
+mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
+                          const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, const mt_raw_msg* msgs,
+                          uint64_t n_msgs, const uint32_t* msg_row_ptr, mt_tick_layout* out) {
+    if (!out || per == 0 || (n_ops && !ops) || (payload_bytes && !payload) || (n_msgs && (!msgs || !msg_row_ptr)))
+        return MT_ERR_ARG;
+    uint32_t mx = 0;
+    if (!row_ptr_ok(doc_row_ptr, n_docs, n_ops, &mx) || (msgs && !row_ptr_ok(msg_row_ptr, n_docs, n_msgs, nullptr)))
+        return MT_ERR_ARG;
+    const uint32_t T = std::max<uint32_t>(1, (mx + per - 1) / per);
+    // documents in nt contiguous ranges; per range and tick: records, payload bytes, messages
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    const unsigned R = n_docs < 4096 ? 1u : nt;
+    std::vector<uint64_t> cnt((size_t)R * T * 3, 0);
+    std::atomic<bool> bad{false};
+    auto tick_of = [&](uint32_t d, uint64_t rec) { return (uint32_t)((rec - doc_row_ptr[d]) / per); };
+    // the tick of message i of document d (its record's, else the previous record's, else 0)
+    auto run = [&](unsigned r, bool write, const std::vector<uint64_t>* base) {
+        const uint32_t d0 = (uint32_t)((uint64_t)n_docs * r / R), d1 = (uint32_t)((uint64_t)n_docs * (r + 1) / R);
+        uint64_t* c = cnt.data() + (size_t)r * T * 3;
+        std::vector<uint64_t> o, p, m, start;  // write cursors per tick; a document's first record per tick
+        if (write) {
+            start.resize(T);
+            o.resize(T);
+            p.resize(T);
+            m.resize(T);
+            for (uint32_t t = 0; t < T; t++) {
+                o[t] = (*base)[((size_t)r * T + t) * 3 + 0];
+                p[t] = (*base)[((size_t)r * T + t) * 3 + 1];
+                m[t] = (*base)[((size_t)r * T + t) * 3 + 2];
+            }
+        }
+        for (uint32_t d = d0; d < d1; d++) {
+            if (write) start = o;
+            for (uint64_t i = doc_row_ptr[d]; i < doc_row_ptr[d + 1]; i++) {
+                const uint32_t t = tick_of(d, i);
+                const mt_op_rec& x = ops[i];
+                if ((uint64_t)x.payload_off + x.payload_len > payload_bytes) {
+                    bad = true;
+                    return;
+                }
+                if (!write) {
+                    c[t * 3 + 0]++;
+                    c[t * 3 + 1] += x.payload_len;
+                    continue;
+                }
+                mt_op_rec y = x;
+                y.payload_off = (uint32_t)(p[t] - out->tick_payload[t]);
+                memcpy(out->payload + p[t], payload + x.payload_off, x.payload_len);
+                p[t] += x.payload_len;
+                out->ops[o[t]++] = y;
+            }
+            if (write)
+                for (uint32_t t = 0; t < T; t++) {
+                    out->row_ptrs[(size_t)t * (n_docs + 1) + d + 1] = (uint32_t)(o[t] - out->tick_ops[t]);
+                }
+            if (!msgs) continue;
+            uint32_t t = 0;
+            for (uint64_t i = msg_row_ptr[d]; i < msg_row_ptr[d + 1]; i++) {
+                const mt_raw_msg& x = msgs[i];
+                if (x.op_index) {
+                    const uint64_t rec = x.op_index - 1;
+                    if (rec < doc_row_ptr[d] || rec >= doc_row_ptr[d + 1]) {
+                        bad = true;  // (a message carries a record of its own document)
+                        return;
+                    }
+                    t = tick_of(d, rec);
+                }
+                if (!write) {
+                    c[t * 3 + 2]++;
+                    continue;
+                }
+                mt_raw_msg y = x;
+                if (x.op_index) {
+                    // the record's index inside its tick
+                    const uint64_t rec = x.op_index - 1;
+                    const uint64_t first = doc_row_ptr[d] + (uint64_t)t * per;  // the document's first record of tick t
+                    y.op_index = (uint32_t)(start[t] - out->tick_ops[t] + (rec - first) + 1);
+                }
+                out->msgs[m[t]++] = y;
+            }
+            if (write)
+                for (uint32_t tt = 0; tt < T; tt++)
+                    out->msg_row_ptrs[(size_t)tt * (n_docs + 1) + d + 1] = (uint32_t)(m[tt] - out->tick_msgs[tt]);
+        }
+    };
+    auto par = [&](bool write, const std::vector<uint64_t>* base) {
+        if (R == 1) return run(0, write, base);
+        std::vector<std::thread> th;
+        for (unsigned r = 0; r < R; r++) th.emplace_back([&, r] { run(r, write, base); });
+        for (auto& x : th) x.join();
+    };
+    par(false, nullptr);
+    if (bad) return MT_ERR_ARG;
+    // tick totals, and each range's first record / byte / message inside each tick
+    std::vector<uint64_t> base((size_t)R * T * 3);
+    std::vector<uint64_t> to(T + 1, 0), tp(T + 1, 0), tm(T + 1, 0);
+    for (uint32_t t = 0; t < T; t++) {
+        uint64_t a = to[t], b = tp[t], c = tm[t];
+        for (unsigned r = 0; r < R; r++) {
+            const uint64_t* q = cnt.data() + ((size_t)r * T + t) * 3;
+            base[((size_t)r * T + t) * 3 + 0] = a;
+            base[((size_t)r * T + t) * 3 + 1] = b;
+            base[((size_t)r * T + t) * 3 + 2] = c;
+            a += q[0];
+            b += q[1];
+            c += q[2];
+        }
+        to[t + 1] = a;
+        tp[t + 1] = b;
+        tm[t + 1] = c;
+    }
+    out->n_ticks = T;
+    out->payload_bytes = tp[T];
+    if (!out->ops) return MT_OK;  // (the sizing call)
+    if (!out->payload && tp[T]) return MT_ERR_ARG;
+    if (!out->row_ptrs || !out->tick_ops || !out->tick_payload ||
+        (msgs && (!out->msgs || !out->msg_row_ptrs || !out->tick_msgs)))
+        return MT_ERR_ARG;
+    for (uint32_t t = 0; t <= T; t++) {
+        out->tick_ops[t] = to[t];
+        out->tick_payload[t] = tp[t];
+        if (msgs) out->tick_msgs[t] = tm[t];
+    }
+    for (uint32_t t = 0; t < T; t++) {
+        out->row_ptrs[(size_t)t * (n_docs + 1)] = 0;
+        if (msgs) out->msg_row_ptrs[(size_t)t * (n_docs + 1)] = 0;
+    }
+    // (a document's row in tick t is written before its messages read it: one range writes both)
+    par(true, &base);
+    return bad ? MT_ERR_ARG : MT_OK;
 }
 
 static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t doc_id_base, const uint32_t* ids,
@@ -1180,113 +1580,6 @@ mt_status mt_submit(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const ui
     if (st) return st;
     st = mt_batch_apply(e, b);
     mt_batch_free(e, b);
-    return st;
-}
-
-// mt_submit with the upload overlapped: the documents are cut into n_chunks ranges of about equal op
-// counts; every range's records, payload bytes and its own row pointers (zero-length rows outside the
-// range: the same batch layout, so no kernel changes) go over PCIe on a copy stream, queued at once,
-// and the engine applies range k as soon as its copy has landed, while the DMA engine moves range
-// k + 1.  Documents are independent, so applying them range by range ends in the same states.
-mt_status mt_submit_pipelined(mt_engine* e, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
-                              uint64_t payload_bytes, const uint32_t* doc_row_ptr, uint32_t n_chunks) {
-    if (!e || !doc_row_ptr || n_chunks == 0) return MT_ERR_ARG;
-    const uint32_t D = e->n_docs;
-    if (doc_row_ptr[D] != n_ops) return MT_ERR_ARG;
-    for (uint32_t d = 0; d < D; d++)
-        if (doc_row_ptr[d + 1] < doc_row_ptr[d]) return MT_ERR_ARG;
-    n_chunks = std::min<uint32_t>(n_chunks, std::max<uint32_t>(1, D));
-    HIP_OK(hipSetDevice(e->cfg.device));
-    // the records' checks, as mt_batch_upload makes them (bit 0: a payload out of bounds, bit 1: wide)
-    auto scan_range = [&](uint64_t lo, uint64_t hi) {
-        bool bad = false, wide = false;
-        for (uint64_t i = lo; i < hi; i++) {
-            bad |= (uint64_t)ops[i].payload_off + ops[i].payload_len > payload_bytes;
-            wide |= wide_rec(ops[i]);
-        }
-        return (bad ? 1 : 0) | (wide ? 2 : 0);
-    };
-    int flags = 0;
-    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
-    if (n_ops < (1u << 20) || nt == 1) {
-        flags = scan_range(0, n_ops);
-    } else {
-        std::vector<std::thread> th;
-        std::vector<int> res(nt, 0);
-        for (unsigned t = 0; t < nt; t++)
-            th.emplace_back([&, t] { res[t] = scan_range(n_ops * t / nt, n_ops * (t + 1) / nt); });
-        for (auto& x : th) x.join();
-        for (int r : res) flags |= r;
-    }
-    if (flags & 1) return MT_ERR_ARG;
-    // document ranges [cut[k], cut[k+1]) of about n_ops / n_chunks records each
-    std::vector<uint32_t> cut(n_chunks + 1, D);
-    cut[0] = 0;
-    for (uint32_t k = 1, d = 0; k < n_chunks; k++) {
-        const uint64_t want = n_ops * k / n_chunks;
-        while (d < D && doc_row_ptr[d] < want) d++;
-        cut[k] = std::max(cut[k - 1], d);
-    }
-    std::vector<mt_batch> bs(n_chunks);
-    std::vector<uint32_t> rp((size_t)n_chunks * (D + 1));
-    mt_op_rec* d_ops = nullptr;
-    uint8_t* d_pay = nullptr;
-    uint32_t* d_rp = nullptr;
-    std::vector<hipEvent_t> evs(n_chunks, nullptr);
-    mt_status st = MT_OK;
-    hipStream_t cs = nullptr;
-    auto cleanup = [&]() {
-        if (cs) (void)hipStreamSynchronize(cs);
-        (void)hipStreamSynchronize(e->stream);
-        for (auto ev : evs)
-            if (ev) (void)hipEventDestroy(ev);
-        if (cs) (void)hipStreamDestroy(cs);
-        if (d_ops) (void)hipFree(d_ops);
-        if (d_pay) (void)hipFree(d_pay);
-        if (d_rp) (void)hipFree(d_rp);
-    };
-    if (hipMalloc(&d_ops, std::max<uint64_t>(1, n_ops) * sizeof(mt_op_rec)) != hipSuccess ||
-        hipMalloc(&d_pay, std::max<uint64_t>(1, payload_bytes)) != hipSuccess ||
-        hipMalloc(&d_rp, rp.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) {
-        cleanup();
-        return MT_ERR_NOMEM;
-    }
-    for (uint32_t k = 0; k < n_chunks && !st; k++) {
-        const uint32_t a = cut[k], b = cut[k + 1];
-        uint32_t* r = rp.data() + (size_t)k * (D + 1);
-        uint32_t mx = 0;
-        for (uint32_t d = 0; d <= D; d++) r[d] = doc_row_ptr[std::min(std::max(d, a), b)];
-        for (uint32_t d = a; d < b; d++) mx = std::max(mx, doc_row_ptr[d + 1] - doc_row_ptr[d]);
-        const uint64_t o0 = doc_row_ptr[a], o1 = doc_row_ptr[b];
-        uint64_t p0 = payload_bytes, p1 = 0;  // the range's payload bytes (offsets may interleave)
-        for (uint64_t i = o0; i < o1; i++) {
-            p0 = std::min<uint64_t>(p0, ops[i].payload_off);
-            p1 = std::max<uint64_t>(p1, (uint64_t)ops[i].payload_off + ops[i].payload_len);
-        }
-        if (hipEventCreateWithFlags(&evs[k], hipEventDisableTiming) != hipSuccess ||
-            (o1 > o0 && hipMemcpyAsync(d_ops + o0, ops + o0, (o1 - o0) * sizeof(mt_op_rec), hipMemcpyHostToDevice,
-                                       cs) != hipSuccess) ||
-            (p1 > p0 && hipMemcpyAsync(d_pay + p0, payload + p0, p1 - p0, hipMemcpyHostToDevice, cs) != hipSuccess) ||
-            hipMemcpyAsync(d_rp + (size_t)k * (D + 1), r, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, cs) !=
-                hipSuccess ||
-            hipEventRecord(evs[k], cs) != hipSuccess)
-            st = MT_ERR_HIP;
-        bs[k].ops = d_ops;
-        bs[k].payload = d_pay;
-        bs[k].row_ptr = d_rp + (size_t)k * (D + 1);
-        bs[k].n_ops = o1 - o0;
-        bs[k].payload_bytes = payload_bytes;
-        bs[k].n_docs = D;
-        bs[k].max_ops_per_doc = mx;
-        bs[k].wide = (flags & 2) != 0;
-    }
-    for (uint32_t k = 0; k < n_chunks && !st; k++) {
-        if (hipStreamWaitEvent(e->stream, evs[k], 0) != hipSuccess) st = MT_ERR_HIP;
-        else st = mt_batch_apply(e, &bs[k]);
-    }
-    cleanup();
-    for (auto& b : bs) b.ops = nullptr, b.payload = nullptr, b.row_ptr = nullptr;  // (freed above)
     return st;
 }
 

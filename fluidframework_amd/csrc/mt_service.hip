@@ -382,7 +382,10 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n_docs) return;
     const mt_doc_scalars sc = g.sc[d];
-    if (sc.win_op < 0 || (sc.err != MT_DERR_SEQ_ORDER && sc.err != MT_DERR_MSN_ORDER)) return;
+    if (sc.win_op < 0) return;
+    // consumed: the index names a record of this batch only, which a later batch's fixup must not read
+    g.sc[d].win_op = -2;
+    if (sc.err != MT_DERR_SEQ_ORDER && sc.err != MT_DERR_MSN_ORDER) return;
     const mt_op_rec o = ops[sc.win_op];
     if (o.seq != sc.err_seq || MT_OP_TYPE(o) != MT_OP_INSERT || o.payload_len <= MT_OP_PAIRS_LEN(o)) return;
     const size_t so = (size_t)d * g.segcap;
@@ -391,11 +394,13 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
     int64_t len = 0;
     for (int i = 0; i < sc.nseg; i++) {  // nodeLength leaf branch (mergeTree.ts:1667-1697)
-        const bool seen = mt_gclient(g, wdoc, so + i) == C || g.seq[so + i] <= R;
+        // (an editing client's pending local edits carry seq / removedSeq -1, UnassignedSequenceNumber,
+        // which no refSeq has seen)
+        const bool seen = mt_gclient(g, wdoc, so + i) == C || (g.seq[so + i] != -1 && g.seq[so + i] <= R);
         const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
                                : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
         const bool hid = (g.flags[so + i] & MT_SF_REMOVED) &&
-                         (mt_grclient(g, wdoc, so + i) == C || ov || g.rseq[so + i] <= R);
+                         (mt_grclient(g, wdoc, so + i) == C || ov || (g.rseq[so + i] != -1 && g.rseq[so + i] <= R));
         if (seen && !hid) len += g.len[so + i];
     }
     if ((int64_t)o.pos1 > len) g.sc[d].err = MT_DERR_INSERT_FAILED;
@@ -623,12 +628,16 @@ extern "C" hipError_t mt_launch_tiles(const mt_gstate* g, const mt_tile_query* q
 // exceeds pos -- a wave prefix sum per 64 leaves, stopping at the chunk that holds it.  getPosition
 // (mergeTree.ts:1585-1602) sums the local view's lengths before the leaf.
 __global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_pos_query* __restrict__ q, uint32_t nq,
-                                                        mt_pos_result* __restrict__ out) {
+                                                        uint32_t n_docs, mt_pos_result* __restrict__ out) {
     const uint32_t w = blockIdx.x;
     if (w >= nq) return;
     const int lane = lane_id();
     const mt_pos_query qq = q[w];
     const uint32_t d = qq.doc;
+    if (d >= n_docs || qq.kind > MT_POS_OF_ORDINAL) {  // (device-resident queries are not checked on the host)
+        if (lane == 0) out[w] = mt_pos_result{MT_POS_BAD_QUERY, 0, 0, 0};
+        return;
+    }
     const mt_doc_scalars sc = g.sc[d];
     const int n = sc.nseg;
     const size_t so = (size_t)d * g.segcap;
@@ -639,10 +648,11 @@ __global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_po
     auto view_len = [&](int i) -> int {  // nodeLength's leaf branch (mergeTree.ts:1659-1697)
         const bool rm = (g.flags[so + i] & MT_SF_REMOVED) != 0;
         if (local) return rm ? 0 : (int)g.len[so + i];
-        const bool seen = mt_gclient(g, wdoc, so + i) == C || g.seq[so + i] <= R;
+        // (pending local edits: seq / removedSeq -1, UnassignedSequenceNumber, seen by no refSeq)
+        const bool seen = mt_gclient(g, wdoc, so + i) == C || (g.seq[so + i] != -1 && g.seq[so + i] <= R);
         const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
                                : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
-        const bool hid = rm && (mt_grclient(g, wdoc, so + i) == C || ov || g.rseq[so + i] <= R);
+        const bool hid = rm && (mt_grclient(g, wdoc, so + i) == C || ov || (g.rseq[so + i] != -1 && g.rseq[so + i] <= R));
         return (seen && !hid) ? (int)g.len[so + i] : 0;
     };
     mt_pos_result r{-1, 0, 0, 0};
@@ -889,10 +899,10 @@ extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32
     return hipGetLastError();
 }
 
-extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, mt_pos_result* out,
+extern "C" hipError_t mt_launch_resolve(const mt_gstate* g, const mt_pos_query* q, uint32_t n, uint32_t n_docs, mt_pos_result* out,
                                         hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(mt_resolve_kernel, dim3(n), dim3(64), 0, st, *g, q, n, out);
+    hipLaunchKernelGGL(mt_resolve_kernel, dim3(n), dim3(64), 0, st, *g, q, n, n_docs, out);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_seginfo(const mt_gstate* g, const uint32_t* docs, const int32_t* ords, uint32_t n,

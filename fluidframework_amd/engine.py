@@ -71,8 +71,6 @@ def lib():
         L.mt_batch_apply.argtypes = [vp, vp]
         L.mt_batch_free.argtypes = [vp, vp]
         L.mt_submit.argtypes = [vp, vp, u64, vp, u64, vp]
-        if hasattr(L, 'mt_submit_pipelined'):  # (absent from older builds kept for A/Bs)
-            L.mt_submit_pipelined.argtypes = [vp, vp, u64, vp, u64, vp, u32]
         L.mt_sync.argtypes = [vp]
         L.mt_get_length.argtypes = [vp, u32, ctypes.POINTER(u32)]
         L.mt_get_text.argtypes = [vp, u32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
@@ -205,14 +203,12 @@ class MergeEngine:
                                _ptr(batch.row_ptr)), 'mt_submit')
         return self
 
-    def apply_pipelined(self, batch: OpBatch, chunks=4):
-        """apply() with the upload overlapped (mt_submit_pipelined): document ranges copied on a
-        stream of their own while the previous range applies; the same states.  The batch's arrays
-        should be page-locked (hipmem.PinnedArray) for the copies to run asynchronously."""
-        assert batch.n_docs == self.n_docs, 'a batch covers every document of the engine'
-        _check(lib().mt_submit_pipelined(self.h, _ptr(batch.ops), batch.n_ops, _ptr(batch.payload),
-                                         len(batch.payload), _ptr(batch.row_ptr), chunks), 'mt_submit_pipelined')
-        return self
+    def apply_ticks(self, log, deli=None):
+        """A tick-major feed (ticks.TickLog) from host memory with the upload overlapped
+        (mt_submit_ticks; with a DeliSequencer, each tick's raw messages are ticketed first:
+        mt_submit_ticks_deli).  The same states as apply() of each tick in order."""
+        from .ticks import submit_ticks
+        return submit_ticks(self, log, deli)
 
     def stage(self, batch: OpBatch):
         assert batch.n_docs == self.n_docs
@@ -296,6 +292,12 @@ class MergeEngine:
         out = np.zeros(len(q), dtype=POS_RESULT_DTYPE)
         _check(lib().mt_resolve_positions(self.h, _ptr(q), len(q), _ptr(out)), 'mt_resolve_positions')
         return out
+
+    def resolve_positions_device(self, d_queries, n, d_out):
+        """mt_resolve_positions_device: device-resident POS_QUERY_DTYPE rows -> POS_RESULT_DTYPE rows
+        (device pointers as ints; asynchronous on the engine's stream, complete after sync())."""
+        _check(lib().mt_resolve_positions_device(self.h, d_queries, n, d_out), 'mt_resolve_positions_device')
+        _check(lib().mt_sync(self.h), 'mt_sync')
 
     def regen_drain(self, doc):
         """The ops the document regenerated at its MT_SEQ_REGEN records (Client.regeneratePendingOp)

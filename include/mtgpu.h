@@ -243,11 +243,7 @@ mt_status mt_batch_free(mt_engine* eng, mt_batch* batch);
 /* upload + apply + free (the synchronous drop-in for a loop of applyMsg calls) */
 mt_status mt_submit(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops,
                     const uint8_t* payload, uint64_t payload_bytes, const uint32_t* doc_row_ptr);
-/* mt_submit with the upload overlapped with the apply (from page-locked host memory): the documents
- * are cut into n_chunks ranges of about equal op counts, every range is copied on a stream of its
- * own, and range k is applied while range k + 1 is in flight.  The same states as mt_submit. */
-mt_status mt_submit_pipelined(mt_engine* eng, const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload,
-                              uint64_t payload_bytes, const uint32_t* doc_row_ptr, uint32_t n_chunks);
+/* (mt_submit with the upload overlapped: mt_submit_ticks, "tick-major feed" below) */
 mt_status mt_sync(mt_engine* eng);
 
 /* Readout (synchronises).  Text = MergeTreeTextHelper.getText for the observer, as UTF-16 code
@@ -281,14 +277,15 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
  * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),
  * reading MT_CLASS_C64 | capacity, then the editing form's other sizes, MT_CLASS_EDITING | 256 / 512
  * (LDS) and | 2048 / 4096 (HBM workspace), then MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024 / 4096 (the
- * HBM-workspace form with 256 pending-edit slots), then the wide form per class from 2048 on,
- * MT_CLASS_WIDE | capacity; MT_ERR_ARG past the last): each class is one kernel instantiation (see
+ * HBM-workspace form with 256 pending-edit slots), then the wide form per class from the 256 class on
+ * (staged in LDS up to 512 segments, in an HBM workspace above), MT_CLASS_WIDE | capacity; MT_ERR_ARG
+ * past the last): each class is one kernel instantiation (see
  * mt_class_kernel_name). */
 #define MT_CLASS_EDITING 0x40000000u
 #define MT_CLASS_GROUPS 0x08000000u  /* with MT_CLASS_EDITING: the form for more than 64 pending edits */
 #define MT_CLASS_LDS 0x20000000u
 #define MT_CLASS_C64 0x10000000u
-#define MT_CLASS_WIDE 0x04000000u  /* the wide form (include/mtgpu.h "limits"), HBM workspace */
+#define MT_CLASS_WIDE 0x04000000u  /* the wide form (include/mtgpu.h "limits") */
 mt_status mt_last_apply_class_stats(mt_engine* eng, uint32_t cls, uint32_t* capacity, float* kernel_ms,
                                     uint32_t* launches, uint64_t* alg_bytes);
 /* Kernel symbol (as a rocprof trace names it) that applies documents of capacity class
@@ -385,7 +382,10 @@ typedef struct mt_pos_result {  /* 16 bytes */
     uint32_t length;            /* its cachedLength */
 } mt_pos_result;
 mt_status mt_resolve_positions(mt_engine* eng, const mt_pos_query* q, uint32_t n, mt_pos_result* out);
-/* the same with device-resident queries and results (no copies, no synchronisation beyond the stream) */
+/* the same with device-resident queries and results (no copies, no synchronisation beyond the stream);
+ * a query the host could not check -- doc >= n_docs or an unknown kind -- gets ordinal
+ * MT_POS_BAD_QUERY instead of an answer */
+#define MT_POS_BAD_QUERY (-2)
 mt_status mt_resolve_positions_device(mt_engine* eng, const mt_pos_query* d_q, uint32_t n, mt_pos_result* d_out);
 
 /* One segment's fields, by ordinal, for a batch of (document, ordinal) pairs (a reader that holds a
@@ -680,6 +680,65 @@ mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms);
 mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);
 /* err = mt_deli_err, index = position of the failing message inside the document's stream */
 mt_status mt_deli_doc_error(mt_deli* dl, uint32_t doc, int32_t* err, int32_t* index);
+
+/* ---- tick-major feed (timed from the first H2D of the op batch) -------------
+ * A serving loop receives, per tick, the next sequenced ops of every document -- what
+ * SharedSegmentSequence.processMergeTreeMsg sees one message at a time
+ * (packages/dds/sequence/src/sequence.ts:593-633), for many documents at once.  mt_submit_ticks
+ * applies a list of such ticks from host memory with the upload overlapped: tick k + 1 (and k + 2)
+ * is copied into a ring of device slots on a copy stream while tick k applies, so every launch
+ * still holds every document of the tick.  The same states as mt_submit of each tick in order.
+ * Host buffers should be page-locked (hipHostMalloc; hipmem.PinnedArray) for the copies to be
+ * asynchronous; they must stay valid until the call returns. */
+typedef struct mt_tick {
+    const mt_op_rec* ops;         /* the tick's records, grouped by document, seq-ascending within one */
+    uint64_t n_ops;
+    const uint8_t* payload;       /* the records' payload_off are offsets into this tick's payload     */
+    uint64_t payload_bytes;
+    const uint32_t* doc_row_ptr;  /* n_docs + 1 entries: [0] = 0, [n_docs] = n_ops, non-decreasing     */
+    /* deli feed (mt_submit_ticks_deli; NULL / 0 otherwise): the tick's raw client messages grouped by
+     * document (msg_row_ptr, n_docs + 1 entries), ticketed before the tick applies; a message with
+     * op_index = k + 1 carries this tick's record k and stamps its seq / msn / ref_seq (fused hand-off,
+     * mt_deli_ticket_device). */
+    const mt_raw_msg* msgs;
+    uint64_t n_msgs;
+    const uint32_t* msg_row_ptr;
+    mt_ticket* tickets;           /* optional: one ticket per message, copied back to the host         */
+} mt_tick;
+/* Apply ticks[0 .. n_ticks) in order.  Each tick is checked on the host while earlier ticks apply
+ * (row pointers, payload bounds, as mt_batch_upload does); a malformed tick returns MT_ERR_ARG with
+ * the ticks before it applied, as a loop of applyMsg stops at the message that throws.
+ * mt_last_apply_stats / mt_last_apply_class_stats then cover the whole call. */
+mt_status mt_submit_ticks(mt_engine* eng, const mt_tick* ticks, uint32_t n_ticks);
+/* The same with each tick's raw messages ticketed by `dl` on the engine's stream first (deli -> apply
+ * in one pipeline; the deli must be on the engine's device; its documents are the engine's).  A
+ * document's mt_deli_doc_error index is then relative to the tick it failed in. */
+mt_status mt_submit_ticks_deli(mt_engine* eng, mt_deli* dl, const mt_tick* ticks, uint32_t n_ticks);
+
+/* Host tooling (no device work): lays a document-major CSR op log (and, optionally, its raw
+ * messages in the mt_deli_raw_stream layout, op_index = 1 + the record's index in `ops`) out
+ * tick-major for mt_submit_ticks: tick t holds the records [t * per, (t + 1) * per) of every
+ * document, grouped by document, with the payload bytes of the tick compacted in record order
+ * (payload_off rebased to the tick).  A message carrying a record goes to that record's tick (its
+ * op_index rebased to the tick); a message carrying none to the tick of the document's previous
+ * record (tick 0 before the first).  Call first with out->ops == NULL: n_ticks and payload_bytes are
+ * filled in; then with every output array allocated. */
+typedef struct mt_tick_layout {
+    uint32_t n_ticks;          /* out: ceil(max ops per document / per), at least 1                    */
+    uint32_t pad;
+    uint64_t payload_bytes;    /* out: the compacted payload of all ticks                               */
+    mt_op_rec* ops;            /* n_ops records                                                         */
+    uint8_t* payload;          /* payload_bytes                                                         */
+    uint32_t* row_ptrs;        /* n_ticks * (n_docs + 1): tick t's doc_row_ptr at t * (n_docs + 1)      */
+    uint64_t* tick_ops;        /* n_ticks + 1: tick t's records are ops[tick_ops[t] .. tick_ops[t + 1]) */
+    uint64_t* tick_payload;    /* n_ticks + 1: its payload bytes                                        */
+    mt_raw_msg* msgs;          /* n_msgs (with msgs)                                                    */
+    uint32_t* msg_row_ptrs;    /* n_ticks * (n_docs + 1) (with msgs)                                    */
+    uint64_t* tick_msgs;       /* n_ticks + 1 (with msgs)                                               */
+} mt_tick_layout;
+mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
+                          const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, const mt_raw_msg* msgs,
+                          uint64_t n_msgs, const uint32_t* msg_row_ptr, mt_tick_layout* out);
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,7 @@ class BatchEngine {
         this.recording = false;
         this.eventsPerDoc = opts.eventsPerDoc || (1 << 16);
         this.labelDecl = [];  // [doc, tile key, range key] to declare before the next submit
+        this.gen = 0;         // bumped by every submit: segment descriptors are valid within one generation
     }
 
     _enableEvents() {
@@ -82,6 +83,7 @@ class BatchEngine {
     _encode() {
         for (const [doc, tk, rk] of this.labelDecl) native.setLabelKeys(this.handle, doc, tk, rk);
         this.labelDecl = [];
+        this.gen++;
         const n = this.maxDocs;
         const rowPtr = new Uint32Array(n + 1);
         let nops = 0, nbytes = 0;
@@ -570,41 +572,44 @@ class BatchClient {
         return { ordinal: r.readInt32LE(0), offset: r.readInt32LE(4), position: r.readInt32LE(8), length: r.readUInt32LE(12) };
     }
     _descriptor(ordinal, position, cachedLength) {
-        const self = this;
-        let info;
-        const load = () => {
-            if (info) return info;
-            const docs = Buffer.alloc(4), ords = Buffer.alloc(4);
-            docs.writeUInt32LE(self.doc, 0);
-            ords.writeInt32LE(ordinal, 0);
-            const b = native.segmentInfos(self.engine.handle, docs, ords);
-            const flags = b.readUInt32LE(20), removed = (flags & 1) !== 0;
-            const overlap = [];
-            const lo = b.readUInt32LE(32), hi = b.readUInt32LE(36);
-            for (let c = 0; c < 32; c++) if ((lo >>> c) & 1) overlap.push(c);
-            for (let c = 0; c < 32; c++) if ((hi >>> c) & 1) overlap.push(32 + c);
-            for (let q = 0; q < 16; q++) { const c = b.readUInt16LE(72 + 2 * q); if (!c) break; overlap.push(c); }
-            let properties;
-            if (flags & 2) {
-                properties = {};
-                for (let kid = 0; kid < 16; kid++) {
-                    const vid = b.readUInt16LE(40 + 2 * kid);
-                    if (vid) properties[self.keys[kid]] = self.values[kid][vid];
-                }
+        // the segment's fields are gathered now (one small device gather), so the descriptor is a
+        // self-consistent snapshot of the segment as of this query; its text is read on first access,
+        // which must come before the document next changes (the arena is rewritten by later ops)
+        const self = this, gen = this.engine.gen;
+        const docs = Buffer.alloc(4), ords = Buffer.alloc(4);
+        docs.writeUInt32LE(self.doc, 0);
+        ords.writeInt32LE(ordinal, 0);
+        const b = native.segmentInfos(self.engine.handle, docs, ords);
+        const flags = b.readUInt32LE(20), removed = (flags & 1) !== 0;
+        const overlap = [];
+        const lo = b.readUInt32LE(32), hi = b.readUInt32LE(36);
+        for (let c = 0; c < 32; c++) if ((lo >>> c) & 1) overlap.push(c);
+        for (let c = 0; c < 32; c++) if ((hi >>> c) & 1) overlap.push(32 + c);
+        for (let q = 0; q < 16; q++) { const c = b.readUInt16LE(72 + 2 * q); if (!c) break; overlap.push(c); }
+        let properties;
+        if (flags & 2) {
+            properties = {};
+            for (let kid = 0; kid < 16; kid++) {
+                const vid = b.readUInt16LE(40 + 2 * kid);
+                if (vid) properties[self.keys[kid]] = self.values[kid][vid];
             }
-            info = { seq: b.readInt32LE(0), clientId: b.readInt32LE(8),
-                removedSeq: removed ? b.readInt32LE(4) : undefined, removedClientId: removed ? b.readInt32LE(12) : undefined,
-                removedClientOverlap: overlap.length ? overlap : undefined, properties,
-                marker: (flags & 16) !== 0, toff: b.readUInt32LE(24), len: b.readUInt32LE(16) };
-            return info;
-        };
-        const text = () => native.segmentText(self.engine.handle, self.doc, load().toff, load().len);
-        const d = { ordinal, position, cachedLength };
-        for (const k of ["seq", "clientId", "removedSeq", "removedClientId", "removedClientOverlap", "properties"]) {
-            Object.defineProperty(d, k, { get: () => load()[k], enumerable: true });
         }
-        Object.defineProperty(d, "text", { get: () => (load().marker ? undefined : text()), enumerable: true });
-        Object.defineProperty(d, "refType", { get: () => (load().marker ? text().charCodeAt(0) : undefined), enumerable: true });
+        const marker = (flags & 16) !== 0, toff = b.readUInt32LE(24), len = b.readUInt32LE(16);
+        let txt;
+        const text = () => {
+            if (txt === undefined) {
+                if (self.engine.gen !== gen || self.engine.pending) {
+                    throw new Error("BatchClient: a segment's text read after the document changed (query it again)");
+                }
+                txt = native.segmentText(self.engine.handle, self.doc, toff, len);
+            }
+            return txt;
+        };
+        const d = { ordinal, position, cachedLength, seq: b.readInt32LE(0), clientId: b.readInt32LE(8),
+            removedSeq: removed ? b.readInt32LE(4) : undefined, removedClientId: removed ? b.readInt32LE(12) : undefined,
+            removedClientOverlap: overlap.length ? overlap : undefined, properties };
+        Object.defineProperty(d, "text", { get: () => (marker ? undefined : text()), enumerable: true });
+        Object.defineProperty(d, "refType", { get: () => (marker ? text().charCodeAt(0) : undefined), enumerable: true });
         return d;
     }
     /** Client.getContainingSegment (client.ts:1004-1007): {segment, offset} in the local view. */

@@ -175,6 +175,7 @@ function loadSnapshots(engine, entries) {
         client.currentSeq = doc.seq;
         client.minSeq = doc.minSeq;
     });
+    engine.gen++;  // (segment descriptors of the loaded documents are stale from here on)
     native.docsLoad(engine.handle, docIds, segRow, Buffer.concat(segRows.length ? segRows : [Buffer.alloc(0)]),
         Buffer.concat(texts.length ? texts : [Buffer.alloc(0)]), minSeq, curSeq);
     engine.flush();  // the body appends

@@ -178,6 +178,61 @@ def test_c5_joins_through_deli_then_apply(oracle_lib):
     assert all(eng.error(d) == (0, 0) for d in range(0, n, 97))
 
 
+def test_c5_tick_feed_through_deli(oracle_lib):
+    """C5's raw streams as a tick-major feed from page-locked host memory (mt_submit_ticks_deli):
+    tick 0 carries every document's 8 joins and first 32 op messages, each later tick the next 32;
+    each tick is ticketed by deli on the engine's stream (fused stamping into the tick's records)
+    and then applied, with the next ticks' copies in flight.  Tickets and final states equal the
+    HBM-resident deli -> apply of the whole stream (itself pinned to the oracles above)."""
+    from fluidframework_amd.deli import RAW_DTYPE, TICKET_DTYPE, batch_device_ptrs
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.hipmem import DeviceBuffer
+    from fluidframework_amd.oplog import CONFIGS
+    from fluidframework_amd.ticks import TickLog
+    cfg = dict(CONFIGS['C5'])
+    cfg.pop('n_docs')
+    n, n_join = 1536, cfg['n_clients']
+    eng = MergeEngine(n, ops_per_launch=32)
+    dev = eng.synthesize(seed=7, **cfg)
+    host = dev.to_host()
+    d_ops, _, d_row = batch_device_ptrs(dev)
+    n_msgs = dev.n_ops + n * n_join
+    msgs = DeviceBuffer(n_msgs * RAW_DTYPE.itemsize)
+    mrow = DeviceBuffer((n + 1) * 4)
+    tick = DeviceBuffer(n_msgs * TICKET_DTYPE.itemsize)
+    dl = _seq(n)
+    dl.restore_all(seq=0, clients={})
+    dl.raw_stream(d_ops, d_row, n, n_join, msgs.ptr, mrow.ptr)
+    dl.sync()
+    raw, rp = msgs.download(RAW_DTYPE), mrow.download(np.uint32)
+    dl.ticket_device(msgs.ptr, mrow.ptr, n, tick.ptr, d_ops, dev.n_ops)
+    dl.sync()
+    want_t = tick.download(TICKET_DTYPE)
+    eng.reset()
+    eng.apply_staged(dev)
+    want_cs = eng.checksums()
+    for b in (32, 16):
+        log = TickLog.from_batch(host, 32, msgs=raw, msg_row_ptr=rp, tickets=True)
+        assert log.n_ticks == 8
+        e2 = MergeEngine(n, ops_per_launch=b)
+        dl.restore_all(seq=0, clients={})
+        e2.apply_ticks(log, deli=dl)
+        assert np.array_equal(e2.checksums(), want_cs), b
+        # the tickets, back in each document's order
+        got = np.zeros(n_msgs, dtype=TICKET_DTYPE)
+        for d in range(n):
+            parts = []
+            for t in range(log.n_ticks):
+                r = log.msg_row_ptrs[t * (n + 1):(t + 1) * (n + 1)]
+                m0 = int(log.tick_msgs[t])
+                parts.append(log.tickets[m0 + int(r[d]):m0 + int(r[d + 1])])
+            got[rp[d]:rp[d + 1]] = np.concatenate(parts)
+        assert np.array_equal(_tickets(got), _tickets(want_t))
+        assert all(e2.error(d) == (0, 0) for d in range(0, n, 97))
+        e2.close()
+        log.free()
+
+
 def test_unsent_messages_halt_the_document(oracle_lib):
     """a message deli does not send (here a csn gap and a refSeq below the msn, both
     nacked, lambda.ts:269-275, 319-335) stamps MT_SEQ_NACK into its op record, never the local-edit

@@ -57,19 +57,50 @@ def test_fullshape_bit_exact(name, b):
     assert all(eng.error(d) == (0, 0) for d in range(0, batch.n_docs, 7))
 
 
-@pytest.mark.parametrize('chunks', [1, 3, 8])
+@pytest.mark.parametrize('per,b', [(32, 32), (64, 32), (5, 0)])
 @pytest.mark.parametrize('name', ['full_c4', 'fuzz_1k'])
-def test_pipelined_submit_equals_reference(name, chunks):
-    """mt_submit_pipelined (document ranges uploaded on a copy stream while the previous range
-    applies) ends in the reference's states, as mt_submit does, at 1, 3 and 8 ranges."""
+def test_tick_feed_equals_reference(name, per, b):
+    """mt_submit_ticks (the tick-major feed: tick k + 1 copied from page-locked host memory into a
+    ring of device slots while tick k applies) ends in the reference's states, as mt_submit does:
+    ticks of 32 ops per document applied as one launch, ticks of 64 as two launches of 32, and
+    ticks of 5 in one launch each."""
     from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.ticks import TickLog
     batch, fx = load_fullshape(name)
-    eng = MergeEngine(batch.n_docs, ops_per_launch=32)
-    eng.apply_pipelined(batch, chunks=chunks)
+    log = TickLog.from_batch(batch, per)
+    eng = MergeEngine(batch.n_docs, ops_per_launch=b)
+    eng.apply_ticks(log)
     got = ['%016x' % c for c in eng.checksums()]
     bad = [d for d in range(batch.n_docs) if got[d] != fx['checksum'][d]]
-    assert not bad, f'{name} chunks={chunks}: {len(bad)} documents differ, first {bad[:5]}'
+    assert not bad, f'{name} per={per}: {len(bad)} documents differ, first {bad[:5]}: {eng.error(bad[0])}'
+    # launches and algorithmic bytes cover the whole call
+    _, _, launches, nbytes = eng.last_stats()
+    assert launches >= log.n_ticks and nbytes > 0
+    # the same feed again after a reset: the ring is reused
+    eng.reset()
+    eng.apply_ticks(log)
+    assert ['%016x' % c for c in eng.checksums()] == got
     eng.close()
+    log.free()
+
+
+def test_tick_feed_stops_at_a_malformed_tick():
+    """A tick whose payload bounds are broken is refused (MT_ERR_ARG) with the ticks before it applied,
+    as a loop of applyMsg stops at the message that throws."""
+    from fluidframework_amd.engine import MergeEngine, MtError
+    from fluidframework_amd.ticks import TickLog
+    batch, fx = load_golden('synth_c2')
+    log = TickLog.from_batch(batch, 16)
+    t2 = log.tick_batch(2)
+    t2.ops['payload_off'][0] = 1 << 30
+    t2.ops['payload_len'][0] = 4
+    ref = MergeEngine(batch.n_docs, ops_per_launch=16)
+    for t in range(2):
+        ref.apply(log.tick_batch(t))
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    with pytest.raises(MtError):
+        eng.apply_ticks(log)
+    assert np.array_equal(eng.checksums(), ref.checksums())
 
 
 @pytest.mark.parametrize('cfg_name', ['C2', 'C3', 'C4'])

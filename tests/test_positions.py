@@ -99,7 +99,7 @@ def test_resolve_positions_on_editing_documents():
     from fluidframework_amd.oplog import OpBatch
     with open(os.path.join(GOLDEN, 'local.expected.jsonl')) as f:
         exp = [json.loads(x) for x in f if x.strip()]
-    checked = 0
+    checked = pending_docs = 0
     for log in ('local_rounds', 'local_lag'):
         src = OpBatch.load(os.path.join(GOLDEN, log + '.mtlog'))
         last = {r['doc']: r['states'][-1] for r in exp if r['log'] == log and r['states'] and not r['err']}
@@ -118,6 +118,19 @@ def test_resolve_positions_on_editing_documents():
             for p in range(0, n + 2, max(1, n // 16)):
                 rows.append((k, p, POS_LOCAL, 0, POS_CONTAINING))
                 want.append(_expected(st, p, None, 0))
+            # remote clients' views (resolveRemoteClientPosition): pending local inserts and removals
+            # carry seq / removedSeq -1 (UnassignedSequenceNumber), which no refSeq has seen
+            ops = src.ops[int(src.row_ptr[d]):int(src.row_ptr[d]) + last[d][0]]
+            own = set(int(c) for c in ops['client'][ops['seq'] == -1])
+            pend = sum(1 for sg in st['segs'] if sg[1] == -1 or sg[3] == -1 and sg[4] != -1)
+            pending_docs += pend > 0
+            clients = sorted({sg[2] for sg in st['segs'] if sg[2] > 0} - own)[:2]
+            for c in clients:
+                for rs in (st['msn'], st['seq']):
+                    vlen = sum(_view_len(sg, rs, c) for sg in st['segs'])
+                    for p in range(0, vlen + 2, max(1, vlen // 8)):
+                        rows.append((k, p, rs, c, POS_CONTAINING))
+                        want.append(_expected(st, p, rs, c))
         got = eng.resolve_positions(np.array(rows, dtype=POS_QUERY_DTYPE))
         for k, (g, w) in enumerate(zip(got, want)):
             if w[0] < 0:
@@ -125,4 +138,24 @@ def test_resolve_positions_on_editing_documents():
             else:
                 assert (int(g['ordinal']), int(g['offset']), int(g['position']), int(g['length'])) == w, (log, rows[k])
         checked += len(rows)
-    assert checked > 100
+    assert checked > 100 and pending_docs > 0
+
+
+def test_device_queries_out_of_range_are_flagged():
+    """mt_resolve_positions_device takes device-resident queries the host never sees: a query naming a
+    document past n_docs or an unknown kind gets ordinal MT_POS_BAD_QUERY (-2), never a read out of
+    bounds, and the queries around it are answered."""
+    from fluidframework_amd.engine import POS_CONTAINING, POS_LOCAL, POS_QUERY_DTYPE, POS_RESULT_DTYPE, MergeEngine
+    from fluidframework_amd.hipmem import DeviceBuffer
+    batch, exp = load_golden('synth_c3')
+    eng = MergeEngine(batch.n_docs, ops_per_launch=32)
+    eng.apply(batch)
+    rows = [(0, 0, POS_LOCAL, 0, POS_CONTAINING), (batch.n_docs, 0, POS_LOCAL, 0, POS_CONTAINING),
+            (1 << 30, 5, 3, 1, POS_CONTAINING), (1, 0, POS_LOCAL, 0, 7), (1, 1, POS_LOCAL, 0, POS_CONTAINING)]
+    q = np.array(rows, dtype=POS_QUERY_DTYPE)
+    want = eng.resolve_positions(q[[0, 4]])
+    dq, dr = DeviceBuffer(q.nbytes).upload(q), DeviceBuffer(len(q) * POS_RESULT_DTYPE.itemsize)
+    eng.resolve_positions_device(dq.ptr, len(q), dr.ptr)
+    got = dr.download(POS_RESULT_DTYPE)
+    assert list(got['ordinal'][[1, 2, 3]]) == [-2, -2, -2]
+    assert got[0] == want[0] and got[4] == want[1]

@@ -14,7 +14,7 @@ for r in 1 2; do
         for b in $BS; do
             echo "round $r config $c b $b" >> gpurun_out/ab_b_$c.log
             timeout -k 10 240 python bench.py --config $c --ops-per-launch $b --steps 3 --warmup 1 --no-cpu-baseline \
-                --no-slow-paths --no-h2d >> gpurun_out/ab_b_$c.log 2>> gpurun_out/ab_b.err || exit 1
+                --no-slow-paths >> gpurun_out/ab_b_$c.log 2>> gpurun_out/ab_b.err || exit 1
         done
     done
 done

@@ -14,7 +14,7 @@ python3 tools/pmc_traffic.py $OUT/fetch/fetch_results.db $OUT/write/write_result
 python3 tools/rocpd_summary.py $OUT/req/req_results.db --pmc > $OUT/req.txt || exit 1
 cat $OUT/known.json; cat $OUT/req.txt | cut -c1-220
 if [ -n "$BENCH_CONFIG" ]; then
-  MTGPU_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $OUT/breq -o breq -- python3 bench.py --config $BENCH_CONFIG --steps 1 --warmup 0 --no-cpu-baseline --no-h2d --no-slow-paths > $OUT/breq.log 2>&1 || { tail -5 $OUT/breq.log; exit 1; }
+  MTGPU_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $OUT/breq -o breq -- python3 bench.py --config $BENCH_CONFIG --steps 1 --warmup 0 --no-cpu-baseline --no-slow-paths > $OUT/breq.log 2>&1 || { tail -5 $OUT/breq.log; exit 1; }
   python3 tools/rocpd_summary.py $OUT/breq/breq_results.db --pmc > $OUT/breq.txt || exit 1
   grep -E "reg_apply|Kernel|kernel" $OUT/breq.txt | head -20 | cut -c1-220
 fi

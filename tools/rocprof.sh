@@ -10,11 +10,11 @@ export TMPDIR=/tmp
 CONFIG=${CONFIG:-C3}
 OUT=gpurun_out/rp_$CONFIG
 mkdir -p $OUT
-MTGPU_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python3 bench.py --config $CONFIG --steps 2 --warmup 1 --no-cpu-baseline --no-h2d --no-slow-paths > $OUT/kt_bench.log 2>&1 || exit 1
+MTGPU_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python3 bench.py --config $CONFIG --steps 2 --warmup 1 --no-cpu-baseline --no-slow-paths > $OUT/kt_bench.log 2>&1 || exit 1
 SP=--no-slow-paths
 [ -n "$SLOW" ] && SP=
-MTGPU_SERIAL=1 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch -- python3 bench.py --config $CONFIG --steps 1 --warmup 0 --no-cpu-baseline --no-h2d $SP > $OUT/fetch.log 2>&1 || exit 1
-MTGPU_SERIAL=1 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write -- python3 bench.py --config $CONFIG --steps 1 --warmup 0 --no-cpu-baseline --no-h2d $SP > $OUT/write.log 2>&1 || exit 1
+MTGPU_SERIAL=1 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch -- python3 bench.py --config $CONFIG --steps 1 --warmup 0 --no-cpu-baseline $SP > $OUT/fetch.log 2>&1 || exit 1
+MTGPU_SERIAL=1 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write -- python3 bench.py --config $CONFIG --steps 1 --warmup 0 --no-cpu-baseline $SP > $OUT/write.log 2>&1 || exit 1
 python3 tools/rocpd_summary.py $OUT/kt/kt_results.db --csv $OUT/kernel_stats.csv || exit 1
 python3 tools/pmc_traffic.py $OUT/fetch/fetch_results.db $OUT/write/write_results.db $OUT/pmc_traffic.json || exit 1
 python3 tools/tick_gaps.py $OUT/kt/kt_results.db > $OUT/tick_gaps.txt || exit 1

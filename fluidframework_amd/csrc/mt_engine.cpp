@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -1145,8 +1146,12 @@ constexpr int kRing = 3;  // device slots of mt_submit_ticks: two ticks in fligh
 
 // slot buffers of at least the given sizes (called with nothing in flight on the engine)
 mt_status ring_reserve(mt_engine* e, uint64_t n_ops, uint64_t pay, uint64_t n_msgs) {
-    if (!e->h2d && hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking) != hipSuccess) return MT_ERR_HIP;
-    if (!e->d2h && hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking) != hipSuccess) return MT_ERR_HIP;
+    // (the copy streams at the greatest priority: the runtime gives them a hardware queue of their own
+    // where it keeps one per priority, so their packets never sit in front of the apply's)
+    int lo_pri = 0, hi_pri = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
+    if (!e->h2d && hipStreamCreateWithPriority(&e->h2d, hipStreamNonBlocking, hi_pri) != hipSuccess) return MT_ERR_HIP;
+    if (!e->d2h && hipStreamCreateWithPriority(&e->d2h, hipStreamNonBlocking, hi_pri) != hipSuccess) return MT_ERR_HIP;
     const size_t rp = ((size_t)e->cfg.max_docs + 1) * sizeof(uint32_t);
     for (auto& s : e->ring) {
         if (!s.ready) {
@@ -1217,17 +1222,28 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
     mt_status st = ring_reserve(e, mo, mp, mm);
     if (st) return st;
     mt_batch bs[kRing];
-    // tick k: checked on the host, then copied into its slot once the slot's previous tick has
-    // applied and its tickets have gone back
+    // (MTGPU_TICK_TRACE=1: the host's time in the checks and in the apply loop, to stderr)
+    double t_check = 0, t_apply = 0, t_copy = 0, t_wait = 0;
+    const auto t_start = std::chrono::steady_clock::now();
+    // tick k: checked on the host, then copied into its slot.  Every dependency between the copies and
+    // the apply is kept by the host, not by a stream waiting on another stream's event: the streams
+    // share the device's few hardware queues (GPU_MAX_HW_QUEUES), where such a wait holds up every
+    // later packet of its queue -- a tick's apply then waited for the next ticks' copies.  The host
+    // already synchronises once per tick (the bin counts), so the ordering costs nothing:
+    //   * tick k is copied when its slot's previous tick (k - kRing) has applied and its tickets have
+    //     gone back (both complete by then: the host issues the copy after tick k - kRing + 1's bin);
+    //   * tick k applies once the host has seen its copy land (issued two ticks earlier).
     auto stage = [&](uint32_t k) -> mt_status {
         const mt_tick& t = ticks[k];
         auto& s = e->ring[k % kRing];
         mt_batch& b = bs[k % kRing];
         uint32_t mx = 0;
+        const auto c0 = std::chrono::steady_clock::now();
         if (!row_ptr_ok(t.doc_row_ptr, D, t.n_ops, &mx) || (t.n_msgs && !row_ptr_ok(t.msg_row_ptr, D, t.n_msgs, nullptr)))
             return MT_ERR_ARG;
         const int flags = scan_records(t.ops, t.n_ops, t.payload_bytes);
         if (flags & 1) return MT_ERR_ARG;
+        t_check += std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
         b = mt_batch();
         b.ops = s.ops;
         b.payload = s.pay;
@@ -1237,8 +1253,9 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
         b.n_docs = D;
         b.max_ops_per_doc = mx;
         b.wide = (flags & 2) != 0;
-        HIP_OK(hipStreamWaitEvent(e->h2d, s.applied, 0));
-        HIP_OK(hipStreamWaitEvent(e->h2d, s.drained, 0));
+        const auto q0 = std::chrono::steady_clock::now();
+        HIP_OK(hipEventSynchronize(s.applied));
+        HIP_OK(hipEventSynchronize(s.drained));
         if (t.n_ops) HIP_OK(hipMemcpyAsync(s.ops, t.ops, t.n_ops * sizeof(mt_op_rec), hipMemcpyHostToDevice, e->h2d));
         if (t.payload_bytes) HIP_OK(hipMemcpyAsync(s.pay, t.payload, t.payload_bytes, hipMemcpyHostToDevice, e->h2d));
         HIP_OK(hipMemcpyAsync(s.rp, t.doc_row_ptr, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->h2d));
@@ -1247,6 +1264,7 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
             HIP_OK(hipMemcpyAsync(s.mrp, t.msg_row_ptr, (D + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, e->h2d));
         }
         HIP_OK(hipEventRecord(s.ready, e->h2d));
+        t_copy += std::chrono::duration<double>(std::chrono::steady_clock::now() - q0).count();
         return MT_OK;
     };
     if ((st = apply_begin(e))) return st;
@@ -1260,11 +1278,11 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
     };
     for (uint32_t k = 0; k + 1 < kRing; k++) stage_or_stop(k);
     for (uint32_t k = 0; k < limit && !st; k++) {
-        stage_or_stop(k + kRing - 1);
-        if (k >= limit) break;
         auto& s = e->ring[k % kRing];
         const mt_tick& t = ticks[k];
-        HIP_OK(hipStreamWaitEvent(e->stream, s.ready, 0));
+        const auto w0 = std::chrono::steady_clock::now();
+        HIP_OK(hipEventSynchronize(s.ready));
+        t_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
         if (t.n_msgs) {
             if ((st = mt_deli_ticket_on_stream(dl, e->cfg.device, e->stream, s.msgs, s.mrp, D, s.tk, s.ops, t.n_ops)))
                 break;
@@ -1275,13 +1293,23 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
                 HIP_OK(hipEventRecord(s.drained, e->d2h));
             }
         }
+        const auto a0 = std::chrono::steady_clock::now();
         if ((st = apply_launches(e, &bs[k % kRing], nk))) break;
+        t_apply += std::chrono::duration<double>(std::chrono::steady_clock::now() - a0).count();
         HIP_OK(hipEventRecord(s.applied, e->stream));
+        // the next tick's copy goes out while this one applies (its slot's tick, k - 1, is done: this
+        // tick's bin followed it on the engine stream)
+        stage_or_stop(k + kRing - 1);
     }
     // (on an error the ticks in flight still land before the slots can be reused or freed)
     const mt_status se = apply_end(e, nk);
     HIP_OK(hipStreamSynchronize(e->h2d));
     HIP_OK(hipStreamSynchronize(e->d2h));
+    if (const char* tv = getenv("MTGPU_TICK_TRACE"); tv && tv[0] == '1')
+        fprintf(stderr, "mt_submit_ticks: %u ticks, %.2f ms: host checks %.2f ms, copy enqueue %.2f ms, waits for copies "
+                "%.2f ms, apply loop %.2f ms, GPU wall %.2f ms\n", n,
+                1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
+                1e3 * t_check, 1e3 * t_copy, 1e3 * t_wait, 1e3 * t_apply, e->last_wall_ms);
     return st ? st : se ? se : refused;
 }
 }  // namespace

@@ -102,7 +102,14 @@ def test_resolve_positions_on_editing_documents():
     checked = pending_docs = 0
     for log in ('local_rounds', 'local_lag'):
         src = OpBatch.load(os.path.join(GOLDEN, log + '.mtlog'))
-        last = {r['doc']: r['states'][-1] for r in exp if r['log'] == log and r['states'] and not r['err']}
+        def pending(st):
+            return any(sg[1] == -1 or (sg[3] == -1 and sg[4] != -1) for sg in st['segs'])
+        # per document its last checkpoint with edits still pending, else its last one
+        last = {}
+        for r in exp:
+            if r['log'] == log and r['states'] and not r['err']:
+                pend = [c for c in r['states'] if pending(c[1])]
+                last[r['doc']] = pend[-1] if pend else r['states'][-1]
         docs = sorted(last)
         # each document's records up to its last checkpoint: the engine ends in that state
         idx = np.concatenate([np.arange(int(src.row_ptr[d]), int(src.row_ptr[d]) + last[d][0]) for d in docs])
@@ -122,8 +129,7 @@ def test_resolve_positions_on_editing_documents():
             # carry seq / removedSeq -1 (UnassignedSequenceNumber), which no refSeq has seen
             ops = src.ops[int(src.row_ptr[d]):int(src.row_ptr[d]) + last[d][0]]
             own = set(int(c) for c in ops['client'][ops['seq'] == -1])
-            pend = sum(1 for sg in st['segs'] if sg[1] == -1 or sg[3] == -1 and sg[4] != -1)
-            pending_docs += pend > 0
+            pending_docs += pending(st)
             clients = sorted({sg[2] for sg in st['segs'] if sg[2] > 0} - own)[:2]
             for c in clients:
                 for rs in (st['msn'], st['seq']):

@@ -90,6 +90,8 @@ def parse():
                    help='rank exchange: RCCL over xGMI (default for N > 1; "rccl" also at N = 1, a one-rank '
                         'communicator), or gloo (ranks sharing one GPU, tests)')
     p.add_argument('--devices', default='', help='device of each local rank, e.g. "0,0" (default: rank i -> GPU i)')
+    p.add_argument('--hbm-only', action='store_true',
+                   help='tooling (A/Bs, profiles): skip the host-fed steps; value is then the HBM-resident figure')
     p.add_argument('--no-tickets', action='store_true', help='C5: the host-fed steps do not copy the tickets back')
     p.add_argument('--no-slow-paths', action='store_true',
                    help='skip the N=1 side lines for the paths off the narrow register engine (C3 with delta '
@@ -189,8 +191,10 @@ def main():
     # tick k + 1 on a copy stream while tick k applies.  Laying the log out is log generation (not
     # timed); the upload, deli and the apply are.
     t0 = time.time()
-    host = dev.to_host()
-    if deli is None:
+    host = dev.to_host() if not args.hbm_only else None
+    if args.hbm_only:
+        log = None
+    elif deli is None:
         log = TickLog.from_batch(host, args.ops_per_launch)
     else:
         log = TickLog.from_batch(host, args.ops_per_launch, msgs=d_msgs.download(RAW_DTYPE, n_msgs),
@@ -236,17 +240,22 @@ def main():
         barrier()
         return comm.max(time.perf_counter() - t0), kern_ms, wall_ms, launches, alg_bytes, cls
 
+    main_step = step_hbm if args.hbm_only else step
     for _ in range(args.warmup):
-        step()
+        main_step()
     ref_cs = eng.checksums() if deli is not None and args.warmup else None
-    elapsed, kern_ms, wall_ms, launches, alg_bytes, cls = timed(step)
+    deli_ms = 0.0
+    elapsed, kern_ms, wall_ms, launches, alg_bytes, cls = timed(main_step)
     cs_fed = eng.checksums()
-    tk_ok = bool(np.all(log.tickets['status'] == 1)) if deli is not None and log.tickets is not None else None
+    tk_ok = bool(np.all(log.tickets['status'] == 1)) if log is not None and log.tickets is not None else None
 
     # the HBM-resident figure (side field): the same steps with the log generated in HBM
-    step_hbm()
-    deli_ms = 0.0
-    elapsed_hbm = timed(step_hbm)[0]
+    if args.hbm_only:
+        elapsed_hbm = elapsed
+    else:
+        step_hbm()
+        deli_ms = 0.0
+        elapsed_hbm = timed(step_hbm)[0]
 
     # the dominant kernel's roofline: one more (untimed) step with the classes serialized, so each
     # class kernel has the GPU to itself and its launch duration is its own (in the timed steps the
@@ -263,7 +272,13 @@ def main():
     # SURVEY.md §8(d)'s b = infinity figure (the minimal traffic of the job): every op record and its
     # payload read once, each document's state read once (empty after the reset: its 80-byte scalar
     # header) and written once (35 B per final segment + the header)
-    ops_b = n_ops * 32 + float(log.tick_payload[-1])
+    if log is not None:
+        pay_b = float(log.tick_payload[-1])
+    else:  # the mean payload per op from the first 512 documents' logs
+        samp = dev.to_host(0, min(n_docs, 512))
+        pay_b = float(samp.ops['payload_len'].astype(np.float64).sum()) * n_ops / max(1, samp.n_ops)
+        del samp
+    ops_b = n_ops * 32 + pay_b
     min_bytes = ops_b + 35.0 * float(eng.seg_counts().astype(np.float64).sum()) + 2 * 80.0 * n_docs
     assert np.array_equal(cs_fed, cs), 'the host-fed tick steps differ from the HBM-resident replay'
     if deli is None:
@@ -274,11 +289,13 @@ def main():
         t = d_tick.download(TICKET_DTYPE)
         assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
         assert tk_ok is not False, 'a ticket of the host-fed steps is not SENT'
-    upload = {'bytes_per_step': log.upload_bytes(), 'ticks': log.n_ticks, 'layout_s': round(layout_s, 2),
+    upload = None if log is None else {
+              'bytes_per_step': log.upload_bytes(), 'ticks': log.n_ticks, 'layout_s': round(layout_s, 2),
               'note': 'page-locked host memory, tick-major (mt_log_to_ticks), payload compacted per tick; '
                       'copied on a copy stream into a ring of 3 device slots while the previous tick applies'
                       + ('; tickets copied back per tick' if deli is not None and not args.no_tickets else '')}
-    log.free()
+    if log is not None:
+        log.free()
 
     # final per-document checksum gather to rank 0 (RCCL ncclGather from HBM; the only collective)
     parts = comm.gather_checksums(eng, max_docs)
@@ -324,8 +341,10 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'int32',
-            'data': 'synthetic (device-generated observer-driven op logs, mt_synth.h), fed from page-locked host '
-                    'memory tick by tick inside the timed region (SURVEY.md 8(d): from the first H2D)',
+            'data': 'synthetic (device-generated observer-driven op logs, mt_synth.h), ' + (
+                'HBM-resident (--hbm-only tooling run)' if args.hbm_only else
+                'fed from page-locked host memory tick by tick inside the timed region (SURVEY.md 8(d): from the '
+                'first H2D)'),
             'config': {
                 'workload': f'{args.config}: {docs_per_gpu} docs/GPU x {cfg["n_clients"]} clients x {ops_per_doc} '
                             f'sequenced ops/doc ({CONFIG_NAMES.get(args.config, args.config)}), '

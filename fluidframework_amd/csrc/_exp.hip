@@ -1421,13 +1421,21 @@ struct RWave {
                 Cut cut{};
                 int k = 0, ba = 0, be = 0, t = -1;
                 if (!placing) {
+#ifdef STUB_SPLIT
+                    if (true) {
+#else
                     if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, cut, k, ba, be)) {
+#endif
                         if (err) return;
                         continue;
                     }
                     kl = k - 1;
                 } else {
+#ifdef STUB_PLACE
+                    t = 1; k = op.pos1 & 7;
+#else
                     t = place_prep(op, pay, tlen, np, e, k, ba, be, uni(kl));
+#endif
                     if (t < 0) return;
                 }
                 // (uniform by construction; the phi that merges the two prep paths is not
@@ -1436,7 +1444,11 @@ struct RWave {
                 ba = uni(ba);
                 be = uni(be);
                 t = uni(t);
+#ifdef STUB_INSAT
+                const bool ok = k != 12345;
+#else
                 const bool ok = insert_at(k, ba, be, e, S, cut, !placing);
+#endif
                 if (placing) {
                     PROF_END(prof, P_INSERT, t1);
                 } else {
@@ -1445,7 +1457,9 @@ struct RWave {
                 if (!ok) return;
                 if (placing && S > min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
                     // the new segment's block after a possible split: the one holding slot k
+#ifndef STUB_LRU
                     if (!add_lru(block_start(k), t, S)) return;
+#endif
                 }
                 if (EV && placing)  // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988)
                     emit(MT_EV_INSERT, MT_EVF_FIRST, live_before(k), local_before(k), (uint32_t)tlen);
@@ -1453,7 +1467,9 @@ struct RWave {
             if (EV && ins && tlen == 0) emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
             if (!ins) {
                 PROF_BEGIN(t2, P_RANGE);
+#ifndef STUB_RANGE
                 range_action(op, pay, tlen, np);
+#endif
                 PROF_END(prof, P_RANGE, t2);
             }
             if (err) return;
@@ -1472,7 +1488,9 @@ struct RWave {
                 min_seq = msn;
             }
             PROF_BEGIN(t3, P_ZAMBONI);
+#ifndef STUB_ZAM
             zamboni();
+#endif
             PROF_END(prof, P_ZAMBONI, t3);
             if (err) return;
         }
@@ -1928,13 +1946,7 @@ MT_DEV KGState& kernarg_gstate() {
 // K = 11 / 12 at 3) measured 1.2-2.6x slower (profiles/r03_ab_occupancy.log).  The small classes
 // (documents up to ~125 segments, C5's) run at K = 2: 7 and K = 3: 6 waves, +3.3 % on C5 against 5 / 5
 // and +2.5 % against 8 / 7 (profiles/r04_ab_small_occupancy*_C5.log).
-// Round 5 re-picked three classes with the PMC traffic in the A/B (profiles/r05_ab_occupancy/): K = 7
-// at 3 waves is spill-free (158 VGPRs; 176 B of scratch at 4) and faster (C3's 448 class 50.6 -> 43.9 ms,
-// its traffic 13.3x -> 1.19x its algorithmic bytes); K = 2 at 6 and K = 3 at 5 waves keep 24 / 28 B of
-// scratch instead of 60 / 104 B (C5 traffic 3.9x -> 2.6x and 12.0x -> 2.0x) for 1 % of C5's rate.
-constexpr int wpe_default(int K) {
-    return K <= 2 ? 6 : K == 3 ? 5 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 10 ? 3 : 2;
-}
+constexpr int wpe_default(int K) { return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2; }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV
 #define MT_WPE_OV {0}

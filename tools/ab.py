@@ -21,7 +21,7 @@ res = {lib: [] for lib in a.libs}
 for r in range(a.reps):
     for lib in a.libs:
         env = dict(os.environ, MTGPU_LIB=os.path.abspath(lib))
-        cmd = [sys.executable, os.path.join(HERE, 'bench.py'), '--no-cpu-baseline', '--no-slow-paths',
+        cmd = [sys.executable, os.path.join(HERE, 'bench.py'), '--no-cpu-baseline', '--no-slow-paths', '--hbm-only',
                '--config', a.config,
                '--steps', str(a.steps), '--warmup', '1'] + (['--docs', str(a.docs)] if a.docs else [])
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)

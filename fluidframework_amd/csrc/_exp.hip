@@ -439,6 +439,24 @@ struct RWave {
         const int jk = uni(k % K);
         return (uint32_t)__builtin_amdgcn_readlane((int)li[jk], k / K);
     }
+#ifdef SEL_SET
+    MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
+        const int lk = k / K, jk = uni(k % K);
+        const bool me = lane == lk;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const bool h = me && jk == j;
+            li[j] = h ? lv : li[j];
+            cf[j] = h ? cv : cf[j];
+        }
+    }
+    MT_DEV void set_cum(int k, int32_t v) {
+        const int lk = k / K, jk = uni(k % K);
+        const bool me = lane == lk;
+#pragma unroll
+        for (int j = 0; j < K; j++) cum[j] = (me && jk == j) ? v : cum[j];
+    }
+#else
     MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
         const int lk = k / K, jk = uni(k % K);
         const bool me = lane == lk;
@@ -449,6 +467,7 @@ struct RWave {
         const int lk = k / K, jk = uni(k % K);
         cum[jk] = lane == lk ? v : cum[jk];
     }
+#endif
 
     // insert e at slot p: slots >= p move one register right
     template <bool CUM>
@@ -924,7 +943,9 @@ struct RWave {
         const uint32_t pcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, p);
         const uint32_t lcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, (int)lastq);
         const uint32_t anynl = __ballot(in_run && (vcf & F_HASNL)) ? F_HASNL : 0u;
+#ifndef STUB_SETLI
         set_li_cf(__builtin_amdgcn_readlane(vslot, p), total | (pid_ << kLenBits), (pcf & ~F_NL) | (lcf & F_NL) | anynl);
+#endif
     }
 
     // scourNode on the leaf block whose slots are [a, e) (mergeTree.ts:1289-1365); returns the
@@ -1059,7 +1080,9 @@ struct RWave {
             const uint64_t runm = __ballot(vtgt == p);
             runs &= ~runm;
             PROF_CNT(P_N_APPEND, __popcll(runm));
+#ifndef STUB_APPEND
             append_run(p, (uint32_t)runm, vli, vcf, vslot);
+#endif
             if (err) return cnt;
         }
         // unlink: the slots become dead in place (their block marks stay)
@@ -1146,10 +1169,17 @@ struct RWave {
     // site: step 0 scours the popped segment's block; on underflow steps 1..m scour every
     // sibling under its parent (pack's scourNode loop), then repack.
     MT_DEV void zamboni() {
+#ifdef UNROLL_IT
+#pragma unroll
+#endif
         for (int it = 0; it < 2; it++) {
             if (heap_n == 0 || uni(s.hseq[1]) > min_seq) break;
             PROF_BEGIN(tz, P_ZPOP);
+#ifndef STUB_POP
             const int id = heap_pop();
+#else
+            const int id = uni(s.hslot[1]);
+#endif
             if (id == (int)kDead) continue;
             const int k = slot_of_id(id);
             if (k < 0) continue;
@@ -1167,7 +1197,11 @@ struct RWave {
                 }
                 PROF_BEGIN(ts, P_SCOUR);
                 PROF_CNT(P_N_SCOUR, 1);
+#ifndef STUB_SCOUR
                 const int kept = scour(aa, ee);
+#else
+                const int kept = live_in(aa, ee) - 1;
+#endif
                 PROF_END(prof, P_SCOUR, ts);
                 if (err) return;
                 if (step == 0) {
@@ -1182,7 +1216,9 @@ struct RWave {
                 if (step == m) break;
             }
             PROF_BEGIN(tr, P_REPACK);
+#ifndef STUB_REPACK
             if (P >= 0) repack_leaf(P, fc, m, total, A, ee);
+#endif
             PROF_END(prof, P_REPACK, tr);
             if (err) return;
         }
@@ -1589,6 +1625,22 @@ struct RWave {
     // interior-level rows by chunks of 64) and waited for once, then the LDS images and the register
     // state are built from the registers.  (Before: a loop per array with a dependent load per
     // iteration, ~20 serialized memory round trips per launch.)
+    MT_DEV void load_stub(KGState& g, uint32_t d) {
+        const MT_GLOB mt_doc_scalars& sc = gp(g.sc)[d];
+        const int n = uni(sc.nseg);
+        nlev = uni(sc.nlev); heap_n = uni(sc.heap_n); cur_seq = uni(sc.cur_seq); min_seq = uni(sc.min_seq);
+        err = uni(sc.err); err_seq = uni(sc.err_seq); text_top = uniu(sc.text_top); text_half = uniu(sc.text_half);
+        nb0 = uni(sc.nb[0]); next_id = n; nlive = n; ns = n;
+        const size_t so = (size_t)d * g.segcap;
+        const int i0 = lane * K;
+        bsm = lvm = sc0 = sc1 = 0u;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            seq[j] = gp(g.seq)[so + i0 + j]; rseq[j] = gp(g.rseq)[so + i0 + j]; li[j] = gp(g.len)[so + i0 + j];
+            cf[j] = gp(g.flags)[so + i0 + j]; ov[j] = (uint32_t)gp(g.ovl)[so + i0 + j]; cum[j] = 0;
+            lvm |= (i0 + j < n) ? (1u << j) : 0u;
+        }
+    }
     MT_DEV void load(KGState& g, uint32_t d) {
         const MT_GLOB mt_doc_scalars& sc = gp(g.sc)[d];
         const int n = uni(sc.nseg);
@@ -1968,7 +2020,11 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     PROF_BEGIN(tl, P_LOAD);
+#ifndef STUB_LOAD
     wv.load(kernarg_gstate(), d);
+#else
+    wv.load_stub(kernarg_gstate(), d);
+#endif
     PROF_END(wv.prof, P_LOAD, tl);
     // software pipeline: op i's payload was loaded at the end of op i-1's apply and op i+1's is
     // issued at the end of op i's, so every wait for a prefetch finds it a whole op old (a prefetch
@@ -1989,7 +2045,11 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
         const mt_op_rec op = op_from_block(blk0, (i - a) & 7u);
         wv.pb = pb;
         PROF_BEGIN(top, P_OP);
+#ifndef STUB_APPLY
         wv.apply(op, payload);
+#else
+        wv.scan(op.ref_seq, op.client);
+#endif
         PROF_END(wv.prof, P_OP, top);
 #ifdef MT_PROF
         wv.prof[P_OPS]++;
@@ -2014,7 +2074,11 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
         }
     }
     PROF_BEGIN(tt, P_STORE);
+#ifndef STUB_STORE
     wv.store(kernarg_gstate(), d);
+#else
+    if (wv.ns == 12345) wv.store(kernarg_gstate(), d);
+#endif
     PROF_END(wv.prof, P_STORE, tt);
 #ifdef MT_PROF
     if (wv.lane == 0)

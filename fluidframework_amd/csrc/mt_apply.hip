@@ -2350,7 +2350,8 @@ extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, con
 
 // editing documents above MT_LOC_CAP segments (mt_bin_kernel's last editing buckets): the editing
 // form with its structure in the HBM workspace (n_docs * mt_lds_bytes_loc(cap_class) bytes)
-// (gw = 4: the MT_WIDE_GROUPS documents' form, 256 pending edits, at 1024 / 4096 slots)
+// (gw = MT_LOC_GW: the MT_WIDE_GROUPS documents' form, MT_LOC_GROUPS_WIDE pending edits, at 1024 / 4096 /
+// 8192 slots)
 extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gstate* g, const mt_op_rec* ops,
                                               const uint8_t* payload, const uint32_t* row_ptr,
                                               const uint32_t* doc_ids, uint32_t n_docs, uint32_t op_lo,
@@ -2365,10 +2366,10 @@ extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gs
     }
     MT_LAUNCH_LOCB(2048, 1)
     MT_LAUNCH_LOCB(4096, 1)
-    MT_LAUNCH_LOCB(1024, 4)
-    MT_LAUNCH_LOCB(4096, 4)
+    MT_LAUNCH_LOCB(1024, MT_LOC_GW)
+    MT_LAUNCH_LOCB(4096, MT_LOC_GW)
     MT_LAUNCH_LOCB(8192, 1)
-    MT_LAUNCH_LOCB(8192, 4)
+    MT_LAUNCH_LOCB(8192, MT_LOC_GW)
 #undef MT_LAUNCH_LOCB
     return hipErrorInvalidValue;
 }
@@ -2376,10 +2377,10 @@ extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gs
 extern "C" size_t mt_lds_bytes_loc(int cap_class, int gw) {
     if (gw == 1 && cap_class == 2048) return sizeof(mt::Lds<2048, true>);
     if (gw == 1 && cap_class == 4096) return sizeof(mt::Lds<4096, true>);
-    if (gw == 4 && cap_class == 1024) return sizeof(mt::Lds<1024, true, false, 4>);
-    if (gw == 4 && cap_class == 4096) return sizeof(mt::Lds<4096, true, false, 4>);
+    if (gw == MT_LOC_GW && cap_class == 1024) return sizeof(mt::Lds<1024, true, false, MT_LOC_GW>);
+    if (gw == MT_LOC_GW && cap_class == 4096) return sizeof(mt::Lds<4096, true, false, MT_LOC_GW>);
     if (gw == 1 && cap_class == 8192) return sizeof(mt::Lds<8192, true>);
-    if (gw == 4 && cap_class == 8192) return sizeof(mt::Lds<8192, true, false, 4>);
+    if (gw == MT_LOC_GW && cap_class == 8192) return sizeof(mt::Lds<8192, true, false, MT_LOC_GW>);
     return 0;
 }
 

@@ -101,7 +101,7 @@ constexpr int kWideClasses = kNumClasses - kFirstWide;
 // both forms at 8192)
 constexpr int kLocForms = 8;
 const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096, 1024, 4096, 8192, 8192};
-const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, 4, 4, 1, 4};
+const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, MT_LOC_GW, MT_LOC_GW, 1, MT_LOC_GW};
 constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
 // the register engine's C64 form per class, the other editing forms
@@ -272,7 +272,7 @@ static bool grow_big(mt_engine* e, uint32_t rows) {
 }
 static bool grow_gx(mt_engine* e, uint32_t rows) {
     mt_gstate& g = e->g;
-    const size_t n = (size_t)rows * MT_LOC_BIGCAP * 4, u = (size_t)e->ngx * MT_LOC_BIGCAP * 4;
+    const size_t n = (size_t)rows * MT_LOC_BIGCAP * MT_LOC_GW, u = (size_t)e->ngx * MT_LOC_BIGCAP * MT_LOC_GW;
     void *gm = nullptr, *lx = nullptr;
     if (!pool_alloc(&gm, n * 8) || !pool_alloc(&lx, (size_t)rows * sizeof(mt_locx))) {
         for (void* q : {gm, lx})
@@ -1656,8 +1656,8 @@ mt_status mt_class_kernel_name(mt_engine* e, uint32_t capacity, char* buf, uint6
     if (!e || !buf || !cap) return MT_ERR_ARG;
     char tmp[96];
     if ((capacity & MT_CLASS_EDITING) && (capacity & MT_CLASS_GROUPS))
-        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 4>",
-                 capacity & ~(uint32_t)(MT_CLASS_EDITING | MT_CLASS_GROUPS));
+        snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, %d>",
+                 capacity & ~(uint32_t)(MT_CLASS_EDITING | MT_CLASS_GROUPS), MT_LOC_GW);
     else if ((capacity & MT_CLASS_EDITING) && (capacity & ~(uint32_t)MT_CLASS_EDITING) > MT_LOC_CAP)
         snprintf(tmp, sizeof tmp, "mt::apply_kernel_g<%u, false, true, 1>", capacity & ~(uint32_t)MT_CLASS_EDITING);
     else if (capacity & MT_CLASS_EDITING)

@@ -71,7 +71,8 @@ struct mt_loc {
 // An editing document past 64 pending edits (MT_WIDE_GROUPS) keeps up to MT_LOC_GROUPS_WIDE: its
 // group masks take MT_LOC_GROUPS_WIDE / 64 words per segment (mt_gstate.gmx) and each group's
 // creation stamp and localSeq live here (bit / index = ordinal % MT_LOC_GROUPS_WIDE)
-#define MT_LOC_GROUPS_WIDE 256
+#define MT_LOC_GROUPS_WIDE 512
+#define MT_LOC_GW (MT_LOC_GROUPS_WIDE / 64)  // group-mask words per segment of such a document
 struct mt_locx {
     uint32_t gt[MT_LOC_GROUPS_WIDE];
     uint32_t gls[MT_LOC_GROUPS_WIDE];
@@ -136,7 +137,7 @@ struct mt_gstate {
     uint64_t* lsqb;
     uint32_t* locbig;  // [doc]
     // MT_WIDE_GROUPS documents: a row of the group pool (locgx[doc], or MT_NO_ROW), the group masks,
-    // 4 words per segment ([row][MT_LOC_BIGCAP][4]), and the groups' stamps / localSeqs ([row])
+    // MT_LOC_GW words per segment ([row][MT_LOC_BIGCAP][MT_LOC_GW]), and the groups' stamps / localSeqs ([row])
     uint64_t* gmx;
     mt_locx* locx;
     uint32_t* locgx;   // [doc]

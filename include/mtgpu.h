@@ -90,7 +90,7 @@ enum mt_op_flags {
  * blockInsert's continuePredicate, pending property keys).  Such a document runs on the LDS
  * engine's editing form (in LDS up to MT_LOC_CAP = 1024 segments, then with its structure in an HBM
  * workspace at 2048 / 4096 / 8192; past 64 pending edits at once the workspace form with 256
- * pending-edit slots, for good; at most 8192 segments and 256 pending edits; beyond:
+ * pending-edit slots, for good; at most 8192 segments and 512 pending edits; beyond:
  * MT_DERR_CAPACITY); its delta events include the local edits' callbacks (seq -1). */
 #define MT_SEQ_LOCAL (-1)
 /* Reconnect (Client.regeneratePendingOp, client.ts:708-766, 855-893): a record with seq =
@@ -277,7 +277,7 @@ mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
  * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),
  * reading MT_CLASS_C64 | capacity, then the editing form's other sizes, MT_CLASS_EDITING | 256 / 512
  * (LDS) and | 2048 / 4096 (HBM workspace), then MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024 / 4096 (the
- * HBM-workspace form with 256 pending-edit slots), then the wide form per class from the 256 class on
+ * HBM-workspace form with 512 pending-edit slots), then the wide form per class from the 256 class on
  * (staged in LDS up to 512 segments, in an HBM workspace above), MT_CLASS_WIDE | capacity; MT_ERR_ARG
  * past the last): each class is one kernel instantiation (see
  * mt_class_kernel_name). */

@@ -140,9 +140,12 @@ function farm(seed, nOps, nClients, partial, markers, reconnect, offline) {
     while (made < nOps) {
         // offline: now and then c1 goes offline for 12-24 rounds, editing more per round; its
         // messages are held (so its pending edits pile up past 64) and it receives nothing
-        if (offline && !away && r() < 0.08) away = 12 + ri(13);
+        // (offline 2: long sessions, 90-120 rounds at 3-7 edits each, so 400+ of c1's edits are
+        // pending at once -- capped at 480)
+        if (offline && !away && r() < (offline === 2 ? 0.05 : 0.08)) away = offline === 2 ? 90 + ri(31) : 12 + ri(13);
         for (let i = 0; i < nClients; i++) {
-            const k = away && i === 0 ? 1 + ri(5) : r() < 0.6 ? 1 + ri(3) : 0;
+            let k = away && i === 0 ? (offline === 2 ? 3 + ri(5) : 1 + ri(5)) : r() < 0.6 ? 1 + ri(3) : 0;
+            if (away && i === 0 && offline === 2) k = Math.min(k, 480 - queue.filter((q) => q.client === 1).length);
             for (let q = 0; q < k; q++) localOp(i);
         }
         // reconnect (client.reconnectFarm.spec.ts): c1's messages of this round are never sequenced;
@@ -174,10 +177,17 @@ function farm(seed, nOps, nClients, partial, markers, reconnect, offline) {
             for (let i = 0; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
         }
     }
+    if (offline === 2 && queue.length) {  // (a long session may outlast the edits: c1 comes back at the end)
+        sequenceAll(false);
+        for (let i = 1; i < nClients; i++) while (cursor[i] < seqd.length) deliver(i);
+    }
     while (cursor[0] < seqd.length) deliver(0);
     const txt = (c) => c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId());
     const t0 = txt(clients[0]);
-    for (const c of clients) if (txt(c) !== t0) return null;  // the clients diverged: drop the run
+    for (const c of clients) if (txt(c) !== t0) {  // the clients diverged: drop the run
+        if (process.env.FARM_DEBUG) process.stderr.write(`local_farm: diverged (${clients.map((x) => txt(x).length)})\n`);
+        return null;
+    }
     return reconnect ? { log, regen } : log;
 }
 
@@ -189,11 +199,13 @@ for (let d = 0, k = 0; d < nDocs; k++) {
     let log = null;
     try {  // (offline runs: a reference client may throw "MergeTree insert failed" -- dropped like a divergence)
         log = farm(seed * 7919 + k, nOps, nClients || 4, partial === 1, markers === 1, reconnect === 1,
-                   offline === 1);
+                   offline || 0);
     } catch (err) {
-        if (offline !== 1) throw err;
+        if (!offline) throw err;
+        if (process.env.FARM_DEBUG && dropped < 5) process.stderr.write(`local_farm: run ${k}: ${err.message}\n`);
     }
     if (log) { docs.push(log); d++; } else dropped++;
+    if (offline === 2 && k % 10 === 9) process.stderr.write(`local_farm: ${k + 1} runs, ${dropped} dropped\n`);
 }
 process.stderr.write(`local_farm: ${nDocs} documents, ${dropped} runs dropped (clients diverged)\n`);
 process.stdout.write(JSON.stringify({ docs }) + "\n");

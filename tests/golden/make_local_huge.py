@@ -6,7 +6,11 @@ lagging:
   * local_huge: 2 documents, 32000 edits over all clients: they grow past 1024 segments;
   * local_offline: 6 documents, 3000 edits; c1 goes offline for 12-24 rounds now and then (its
     messages held, nothing delivered) so that 110-170 of its edits are pending at once (the
-    reference client throws "MergeTree insert failed" on some such runs: the farm drops those).
+    reference client throws "MergeTree insert failed" on some such runs: the farm drops those);
+  * local_offline_long: 3 documents, 1500 edits; c1 stays offline for 90-120 rounds at 3-7 edits a
+    round, so 400-484 of its edits are pending at once (the farm caps them at 480 while it is away;
+    runs in which the reference's own clients diverge are dropped).
+    python tests/golden/make_local_huge.py [--only=local_offline_long]
 <name>.expected.jsonl holds the reference Client c1's canonical state at 6 checkpoints and at the
 end (one JSON line per document, like local.expected.jsonl); local_offline.events.jsonl the count and
 SHA-256 of c1's delta callbacks per document (like local_events.jsonl)."""
@@ -22,15 +26,18 @@ sys.path.insert(0, HERE)
 
 from make_golden import build_log  # noqa: E402
 
-LOGS = (('local_huge', 2, 22, 32000, 0), ('local_offline', 6, 33, 3000, 1))
-# (name, docs, seed, edits over all clients, offline); 4 clients, c1 lagging, 6 checkpoints
+LOGS = (('local_huge', 2, 22, 32000, 0), ('local_offline', 6, 33, 3000, 1), ('local_offline_long', 3, 44, 1500, 2))
+# (name, docs, seed, edits over all clients, offline: 1 = sessions of 12-24 rounds, 2 = of 90-120 rounds
+# with up to 480 of c1's edits pending); 4 clients, c1 lagging, 6 checkpoints
 N_CLIENTS, PARTIAL, N_CK = 4, 1, 6
 
 
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
+    only = [a.split('=', 1)[1] for a in sys.argv[1:] if a.startswith('--only=')]
     for name, n_docs, seed, n_ops, offline in LOGS:
-        make(name, n_docs, seed, n_ops, offline)
+        if not only or name in only[0].split(','):
+            make(name, n_docs, seed, n_ops, offline)
 
 
 def make(name, n_docs, seed, n_ops, offline):

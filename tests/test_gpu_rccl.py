@@ -45,7 +45,7 @@ def test_bench_with_a_one_rank_rccl_communicator():
     """bench.py --comm rccl at world size 1: the headline script's RCCL path end to end."""
     env = dict(os.environ, MTGPU_RUN_ID=uuid.uuid4().hex)
     out = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--comm', 'rccl', '--docs', '2048',
-                          '--ops', '128', '--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-h2d'],
+                          '--ops', '128', '--steps', '1', '--warmup', '0', '--no-cpu-baseline'],
                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().split('\n')[-1])

@@ -7,7 +7,9 @@ reference Client c1 replaying <log>.mtlog (tests/golden/make_local_huge.py: the 
 of reference clients, 4 clients, c1 lagging), at checkpoints and at the end:
   * local_huge: 32000 edits; both documents pass 1024 segments (up to 1609) with edits pending;
   * local_offline: c1 goes offline for 12-24 rounds now and then, so 110-170 of its edits are
-    pending at once (acked in order when it comes back)."""
+    pending at once (acked in order when it comes back);
+  * local_offline_long: c1 stays offline for 90-120 rounds, so 400-484 of its edits are pending at once
+    (the form's 512 pending-edit slots), and its documents pass 1024 segments meanwhile."""
 import json
 import os
 
@@ -19,6 +21,7 @@ from test_local import checkpoint_batch, prefix
 
 NAME = 'local_huge'
 OFFLINE = 'local_offline'
+OFFLINE_LONG = 'local_offline_long'
 
 
 def load_rows(name=NAME):
@@ -56,7 +59,16 @@ def test_offline_fixture_has_more_than_64_pending_edits():
     assert min(pend) > 100, pend
 
 
-@pytest.mark.parametrize('name', [NAME, OFFLINE])
+def test_long_offline_fixture_has_400_pending_edits():
+    from fluidframework_amd.oplog import OpBatch
+    b = OpBatch.load(os.path.join(GOLDEN, OFFLINE_LONG + '.mtlog'))
+    rows = load_rows(OFFLINE_LONG)
+    assert all(r['err'] is None for r in rows)
+    pend = [max_pending(b, d) for d in range(b.n_docs)]
+    assert min(pend) > 400 and max(pend) <= 512, pend
+
+
+@pytest.mark.parametrize('name', [NAME, OFFLINE, OFFLINE_LONG])
 def test_oracle_editing_client_matches_reference_beyond_lds_limits(oracle_lib, name):
     from fluidframework_amd.oplog import OpBatch
     batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
@@ -69,12 +81,13 @@ def test_oracle_editing_client_matches_reference_beyond_lds_limits(oracle_lib, n
             assert oracle_lib.Oracle(1).apply(prefix(batch, d, k)).state(0) == want, (d, k)
 
 
-def test_oracle_events_past_64_pending_edits_match_reference(oracle_lib):
+@pytest.mark.parametrize('name', [OFFLINE, OFFLINE_LONG])
+def test_oracle_events_past_64_pending_edits_match_reference(oracle_lib, name):
     import hashlib
     from fluidframework_amd.oplog import OpBatch
-    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
     o = oracle_lib.Oracle(batch.n_docs).record_events().apply(batch)
-    with open(os.path.join(GOLDEN, OFFLINE + '.events.jsonl')) as f:
+    with open(os.path.join(GOLDEN, name + '.events.jsonl')) as f:
         gold = [json.loads(x) for x in f]
     for g in gold:
         ev = o.events(g['doc'])
@@ -108,16 +121,16 @@ def test_engine_editing_form_past_1024_segments_matches_reference(b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('b', [1, 32])
-def test_engine_editing_form_past_64_pending_edits_matches_reference(b):
+@pytest.mark.parametrize('name,b', [(OFFLINE, 1), (OFFLINE, 32), (OFFLINE_LONG, 1), (OFFLINE_LONG, 32)])
+def test_engine_editing_form_past_64_pending_edits_matches_reference(name, b):
     """110-170 pending edits at once: every checkpoint state and the final state equal the
-    reference's; the documents ran on the form with 256 pending-edit slots (class stats
-    MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024, mt::apply_kernel_g<1024, false, true, 4>), which they
+    reference's; the documents ran on the form with 512 pending-edit slots (class stats
+    MT_CLASS_EDITING | MT_CLASS_GROUPS | 1024, mt::apply_kernel_g<1024, false, true, 8>), which they
     enter with edits pending (their group masks and stamps re-laid) and keep for good."""
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import OpBatch
-    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
-    rows = load_rows(OFFLINE)
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
+    rows = load_rows(name)
     groups = 0x40000000 | 0x08000000 | 1024
     for q in range(len(rows[0]['states'])):
         cb = checkpoint_batch(batch, rows, q)
@@ -127,24 +140,27 @@ def test_engine_editing_form_past_64_pending_edits_matches_reference(b):
         for i, r in enumerate(rows):
             assert eng.error(i) == (0, 0), (r['doc'], q, eng.error(i))
             assert eng.state(i) == r['states'][q][1], (r['doc'], q, b)
-        if max(max_pending(cb, i) for i in range(cb.n_docs)) > 64:
+        if name == OFFLINE and max(max_pending(cb, i) for i in range(cb.n_docs)) > 64:
             assert used.get(groups, 0) > 0, used
-            assert eng.class_kernel(groups) == 'mt::apply_kernel_g<1024, false, true, 4>'
+        if name == OFFLINE_LONG and max(max_pending(cb, i) for i in range(cb.n_docs)) > 64:
+            assert any(cap & 0x08000000 for cap in used), used  # (at 1024 or, past 1024 segments, 4096 slots)
+            assert eng.class_kernel(groups) == 'mt::apply_kernel_g<1024, false, true, 8>'
         eng.close()
 
 
 @pytest.mark.gpu
-def test_engine_editing_form_past_64_pending_edits_events_match_reference():
+@pytest.mark.parametrize('name', [OFFLINE, OFFLINE_LONG])
+def test_engine_editing_form_past_64_pending_edits_events_match_reference(name):
     """The delta callbacks the wide-group form records (mt_events_enable) equal the reference
-    client's (tests/golden/local_offline.events.jsonl: count + SHA-256 per document)."""
+    client's (tests/golden/<name>.events.jsonl: count + SHA-256 per document)."""
     import hashlib
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.oplog import OpBatch
-    batch = OpBatch.load(os.path.join(GOLDEN, OFFLINE + '.mtlog'))
+    batch = OpBatch.load(os.path.join(GOLDEN, name + '.mtlog'))
     eng = MergeEngine(batch.n_docs, ops_per_launch=16).enable_events(1 << 16)
     eng.apply(batch)
     got = eng.drain_events()
-    with open(os.path.join(GOLDEN, OFFLINE + '.events.jsonl')) as f:
+    with open(os.path.join(GOLDEN, name + '.events.jsonl')) as f:
         gold = [json.loads(x) for x in f]
     for g in gold:
         d = g['doc']

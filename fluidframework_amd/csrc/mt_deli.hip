@@ -29,26 +29,42 @@ namespace mtd {
 
 enum : int { CL_JOINED = 1, CL_NACK = 2 };
 
-// per-document state in HBM (structure of arrays; client arrays are [doc * 64 + client])
+// per-document state in HBM (structure of arrays; client arrays are [doc * 64 + client]); a
+// document that ever sees a client id >= 64 is promoted, for good, to a row of the big pool
+// ([row * MT_DELI_MAX_CLIENTS + client]) and ticketed by the wide form (one document per wave)
 struct DeliState {
     int4* sc;         // {sequenceNumber, minimumSequenceNumber, lastSentMSN, err}
     int32_t* err_at;  // message index (inside the document's stream) of the sticky error
     int32_t* csn;
     int32_t* ref;
     uint8_t* fl;      // CL_JOINED | CL_NACK
+    uint32_t* big;    // per document: its row of the big pool, or kNoRow
+    int32_t* bcsn;    // big pool: [row][MT_DELI_MAX_CLIENTS]
+    int32_t* bref;
+    uint8_t* bfl;
+    uint32_t big_cap; // rows in the big pool
+    uint32_t* ctl;    // [0] rows in use, [1] documents queued for the wide form in this call
+    uint32_t* queue;  // [max_docs]: those documents
+    int32_t* resume;  // per queued document: its first message the wide form tickets
 };
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
-constexpr int kGroup = 8;                             // lanes per document
-constexpr int kPerLane = MT_MAX_CLIENTS / kGroup;     // client slots per lane
+constexpr int kPerLane = 8;                           // client slots per lane
 typedef int32_t V8 __attribute__((ext_vector_type(kPerLane)));
 
-// min over the 8 lanes of a document's group, in every lane of the group: quad_perm [1,0,3,2],
-// quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i inside each half-row)
+// min over the G lanes of a document's group, in every lane of the group: G = 8 with quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], then row_half_mirror (lane i <-> 7-i inside each half-row); G = 64
+// the whole wave
+template <int G>
 MT_DEV int group_min(int v) {
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0xB1, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x4E, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x141, 0xf, 0xf, false));
-    return v;
+    if constexpr (G == 64) {
+        return wave_min(v);
+    } else {
+        v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0xB1, 0xf, 0xf, false));
+        v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x4E, 0xf, 0xf, false));
+        v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x141, 0xf, 0xf, false));
+        return v;
+    }
 }
 // slot k of a lane's 8 client slots (k differs between groups: a select chain, not an index)
 MT_DEV int pick(const V8& a, int k) {
@@ -58,65 +74,62 @@ MT_DEV int pick(const V8& a, int k) {
     return r;
 }
 
-// Eight documents per wave, eight lanes per document; lane q of a document's group owns its
-// clients 8q..8q+7 (csn, refSeq in VGPRs; joined / nacked as 2-bit fields of one VGPR).  Every
-// branch of ticket() is evaluated as per-lane selects, so the CU's four SIMDs do the work in
-// parallel (a wave-per-document form runs the decision tree on the CU's single scalar unit).
-// A client lookup is one ds_bpermute from its owner lane; the heap minimum is 8 local mins and
-// three DPP steps.  Messages are staged through LDS eight per document at a time (one coalesced
-// 16-byte load per lane, prefetched a chunk ahead); tickets go back the same way.
-__global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __restrict__ msgs,
-                                                  const uint32_t* __restrict__ row_ptr, uint32_t n_docs,
-                                                  int4* __restrict__ out, mt_op_rec* __restrict__ ops,
-                                                  uint64_t n_ops) {
-    __shared__ int4 stage[64];
+// One document per group of G lanes, lane q of the group owning the document's clients
+// 8q..8q+7 (csn, refSeq in VGPRs; joined / nacked as 2-bit fields of one VGPR): G = 8, eight
+// documents per wave, 64 clients each (the common form); G = 64, one document per wave with 512
+// (the wide form, for documents past client 63).  Every branch of ticket() is evaluated as per-lane
+// selects, so the CU's four SIMDs do the work in parallel (a wave-per-document form runs the
+// decision tree on the CU's single scalar unit).  A client lookup is one ds_bpermute from its owner
+// lane; the heap minimum is 8 local mins and a group reduction.  Messages are staged through LDS G
+// per document at a time (one coalesced 16-byte load per lane, prefetched a chunk ahead); tickets
+// go back the same way.  Messages [m0, len) of the document's stream are ticketed; in the G = 8 form
+// a message from a client >= 64 stops the document there and queues it for the wide form
+// (`stop`), which promotes it and tickets the rest.
+template <int G>
+MT_DEV void deli_group(DeliState& g, const int4* __restrict__ msgs, uint32_t d, bool live, uint32_t r0, int len,
+                       int m0, int32_t* ccsn_p, int32_t* cref_p, uint8_t* cfl_p, int4* __restrict__ out,
+                       mt_op_rec* __restrict__ ops, uint64_t n_ops, int4 (&stage)[64]) {
+    constexpr int NC = G * kPerLane;  // clients this form holds
     const int lane = lane_id();
-    const int li = lane & (kGroup - 1), gbase = lane & ~(kGroup - 1);
-    const uint32_t d = blockIdx.x * (64 / kGroup) + (uint32_t)(lane / kGroup);
-    const bool live = d < n_docs;
-    uint32_t r0 = 0;
-    int len = 0;
-    if (live) {
-        r0 = row_ptr[d];
-        len = (int)(row_ptr[d + 1] - r0);
-    }
-    const int maxlen = -wave_min(-len);  // wave-uniform trip count
-    if (maxlen == 0) return;
+    const int li = lane & (G - 1), gbase = lane & ~(G - 1);
     int4 s0 = make_int4(0, 0, 0, 0);
     int err_at = -1;
     V8 csn = 0, ref = 0;
     uint32_t fl = 0;
-    const size_t cb = (size_t)d * MT_MAX_CLIENTS + (size_t)li * kPerLane;
     if (live) {
         s0 = g.sc[d];
         err_at = g.err_at[d];
-        const int4 c0 = *reinterpret_cast<const int4*>(g.csn + cb), c1 = *reinterpret_cast<const int4*>(g.csn + cb + 4);
-        const int4 f0 = *reinterpret_cast<const int4*>(g.ref + cb), f1 = *reinterpret_cast<const int4*>(g.ref + cb + 4);
+        const int4 c0 = *reinterpret_cast<const int4*>(ccsn_p), c1 = *reinterpret_cast<const int4*>(ccsn_p + 4);
+        const int4 f0 = *reinterpret_cast<const int4*>(cref_p), f1 = *reinterpret_cast<const int4*>(cref_p + 4);
         csn = V8{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
         ref = V8{f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-        const uint2 fb = *reinterpret_cast<const uint2*>(g.fl + cb);
+        const uint2 fb = *reinterpret_cast<const uint2*>(cfl_p);
 #pragma unroll
         for (int i = 0; i < kPerLane; i++) fl |= (((i < 4 ? fb.x >> (8 * i) : fb.y >> (8 * (i - 4)))) & 3u) << (2 * i);
     }
     int seq = s0.x, msn = s0.y, last = s0.z, err = s0.w;
-
+    int stop = -1;  // (G = 8) the message from a client >= 64 this document stops at
+    const int maxlen = -wave_min(live ? -len : 0);  // wave-uniform trip count
     int4 nxt = make_int4(0, 0, 0, 0);
-    if (li < len) nxt = msgs[r0 + li];
-    for (int jb = 0; jb < maxlen; jb += kGroup) {
+    if (live && m0 + li < len) nxt = msgs[r0 + m0 + li];
+    for (int jb = m0; jb < maxlen; jb += G) {
         const int4 cur = nxt;
-        if (jb + kGroup + li < len) nxt = msgs[r0 + jb + kGroup + li];  // next chunk in flight
+        if (live && jb + G + li < len) nxt = msgs[r0 + jb + G + li];  // next chunk in flight
         wave_sync();
         stage[lane] = cur;
         wave_sync();
         int4 t = make_int4(0, 0, 0, 0);
-        const int steps = min(kGroup, maxlen - jb);
+        const int steps = min(G, maxlen - jb);
         for (int jj = 0; jj < steps; jj++) {
             const int4 mm = stage[gbase + jj];
-            const bool act = live && jb + jj < len;
             const int mc = mm.x, mr = mm.y;
             const int c = mm.z & 0xFFFF, kind = (mm.z >> 16) & 0xFF;
-            const bool bad = c >= MT_MAX_CLIENTS || kind > MT_RAW_CONTROL;
-            const int cq = c & (kPerLane - 1), owner = gbase + ((c / kPerLane) & (kGroup - 1));
+            if (G == 8 && live && jb + jj < len && !err && stop < 0 && c >= NC && c < MT_DELI_MAX_CLIENTS &&
+                kind <= MT_RAW_CONTROL)
+                stop = jb + jj;  // (group-uniform: every lane of the group reads the same message)
+            const bool act = live && jb + jj < len && stop < 0;
+            const bool bad = c >= NC || kind > MT_RAW_CONTROL;
+            const int cq = c & (kPerLane - 1), owner = gbase + ((c / kPerLane) & (G - 1));
             // client c's record, from its owner lane
             const int ccsn = __builtin_amdgcn_ds_bpermute(owner << 2, pick(csn, cq));
             const int cfl = __builtin_amdgcn_ds_bpermute(owner << 2, (int)((fl >> (2 * cq)) & 3u));
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
             int mv = INT_MAX;
 #pragma unroll
             for (int i = 0; i < kPerLane; i++) mv = min(mv, ((fl >> (2 * i)) & 1u) ? ref[i] : INT_MAX);
-            mv = group_min(mv);
+            mv = group_min<G>(mv);
             const bool none = mv == INT_MAX;
             int msn2 = none ? s2 : mv;
             // send type (:457-517)
@@ -202,12 +215,12 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
                     tst = st;
                 }
             } else if (act && !err) {
-                err = c >= MT_MAX_CLIENTS ? MT_DELI_ERR_CLIENT : MT_DELI_ERR_KIND;
+                err = c >= NC ? MT_DELI_ERR_CLIENT : MT_DELI_ERR_KIND;
                 err_at = jb + jj;
             }
             if (li == jj) t = make_int4(ts, tm, to, tst);
         }
-        if (jb + li < len) {
+        if (live && jb + li < len && (stop < 0 || jb + li < stop)) {
             out[r0 + jb + li] = t;
             // my message of this chunk is still staged: its op_index links the op record
             const uint32_t opi = (uint32_t)stage[lane].w;
@@ -223,11 +236,16 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
     if (li == 0) {
         g.sc[d] = make_int4(seq, msn, last, err);
         g.err_at[d] = err_at;
+        if (G == 8 && stop >= 0) {  // the rest of the stream goes to the wide form
+            const uint32_t q = atomicAdd(&g.ctl[1], 1u);
+            g.queue[q] = d;
+            g.resume[d] = stop;
+        }
     }
-    *reinterpret_cast<int4*>(g.csn + cb) = make_int4(csn[0], csn[1], csn[2], csn[3]);
-    *reinterpret_cast<int4*>(g.csn + cb + 4) = make_int4(csn[4], csn[5], csn[6], csn[7]);
-    *reinterpret_cast<int4*>(g.ref + cb) = make_int4(ref[0], ref[1], ref[2], ref[3]);
-    *reinterpret_cast<int4*>(g.ref + cb + 4) = make_int4(ref[4], ref[5], ref[6], ref[7]);
+    *reinterpret_cast<int4*>(ccsn_p) = make_int4(csn[0], csn[1], csn[2], csn[3]);
+    *reinterpret_cast<int4*>(ccsn_p + 4) = make_int4(csn[4], csn[5], csn[6], csn[7]);
+    *reinterpret_cast<int4*>(cref_p) = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    *reinterpret_cast<int4*>(cref_p + 4) = make_int4(ref[4], ref[5], ref[6], ref[7]);
     uint2 fb = make_uint2(0u, 0u);
 #pragma unroll
     for (int i = 0; i < kPerLane; i++) {
@@ -235,7 +253,95 @@ __global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __res
         if (i < 4) fb.x |= v << (8 * i);
         else fb.y |= v << (8 * (i - 4));
     }
-    *reinterpret_cast<uint2*>(g.fl + cb) = fb;
+    *reinterpret_cast<uint2*>(cfl_p) = fb;
+}
+
+// eight documents per wave (the common form); a document already promoted to the big pool is
+// queued for the wide form whole
+__global__ __launch_bounds__(64) void deli_kernel(DeliState g, const int4* __restrict__ msgs,
+                                                  const uint32_t* __restrict__ row_ptr, uint32_t n_docs,
+                                                  int4* __restrict__ out, mt_op_rec* __restrict__ ops,
+                                                  uint64_t n_ops) {
+    __shared__ int4 stage[64];
+    const int lane = lane_id();
+    const int li = lane & 7;
+    const uint32_t d = blockIdx.x * 8 + (uint32_t)(lane / 8);
+    bool live = d < n_docs;
+    uint32_t r0 = 0;
+    int len = 0;
+    if (live) {
+        r0 = row_ptr[d];
+        len = (int)(row_ptr[d + 1] - r0);
+        if (g.big[d] != kNoRow) {  // promoted earlier: the wide form tickets it
+            if (len > 0 && li == 0) {
+                const uint32_t q = atomicAdd(&g.ctl[1], 1u);
+                g.queue[q] = d;
+                g.resume[d] = 0;
+            }
+            live = false;
+        }
+    }
+    if (wave_ballot(live && len > 0) == 0) return;
+    const size_t cb = (size_t)(live ? d : 0) * MT_MAX_CLIENTS + (size_t)li * kPerLane;
+    deli_group<8>(g, msgs, d, live, r0, len, 0, g.csn + cb, g.ref + cb, g.fl + cb, out, ops, n_ops, stage);
+}
+
+// the wide form: the queued documents, one per wave (persistent over the queue); a document's first
+// visit promotes it -- a row of the big pool, its 64 clients' state copied in
+__global__ __launch_bounds__(64) void deli_wide_kernel(DeliState g, const int4* __restrict__ msgs,
+                                                       const uint32_t* __restrict__ row_ptr, int4* __restrict__ out,
+                                                       mt_op_rec* __restrict__ ops, uint64_t n_ops) {
+    __shared__ int4 stage[64];
+    const int lane = lane_id();
+    const uint32_t nq = g.ctl[1];
+    for (uint32_t i = blockIdx.x; i < nq; i += gridDim.x) {
+        const uint32_t d = g.queue[i];
+        const uint32_t r0 = row_ptr[d];
+        const int len = (int)(row_ptr[d + 1] - r0);
+        const int m0 = g.resume[d];
+        uint32_t row = g.big[d];
+        if (row == kNoRow) {
+            uint32_t r = 0;
+            if (lane == 0) r = atomicAdd(&g.ctl[0], 1u);
+            r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+            if (r >= g.big_cap) {  // no row left: the document halts at the message that needed one
+                if (lane == 0) {
+                    int4 sc = g.sc[d];
+                    if (!sc.w) {
+                        sc.w = MT_DELI_ERR_CLIENT;
+                        g.err_at[d] = m0;
+                    }
+                    g.sc[d] = sc;
+                }
+                wave_sync();
+                const int4 sc = g.sc[d];
+                for (int j = m0 + lane; j < len; j += 64) {
+                    const int4 m = msgs[r0 + j];
+                    out[r0 + j] = make_int4(sc.x, sc.y, m.y, MT_TK_HALTED);
+                    const uint32_t opi = (uint32_t)m.w;
+                    if (ops && opi && opi <= n_ops) {
+                        mt_op_rec* o = ops + (opi - 1u);
+                        o->seq = MT_SEQ_NACK;
+                        o->msn = sc.y;
+                        o->ref_seq = m.y;
+                    }
+                }
+                continue;
+            }
+            row = r;
+            const size_t src = (size_t)d * MT_MAX_CLIENTS, dst = (size_t)row * MT_DELI_MAX_CLIENTS;
+            for (int c = lane; c < MT_DELI_MAX_CLIENTS; c += 64) {
+                const bool in = c < MT_MAX_CLIENTS;
+                g.bcsn[dst + c] = in ? g.csn[src + c] : 0;
+                g.bref[dst + c] = in ? g.ref[src + c] : 0;
+                g.bfl[dst + c] = in ? g.fl[src + c] : (uint8_t)0;
+            }
+            __threadfence_block();
+            if (lane == 0) g.big[d] = row;
+        }
+        const size_t cb = (size_t)row * MT_DELI_MAX_CLIENTS + (size_t)lane * kPerLane;
+        deli_group<64>(g, msgs, d, true, r0, len, m0, g.bcsn + cb, g.bref + cb, g.bfl + cb, out, ops, n_ops, stage);
+    }
 }
 
 // every document from one checkpoint (bench tooling)
@@ -250,6 +356,8 @@ __global__ void restore_all_kernel(DeliState g, uint32_t n_docs, mt_deli_checkpo
     if (c == 0) {
         g.sc[d] = make_int4(ck.seq, ck.msn, ck.last_sent_msn, 0);
         g.err_at[d] = -1;
+        g.big[d] = kNoRow;  // (every document restored: the big pool starts over)
+        if (d == 0) g.ctl[0] = 0u;
     }
 }
 
@@ -326,6 +434,8 @@ struct mt_deli {
     mtd::DeliState g{};
     hipEvent_t e0 = nullptr, e1 = nullptr;
 };
+// rows of the big pool (documents past client 63 at once): one per 16 documents, at least 64
+static uint32_t deli_big_rows(uint32_t max_docs) { return std::max<uint32_t>(64u, max_docs / 16u); }
 
 #define DL_HIP(x)                                                                                            \
     do {                                                                                                     \
@@ -344,13 +454,25 @@ int32_t ckpt_msn(const mt_deli_checkpoint& ck) {
         if (ck.clients[c].joined) m = std::min(m, ck.clients[c].ref_seq);
     return m == INT_MAX ? ck.seq : m;
 }
-mt_status launch_ticket(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row, uint32_t n_docs,
-                        mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops) {
-    DL_HIP(hipEventRecord(dl->e0, dl->stream));
-    hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, dl->stream, dl->g,
+// the common form over every document, then the wide form over the documents it queued (past client
+// 63: promoted now or earlier), on one stream
+mt_status launch_forms(mt_deli* dl, hipStream_t st, const mt_raw_msg* d_msgs, const uint32_t* d_row, uint32_t n_docs,
+                       mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops) {
+    DL_HIP(hipMemsetAsync(dl->g.ctl + 1, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, st, dl->g,
                        reinterpret_cast<const int4*>(d_msgs), d_row, n_docs, reinterpret_cast<int4*>(d_out), d_ops,
                        n_ops);
     DL_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mtd::deli_wide_kernel, dim3(std::min<uint32_t>(1024u, n_docs)), dim3(64), 0, st, dl->g,
+                       reinterpret_cast<const int4*>(d_msgs), d_row, reinterpret_cast<int4*>(d_out), d_ops, n_ops);
+    DL_HIP(hipGetLastError());
+    return MT_OK;
+}
+mt_status launch_ticket(mt_deli* dl, const mt_raw_msg* d_msgs, const uint32_t* d_row, uint32_t n_docs,
+                        mt_ticket* d_out, mt_op_rec* d_ops, uint64_t n_ops) {
+    DL_HIP(hipEventRecord(dl->e0, dl->stream));
+    const mt_status st = launch_forms(dl, dl->stream, d_msgs, d_row, n_docs, d_out, d_ops, n_ops);
+    if (st) return st;
     DL_HIP(hipEventRecord(dl->e1, dl->stream));
     return MT_OK;
 }
@@ -365,13 +487,24 @@ mt_status mt_deli_create(int32_t device, uint32_t max_docs, mt_deli** out) {
     dl->device = device;
     dl->max_docs = max_docs;
     const size_t nc = (size_t)max_docs * MT_MAX_CLIENTS;
+    dl->g.big_cap = deli_big_rows(max_docs);
+    const size_t nb = (size_t)dl->g.big_cap * MT_DELI_MAX_CLIENTS;
     bool ok = hipStreamCreateWithFlags(&dl->stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreate(&dl->e0) == hipSuccess && hipEventCreate(&dl->e1) == hipSuccess &&
               hipMalloc(&dl->g.sc, max_docs * sizeof(int4)) == hipSuccess &&
               hipMalloc(&dl->g.err_at, max_docs * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dl->g.csn, nc * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dl->g.ref, nc * sizeof(int32_t)) == hipSuccess &&
-              hipMalloc(&dl->g.fl, nc) == hipSuccess;
+              hipMalloc(&dl->g.fl, nc) == hipSuccess &&
+              hipMalloc(&dl->g.big, max_docs * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.resume, max_docs * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.queue, max_docs * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.ctl, 4 * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.bcsn, nb * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.bref, nb * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&dl->g.bfl, nb) == hipSuccess &&
+              hipMemset(dl->g.big, 0xFF, max_docs * sizeof(uint32_t)) == hipSuccess &&
+              hipMemset(dl->g.ctl, 0, 4 * sizeof(uint32_t)) == hipSuccess;
     if (!ok) {
         mt_deli_destroy(dl);
         return MT_ERR_NOMEM;
@@ -389,11 +522,10 @@ mt_status mt_deli_destroy(mt_deli* dl) {
     if (!dl) return MT_ERR_ARG;
     hipSetDevice(dl->device);
     if (dl->stream) hipStreamSynchronize(dl->stream);
-    hipFree(dl->g.sc);
-    hipFree(dl->g.err_at);
-    hipFree(dl->g.csn);
-    hipFree(dl->g.ref);
-    hipFree(dl->g.fl);
+    for (void* p : {(void*)dl->g.sc, (void*)dl->g.err_at, (void*)dl->g.csn, (void*)dl->g.ref, (void*)dl->g.fl,
+                    (void*)dl->g.big, (void*)dl->g.resume, (void*)dl->g.queue, (void*)dl->g.ctl, (void*)dl->g.bcsn,
+                    (void*)dl->g.bref, (void*)dl->g.bfl})
+        if (p) hipFree(p);
     if (dl->e0) hipEventDestroy(dl->e0);
     if (dl->e1) hipEventDestroy(dl->e1);
     if (dl->stream) hipStreamDestroy(dl->stream);
@@ -429,6 +561,9 @@ mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_
     DL_HIP(hipMemcpyAsync(dl->g.csn + c0, csn.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, dl->stream));
     DL_HIP(hipMemcpyAsync(dl->g.ref + c0, ref.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, dl->stream));
     DL_HIP(hipMemcpyAsync(dl->g.fl + c0, fl.data(), nc, hipMemcpyHostToDevice, dl->stream));
+    // (a restored document is back in the common form; a row it held in the big pool is not reused
+    // until mt_deli_restore_all)
+    DL_HIP(hipMemsetAsync(dl->g.big + doc0, 0xFF, n * sizeof(uint32_t), dl->stream));
     DL_HIP(hipStreamSynchronize(dl->stream));
     return MT_OK;
 }
@@ -496,11 +631,7 @@ mt_status mt_deli_ticket_on_stream(mt_deli* dl, int32_t device, hipStream_t st, 
                                    uint64_t n_ops) {
     if (!dl || dl->device != device || n_docs > dl->max_docs) return MT_ERR_ARG;
     if (n_docs == 0) return MT_OK;
-    hipLaunchKernelGGL(mtd::deli_kernel, dim3((n_docs + 7) / 8), dim3(64), 0, st, dl->g,
-                       reinterpret_cast<const int4*>(d_msgs), d_row_ptr, n_docs, reinterpret_cast<int4*>(d_out), d_ops,
-                       n_ops);
-    DL_HIP(hipGetLastError());
-    return MT_OK;
+    return launch_forms(dl, st, d_msgs, d_row_ptr, n_docs, d_out, d_ops, n_ops);
 }
 
 mt_status mt_deli_raw_from_ops(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t* d_row_ptr, uint32_t n_docs,
@@ -540,31 +671,55 @@ mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms) {
     return MT_OK;
 }
 
+}  // extern "C"
+
+// clients [c0, c0 + n) of a document, from its row of the big pool once promoted
+static mt_status read_clients(mt_deli* dl, uint32_t doc, uint32_t c0, uint32_t n, mt_deli_client* out) {
+    uint32_t row = mtd::kNoRow;
+    DL_HIP(hipStreamSynchronize(dl->stream));
+    DL_HIP(hipMemcpy(&row, dl->g.big + doc, sizeof row, hipMemcpyDeviceToHost));
+    std::vector<int32_t> csn(n, 0), ref(n, 0);
+    std::vector<uint8_t> fl(n, 0);
+    const bool big = row != mtd::kNoRow;
+    const uint32_t m = big ? n : (c0 < MT_MAX_CLIENTS ? std::min(n, MT_MAX_CLIENTS - c0) : 0u);
+    const size_t o = big ? (size_t)row * MT_DELI_MAX_CLIENTS + c0 : (size_t)doc * MT_MAX_CLIENTS + c0;
+    if (m) {
+        DL_HIP(hipMemcpy(csn.data(), (big ? dl->g.bcsn : dl->g.csn) + o, m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        DL_HIP(hipMemcpy(ref.data(), (big ? dl->g.bref : dl->g.ref) + o, m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        DL_HIP(hipMemcpy(fl.data(), (big ? dl->g.bfl : dl->g.fl) + o, m, hipMemcpyDeviceToHost));
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        const bool joined = (fl[i] & mtd::CL_JOINED) != 0;
+        out[i] = mt_deli_client{};
+        out[i].joined = joined;
+        out[i].nack = (fl[i] & mtd::CL_NACK) != 0;
+        out[i].csn = joined ? csn[i] : 0;
+        out[i].ref_seq = joined ? ref[i] : 0;
+    }
+    return MT_OK;
+}
+
+extern "C" {
+
 mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out) {
     if (!dl || !out || doc >= dl->max_docs) return MT_ERR_ARG;
     DL_HIP(hipSetDevice(dl->device));
     int4 sc;
-    int32_t csn[MT_MAX_CLIENTS], ref[MT_MAX_CLIENTS];
-    uint8_t fl[MT_MAX_CLIENTS];
-    const size_t c0 = (size_t)doc * MT_MAX_CLIENTS;
     DL_HIP(hipStreamSynchronize(dl->stream));
     DL_HIP(hipMemcpy(&sc, dl->g.sc + doc, sizeof sc, hipMemcpyDeviceToHost));
-    DL_HIP(hipMemcpy(csn, dl->g.csn + c0, sizeof csn, hipMemcpyDeviceToHost));
-    DL_HIP(hipMemcpy(ref, dl->g.ref + c0, sizeof ref, hipMemcpyDeviceToHost));
-    DL_HIP(hipMemcpy(fl, dl->g.fl + c0, sizeof fl, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof *out);
     out->seq = sc.x;
     out->msn = sc.y;
     out->last_sent_msn = sc.z;
     out->err = sc.w;
-    for (int c = 0; c < MT_MAX_CLIENTS; c++) {
-        const bool joined = (fl[c] & mtd::CL_JOINED) != 0;
-        out->clients[c].joined = joined;
-        out->clients[c].nack = (fl[c] & mtd::CL_NACK) != 0;
-        out->clients[c].csn = joined ? csn[c] : 0;
-        out->clients[c].ref_seq = joined ? ref[c] : 0;
-    }
-    return MT_OK;
+    return read_clients(dl, doc, 0, MT_MAX_CLIENTS, out->clients);
+}
+
+mt_status mt_deli_get_clients(mt_deli* dl, uint32_t doc, uint32_t first, uint32_t n, mt_deli_client* out) {
+    if (!dl || (n && !out) || doc >= dl->max_docs || first > MT_DELI_MAX_CLIENTS || n > MT_DELI_MAX_CLIENTS - first)
+        return MT_ERR_ARG;
+    DL_HIP(hipSetDevice(dl->device));
+    return read_clients(dl, doc, first, n, out);
 }
 
 mt_status mt_deli_doc_error(mt_deli* dl, uint32_t doc, int32_t* err, int32_t* index) {

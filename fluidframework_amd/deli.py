@@ -20,7 +20,8 @@ DROPPED, SENT, LATER, NEVER, NACK_GAP, NACK_CLIENT, NACK_REFSEQ, HALTED = range(
 STATUS_NAMES = ['dropped', 'sent', 'later', 'never', 'nack-gap', 'nack-client', 'nack-refseq', 'halted']
 DELI_ERRORS = {0: None, 1: 'client id out of range', 2: 'unknown message kind',
                3: 'assert(referenceSequenceNumber >= minimumSequenceNumber) (lambda.ts:426-428)'}
-MAX_CLIENTS = 64
+MAX_CLIENTS = 512  # include/mtgpu.h MT_DELI_MAX_CLIENTS (up to 63: eight documents per wave; then the wide form)
+CKPT_CLIENTS = 64  # mt_deli_checkpoint's client slots
 
 RAW_DTYPE = np.dtype([('csn', '<i4'), ('ref_seq', '<i4'), ('client', '<u2'), ('kind', 'u1'), ('pad', 'u1'),
                       ('op_index', '<u4')])  # 1 + linked op record (fused hand-off), 0 = none
@@ -35,7 +36,7 @@ class _Client(ctypes.Structure):
 
 class _Checkpoint(ctypes.Structure):
     _fields_ = [('seq', ctypes.c_int32), ('msn', ctypes.c_int32), ('last_sent_msn', ctypes.c_int32),
-                ('err', ctypes.c_int32), ('clients', _Client * MAX_CLIENTS)]
+                ('err', ctypes.c_int32), ('clients', _Client * CKPT_CLIENTS)]
 
 
 _bound = False
@@ -57,11 +58,12 @@ def _lib():
         L.mt_deli_sync.argtypes = [vp]
         L.mt_deli_last_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.mt_deli_get_checkpoint.argtypes = [vp, u32, vp]
+        L.mt_deli_get_clients.argtypes = [vp, u32, u32, u32, vp]
         L.mt_deli_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.mt_batch_device_ptrs.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]
         for name in ('mt_deli_create', 'mt_deli_destroy', 'mt_deli_restore', 'mt_deli_restore_all', 'mt_deli_ticket',
                      'mt_deli_ticket_device', 'mt_deli_raw_from_ops', 'mt_deli_raw_stream', 'mt_deli_sync', 'mt_deli_last_ms',
-                     'mt_deli_get_checkpoint', 'mt_deli_doc_error', 'mt_batch_device_ptrs'):
+                     'mt_deli_get_checkpoint', 'mt_deli_get_clients', 'mt_deli_doc_error', 'mt_batch_device_ptrs'):
             getattr(L, name).restype = ctypes.c_int
         _bound = True
     return L
@@ -72,8 +74,8 @@ def make_checkpoint(seq=0, clients=None, last_sent_msn=0):
     ck = _Checkpoint()
     ck.seq, ck.last_sent_msn = seq, last_sent_msn
     for c, (csn, ref, nack) in (clients or {}).items():
-        if not 0 <= c < MAX_CLIENTS:
-            raise MtError(f'client id {c} out of range')
+        if not 0 <= c < CKPT_CLIENTS:
+            raise MtError(f'client id {c} out of range of a checkpoint')
         ck.clients[c].csn, ck.clients[c].ref_seq = csn, ref
         ck.clients[c].joined, ck.clients[c].nack = 1, int(bool(nack))
     return ck
@@ -143,12 +145,15 @@ class DeliSequencer:
         return ms.value
 
     def checkpoint(self, doc):
-        """generateDeliCheckpoint (lambda.ts:754-764), device-representable part."""
+        """generateDeliCheckpoint (lambda.ts:754-764), device-representable part: every joined client
+        (ids up to MAX_CLIENTS - 1, mt_deli_get_clients)."""
         ck = _Checkpoint()
         _check(_lib().mt_deli_get_checkpoint(self.h, doc, ctypes.byref(ck)), 'mt_deli_get_checkpoint')
+        cl = (_Client * MAX_CLIENTS)()
+        _check(_lib().mt_deli_get_clients(self.h, doc, 0, MAX_CLIENTS, ctypes.cast(cl, ctypes.c_void_p)),
+               'mt_deli_get_clients')
         return {'seq': ck.seq, 'msn': ck.msn, 'last_sent_msn': ck.last_sent_msn, 'err': ck.err,
-                'clients': {c: (ck.clients[c].csn, ck.clients[c].ref_seq, bool(ck.clients[c].nack))
-                            for c in range(MAX_CLIENTS) if ck.clients[c].joined}}
+                'clients': {c: (cl[c].csn, cl[c].ref_seq, bool(cl[c].nack)) for c in range(MAX_CLIENTS) if cl[c].joined}}
 
     def error(self, doc):
         err, idx = ctypes.c_int32(), ctypes.c_int32()

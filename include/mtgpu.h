@@ -572,7 +572,7 @@ mt_status mt_comm_barrier(mt_comm* comm);
  *   ClientSequenceNumberManager          deli/clientSeqManager.ts:70-143 (upsert/remove/min refSeq)
  *   new DeliLambda(.., lastCheckpoint)   lambda.ts:112-171 (clients + sequenceNumber from IDeliState)
  * Raw messages arrive grouped by document (CSR row_ptr, each document's messages in log order);
- * client ids are per-document short ids 0..63 interned by the host (the reference keys clients by
+ * client ids are per-document short ids 0..511 interned by the host (the reference keys clients by
  * their long id string).  One output ticket per raw message.  Out of scope: branch Integrate
  * messages, idle-client eviction and NoClient/idle timers (they only enqueue new raw messages back
  * to the ordering service, which a host feeds in as MT_RAW_LEAVE / MT_RAW_SERVER_NOOP), summarize
@@ -591,7 +591,8 @@ typedef enum mt_raw_kind {
 typedef struct mt_raw_msg {  /* 16 bytes */
     int32_t csn;             /* operation.clientSequenceNumber                                     */
     int32_t ref_seq;         /* operation.referenceSequenceNumber; -1 = REST op (revved to its seq) */
-    uint16_t client;         /* short id of the sending client, or of the joiner / leaver (< 64)   */
+    uint16_t client;         /* short id of the sending client, or of the joiner / leaver
+                                (< MT_DELI_MAX_CLIENTS)                                              */
     uint8_t kind;            /* mt_raw_kind                                                        */
     uint8_t pad;
     uint32_t op_index;       /* fused hand-off (mt_deli_ticket_device with d_ops): 1 + index of the op
@@ -618,10 +619,17 @@ typedef struct mt_ticket {  /* 16 bytes */
     uint8_t pad[3];
 } mt_ticket;
 
+/* Client ids: a document holds short ids 0..MT_DELI_MAX_CLIENTS-1.  Up to id 63 it is ticketed eight
+ * documents per wave; its first message from a client >= 64 promotes it, for good, to the wide form
+ * (one document per wave, its clients in a row of the deli's big pool: one row per 16 documents of
+ * max_docs, at least 64; mt_deli_restore_all empties the pool).  The reference keeps a Map and a heap
+ * (clientSeqManager.ts:70-143, joins at lambda.ts:280-306): no limit. */
+#define MT_DELI_MAX_CLIENTS 512
+
 /* per-document sticky deli errors (the reference lambda throws / has no representation) */
 typedef enum mt_deli_err {
     MT_DELI_OK = 0,
-    MT_DELI_ERR_CLIENT = 1, /* short client id >= MT_MAX_CLIENTS                                    */
+    MT_DELI_ERR_CLIENT = 1, /* short client id >= MT_DELI_MAX_CLIENTS, or no big-pool row left      */
     MT_DELI_ERR_KIND = 2,   /* unknown mt_raw_kind                                                  */
     MT_DELI_ERR_ASSERT = 3  /* assert(refSeq >= msn) lambda.ts:426-428 (a client no-op with ref -1) */
 } mt_deli_err;
@@ -677,7 +685,9 @@ mt_status mt_deli_raw_stream(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t
 mt_status mt_deli_sync(mt_deli* dl);
 /* Kernel time of the last mt_deli_ticket / mt_deli_ticket_device (HIP events around the launch). */
 mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms);
-mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);
+mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);  /* (clients < 64) */
+/* clients [first, first + n) of a document (any id < MT_DELI_MAX_CLIENTS; not joined: zeros) */
+mt_status mt_deli_get_clients(mt_deli* dl, uint32_t doc, uint32_t first, uint32_t n, mt_deli_client* out);
 /* err = mt_deli_err, index = position of the failing message inside the document's stream */
 mt_status mt_deli_doc_error(mt_deli* dl, uint32_t doc, int32_t* err, int32_t* index);
 

@@ -9,7 +9,8 @@
 // (DeliLambda.ticket, lambda.ts:255-544) and returns, per message in queue order, what the
 // lambda would have produced: a sequenced message (sequenceNumber, minimumSequenceNumber,
 // referenceSequenceNumber) and whether it is sent now / later / never, a nack with its reason,
-// or nothing (a dropped duplicate).  Client ids are interned per document (short ids < 64).
+// or nothing (a dropped duplicate).  Client ids are interned per document (short ids < 512: include/
+// mtgpu.h MT_DELI_MAX_CLIENTS; past 63 the document is ticketed by the engine's wide form).
 const path = require("path");
 
 const native = require(path.join(__dirname, "mtgpu.node"));
@@ -17,7 +18,7 @@ const native = require(path.join(__dirname, "mtgpu.node"));
 const OP = 0, NOOP = 1, NOOP_DATA = 2, JOIN = 3, LEAVE = 4, SERVER_NOOP = 5, NOCLIENT = 6, CONTROL = 7;
 const STATUS = ["dropped", "sent", "later", "never", "nack", "nack", "nack", "halted"];
 const NACK_REASON = { 4: "Gap detected in incoming op", 5: "Nonexistent client", 6: "Refseq below msn" };
-const MAX_CLIENTS = 64;
+const MAX_CLIENTS = 512;  // include/mtgpu.h MT_DELI_MAX_CLIENTS
 const REC = 16;
 
 class DeliSequencer {
@@ -26,7 +27,7 @@ class DeliSequencer {
         this.handle = native.createDeli({ device: opts.device || 0, maxDocs: this.maxDocs });
         this.ids = Array.from({ length: this.maxDocs }, () => new Map());  // long client id -> short
         // short ids given back by processed leaves, reused before new ones (Fluid gives every
-        // connection a new client id, so a long-lived document sees far more than 64 of them)
+        // connection a new client id, so a long-lived document sees far more than 512 of them)
         this.free = Array.from({ length: this.maxDocs }, () => []);
         this.next = new Uint32Array(this.maxDocs);
         this.queues = Array.from({ length: this.maxDocs }, () => []);

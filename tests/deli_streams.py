@@ -66,7 +66,7 @@ def random_stream(rng, n_msgs, n_clients=12, p_assert=0.0, wide=False):
     for _ in range(n_msgs):
         r = rng.random()
         if wide and rng.random() < 0.01:
-            m = (od.OP, 64 + rng.randrange(8), 1, shadow.seq)
+            m = (od.OP, od.MAX_CLIENTS + rng.randrange(8), 1, shadow.seq)
         elif r < 0.08:
             m = (od.JOIN, rng.choice(pool), -1, -1)
         elif r < 0.12:

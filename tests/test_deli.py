@@ -77,4 +77,4 @@ def test_errors_are_sticky():
     assert (d.err, d.err_at) == (od.ERR_ASSERT, 1)
     assert d.ticket(od.OP, 3, 1, 0)[3] == od.HALTED
     e = od.DeliDoc()
-    assert e.ticket(od.OP, 70, 1, 0)[3] == od.HALTED and e.err == od.ERR_CLIENT
+    assert e.ticket(od.OP, od.MAX_CLIENTS + 6, 1, 0)[3] == od.HALTED and e.err == od.ERR_CLIENT

@@ -70,6 +70,62 @@ def test_batches_continue_the_state():
         assert np.array_equal(got, want[rp[d]:rp[d + 1]]), d
 
 
+@pytest.mark.parametrize('seed,n_clients,n_msgs', [(11, 96, 1500), (12, 300, 2500)])
+def test_documents_past_64_clients_against_oracle(seed, n_clients, n_msgs):
+    """Documents whose joined clients pass 63 (96, 300 client ids): their first message from a client
+    >= 64 promotes them to the wide form (one document per wave, 512 clients), mid-stream; tickets and
+    checkpoints (every client) equal the restatement's, in one launch and in two (the promotion and
+    the big-pool state carry across calls)."""
+    streams = random_streams(48, n_msgs, seed=seed, n_clients=n_clients)
+    streams[1] = []
+    want, docs = oracle_tickets(streams)
+    assert max(c for s in streams for (_, c, _, _) in s) >= 64
+    dl = _seq(len(streams))
+    got = _tickets(dl.ticket(*to_batch(streams)))
+    bad = np.nonzero(np.any(got != want, axis=1))[0]
+    assert not len(bad), f'{len(bad)} tickets differ, first {int(bad[0])}: got {got[bad[0]]} want {want[bad[0]]}'
+    for d in range(len(streams)):
+        ck, o = dl.checkpoint(d), docs[d].checkpoint()
+        assert (ck['seq'], ck['msn'], ck['last_sent_msn'], ck['err']) == (o['seq'], o['msn'], o['last_sent_msn'],
+                                                                         o['err']), d
+        assert ck['clients'] == o['clients'], d
+    # the same streams in two launches
+    dl2 = _seq(len(streams))
+    a = [s[:len(s) // 3] for s in streams]
+    b = [s[len(s) // 3:] for s in streams]
+    ta, tb = _tickets(dl2.ticket(*to_batch(a))), _tickets(dl2.ticket(*to_batch(b)))
+    _, rp = to_batch(streams)
+    _, rp_a = to_batch(a)
+    _, rp_b = to_batch(b)
+    for d in range(len(streams)):
+        two = np.concatenate([ta[rp_a[d]:rp_a[d + 1]], tb[rp_b[d]:rp_b[d + 1]]])
+        assert np.array_equal(two, want[rp[d]:rp[d + 1]]), d
+        assert dl2.checkpoint(d)['clients'] == docs[d].checkpoint()['clients'], d
+
+
+def test_big_pool_exhausted_halts_the_document():
+    """The big pool holds max(64, max_docs / 16) documents past client 63: with 80 such documents the
+    80 - 64 promoted last halt at the message that needed a row (MT_DELI_ERR_CLIENT, the rest of
+    their tickets HALTED); the others are ticketed as the restatement does."""
+    streams = []
+    for d in range(80):
+        s = [(od.JOIN, c, -1, -1) for c in range(60, 70)] + [(od.OP, 65, 1, 10), (od.OP, 61, 1, 11)]
+        streams.append(s)
+    want, _ = oracle_tickets(streams)
+    dl = _seq(len(streams))
+    got = _tickets(dl.ticket(*to_batch(streams)))
+    _, rp = to_batch(streams)
+    halted = [d for d in range(80) if dl.error(d)[0]]
+    assert len(halted) == 16, halted
+    for d in range(80):
+        g, w = got[rp[d]:rp[d + 1]], want[rp[d]:rp[d + 1]]
+        if d in halted:
+            assert dl.error(d) == (od.ERR_CLIENT, 4)  # the join of client 64
+            assert np.array_equal(g[:4], w[:4]) and np.all(g[4:, 3] == od.HALTED), d
+        else:
+            assert np.array_equal(g, w), d
+
+
 def test_restore_from_checkpoints():
     streams = random_streams(32, 400, seed=21, n_clients=30)
     cks = []

@@ -73,7 +73,7 @@ MT_DEV LocRow loc_row(const mt_gstate& g, uint32_t d) {
 }
 
 // W: a wide document (include/mtgpu.h "limits"): per slot also the overlap ids >= 64 (ovx) and the
-// property words ph / pxl / pxh (u16 value ids, keys 8..15); UTF-16 text.  GW: (LOC) group-mask
+// property words ph / pxl / pxh / pxx (u16 value ids, keys 8..31); UTF-16 text.  GW: (LOC) group-mask
 // words per slot, 64 GW pending edits at most (GW > 1: MT_WIDE_GROUPS documents, HBM workspace only)
 template <int CAP, bool LOC = false, bool W = false, int GW = 1>
 struct Lds {
@@ -117,6 +117,7 @@ struct Lds {
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
     uint64_t pxh[W ? CAP : 1];
+    uint64_t pxx[W ? 4 * CAP : 1];  // keys 16..31: [slot][4] (mt_state.h pxx)
     uint32_t wide;                // the document's mt_doc_scalars.wide bits
     uint32_t lkeys;               // its declared label keys (mt_doc_scalars.label_keys)
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
@@ -192,7 +193,7 @@ struct Wave {
             uint64_t* x = &s.ovx[MT_OVX_WORDS * slot];
             if (mt_ovx_has(x, (uint32_t)C)) return true;
             if (mt_ovx_id(x, MT_OVX_IDS - 1)) return false;  // full: MT_DERR_LIMITS
-            uint64_t out[MT_OVX_WORDS] = {0, 0, 0, 0};  // insert C into the ascending u16 list
+            uint64_t out[MT_OVX_WORDS] = {};  // insert C into the ascending u16 list
             int j = 0;
             bool done = false;
             auto put = [&](uint32_t v) {
@@ -214,31 +215,38 @@ struct Wave {
         }
         return false;
     }
+    // (W) the words holding key k of a slot: its low-byte and high-byte words
+    MT_DEV uint64_t* plo(int sl, int k) {
+        return k < 8 ? &s.props[sl] : k < 16 ? &s.pxl[sl] : &s.pxx[4 * sl + 2 * ((k - 16) >> 3)];
+    }
+    MT_DEV uint64_t* phi(int sl, int k) {
+        return k < 8 ? &s.ph[sl] : k < 16 ? &s.pxh[sl] : &s.pxx[4 * sl + 2 * ((k - 16) >> 3) + 1];
+    }
     // value id of key k of a slot (0 = absent)
-    MT_DEV uint32_t pval(int sl, int k) const {
+    MT_DEV uint32_t pval(int sl, int k) {
         const int sh = 8 * (k & 7);
-        if constexpr (W) {
-            const uint64_t lo = k < 8 ? s.props[sl] : s.pxl[sl], hi = k < 8 ? s.ph[sl] : s.pxh[sl];
-            return (uint32_t)((lo >> sh) & 0xFFu) | ((uint32_t)((hi >> sh) & 0xFFu) << 8);
-        }
+        if constexpr (W)
+            return (uint32_t)((*plo(sl, k) >> sh) & 0xFFu) | ((uint32_t)((*phi(sl, k) >> sh) & 0xFFu) << 8);
         return k < 8 ? (uint32_t)((s.props[sl] >> sh) & 0xFFu) : 0u;
     }
     MT_DEV void pset(int sl, int k, uint32_t v) {
         const int sh = 8 * (k & 7);
         const uint64_t m = ~(0xFFull << sh);
-        if (k < 8) s.props[sl] = (s.props[sl] & m) | ((uint64_t)(v & 0xFFu) << sh);
         if constexpr (W) {
-            if (k < 8) {
-                s.ph[sl] = (s.ph[sl] & m) | ((uint64_t)(v >> 8) << sh);
-            } else {
-                s.pxl[sl] = (s.pxl[sl] & m) | ((uint64_t)(v & 0xFFu) << sh);
-                s.pxh[sl] = (s.pxh[sl] & m) | ((uint64_t)(v >> 8) << sh);
-            }
+            uint64_t* lo = plo(sl, k);
+            uint64_t* hi = phi(sl, k);
+            *lo = (*lo & m) | ((uint64_t)(v & 0xFFu) << sh);
+            *hi = (*hi & m) | ((uint64_t)(v >> 8) << sh);
+        } else if (k < 8) {
+            s.props[sl] = (s.props[sl] & m) | ((uint64_t)(v & 0xFFu) << sh);
         }
     }
     MT_DEV void pclear(int sl) {
         s.props[sl] = 0;
-        if constexpr (W) s.ph[sl] = s.pxl[sl] = s.pxh[sl] = 0;
+        if constexpr (W) {
+            s.ph[sl] = s.pxl[sl] = s.pxh[sl] = 0;
+            for (int q = 0; q < 4; q++) s.pxx[4 * sl + q] = 0;
+        }
     }
     MT_DEV void pcopy(int dst, int src) {
         s.props[dst] = s.props[src];
@@ -246,11 +254,16 @@ struct Wave {
             s.ph[dst] = s.ph[src];
             s.pxl[dst] = s.pxl[src];
             s.pxh[dst] = s.pxh[src];
+            for (int q = 0; q < 4; q++) s.pxx[4 * dst + q] = s.pxx[4 * src + q];
         }
     }
     MT_DEV bool peq(int a, int b) const {
         if (s.props[a] != s.props[b]) return false;
-        if constexpr (W) return s.ph[a] == s.ph[b] && s.pxl[a] == s.pxl[b] && s.pxh[a] == s.pxh[b];
+        if constexpr (W) {
+            if (s.ph[a] != s.ph[b] || s.pxl[a] != s.pxl[b] || s.pxh[a] != s.pxh[b]) return false;
+            for (int q = 0; q < 4; q++)
+                if (s.pxx[4 * a + q] != s.pxx[4 * b + q]) return false;
+        }
         return true;
     }
     // the op's (key, value) pairs onto a slot's props (properties.ts:95-116)
@@ -337,7 +350,7 @@ struct Wave {
             uint32_t ln = 0;
             uint32_t pm = 0;
             uint8_t xf = 0;
-            uint16_t pv[16] = {0};
+            uint16_t pv[kKeys] = {0};
             int sl = 0;
             if (i < n) {
                 sl = s.order[i];
@@ -388,11 +401,11 @@ struct Wave {
                 e.seq = s.evseq;
                 e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
                 e.flags = (uint8_t)((idx == 0 ? MT_EVF_FIRST : 0) | xf);
-                e.pmask = (uint16_t)pm;
+                e.pmask = pm;
                 e.leaf = i;
                 e.pos = lpos + incl - ll;
                 e.len = ln;
-                for (int k = 0; k < 16; k++) e.pvals[k] = (pm >> k) & 1u ? pv[k] : (uint16_t)0;
+                for (int k = 0; k < kKeys; k++) e.pvals[k] = (pm >> k) & 1u ? pv[k] : (uint16_t)0;
                 ev[e0 + idx] = e;
             }
             cnt += __popcll(m);
@@ -1809,6 +1822,7 @@ struct Wave {
                 s.ph[i] = was_wide ? g.ph[so + i] : 0ull;
                 s.pxl[i] = was_wide ? g.pxl[so + i] : 0ull;
                 s.pxh[i] = was_wide ? g.pxh[so + i] : 0ull;
+                for (int q = 0; q < 4; q++) s.pxx[4 * i + q] = was_wide ? g.pxx[4 * (so + i) + q] : 0ull;
             }
         }
         if (lane == 0) {
@@ -1992,6 +2006,7 @@ struct Wave {
                 g.ph[so + i] = s.ph[sl];
                 g.pxl[so + i] = s.pxl[sl];
                 g.pxh[so + i] = s.pxh[sl];
+                for (int q = 0; q < 4; q++) g.pxx[4 * (so + i) + q] = s.pxx[4 * sl + q];
             }
         }
         if constexpr (LOC) {

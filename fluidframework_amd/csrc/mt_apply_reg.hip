@@ -64,12 +64,12 @@ typedef const MT_KARG mt_gstate KGState;
 typedef uint32_t EvWords __attribute__((ext_vector_type(4)));
 // one 64-byte event row through a global pointer: four 16-byte stores
 MT_DEV void put_event(MT_GLOB mt_event* p, const mt_event& e) {
-    static_assert(sizeof(mt_event) == 64, "mt_event");
-    EvWords w[4];
+    static_assert(sizeof(mt_event) == 96, "mt_event");
+    EvWords w[6];
     __builtin_memcpy(w, &e, sizeof w);
     MT_GLOB EvWords* q = reinterpret_cast<MT_GLOB EvWords*>(p);
 #pragma unroll
-    for (int i = 0; i < 4; i++) q[i] = w[i];
+    for (int i = 0; i < 6; i++) q[i] = w[i];
 }
 
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -404,7 +404,7 @@ struct RWave {
 #pragma unroll
                         for (int k = 0; k < 8; k++) oldnz |= ((old >> (8 * k)) & 0xFFu) ? (1u << k) : 0u;
                         const uint32_t pm = okeys | (rewrite ? (oldnz & ~onz) : 0u);
-                        e.pmask = (uint16_t)pm;
+                        e.pmask = pm;
 #pragma unroll
                         for (int k = 0; k < 8; k++) {
                             const uint32_t ov = (uint32_t)(old >> (8 * k)) & 0xFFu;

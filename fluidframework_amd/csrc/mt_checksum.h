@@ -27,15 +27,22 @@ MT_HD static inline uint64_t mt_seg_hash(uint64_t idx, uint64_t text_hash, int32
 // The overlap term: the ids < 64 as a bitmask; a wide document's ids >= 64 hashed in (mt_ovx_hash:
 // up to eight ids below 256 as their ascending byte list -- round 3's form, so earlier fixtures keep
 // their checksums -- any other list folded id by id).  The props term: the low bytes of the value ids of keys 0..7 (the
-// narrow u64); a wide document's high bytes (hi) and keys 8..15 (xlo, xhi) hashed in.  Both are the
-// narrow word itself whenever the wide part is empty.
+// narrow u64); a wide document's high bytes (hi) and keys 8..15 (xlo, xhi) hashed in, then keys
+// 16..31 (the four pxx words) when any is set.  Both are the narrow word itself whenever the wide
+// part is empty, and a document without keys >= 16 keeps its round-4 checksum.
 MT_HD static inline uint64_t mt_ovl_term(uint64_t mask, uint64_t ovx) {
     return ovx ? mask ^ mt_mix64(ovx ^ 0x4F56584944530000ull) : mask;
 }
-MT_HD static inline uint64_t mt_props_term(uint64_t lo, uint64_t hi, uint64_t xlo, uint64_t xhi) {
-    if (!(hi | xlo | xhi)) return lo;
-    return lo ^ mt_mix64(mt_mix64(hi ^ 0x1111111111111111ull) ^ mt_mix64(xlo ^ 0x2222222222222222ull) ^
-                         mt_mix64(xhi ^ 0x3333333333333333ull));
+MT_HD static inline uint64_t mt_props_term(uint64_t lo, uint64_t hi, uint64_t xlo, uint64_t xhi,
+                                           const uint64_t* y = nullptr) {
+    uint64_t t = lo;
+    if (hi | xlo | xhi)
+        t ^= mt_mix64(mt_mix64(hi ^ 0x1111111111111111ull) ^ mt_mix64(xlo ^ 0x2222222222222222ull) ^
+                      mt_mix64(xhi ^ 0x3333333333333333ull));
+    if (y && (y[0] | y[1] | y[2] | y[3]))
+        t ^= mt_mix64(mt_mix64(y[0] ^ 0x4444444444444444ull) ^ mt_mix64(y[1] ^ 0x5555555555555555ull) ^
+                      mt_mix64(y[2] ^ 0x6666666666666666ull) ^ mt_mix64(y[3] ^ 0x7777777777777777ull));
+    return t;
 }
 // canonical client id of a stored short id: NonCollabClient (snapshot loads) is -2
 MT_HD static inline int32_t mt_canon_client(uint32_t c) { return c == 0xFEu ? -2 : (int32_t)c; }
@@ -50,24 +57,43 @@ MT_HD static inline uint64_t mt_finish_checksum(uint64_t seg_sum, uint64_t tree_
 }
 
 // ---- readers of a document's HBM state, narrow or wide (mt_state.h) ------------------------------
+// the two words (low bytes, high bytes) holding key k's value id of a wide segment at HBM index i
+MT_HD static inline void mt_gpwords(const mt_gstate& g, size_t i, int k, uint64_t& lo, uint64_t& hi) {
+    if (k < 8) {
+        lo = g.props[i];
+        hi = g.ph[i];
+    } else if (k < 16) {
+        lo = g.pxl[i];
+        hi = g.pxh[i];
+    } else {
+        const uint64_t* y = g.pxx + 4 * i + 2 * ((k - 16) >> 3);
+        lo = y[0];
+        hi = y[1];
+    }
+}
 // segment at HBM index i (= doc * segcap + position): value id of key k
 MT_HD static inline uint32_t mt_gprop(const mt_gstate& g, bool wide, size_t i, int k) {
     const int sh = 8 * (k & 7);
     if (!wide) return k < 8 ? (uint32_t)((g.props[i] >> sh) & 0xFFu) : 0u;
-    const uint64_t lo = k < 8 ? g.props[i] : g.pxl[i], hi = k < 8 ? g.ph[i] : g.pxh[i];
+    uint64_t lo, hi;
+    mt_gpwords(g, i, k, lo, hi);
     return (uint32_t)((lo >> sh) & 0xFFu) | ((uint32_t)((hi >> sh) & 0xFFu) << 8);
 }
 // matchProperties' value comparison of two segments (properties.ts:62-93)
 MT_HD static inline bool mt_gprops_eq(const mt_gstate& g, bool wide, size_t a, size_t b) {
     if (g.props[a] != g.props[b]) return false;
-    return !wide || (g.ph[a] == g.ph[b] && g.pxl[a] == g.pxl[b] && g.pxh[a] == g.pxh[b]);
+    if (!wide) return true;
+    if (g.ph[a] != g.ph[b] || g.pxl[a] != g.pxl[b] || g.pxh[a] != g.pxh[b]) return false;
+    for (int q = 0; q < 4; q++)
+        if (g.pxx[4 * a + q] != g.pxx[4 * b + q]) return false;
+    return true;
 }
 MT_HD static inline uint64_t mt_gprops_term(const mt_gstate& g, bool wide, size_t i) {
-    return wide ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i]) : g.props[i];
+    return wide ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i], g.pxx + 4 * i) : g.props[i];
 }
-// A wide segment's overlapping removers >= 64: up to MT_OVX_IDS (16) u16 ids, ascending from the low
-// half-word of x[0], 0 = none (mt_state.h ovx, four words per segment)
-#define MT_OVX_WORDS 4
+// A wide segment's overlapping removers >= 64: up to MT_OVX_IDS (32) u16 ids, ascending from the low
+// half-word of x[0], 0 = none (mt_state.h ovx, MT_OVX_WORDS words per segment)
+#define MT_OVX_WORDS 8
 MT_HD static inline uint32_t mt_ovx_id(const uint64_t* x, int q) {
     return (uint32_t)(x[q >> 2] >> (16 * (q & 3))) & 0xFFFFu;
 }

@@ -230,7 +230,8 @@ static mt_status ensure_wide(mt_engine* e) {
     mt_gstate& g = e->g;
     mt_status st = MT_OK;
     if ((st = dalloc(e, &g.ph, S)) || (st = dalloc(e, &g.pxl, S)) || (st = dalloc(e, &g.pxh, S)) ||
-        (st = dalloc(e, &g.chi, S)) || (st = dalloc(e, &g.ovx, S * MT_OVX_WORDS))) {
+        (st = dalloc(e, &g.pxx, S * 4)) || (st = dalloc(e, &g.chi, S)) ||
+        (st = dalloc(e, &g.ovx, S * MT_OVX_WORDS))) {
         g.ovx = nullptr;  // (the kernels test ovx; the others are freed with the engine)
         return st;
     }
@@ -410,7 +411,7 @@ static bool wide_load_seg(const mt_load_seg& sg) {
     if ((sg.flags & MT_LSF_U16) || (seg_client(sg) >= MT_MAX_CLIENTS && seg_client(sg) != MT_CLIENT_NONCOLLAB) ||
         (sg.rseq >= 0 && seg_rclient(sg) >= MT_MAX_CLIENTS))
         return true;
-    for (int k = 0; k < 16; k++)
+    for (int k = 0; k < MT_MAX_KEYS_WIDE; k++)
         if ((sg.flags & MT_SF_PDEF) && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255)) return true;
     return false;
 }
@@ -600,7 +601,7 @@ mt_status mt_set_label_keys(mt_engine* e, uint32_t doc, int tile_key, int range_
 mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const uint32_t* seg_row_ptr,
                        const mt_load_seg* segs, const uint8_t* text, uint64_t text_bytes, const int32_t* min_seq,
                        const int32_t* cur_seq) {
-    static_assert(sizeof(mt_load_seg) == 64, "mt_load_seg is 64 bytes");
+    static_assert(sizeof(mt_load_seg) == 96, "mt_load_seg is 96 bytes");
     if (!e || (n && (!doc_ids || !seg_row_ptr || !min_seq || !cur_seq))) return MT_ERR_ARG;
     if (n == 0) return MT_OK;
     const uint64_t n_segs = seg_row_ptr[n] - seg_row_ptr[0];
@@ -709,7 +710,7 @@ mt_status mt_resolve_positions_device(mt_engine* e, const mt_pos_query* d_q, uin
 }
 
 mt_status mt_segment_infos(mt_engine* e, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out) {
-    static_assert(sizeof(mt_seg_info) == 104, "mt_seg_info is 104 bytes");
+    static_assert(sizeof(mt_seg_info) == 168, "mt_seg_info is 168 bytes");
     if (!e || (n && (!docs || !ordinals || !out))) return MT_ERR_ARG;
     for (uint32_t i = 0; i < n; i++)
         if (docs[i] >= e->n_docs) return MT_ERR_ARG;
@@ -793,7 +794,7 @@ mt_status mt_range_stacks(mt_engine* e, const mt_tile_query* q, uint32_t n, uint
 }
 
 mt_status mt_events_enable(mt_engine* e, uint32_t per_doc) {
-    static_assert(sizeof(mt_event) == 64, "mt_event is 64 bytes");
+    static_assert(sizeof(mt_event) == 96, "mt_event is 96 bytes");
     if (!e) return MT_ERR_ARG;
     HIP_OK(hipSetDevice(e->cfg.device));
     HIP_OK(hipStreamSynchronize(e->stream));
@@ -1738,7 +1739,7 @@ struct HostDoc {
     bool wide = false;
     std::vector<int32_t> seq, rseq;
     std::vector<uint32_t> len, toff;
-    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
+    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh, pxx;
     std::vector<uint8_t> client, rclient, flags;
     std::vector<uint16_t> chi;                 // (wide) the short ids' high bytes
     std::vector<uint16_t> text;                // the arena's current half, in code units
@@ -1746,7 +1747,8 @@ struct HostDoc {
     uint32_t prop(int i, int k) const {
         const int sh = 8 * (k & 7);
         if (!wide) return k < 8 ? (uint32_t)((props[i] >> sh) & 0xFF) : 0u;
-        const uint64_t lo = k < 8 ? props[i] : pxl[i], hi = k < 8 ? ph[i] : pxh[i];
+        const uint64_t lo = k < 8 ? props[i] : k < 16 ? pxl[i] : pxx[4 * (size_t)i + 2 * ((k - 16) >> 3)];
+        const uint64_t hi = k < 8 ? ph[i] : k < 16 ? pxh[i] : pxx[4 * (size_t)i + 2 * ((k - 16) >> 3) + 1];
         return (uint32_t)((lo >> sh) & 0xFF) | ((uint32_t)((hi >> sh) & 0xFF) << 8);
     }
     std::vector<int> overlap(int i) const {
@@ -1810,6 +1812,7 @@ mt_status read_doc(mt_engine* e, uint32_t d, HostDoc& h) {
         HIP_OK(fetch(h.ph, g.ph, so, n, e->stream));
         HIP_OK(fetch(h.pxl, g.pxl, so, n, e->stream));
         HIP_OK(fetch(h.pxh, g.pxh, so, n, e->stream));
+        HIP_OK(fetch(h.pxx, g.pxx, so * 4, n * 4, e->stream));
     }
     HIP_OK(fetch(h.client, g.client, so, n, e->stream));
     HIP_OK(fetch(h.rclient, g.rclient, so, n, e->stream));
@@ -2018,7 +2021,7 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
     const size_t S = (size_t)n * g.segcap, so = (size_t)d0 * g.segcap;
     std::vector<int32_t> seq, rseq;
     std::vector<uint32_t> len, toff;
-    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh;
+    std::vector<uint64_t> ovl, props, ovx, ph, pxl, pxh, pxx;
     std::vector<uint8_t> client, rclient, flags, lb, ib;
     std::vector<uint16_t> chi;
     bool any_wide = false;
@@ -2035,6 +2038,7 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
         HIP_OK(fetch(ph, g.ph, so, S, e->stream));
         HIP_OK(fetch(pxl, g.pxl, so, S, e->stream));
         HIP_OK(fetch(pxh, g.pxh, so, S, e->stream));
+        HIP_OK(fetch(pxx, g.pxx, so * 4, S * 4, e->stream));
     }
     HIP_OK(fetch(client, g.client, so, S, e->stream));
     HIP_OK(fetch(rclient, g.rclient, so, S, e->stream));
@@ -2062,6 +2066,7 @@ mt_status read_range(mt_engine* e, uint32_t d0, uint32_t n, std::vector<HostDoc>
             h.ph.assign(ph.begin() + a, ph.begin() + a + m);
             h.pxl.assign(pxl.begin() + a, pxl.begin() + a + m);
             h.pxh.assign(pxh.begin() + a, pxh.begin() + a + m);
+            h.pxx.assign(pxx.begin() + a * 4, pxx.begin() + (a + m) * 4);
         }
         h.client.assign(client.begin() + a, client.begin() + a + m);
         h.rclient.assign(rclient.begin() + a, rclient.begin() + a + m);

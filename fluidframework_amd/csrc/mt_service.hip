@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
     const size_t so = (size_t)d * g.segcap;
     uint8_t* arena = g.text + (size_t)d * 2 * g.textcap;  // half 0
     // a document with any segment beyond the narrow limits loads in the wide form (UTF-16 text,
-    // u16 value ids, keys < 16, client ids >= 64; include/mtgpu.h "limits")
+    // u16 value ids, keys < 32, client ids >= 64; include/mtgpu.h "limits")
     bool wdoc = false, lds = false;
     for (int base = 0; base < ns; base += 64) {
         const int i = base + lane;
@@ -94,7 +94,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             const uint32_t c = sg.client | ((uint32_t)sg.client_hi << 8), rc = sg.rclient | ((uint32_t)sg.rclient_hi << 8);
             w = (sg.flags & MT_LSF_U16) || (c >= MT_MAX_CLIENTS && c != MT_CLIENT_NONCOLLAB) ||
                 (sg.rseq >= 0 && rc >= MT_MAX_CLIENTS);
-            for (int k = 0; k < 16; k++) w = w || (pdef && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255));
+            for (int k = 0; k < MT_MAX_KEYS_WIDE; k++)
+                w = w || (pdef && (k >= MT_MAX_KEYS ? sg.props[k] != 0 : sg.props[k] > 255));
             l32 = (c > 32 && c != MT_CLIENT_NONCOLLAB) || (sg.rseq >= 0 && rc > 32);
         }
         wdoc = wdoc || wave_ballot(w) != 0;
@@ -132,8 +133,8 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             uint8_t fl = (uint8_t)((rm ? MT_SF_REMOVED : 0u) | (sg.flags & (MT_SF_PDEF | MT_SF_MARKER)) |
                                    (nl && !mk ? MT_SF_HASNL : 0u));
             if (!mk && l && unit(l - 1) == '\n') fl |= MT_SF_NL;
-            uint64_t w4[4] = {0, 0, 0, 0};  // props as the narrow word + the wide words
-            for (int k = 0; k < 16; k++) {
+            uint64_t w4[8] = {};  // props as the narrow word + the wide words (keys 0..31: lo, hi per 8)
+            for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) {
                 w4[(k >> 3) * 2] |= (uint64_t)(sg.props[k] & 0xFFu) << (8 * (k & 7));
                 w4[(k >> 3) * 2 + 1] |= (uint64_t)(sg.props[k] >> 8) << (8 * (k & 7));
             }
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
                 g.ph[so + i] = w4[1];
                 g.pxl[so + i] = w4[2];
                 g.pxh[so + i] = w4[3];
+                for (int q = 0; q < 4; q++) g.pxx[4 * (so + i) + q] = w4[4 + q];
             }
             g.client[so + i] = sg.client;
             g.rclient[so + i] = rm ? sg.rclient : 0;
@@ -709,15 +711,7 @@ __global__ void mt_seginfo_kernel(mt_gstate g, const uint32_t* __restrict__ docs
         r.wide = wdoc ? 1u : 0u;
         r.overlap = g.ovl[so];
         for (int q = 0; q < MT_OVX_IDS; q++) r.overlap_hi[q] = wdoc ? (uint16_t)mt_ovx_id(g.ovx + MT_OVX_WORDS * so, q) : 0;
-        const uint64_t p = g.props[so];
-        for (int k = 0; k < 8; k++) {
-            uint32_t v = (uint32_t)(p >> (8 * k)) & 0xFFu;
-            if (wdoc) v |= ((uint32_t)(g.ph[so] >> (8 * k)) & 0xFFu) << 8;
-            r.props[k] = (uint16_t)v;
-            if (wdoc)
-                r.props[8 + k] = (uint16_t)(((uint32_t)(g.pxl[so] >> (8 * k)) & 0xFFu) |
-                                            (((uint32_t)(g.pxh[so] >> (8 * k)) & 0xFFu) << 8));
-        }
+        for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) r.props[k] = (uint16_t)mt_gprop(g, wdoc, so, k);
     }
     out[w] = r;
 }

@@ -96,16 +96,18 @@ struct mt_gstate {
     uint64_t* ovl;     // removedClientOverlap as a bitmask over short client ids < 64
     uint64_t* props;   // 8 keys x u8 value id (a wide document: the low bytes of keys 0..7's u16 ids)
     // a wide document's extra state (MT_WIDE_DOC; [doc][segcap], allocated on first need, else null):
-    // ovx = its overlapping removers >= 64 ([doc][segcap][4]: up to MT_OVX_IDS u16 ids ascending from
-    // the low half-word of word 0, 0 = none); chi = the high bytes of its short client ids (client's
-    // in bits 0..7, removedClient's in 8..15); ph = the high bytes of keys 0..7's value ids; pxl / pxh
-    // = keys 8..15, low / high bytes.
+    // ovx = its overlapping removers >= 64 ([doc][segcap][MT_OVX_WORDS]: up to MT_OVX_IDS u16 ids
+    // ascending from the low half-word of word 0, 0 = none); chi = the high bytes of its short client
+    // ids (client's in bits 0..7, removedClient's in 8..15); ph = the high bytes of keys 0..7's value
+    // ids; pxl / pxh = keys 8..15, low / high bytes; pxx = keys 16..31 ([doc][segcap][4]: keys 16..23
+    // low, high bytes, keys 24..31 low, high bytes).
     // Its text arena holds UTF-16 code units (2 bytes each; toff / len / text_top in units).
     uint64_t* ovx;
     uint16_t* chi;
     uint64_t* ph;
     uint64_t* pxl;
     uint64_t* pxh;
+    uint64_t* pxx;
     uint32_t* slab;    // [doc][segcap] a stale marker's cached label value ids: tile key (low 16 bits),
                        // range key (high 16) -- allocated on the first mt_set_label_keys, else null
     uint32_t* slabx;   // [doc][segcap] the editing form's slot-indexed slab during a launch (its LDS

@@ -14,9 +14,9 @@ operation = MergeTreeDeltaType (INSERT 0, REMOVE 1, ANNOTATE 2) or MergeTreeMain
 """
 import numpy as np
 
-EVENT_DTYPE = np.dtype([('seq', '<i4'), ('op', 'i1'), ('flags', 'u1'), ('pmask', '<u2'), ('leaf', '<i4'),
-                        ('pos', '<i4'), ('len', '<u4'), ('pad', '<u4'), ('pvals', '<u2', (16,)), ('pad2', '<u8')])
-assert EVENT_DTYPE.itemsize == 64
+EVENT_DTYPE = np.dtype([('seq', '<i4'), ('op', 'i1'), ('flags', 'u1'), ('pad', '<u2'), ('leaf', '<i4'),
+                        ('pos', '<i4'), ('len', '<u4'), ('pmask', '<u4'), ('pvals', '<u2', (32,)), ('pad2', '<u8')])
+assert EVENT_DTYPE.itemsize == 96
 
 EV_INSERT, EV_REMOVE, EV_ANNOTATE = 0, 1, 2
 EV_APPEND, EV_SPLIT, EV_UNLINK = -1, -2, -3
@@ -28,7 +28,7 @@ OP_NAMES = {EV_INSERT: 'INSERT', EV_REMOVE: 'REMOVE', EV_ANNOTATE: 'ANNOTATE', E
 def property_deltas(pmask, pvals):
     """propertyDeltas of an ANNOTATE record: {"k<id>": previous value id, or None (null)}."""
     out = {}
-    for k in range(16):
+    for k in range(32):
         if (pmask >> k) & 1:
             v = int(pvals[k])
             out['k%d' % k] = v if v else None

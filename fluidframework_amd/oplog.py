@@ -20,6 +20,7 @@ F_REWRITE, F_PROPS, F_GROUP_MORE = 1, 2, 4
 F_MARKER = 128          # insert of a Marker: the one text byte is its ReferenceType (ops.ts:6-16)
 NPAIRS_SHIFT = 3        # bits 3..6: property pairs in the payload, mod 16
 OP_NP16 = 0x40          # type bit 6 (MT_OP_NP16): pair count bit 4 (16 pairs: wide records only)
+OP_NP32 = 0x20          # type bit 5 (MT_OP_NP32): pair count bit 5 (wide records only)
 REF_TILE, REF_NEST_BEGIN, REF_NEST_END = 1, 2, 4
 
 
@@ -27,16 +28,17 @@ OP_WIDE = 0x80          # type bit 7 (MT_OP_WIDE): UTF-16 text, 3-byte pairs (ke
 
 
 def npairs(flags, typ=0):
-    """Property pairs of a record (MT_OP_NPAIRS): flags bits 3..6, plus 16 if type bit 6 is set."""
-    return ((int(flags) >> NPAIRS_SHIFT) & 15) | (16 if int(typ) & OP_NP16 else 0)
+    """Property pairs of a record (MT_OP_NPAIRS): flags bits 3..6, plus 16 if type bit 6 is set and
+    32 if type bit 5 is."""
+    return ((int(flags) >> NPAIRS_SHIFT) & 15) | (16 if int(typ) & OP_NP16 else 0) | (32 if int(typ) & OP_NP32 else 0)
 
 
 def pack_npairs(n, wide):
     """(flags bits, type bits) that carry n property pairs; a narrow record holds at most 8 keys and a
-    wide one 16 (include/mtgpu.h MT_OP_NP16): anything else is rejected, never wrapped."""
-    if n < 0 or n > (16 if wide else 8):
-        raise ValueError('a record carries at most %d property pairs, not %d' % (16 if wide else 8, n))
-    return (n & 15) << NPAIRS_SHIFT, (OP_NP16 if n & 16 else 0)
+    wide one 32 (include/mtgpu.h MT_OP_NP16 / MT_OP_NP32): anything else is rejected, never wrapped."""
+    if n < 0 or n > (32 if wide else 8):
+        raise ValueError('a record carries at most %d property pairs, not %d' % (32 if wide else 8, n))
+    return (n & 15) << NPAIRS_SHIFT, (OP_NP16 if n & 16 else 0) | (OP_NP32 if n & 32 else 0)
 
 
 def encode_text(text, force_wide=False):

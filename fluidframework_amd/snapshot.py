@@ -40,8 +40,8 @@ LSF_U16 = 64                # MT_LSF_U16: the segment's text is UTF-16 code unit
 LOAD_SEG_DTYPE = np.dtype([('seq', '<i4'), ('rseq', '<i4'), ('client', 'u1'), ('rclient', 'u1'), ('flags', 'u1'),
                            ('pad', 'u1'), ('text_off', '<u4'), ('text_len', '<u4'), ('client_hi', 'u1'),
                            ('rclient_hi', 'u1'), ('pad2', '<u2'),
-                           ('props', '<u2', (16,)), ('pad3', '<u8')])
-assert LOAD_SEG_DTYPE.itemsize == 64
+                           ('props', '<u2', (32,)), ('pad3', '<u8')])
+assert LOAD_SEG_DTYPE.itemsize == 96
 
 
 class Interner:
@@ -81,12 +81,12 @@ class ClientInterner(Interner):
 
 class DocInterners:
     """Per-document id spaces: long client ids -> short ids (1..65534 but 254), property keys ->
-    0..15, and per key its values -> 1..65535 (0 = absent; ids are opaque, only equality matters,
+    0..31, and per key its values -> 1..65535 (0 = absent; ids are opaque, only equality matters,
     properties.ts:62-93)."""
 
     def __init__(self):
         self.client = ClientInterner()
-        self.key = Interner(0, 16)
+        self.key = Interner(0, 32)
         self.values = {}
 
     def value(self, kid, v):
@@ -207,7 +207,7 @@ def build_load(docs, interners=None):
             t, seq, client, rseq, rclient, pdef, pv, mk = _spec(spec, it)
             tb, wide_text = encode_text(t)
             n = len(tb) // 2 if wide_text else len(tb)
-            props = [pv.get(k, 0) for k in range(16)]
+            props = [pv.get(k, 0) for k in range(32)]
             rc = rclient if rseq >= 0 else 0
             segs.append((seq, rseq, client & 0xFF, rc & 0xFF,
                          (SF_PDEF if pdef else 0) | (SF_MARKER if mk else 0) | (LSF_U16 if wide_text else 0), 0,

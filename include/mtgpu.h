@@ -50,10 +50,13 @@ enum mt_op_flags {
                                   segment has length 1 and never appends (Marker.canAppend) */
 };
 #define MT_F_NPAIRS_SHIFT 3    /* bits 3..6: number of (key,value) property pairs in the payload, mod 16 */
-/* A record may carry 16 pairs (one per wide key, MT_MAX_KEYS_WIDE): the count's bit 4 is type bit 6
- * (MT_OP_NP16), set only on wide records.  MT_OP_NPAIRS takes the record. */
+/* A wide record may carry up to 32 pairs (one per wide key, MT_MAX_KEYS_WIDE): the count's bit 4 is
+ * type bit 6 (MT_OP_NP16) and its bit 5 type bit 5 (MT_OP_NP32), set only on wide records.
+ * MT_OP_NPAIRS takes the record. */
 #define MT_OP_NP16 0x40u
-#define MT_OP_NPAIRS(o) ((((o).flags >> MT_F_NPAIRS_SHIFT) & 0xF) | (((o).type & MT_OP_NP16) ? 16 : 0))
+#define MT_OP_NP32 0x20u
+#define MT_OP_NPAIRS(o) ((((o).flags >> MT_F_NPAIRS_SHIFT) & 0xF) | (((o).type & MT_OP_NP16) ? 16 : 0) | \
+                         (((o).type & MT_OP_NP32) ? 32 : 0))
 /* an MT_OP_LOAD record's segment client and removedClient (short ids; see MT_OP_LOAD) */
 #define MT_LOAD_CLIENT(o) (((uint32_t)(o).client & 0xFFu) | (((uint32_t)(o).msn & 0xFFu) << 8))
 #define MT_LOAD_RCLIENT(o) (((uint32_t)(o).client >> 8) | ((((uint32_t)(o).msn >> 8) & 0xFFu) << 8))
@@ -64,7 +67,7 @@ enum mt_op_flags {
  * A document that receives a wide op, or a client id >= MT_MAX_CLIENTS, becomes a WIDE document for
  * good (see "limits" below); narrow-form ops apply to wide documents unchanged. */
 #define MT_OP_WIDE 0x80u
-#define MT_OP_TYPE(o) ((o).type & 0x3Fu)
+#define MT_OP_TYPE(o) ((o).type & 0x1Fu)
 #define MT_OP_PAIR_BYTES(o) (((o).type & MT_OP_WIDE) ? 3u : 2u)
 #define MT_OP_PAIRS_LEN(o) (MT_OP_PAIR_BYTES(o) * MT_OP_NPAIRS(o))
 /* a remove or annotate record carries no text: its payload is exactly its pairs (else MT_DERR_BAD_OP) */
@@ -128,19 +131,19 @@ typedef struct mt_op_rec {
  * u64 bitmask), keys < 8 with u8 value ids and one byte per text code unit (Latin-1): the register
  * engine's and the LDS engine's fast forms.  A WIDE document (promoted for good by its first wide
  * op, client id >= 64 or wide snapshot segment) holds client ids < 65535 (u16; 254 = 0xFE is
- * NonCollabClient, so a host interning more than 253 clients skips it), keys < 16 with u16 value
+ * NonCollabClient, so a host interning more than 253 clients skips it), keys < 32 with u16 value
  * ids, UTF-16 text (2 bytes per code unit in the same arena: half the units), and overlap sets of
  * the ids < 64 plus up to MT_OVX_IDS ids >= 64 per segment.  Wide
  * documents run on the LDS engine's wide form (its structure in an HBM workspace); their extra
- * per-segment state (32 B) is allocated by the engine on first need.  Value ids are opaque
+ * per-segment state (122 B) is allocated by the engine on first need.  Value ids are opaque
  * (equality only) and may be interned per key. */
 #define MT_MAX_CLIENTS 64      /* narrow: short client ids 0..63 (overlap set is a u64 bitmask)  */
 #define MT_MAX_KEYS 8          /* narrow: property keys per document (u8 value id per key)      */
 #define MT_MAX_VALUES 255      /* narrow: property value ids 1..255 (0 = absent/null)           */
 #define MT_MAX_CLIENTS_WIDE 65535 /* wide: short client ids 1..65534, except 254 (NonCollabClient) */
-#define MT_MAX_KEYS_WIDE 16    /* wide: property keys 0..15                                      */
+#define MT_MAX_KEYS_WIDE 32    /* wide: property keys 0..31                                      */
 #define MT_MAX_VALUES_WIDE 65535 /* wide: property value ids 1..65535 per key                    */
-#define MT_OVX_IDS 16          /* wide: overlapping removers with ids >= 64 per segment          */
+#define MT_OVX_IDS 32          /* wide: overlapping removers with ids >= 64 per segment          */
 #define MT_MAX_TEXTCAP (4u << 20) /* text arena bytes per document half (mt_cfg.text_capacity)        */
 
 typedef enum mt_status {
@@ -197,8 +200,8 @@ mt_status mt_docs_init(mt_engine* eng, uint32_t n_docs);
 
 /* ---- snapshot load ---------------------------------------------------
  * One segment of a snapshot's header chunk (IJSONSegmentWithMergeInfo, snapshotChunks.ts:60-66,
- * after SnapshotLoader.specToSegment, snapshotLoader.ts:85-117): 32 bytes. */
-typedef struct mt_load_seg {  /* 64 bytes */
+ * after SnapshotLoader.specToSegment, snapshotLoader.ts:85-117): 96 bytes. */
+typedef struct mt_load_seg {  /* 96 bytes */
     int32_t seq;          /* spec.seq, or UniversalSequenceNumber (0) without merge info            */
     int32_t rseq;         /* spec.removedSeq; -1 = not removed                                      */
     uint8_t client;       /* short id of spec.client, or MT_CLIENT_NONCOLLAB                        */
@@ -212,7 +215,7 @@ typedef struct mt_load_seg {  /* 64 bytes */
     uint8_t client_hi;    /* high bytes of the short ids (a wide document's ids >= 256)             */
     uint8_t rclient_hi;
     uint16_t pad2;
-    uint16_t props[16];   /* value id per key (0 = absent)                                           */
+    uint16_t props[MT_MAX_KEYS_WIDE]; /* value id per key (0 = absent)                               */
     uint64_t pad3;
 } mt_load_seg;
 #define MT_LSF_U16 64u
@@ -392,7 +395,7 @@ mt_status mt_resolve_positions_device(mt_engine* eng, const mt_pos_query* d_q, u
  * segment found by mt_resolve_positions, e.g. Client.getPropertiesAtPosition client.ts:1009-1023):
  * one small gather kernel and one copy, not a whole-document read.  ordinal past the document's
  * segments: seq = INT32_MIN.  Text: mt_segment_text. */
-typedef struct mt_seg_info {    /* 104 bytes */
+typedef struct mt_seg_info {    /* 168 bytes */
     int32_t seq;                /* INT32_MIN: no such segment */
     int32_t rseq;               /* removedSeq, -1: not removed */
     int32_t client;             /* short client id; -2 = NonCollabClient (constants.ts:15) */
@@ -402,7 +405,7 @@ typedef struct mt_seg_info {    /* 104 bytes */
     uint32_t toff;              /* its text in the document's arena (code units) */
     uint32_t wide;              /* 1: a wide document (UTF-16 arena) */
     uint64_t overlap;           /* removedClientOverlap: bit c for ids c < 64 */
-    uint16_t props[16];         /* value id per key (0: absent) */
+    uint16_t props[MT_MAX_KEYS_WIDE]; /* value id per key (0: absent) */
     uint16_t overlap_hi[MT_OVX_IDS]; /* a wide document's overlapping removers >= 64, ascending (0: none) */
 } mt_seg_info;
 mt_status mt_segment_infos(mt_engine* eng, const uint32_t* docs, const int32_t* ordinals, uint32_t n, mt_seg_info* out);
@@ -478,16 +481,16 @@ enum mt_event_op {
 #define MT_EVF_NOPD 4u  /* ANNOTATE delta segment whose propertyDeltas is undefined (a remote annotate
                          dropped while the editing client's rewrite is pending) */
 #define MT_EVF_EMPTY 2u   /* the callback's deltaSegments is empty (no segment in this record) */
-typedef struct mt_event {   /* 64 bytes */
+typedef struct mt_event {   /* 96 bytes */
     int32_t seq;            /* sequenceNumber of the message being applied                        */
     int8_t op;              /* mt_event_op                                                        */
     uint8_t flags;          /* MT_EVF_*                                                           */
-    uint16_t pmask;         /* ANNOTATE: keys present in propertyDeltas (bit k = key id k)        */
+    uint16_t pad;
     int32_t leaf;
     int32_t pos;
     uint32_t len;
-    uint32_t pad;
-    uint16_t pvals[16];     /* ANNOTATE: previous value id of key k (0 = null)                    */
+    uint32_t pmask;         /* ANNOTATE: keys present in propertyDeltas (bit k = key id k)        */
+    uint16_t pvals[MT_MAX_KEYS_WIDE]; /* ANNOTATE: previous value id of key k (0 = null)          */
     uint64_t pad2;
 } mt_event;
 /* Start recording: `per_doc` records per document between drains (0 stops recording).  A

@@ -26,12 +26,13 @@ const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3, NOOP = 3;
 const F_REWRITE = 1, F_PROPS = 2, F_GROUP_MORE = 4, F_MARKER = 128;
 const OP_WIDE = 0x80;  // MT_OP_WIDE: UTF-16 text, (key u8, value u16) pairs
 const OP_NP16 = 0x40;  // MT_OP_NP16: property pair count bit 4 (wide records)
+const OP_NP32 = 0x20;  // MT_OP_NP32: property pair count bit 5 (wide records)
 // mt_pos_query (include/mtgpu.h): kinds, and the local view's refSeq
 const POS_CONTAINING = 0, POS_OF_ORDINAL = 1, POS_LOCAL = -2147483648;
 // include/mtgpu.h "limits": the wide form's (a document goes wide with its first op beyond the narrow
 // ones: client id >= 64, key >= 8, value id >= 256 or a code unit above U+00FF)
-const MAX_CLIENTS = 65535, NONCOLLAB_ID = 0xfe, MAX_KEYS = 16, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
-const REC = 32, EVREC = 64;
+const MAX_CLIENTS = 65535, NONCOLLAB_ID = 0xfe, MAX_KEYS = 32, MAX_VALUES = 65535, NARROW_CLIENTS = 64, NARROW_KEYS = 8;
+const REC = 32, EVREC = 96, OVX_IDS = 32;  // (MT_OVX_IDS)
 
 function canonicalJson(v) {
     if (Array.isArray(v)) return "[" + v.map(canonicalJson).join(",") + "]";
@@ -102,9 +103,10 @@ class BatchEngine {
                 const o = i * REC;
                 ops.writeInt32LE(r.seq, o); ops.writeInt32LE(r.ref, o + 4); ops.writeInt32LE(r.msn, o + 8);
                 ops.writeUInt16LE(r.client, o + 12);
-                // 16 pairs (wide only): the count's bit 4 is type bit 6 (include/mtgpu.h MT_OP_NP16)
-                if (r.npairs > 16) throw new Error("BatchClient: more than 16 property pairs in one op");
-                ops.writeUInt8(r.type | ((r.npairs & 16) ? OP_NP16 : 0), o + 14);
+                // 16..32 pairs (wide only): the count's bits 4 / 5 are type bits 6 / 5 (include/mtgpu.h
+                // MT_OP_NP16 / MT_OP_NP32)
+                if (r.npairs > MAX_KEYS) throw new Error(`BatchClient: more than ${MAX_KEYS} property pairs in one op`);
+                ops.writeUInt8(r.type | ((r.npairs & 16) ? OP_NP16 : 0) | ((r.npairs & 32) ? OP_NP32 : 0), o + 14);
                 ops.writeUInt8(r.flags | ((r.npairs & 15) << 3), o + 15);
                 ops.writeInt32LE(r.pos1, o + 16); ops.writeInt32LE(r.pos2, o + 20);
                 ops.writeUInt32LE(off, o + 24); ops.writeUInt32LE(r.payload.length, o + 28);
@@ -170,10 +172,10 @@ class BatchClient {
             if (op >= 0) segment.position = rows.readInt32LE(o + 12);
             const delta = { segment };
             if (op === ANNOTATE && !(flags & 4)) {  // (MT_EVF_NOPD: propertyDeltas undefined)
-                const mask = rows.readUInt16LE(o + 6);
+                const mask = rows.readUInt32LE(o + 20);
                 delta.propertyDeltas = {};
                 for (let k = 0; k < MAX_KEYS; k++) {
-                    if (!((mask >> k) & 1)) continue;
+                    if (!((mask >>> k) & 1)) continue;
                     const v = rows.readUInt16LE(o + 24 + 2 * k);
                     delta.propertyDeltas[this.keys[k]] = v ? this.values[k][v] : null;
                 }
@@ -585,11 +587,11 @@ class BatchClient {
         const lo = b.readUInt32LE(32), hi = b.readUInt32LE(36);
         for (let c = 0; c < 32; c++) if ((lo >>> c) & 1) overlap.push(c);
         for (let c = 0; c < 32; c++) if ((hi >>> c) & 1) overlap.push(32 + c);
-        for (let q = 0; q < 16; q++) { const c = b.readUInt16LE(72 + 2 * q); if (!c) break; overlap.push(c); }
+        for (let q = 0; q < OVX_IDS; q++) { const c = b.readUInt16LE(104 + 2 * q); if (!c) break; overlap.push(c); }
         let properties;
         if (flags & 2) {
             properties = {};
-            for (let kid = 0; kid < 16; kid++) {
+            for (let kid = 0; kid < MAX_KEYS; kid++) {
                 const vid = b.readUInt16LE(40 + 2 * kid);
                 if (vid) properties[self.keys[kid]] = self.values[kid][vid];
             }

@@ -39,8 +39,9 @@ function tileLabels(v) {
 // a record's payload: [text][pairs]; narrow: Latin-1 bytes and (key u8, value u8) pairs; wide
 // (type bit 7, MT_OP_WIDE): UTF-16 LE code units and (key u8, value u16 LE) pairs
 const pairBytes = (r) => (r.type & 0x80 ? 3 : 2);
-// property pairs: flags bits 3..6, plus 16 when type bit 6 (MT_OP_NP16) is set
-const npairsOf = (r) => ((r.flags >> 3) & 15) | (r.type & 0x40 ? 16 : 0);
+// property pairs: flags bits 3..6, plus 16 when type bit 6 (MT_OP_NP16) is set, 32 when type bit 5
+// (MT_OP_NP32) is
+const npairsOf = (r) => ((r.flags >> 3) & 15) | (r.type & 0x40 ? 16 : 0) | (r.type & 0x20 ? 32 : 0);
 function textOf(log, r) {
     const np = npairsOf(r);
     const a = log.payOff + r.poff, b = a + r.plen - pairBytes(r) * np;
@@ -62,7 +63,7 @@ function propsOf(log, r, opts) {
 }
 
 function toOp(log, r, opts) {
-    const type = r.type & 0x3f;
+    const type = r.type & 0x1f;
     if (type === 0 && (r.flags & 128)) {
         const seg = { marker: { refType: textOf(log, r).charCodeAt(0) } };
         if (r.flags & 2) seg.props = propsOf(log, r, opts);

@@ -18,7 +18,7 @@
 const native = require("./mtgpu.node");
 
 const MT_OP_LOAD = 4, F_PROPS = 2, F_MARKER = 128, OP_WIDE = 0x80;  // (npairs: BatchClient's encoder)
-const NONCOLLAB = 0xfe, UNIVERSAL_SEQ = 0, SF_PDEF = 2, SF_MARKER = 16, LSF_U16 = 64, LOAD_SEG = 64;
+const NONCOLLAB = 0xfe, UNIVERSAL_SEQ = 0, SF_PDEF = 2, SF_MARKER = 16, LSF_U16 = 64, LOAD_SEG = 96;
 
 function blobs(tree) {
     if (tree && Array.isArray(tree.entries)) {

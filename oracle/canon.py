@@ -50,12 +50,17 @@ def ovx_hash(ids):
     return h or 1
 
 
-def props_term(lo, hi, xlo, xhi):
-    """the props term: low bytes of keys 0..7; high bytes and keys 8..15 hashed in"""
-    if not (hi | xlo | xhi):
-        return lo
-    return lo ^ mix64(mix64(hi ^ 0x1111111111111111) ^ mix64(xlo ^ 0x2222222222222222) ^
-                      mix64(xhi ^ 0x3333333333333333))
+def props_term(lo, hi, xlo, xhi, y0=0, y1=0, y2=0, y3=0):
+    """the props term: low bytes of keys 0..7; high bytes and keys 8..15 hashed in, then keys 16..31
+    (low / high bytes of 16..23, of 24..31) when any is set"""
+    t = lo
+    if hi | xlo | xhi:
+        t ^= mix64(mix64(hi ^ 0x1111111111111111) ^ mix64(xlo ^ 0x2222222222222222) ^
+                   mix64(xhi ^ 0x3333333333333333))
+    if y0 | y1 | y2 | y3:
+        t ^= mix64(mix64(y0 ^ 0x4444444444444444) ^ mix64(y1 ^ 0x5555555555555555) ^
+                   mix64(y2 ^ 0x6666666666666666) ^ mix64(y3 ^ 0x7777777777777777))
+    return t
 
 
 def utf16_units(text):
@@ -70,7 +75,7 @@ def checksum(state):
     for i, (text, seq, client, rseq, rclient, ov, props) in enumerate(state['segs']):
         mask = sum(1 << o for o in set(ov) if o < 64)
         ovx = ovx_hash(sorted(o for o in set(ov) if o >= 64))
-        w = [0, 0, 0, 0]
+        w = [0] * 8
         if props is not None:
             for k, v in props.items():
                 kid, v = int(k[1:]), int(v)

@@ -52,7 +52,7 @@ namespace {
 constexpr int kMaxNodes = 8;           // MaxNodesInBlock, mergeTree.ts:334
 constexpr int kTextGranularity = 256;  // MergeTree.TextSegmentGranularity, mergeTree.ts:1059
 constexpr int kZamboniMax = 2;         // zamboniSegmentsMaxCount, mergeTree.ts:1061
-constexpr int kMaxKeys = MT_MAX_KEYS_WIDE;  // property keys 0..15 (u16 value ids)
+constexpr int kMaxKeys = MT_MAX_KEYS_WIDE;  // property keys 0..31 (u16 value ids)
 constexpr int32_t kUnassigned = -1;    // UnassignedSequenceNumber, constants.ts
 
 struct Block;
@@ -113,11 +113,11 @@ struct Seg : Node {
 struct Pay {
     std::u16string text;
     int np = 0;
-    uint8_t key[16] = {0};
-    uint16_t val[16] = {0};
+    uint8_t key[64] = {0};   // (MT_OP_NPAIRS: at most 63)
+    uint16_t val[64] = {0};
     bool ok = false;
 };
-// property keys an op may carry: < 8 in the narrow form, < 16 in the wide one (include/mtgpu.h)
+// property keys an op may carry: < 8 in the narrow form, < 32 in the wide one (include/mtgpu.h)
 int keyLimit(const mt_op_rec& op) { return (op.type & MT_OP_WIDE) ? MT_MAX_KEYS_WIDE : MT_MAX_KEYS; }
 Pay decodePay(const mt_op_rec& op, const uint8_t* payload) {
     Pay p;
@@ -216,8 +216,8 @@ struct Doc {
     }
     // propertyDeltas of one delta segment: keys present (bit k) and the previous value id per key
     struct PDelta {
-        uint16_t mask = 0;
-        uint16_t vals[16] = {0};
+        uint32_t mask = 0;
+        uint16_t vals[kMaxKeys] = {0};
     };
     void ev(int op, unsigned flags, int leaf, int pos, int len, const PDelta* pd = nullptr) {
         mt_event e{};
@@ -229,7 +229,7 @@ struct Doc {
         e.len = (uint32_t)len;
         if (pd) {
             e.pmask = pd->mask;
-            for (int k = 0; k < 16; k++) e.pvals[k] = pd->vals[k];
+            for (int k = 0; k < kMaxKeys; k++) e.pvals[k] = pd->vals[k];
         }
         events.push_back(e);
     }
@@ -708,7 +708,7 @@ struct Doc {
         if (s->pendRewrite > 0 && !local) return false;
         auto modify = [&](int k) { return local || s->pend[k] == 0; };
         auto delta = [&](int k, uint16_t prev) {
-            pd.mask |= (uint16_t)(1u << k);
+            pd.mask |= 1u << k;
             pd.vals[k] = prev;
         };
         if (rewrite) {
@@ -1311,10 +1311,15 @@ inline uint64_t fnv1a(const std::u16string& t) {
 // the wide terms of the segment hash (restated from DESIGN.md "Checksum"; the device's statement is
 // fluidframework_amd/csrc/mt_checksum.h)
 inline uint64_t mt_ovl_term(uint64_t mask, uint64_t ovx) { return ovx ? mask ^ mix64(ovx ^ 0x4F56584944530000ull) : mask; }
-inline uint64_t mt_props_term(uint64_t lo, uint64_t hi, uint64_t xlo, uint64_t xhi) {
-    if (!(hi | xlo | xhi)) return lo;
-    return lo ^ mix64(mix64(hi ^ 0x1111111111111111ull) ^ mix64(xlo ^ 0x2222222222222222ull) ^
-                      mix64(xhi ^ 0x3333333333333333ull));
+inline uint64_t mt_props_term(const uint64_t* w) {  // w: the 8 words of keys 0..31 (lo, hi per 8 keys)
+    uint64_t t = w[0];
+    if (w[1] | w[2] | w[3])
+        t ^= mix64(mix64(w[1] ^ 0x1111111111111111ull) ^ mix64(w[2] ^ 0x2222222222222222ull) ^
+                   mix64(w[3] ^ 0x3333333333333333ull));
+    if (w[4] | w[5] | w[6] | w[7])
+        t ^= mix64(mix64(w[4] ^ 0x4444444444444444ull) ^ mix64(w[5] ^ 0x5555555555555555ull) ^
+                   mix64(w[6] ^ 0x6666666666666666ull) ^ mix64(w[7] ^ 0x7777777777777777ull));
+    return t;
 }
 
 }  // namespace
@@ -1349,9 +1354,9 @@ uint64_t doc_checksum(const Doc& doc) {
     DocChecksum d;
     uint64_t idx = 0;
     Doc::walkSegs(doc.root, [&](const Seg* s) {
-        // the wide terms (DESIGN.md "Checksum"): u16 value ids and keys 8..15 as the device's four
+        // the wide terms (DESIGN.md "Checksum"): u16 value ids and keys 8..31 as the device's eight
         // u64 property words, overlap ids >= 64 as its ascending byte list
-        uint64_t w[4] = {0, 0, 0, 0};
+        uint64_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < kMaxKeys; k++) {
             w[(k >> 3) * 2] |= (uint64_t)(s->props[k] & 0xFF) << (8 * (k & 7));
             w[(k >> 3) * 2 + 1] |= (uint64_t)(s->props[k] >> 8) << (8 * (k & 7));
@@ -1369,7 +1374,7 @@ uint64_t doc_checksum(const Doc& doc) {
         const uint64_t th = fnv1a(s->text) ^ (s->marker ? 0x4D41524B45520000ull : 0ull);
         d.seg_sum += mto_seg_hash(idx++, th, s->seq, s->client,
                                   s->removed ? s->rseq : -1, s->removed ? s->rclient : -1,
-                                  mt_ovl_term(s->overlap, ovx), mt_props_term(w[0], w[1], w[2], w[3]),
+                                  mt_ovl_term(s->overlap, ovx), mt_props_term(w),
                                   s->props_defined);
     });
     d.nsegs = (uint32_t)idx;

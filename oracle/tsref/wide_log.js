@@ -33,6 +33,9 @@ const PIECES = ["a", "b", "z", "0", "7", " ", "é", "ü", "中", "文", "字", "
 function main() {
     const [nDocs, seed, opsPerDoc, nClients] = process.argv.slice(2, 6).map((x) => parseInt(x, 10));
     const maxLag = parseInt(process.argv[6] || "8", 10);
+    // property keys: annotates draw keys 0..nKeys-5 (0..11 at the default 16) and a second key from
+    // all nKeys; inserts the first range
+    const nKeys = parseInt(process.argv[7] || "16", 10), k1 = nKeys === 16 ? 11 : nKeys - 5;
     const docs = [];
     for (let d = 0; d < nDocs; d++) {
         const r = rng(seed * 7919 + d * 104729 + 1);
@@ -64,7 +67,7 @@ function main() {
                 let props = null;
                 if (r() < 0.25) {
                     props = {};
-                    props[u(0, 11)] = u(1, 1200);
+                    props[u(0, k1)] = u(1, 1200);
                 }
                 rec = [S, R, msn, id, 0, u(0, L), 0, text, props, 0];
             } else {
@@ -73,8 +76,8 @@ function main() {
                     rec = [S, R, msn, id, 1, a, b, null, null, 0];
                 } else {
                     const props = {};
-                    props[u(0, 11)] = r() < 0.1 ? null : u(1, 1500);
-                    if (r() < 0.4) props[u(0, 15)] = u(1, 400);
+                    props[u(0, k1)] = r() < 0.1 ? null : u(1, 1500);
+                    if (r() < 0.4) props[u(0, nKeys - 1)] = u(1, 400);
                     rec = [S, R, msn, id, 2, a, b, null, props, r() < 0.05 ? 1 : 0];
                 }
             }

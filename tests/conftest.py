@@ -17,7 +17,7 @@ GOLDEN = os.path.join(REPO, 'tests', 'golden')
 GOLDEN_SETS = ['scenarios', 'markers', 'synth_c1', 'synth_c2', 'synth_c3', 'synth_c4', 'synth_tiny', 'synth_markers']
 # beyond the narrow limits (include/mtgpu.h "limits"): UTF-16 text, > 100 client ids, u16 value ids,
 # keys 8..15 -- tests/golden/make_wide.py
-WIDE_SETS = ['wide', 'wide_synth', 'wide_many']
+WIDE_SETS = ['wide', 'wide_synth', 'wide_many', 'wide_xl']
 
 
 # reference pins at the benchmark configs' full shape (tests/golden/make_fullshape.py): the logs are

@@ -13,7 +13,10 @@ is stored as the expected output (the make_golden.py pattern).
     value ids past 255, keys past 7;
   * wide_many.mtlog / .expected.jsonl -- short client ids past 255 (320 clients per document) and
     sixteen overlapping removers >= 64 on one segment (hand-made), plus wide_log.js documents with
-    320 clients.
+    320 clients;
+  * wide_xl.mtlog / .expected.jsonl -- past sixteen: twenty and thirty-two overlapping removers >= 64
+    on one segment, records with 24 and 32 property keys (MT_OP_NP32), keys 16..31 on markers, plus
+    wide_log.js documents drawing from 32 keys.
 Fixtures are data only (inputs and reference outputs).
 """
 import json
@@ -129,9 +132,70 @@ def many():
     return build_log(docs)
 
 
-def synth_docs(n_docs, seed, ops, clients, lag=8):
+def xl():
+    """Past sixteen property keys and sixteen overlapping high-id removers:
+    include/mtgpu.h MT_MAX_KEYS_WIDE = 32, MT_OVX_IDS = 32 (the reference's maps are unbounded:
+    properties.ts:156-170 createMap, mergeTree.ts:2544-2552 addOverlappingClient)."""
+    ids = [k for k in range(1, 140) if k != 254]
+    docs = []
+    # 0: 120 clients insert once each; then 21 clients >= 64 and a narrow one remove one range
+    #    concurrently (twenty overlapping removers >= 64 after the first); later ids see the removal
+    d, s = [], 0
+    for k in ids[:120]:
+        s += 1
+        d.append(I(s, s - 1, 0, k, 0, chr(ord('a') + k % 26)))
+    base = s
+    removers = [64 + j for j in range(21)] + [12]
+    for j, k in enumerate(removers):
+        s += 1
+        d.append(R(s, base, 0, k, 10, 24 + j % 5))
+    s += 1
+    d.append(I(s, s - 1, 0, 119, 5, 'after'))
+    s += 1
+    d.append(A(s, s - 1, 0, 118, 3, 12, {20: 7}))
+    for _ in range(3):  # (the msn stays below the removals: the overlap sets survive in the final state)
+        s += 1
+        d.append(N(s, base - 4))
+    docs.append(d)
+    # 1: thirty-three removers >= 64 on one range: the first takes removedClient, thirty-two
+    #    overlap it (the device list full); then the msn passes everything and zamboni unlinks them
+    d, s = [], 0
+    for k in ids[:110]:
+        s += 1
+        d.append(I(s, s - 1, 0, k, min(s % 5, s - 1), 'pq'))
+    base = s
+    for j in range(33):
+        s += 1
+        d.append(R(s, base, 0, 70 + j, 30, 50))
+    s += 1
+    d.append(I(s, base, 0, 108, 40, 'mid'))
+    for _ in range(3):
+        s += 1
+        d.append(N(s, base - 2))
+    s += 1
+    d.append(N(s, s - 1))
+    docs.append(d)
+    # 2: twenty-four keys: an insert with 24 props (keys 0..23), an annotate setting all 32 (a
+    #    32-pair record: MT_OP_NP32), a rewrite with 20 (five null), null deletes of keys >= 16,
+    #    and segments that differ only in keys >= 16 (zamboni must not merge them)
+    docs.append([I(1, 0, 0, 1, 0, 'twenty four keys', {k: 100 + k for k in range(24)}),
+                 A(2, 1, 0, 2, 2, 9, {k: 1000 + k for k in range(32)}),
+                 A(3, 2, 0, 3, 5, 14, {k: (None if k % 4 == 0 else 2000 + k) for k in range(4, 24)}, flags=1),
+                 A(4, 3, 0, 2, 0, 3, {17: None, 23: None, 31: 5}),
+                 I(5, 4, 1, 4, 3, 'x', {31: 9}),
+                 A(6, 5, 2, 1, 6, 8, {29: 300}),
+                 I(7, 6, 3, 5, 0, 'plain'), N(8, 7), N(9, 8)])
+    # 3: markers with keys >= 16 among UTF-16 text, and an annotate of keys 16..31 across them
+    docs.append([I(1, 0, 0, 1, 0, 'x€y z'), M(2, 1, 0, 2, 1, REF_TILE, {16: 1000, 3: 1}),
+                 M(3, 2, 0, 3, 3, REF_TILE, {30: 2}),
+                 A(4, 3, 0, 1, 0, 6, {k: 40 + k for k in range(16, 32)}), R(5, 4, 1, 2, 0, 1), N(6, 5), N(7, 6)])
+    docs += synth_docs(6, 2031, 800, 140, 10, 32)
+    return build_log(docs)
+
+
+def synth_docs(n_docs, seed, ops, clients, lag=8, keys=16):
     res = subprocess.run(['node', os.path.join(REPO, 'oracle/tsref/wide_log.js'), str(n_docs), str(seed), str(ops),
-                          str(clients), str(lag)], check=True, capture_output=True, text=True)
+                          str(clients), str(lag), str(keys)], check=True, capture_output=True, text=True)
     docs = json.loads(res.stdout)['docs']
     out = []
     for d in docs:
@@ -150,7 +214,8 @@ def synth(n_docs, seed, ops, clients, lag=8):
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, 'oracle/tsref/build_ref.py')])
     replay = os.path.join(REPO, 'oracle/tsref/replay_ref.js')
-    sets = (('wide', scenarios()), ('wide_synth', synth(12, 2027, 700, 120)), ('wide_many', many()))
+    sets = (('wide', scenarios()), ('wide_synth', synth(12, 2027, 700, 120)), ('wide_many', many()),
+            ('wide_xl', xl()))
     for name, batch in sets:
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue

@@ -151,7 +151,7 @@ def _device_limit_batch(oracle_lib, faulty=True):
             rec(201, 200, m, 254, INSERT, 0, 0, b'x')
         if d == 3:   # unknown op type (MT_DERR_BAD_OP)
             rec(201, 200, m, 1, 9)
-        if d == 5:   # property key 8 in a narrow-form op (keys < 8; the wide form carries < 16: MT_DERR_LIMITS)
+        if d == 5:   # property key 8 in a narrow-form op (keys < 8; the wide form carries < 32: MT_DERR_LIMITS)
             rec(201, 200, m, 2, INSERT, 0, 0, b'ab' + bytes([8, 1]), 2 | (1 << 3))
         if d == 7:   # negative position (MT_DERR_BAD_OP)
             rec(201, 200, m, 2, REMOVE, -3, 2)

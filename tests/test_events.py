@@ -65,16 +65,17 @@ def test_golden_events_cover_every_callback_kind():
 def test_callbacks_grouping():
     from fluidframework_amd.events import EVENT_DTYPE, EVF_EMPTY, EVF_FIRST, callbacks
     rows = np.zeros(6, dtype=EVENT_DTYPE)
-    z = [0] * 16
+    z = [0] * 32
+    # (seq, op, flags, pad, leaf, pos, len, pmask, pvals, pad2)
     rows[0] = (7, -2, EVF_FIRST, 0, 3, -1, 2, 0, z, 0)
     rows[1] = (7, -2, 0, 0, 4, -1, 5, 0, z, 0)
     rows[2] = (7, 1, EVF_FIRST | EVF_EMPTY, 0, -1, -1, 0, 0, z, 0)
-    rows[3] = (8, 2, EVF_FIRST, 0b101, 2, 9, 1, 0, [0, 3, 0] + [0] * 13, 0)  # k0, k2 -> null (k1 unmasked)
-    rows[4] = (8, 2, 0, 0b10, 3, 10, 4, 0, [0, 9] + [0] * 14, 0)
-    rows[5] = (8, 2, 0, 1 << 12, 4, 14, 1, 0, [0] * 12 + [40000, 0, 0, 0], 0)  # a wide document's key 12
+    rows[3] = (8, 2, EVF_FIRST, 0, 2, 9, 1, 0b101, [0, 3, 0] + [0] * 29, 0)  # k0, k2 -> null (k1 unmasked)
+    rows[4] = (8, 2, 0, 0, 3, 10, 4, 0b10, [0, 9] + [0] * 30, 0)
+    rows[5] = (8, 2, 0, 0, 4, 14, 1, (1 << 12) | (1 << 27), [0] * 12 + [40000] + [0] * 14 + [5, 0, 0, 0, 0], 0)
     cb = callbacks(rows)
     assert cb == [[7, -2, [[3, -1, 2, None], [4, -1, 5, None]]], [7, 1, []],
-                  [8, 2, [[2, 9, 1, {'k0': None, 'k2': None}], [3, 10, 4, {'k1': 9}], [4, 14, 1, {'k12': 40000}]]]]
+                  [8, 2, [[2, 9, 1, {'k0': None, 'k2': None}], [3, 10, 4, {'k1': 9}], [4, 14, 1, {'k12': 40000, 'k27': 5}]]]]
 
 
 @pytest.mark.parametrize('name', LOGS)

@@ -1,9 +1,10 @@
 """Short client ids past a byte and full overlap lists in the wide form (include/mtgpu.h "limits":
 MT_MAX_CLIENTS_WIDE, MT_OVX_IDS).  The reference's maps are unbounded
 (client.ts:636-660 getOrAddShortClientId, mergeTree.ts:2544-2552 addOverlappingClient); the wide
-form holds short ids up to 65534 (254 is NonCollabClient's) and sixteen overlapping removers >= 64
+form holds short ids up to 65534 (254 is NonCollabClient's) and thirty-two overlapping removers >= 64
 per segment, and halts a document with MT_DERR_LIMITS past that, as the oracle does.  Reference
-pins: tests/golden/wide_many.* (320 clients, 15 overlapping high-id removers on one segment;
+pins: tests/golden/wide_many.* (320 clients, 15 overlapping high-id removers on one segment),
+wide_xl.* (20 and 32 on one segment;
 test_oracle.py / test_gpu_parity.py run every WIDE_SETS entry) and load_wide_many.jsonl (snapshots
 with ids past 255, test_snapshot_load.py)."""
 import json
@@ -55,18 +56,18 @@ def test_client_interner_skips_noncollab():
     assert it('c0') == 1  # stable
 
 
-@pytest.mark.parametrize('n_high', [17, 18])
+@pytest.mark.parametrize('n_high', [33, 34])
 def test_oracle_overlap_list_limit(oracle_lib, n_high):
-    """Sixteen overlapping removers >= 64 fit (17 removers: one removedClient + 16); the seventeenth
+    """Thirty-two overlapping removers >= 64 fit (33 removers: one removedClient + 32); the 33rd
     overlap halts the document with MT_DERR_LIMITS at its message, before any of its edits."""
     batch, n_ins = _overlap_batch(n_high)
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)
-    if n_high == 17:
+    if n_high == 33:
         assert o.error(0) == (0, 0)
         ov = max(len([c for c in s[5] if c >= 64]) for s in o.state(0)['segs'])
-        assert ov == 16
+        assert ov == 32
     else:
-        assert o.error(0) == (MT_DERR_LIMITS, n_ins + 18)
+        assert o.error(0) == (MT_DERR_LIMITS, n_ins + 34)
     assert o.error(1) == (0, 0)
 
 
@@ -90,10 +91,10 @@ def test_batchclient_interns_past_254_clients():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('n_high', [17, 18])
+@pytest.mark.parametrize('n_high', [33, 34])
 def test_engine_overlap_list_limit(oracle_lib, n_high):
-    """The device's wide form agrees with the oracle: state at 16 overlapping high-id removers,
-    MT_DERR_LIMITS (same message) at 17."""
+    """The device's wide form agrees with the oracle: state at 32 overlapping high-id removers,
+    MT_DERR_LIMITS (same message) at 33."""
     from fluidframework_amd.engine import MergeEngine
     batch, _ = _overlap_batch(n_high)
     o = oracle_lib.Oracle(batch.n_docs).apply(batch)

@@ -45,7 +45,7 @@ METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofli
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
-PMC_ROUND = 'r04'
+PMC_ROUND = 'r05'
 CAL_ROUND = 'r04'  # profiles/<round>_js_calibration_<config>.json: r of the JS baseline (oracle/tsref/calibrate.py)
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
@@ -489,7 +489,8 @@ def widen_payloads(batch):
     units -- "a" as U+4E2D, so the documents hold non-Latin-1 text -- and (key u8, value u16) pairs."""
     from fluidframework_amd.oplog import OpBatch
     ops, pay = batch.ops.copy(), batch.payload
-    npairs = ((ops['flags'].astype(np.int64) >> 3) & 0xF) | np.where(ops['type'] & 0x40, 16, 0)
+    npairs = (((ops['flags'].astype(np.int64) >> 3) & 0xF) | np.where(ops['type'] & 0x40, 16, 0) |
+              np.where(ops['type'] & 0x20, 32, 0))
     tl = ops['payload_len'].astype(np.int64) - 2 * npairs
     new_len = 2 * tl + 3 * npairs
     new_off = np.concatenate([[0], np.cumsum(new_len)[:-1]]).astype(np.int64)

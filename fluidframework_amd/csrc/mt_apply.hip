@@ -2283,6 +2283,7 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
         MT_LAUNCH_BIG(8192)
         MT_LAUNCH_BIG(16384)
         MT_LAUNCH_BIG(32768)
+        MT_LAUNCH_BIG(65472)
         default:
             return hipErrorInvalidValue;
     }
@@ -2321,6 +2322,7 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
         MT_LAUNCH_WIDE(8192)
         MT_LAUNCH_WIDE(16384)
         MT_LAUNCH_WIDE(32768)
+        MT_LAUNCH_WIDE(65472)
         default:
             return hipErrorInvalidValue;
     }
@@ -2336,6 +2338,7 @@ extern "C" size_t mt_lds_bytes_wide(int cap_class) {
         case 8192: return sizeof(mt::Lds<8192, false, true>);
         case 16384: return sizeof(mt::Lds<16384, false, true>);
         case 32768: return sizeof(mt::Lds<32768, false, true>);
+        case 65472: return sizeof(mt::Lds<65472, false, true>);
         default: return 0;
     }
 }
@@ -2405,6 +2408,7 @@ extern "C" size_t mt_lds_bytes(int cap_class) {
         case 8192: return sizeof(mt::Lds<8192>);
         case 16384: return sizeof(mt::Lds<16384>);
         case 32768: return sizeof(mt::Lds<32768>);
+        case 65472: return sizeof(mt::Lds<65472>);
         case 128: return sizeof(mt::Lds<128>);
         case 256: return sizeof(mt::Lds<256>);
         case 512: return sizeof(mt::Lds<512>);

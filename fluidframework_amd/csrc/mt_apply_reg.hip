@@ -1922,10 +1922,11 @@ MT_DEV KGState& kernarg_gstate() {
 
 // Waves per SIMD by class.  The register state is 6 K VGPRs per lane and the op path needs ~110
 // more (text compaction reads no register state: compact_text).  The kernels are issue-latency
-// bound, so a class takes the highest occupancy whose spill stays small: K = 4 runs at 5 waves
-// (96 VGPRs, 8 B of scratch per lane), K = 6 and 7 at 4 (128 VGPRs, 8 / 56 B), K = 10 at 3 (48 B);
-// each measured faster than one wave fewer without scratch, while 200+ B of scratch (K = 8 at 4,
-// K = 11 / 12 at 3) measured 1.2-2.6x slower (profiles/r03_ab_occupancy.log).  The small classes
+// bound, so a class takes the highest occupancy whose spill stays small.  Round 3 measured K = 4 at
+// 5 waves, K = 6 and 7 at 4 and K = 10 at 3, each with a few bytes of scratch, faster than one wave
+// fewer without it, while 200+ B of scratch (K = 8 at 4, K = 11 / 12 at 3) measured 1.2-2.6x slower
+// (profiles/r03_ab_occupancy.log); the scratch each class keeps at HEAD is in
+// profiles/r05_resource_usage_reg.txt (tools/resource_usage.py).  The small classes
 // (documents up to ~125 segments, C5's) run at K = 2: 7 and K = 3: 6 waves, +3.3 % on C5 against 5 / 5
 // and +2.5 % against 8 / 7 (profiles/r04_ab_small_occupancy*_C5.log).
 // Round 5 re-picked three classes with the PMC traffic in the A/B (profiles/r05_ab_occupancy/): K = 7

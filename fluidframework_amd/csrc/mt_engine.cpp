@@ -80,12 +80,14 @@ namespace {
 // classes with CAP <= the engine's seg_capacity are used: mt_engine::n_classes)
 // (the register classes step by 64 slots -- K = 2 ... 16 registers per field -- so a document pays
 // for the slots it can reach in a launch, not for the next power of two)
+// (the largest class is 64 K - 64 slots: the LDS engine's slot indices and the heap's positions
+// between launches are u16, 0xFFFF being MT_DEAD_SLOT)
 const int32_t kClasses[] = {128, 192, 256, 320, 384, 448, 512, 576, 640, 704, 768, 832, 896, 960, 1024,
-                            2048, 4096, 8192, 16384, 32768};
-constexpr int kNumClasses = 20;
+                            2048, 4096, 8192, 16384, 32768, 65472};
+constexpr int kNumClasses = 21;
 constexpr int kLdsClasses = 16;  // classes an LDS-resident kernel serves (the generator's)
 constexpr int kFirstLds = 15;    // index of the 2048 class: the first the register engine does not serve
-constexpr int kMaxSegCap = 32768;  // (the LDS engine's slot indices are u16: Lds::order / hslot)
+constexpr int kMaxSegCap = 65472;  // (the LDS engine's slot indices are u16: Lds::order / hslot)
 // bins of a tick (mt_bin_kernel): the classes, the editing documents, and the wide documents of the
 // classes from 2048 up (the LDS engine's wide form, include/mtgpu.h "limits")
 // the wide form serves the classes from 256 segments on: up to 512 staged in LDS, above in the HBM
@@ -115,7 +117,8 @@ const int32_t kClassParams[kNumClasses * 4] = {
     384, 192, 56, 256, 448, 224, 64, 288, 512, 256, 72, 320, 576, 288, 80, 352,
     640, 320, 88, 384, 704, 352, 96, 416, 768, 384, 104, 448, 832, 416, 112, 480,
     896, 448, 120, 512, 960, 480, 128, 544, 1024, 512, 136, 576, 2048, 1024, 264, 1088,
-    4096, 2048, 520, 2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256, 32768, 16384, 4104, 16448};
+    4096, 2048, 520, 2112, 8192, 4096, 1032, 4160, 16384, 8192, 2056, 8256, 32768, 16384, 4104, 16448,
+    65472, 32736, 8192, 32800};
 // the LDS engine serves the classes at 256 / 384 / 512 / 640 / 768 / 896 / 1024 / 2048 slots: the
 // next one up serves a class.  Its LDS (≈ 55 B per slot) sets the waves per CU: the steps between 512
 // and 1024 keep documents of 520-900 slots at 3-4 waves per CU instead of the 1024 form's 2.

@@ -262,7 +262,12 @@ def load_docs(engine, trees, doc_ids=None, interners=None):
     """Load one snapshot per document into `engine` (documents doc_ids, default 0..n-1): the
     header through mt_docs_load, then the body appends through the engine's apply (documents
     without a snapshot in the batch get no ops).  Returns (interners, catch-up ops per doc)."""
-    docs = [LoadedDoc(t) for t in trees]
+    return load_parsed(engine, [LoadedDoc(t) for t in trees], doc_ids, interners)
+
+
+def load_parsed(engine, docs, doc_ids=None, interners=None):
+    """load_docs for documents already parsed: objects with LoadedDoc's fields (header and body
+    specs, seq, min_seq, catchup)."""
     ids = np.arange(len(docs), dtype=np.uint32) if doc_ids is None else np.ascontiguousarray(doc_ids, np.uint32)
     segs, text, rp, mn, cs, body, its = build_load(docs, interners)
     L = lib()

@@ -144,7 +144,7 @@ typedef struct mt_op_rec {
 #define MT_MAX_KEYS_WIDE 32    /* wide: property keys 0..31                                      */
 #define MT_MAX_VALUES_WIDE 65535 /* wide: property value ids 1..65535 per key                    */
 #define MT_OVX_IDS 32          /* wide: overlapping removers with ids >= 64 per segment          */
-#define MT_MAX_TEXTCAP (4u << 20) /* text arena bytes per document half (mt_cfg.text_capacity)        */
+#define MT_MAX_TEXTCAP (64u << 20) /* text arena bytes per document half (mt_cfg.text_capacity)       */
 
 typedef enum mt_status {
     MT_OK = 0,
@@ -182,9 +182,9 @@ typedef struct mt_cfg {
 typedef struct mt_engine mt_engine;
 typedef struct mt_batch mt_batch;
 
-/* seg_capacity: 0 = 2048; 2048 ... 32768 (else MT_ERR_ARG) -- the capacity classes go up to the
- * engine's seg_capacity (2048 / 4096 / 8192 / 16384 / 32768 above the register classes) and every
- * document's slot rows hold the largest one.
+/* seg_capacity: 0 = 2048; 2048 ... 65472 (else MT_ERR_ARG) -- the capacity classes go up to the
+ * engine's seg_capacity (2048 / 4096 / 8192 / 16384 / 32768 / 65472 above the register classes:
+ * 64 K - 64, as slot indices are u16) and every document's slot rows hold the largest one.
  * text_capacity: 0 = 64 KiB; at most MT_MAX_TEXTCAP (MT_ERR_ARG above).  Each document has two
  * halves of this size (compaction copies the live text into the other half); a zamboni append
  * copies its run to the top of the arena, so documents whose live text approaches the capacity
@@ -274,7 +274,7 @@ mt_status mt_last_apply_stats(mt_engine* eng, float* kernel_ms, float* wall_ms, 
  * engine stream (on = 0: each class kernel has the GPU to itself, for per-kernel rooflines). */
 mt_status mt_set_concurrent_classes(mt_engine* eng, int on);
 /* The same, per capacity class (cls = 0, 1, ... for 128, 192, 256 ... 1024 segments in steps of 64,
- * then 2048 / 4096 / 8192 / 16384 / 32768, then one entry for the editing documents' bucket, whose capacity
+ * then 2048 / 4096 / 8192 / 16384 / 32768 / 65472, then one entry for the editing documents' bucket, whose capacity
  * reads MT_CLASS_EDITING | MT_LOC_CAP, then one per register class for the documents the LDS engine
  * runs at that capacity (declared label keys), reading MT_CLASS_LDS | capacity, then one per register
  * class for the documents with client ids above 32 (the register engine's 64-bit overlap form),

@@ -32,7 +32,7 @@ REF_SNAP = '/root/reference/packages/dds/sequence/src/test/snapshots'
 # (set, message index k, mergeTreeSnapshotChunkSize (0 = default))
 LOG_SETS = [('synth_tiny', 384, 0), ('synth_c3', 256, 300), ('synth_c4', 512, 0), ('scenarios', 3, 0),
             ('synth_c1', 1024, 400), ('markers', 4, 0), ('synth_markers', 320, 250),
-            ('wide_many', 330, 200)]
+            ('wide_many', 330, 200), ('wide_xl', 130, 200)]
 # every data file snapshotVersion.spec.ts loads (sequence/src/test/snapshots/{v1,legacy,legacyWithCatchUp}/*)
 REF_FILES = [f'{v}/{k}' for v in ('v1', 'legacy', 'legacyWithCatchUp')
              for k in ('headerOnly', 'headerAndBody', 'largeBody', 'withAnnotations', 'withMarkers')]

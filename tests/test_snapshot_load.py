@@ -20,7 +20,8 @@ import pytest
 
 from conftest import GOLDEN
 
-LOAD_SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny', 'markers', 'synth_markers', 'wide_many']
+LOAD_SETS = ['scenarios', 'synth_c1', 'synth_c3', 'synth_c4', 'synth_tiny', 'markers', 'synth_markers', 'wide_many',
+             'wide_xl']
 REF_DIR = os.path.join(GOLDEN, 'ref_snapshots')
 ERRS = {'MergeTree insert failed': 3, 'sequence#': 1, 'minSequence#': 2}
 

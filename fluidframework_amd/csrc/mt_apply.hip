@@ -113,17 +113,31 @@ struct Lds {
     uint64_t pk[LOC ? CAP : 1];
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
-    uint64_t ovx[W ? MT_OVX_WORDS * CAP : 1];  // (W) overlapping removers >= 64: u16 lists (mt_checksum.h)
+    uint64_t ovx[W ? 4 * CAP : 1];  // (W) overlapping removers >= 64: ids 0..15 of the u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
     uint64_t pxh[W ? CAP : 1];
-    uint64_t pxx[W ? 4 * CAP : 1];  // keys 16..31: [slot][4] (mt_state.h pxx)
     uint32_t wide;                // the document's mt_doc_scalars.wide bits
     uint32_t lkeys;               // its declared label keys (mt_doc_scalars.label_keys)
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
     // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
     uint32_t slab[LOC ? 1 : CAP];
+    // (W) the extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO), last: ids 16..31 of the overlap lists
+    // and keys 16..31 ([slot][4] each, mt_state.h pxx).  The HBM-workspace form keeps it here; the
+    // LDS-staged form launches without these members (kExtBytes less LDS) and stages the extension
+    // of the documents that use it in an HBM region of the same layout (Wave::ext)
+    uint64_t ovh[W ? 4 * CAP : 1];
+    uint64_t pxx[W ? 4 * CAP : 1];
+    static constexpr size_t kExtBytes = W ? 2 * 4 * CAP * sizeof(uint64_t) : 0;
 };
+// (the extension is the struct's tail: a launch may leave it out of its LDS)
+// the LDS of the wide form staged in LDS: Lds without the extension
+template <int CAP>
+constexpr size_t wl_lds_bytes() { return sizeof(Lds<CAP, false, true>) - Lds<CAP, false, true>::kExtBytes; }
+using LdsW256 = Lds<256, false, true>;
+using LdsW512 = Lds<512, false, true>;
+static_assert(offsetof(LdsW256, ovh) + LdsW256::kExtBytes == sizeof(LdsW256), "the wide extension ends Lds");
+static_assert(offsetof(LdsW512, ovh) + LdsW512::kExtBytes == sizeof(LdsW512), "the wide extension ends Lds");
 
 // G = false: the document is staged in the wave's LDS.  G = true (documents above 2048 segments,
 // SURVEY.md §8 a9 "unbounded B-tree"): the same structure lives in a per-wave workspace in HBM
@@ -167,6 +181,11 @@ struct Wave {
     const uint32_t textcap; // code units per half
     mt_event* const ev;     // the document's delta-event records (null: not recording)
     const uint32_t evcap;
+    // (W) the extension's region ([ovh][pxx] as in Lds), and its parts this launch stages (null: not
+    // staged -- mt_state.h MT_WIDE_XO / MT_WIDE_XK, decided by binning)
+    uint64_t* ext = nullptr;
+    uint64_t* xo_p = nullptr;
+    uint64_t* xk_p = nullptr;
     uint32_t rix = 0;       // index of the record being applied within its document
     mt_op_rec* rg = nullptr;  // (LOC) the document's regenerated-op buffer and its payload
     uint8_t* rgp = nullptr;
@@ -177,23 +196,27 @@ struct Wave {
           textcap(tc_bytes / (uint32_t)sizeof(TC)), ev(e), evcap(ec) {}
 
     // ------------------------------------------------------------ wide state
-    // removedClientOverlap holds client C (ids < 64: the bitmask; a wide document's others: ovx)
+    // removedClientOverlap holds client C (ids < 64: the bitmask; a wide document's others: ovx, and
+    // ovh with the extension)
+    MT_DEV const uint64_t* ovx_hi(int slot) const { return xo_p ? xo_p + 4 * slot : nullptr; }
     MT_DEV bool ovl_has(int slot, int C) const {
         if (C < 64) return C >= 0 && ((s.ovl[slot] >> C) & 1ull);
-        if constexpr (W) return mt_ovx_has(&s.ovx[MT_OVX_WORDS * slot], (uint32_t)C);
+        if constexpr (W) return mt_ovx_has2(&s.ovx[4 * slot], ovx_hi(slot), (uint32_t)C);
         return false;
     }
-    // addOverlappingClient (mergeTree.ts:2544-2552); false: a wide segment's ovx list is full
+    // addOverlappingClient (mergeTree.ts:2544-2552); false: a wide segment's list is full (16 ids
+    // without the extension -- binning gives a document that could get there the extension first)
     MT_DEV bool ovl_add(int slot, int C) {
         if (C < 64) {
             s.ovl[slot] |= 1ull << C;
             return true;
         }
         if constexpr (W) {
-            uint64_t* x = &s.ovx[MT_OVX_WORDS * slot];
-            if (mt_ovx_has(x, (uint32_t)C)) return true;
-            if (mt_ovx_id(x, MT_OVX_IDS - 1)) return false;  // full: MT_DERR_LIMITS
-            uint64_t out[MT_OVX_WORDS] = {};  // insert C into the ascending u16 list
+            uint64_t* lo = &s.ovx[4 * slot];
+            const uint64_t* hi = ovx_hi(slot);
+            if (mt_ovx_has2(lo, hi, (uint32_t)C)) return true;
+            if (mt_ovx_id2(lo, hi, xo_p ? MT_OVX_IDS - 1 : 15)) return false;  // full: MT_DERR_LIMITS
+            uint64_t out[8] = {};  // insert C into the ascending u16 list
             int j = 0;
             bool done = false;
             auto put = [&](uint32_t v) {
@@ -201,7 +224,7 @@ struct Wave {
                 j++;
             };
             for (int q = 0; q < MT_OVX_IDS; q++) {
-                const uint32_t v = mt_ovx_id(x, q);
+                const uint32_t v = mt_ovx_id2(lo, hi, q);
                 if (!v) break;
                 if (!done && (uint32_t)C < v) {
                     put((uint32_t)C);
@@ -210,23 +233,38 @@ struct Wave {
                 put(v);
             }
             if (!done) put((uint32_t)C);
-            for (int w = 0; w < MT_OVX_WORDS; w++) x[w] = out[w];
+            for (int w = 0; w < 4; w++) lo[w] = out[w];
+            if (xo_p)
+                for (int w = 0; w < 4; w++) xo_p[4 * slot + w] = out[4 + w];
             return true;
         }
         return false;
     }
+    // a slot's overlap list ids >= 64: copied from another slot / cleared
+    MT_DEV void ovx_copy(int t, int sl) {
+        for (int q = 0; q < 4; q++) s.ovx[4 * t + q] = s.ovx[4 * sl + q];
+        if (xo_p)
+            for (int q = 0; q < 4; q++) xo_p[4 * t + q] = xo_p[4 * sl + q];
+    }
+    MT_DEV void ovx_zero(int t) {
+        for (int q = 0; q < 4; q++) s.ovx[4 * t + q] = 0ull;
+        if (xo_p)
+            for (int q = 0; q < 4; q++) xo_p[4 * t + q] = 0ull;
+    }
     // (W) the words holding key k of a slot: its low-byte and high-byte words
     MT_DEV uint64_t* plo(int sl, int k) {
-        return k < 8 ? &s.props[sl] : k < 16 ? &s.pxl[sl] : &s.pxx[4 * sl + 2 * ((k - 16) >> 3)];
+        return k < 8 ? &s.props[sl] : k < 16 ? &s.pxl[sl] : xk_p + 4 * sl + 2 * ((k - 16) >> 3);
     }
     MT_DEV uint64_t* phi(int sl, int k) {
-        return k < 8 ? &s.ph[sl] : k < 16 ? &s.pxh[sl] : &s.pxx[4 * sl + 2 * ((k - 16) >> 3) + 1];
+        return k < 8 ? &s.ph[sl] : k < 16 ? &s.pxh[sl] : xk_p + 4 * sl + 2 * ((k - 16) >> 3) + 1;
     }
     // value id of key k of a slot (0 = absent)
     MT_DEV uint32_t pval(int sl, int k) {
         const int sh = 8 * (k & 7);
-        if constexpr (W)
+        if constexpr (W) {
+            if (k >= 16 && !xk_p) return 0u;
             return (uint32_t)((*plo(sl, k) >> sh) & 0xFFu) | ((uint32_t)((*phi(sl, k) >> sh) & 0xFFu) << 8);
+        }
         return k < 8 ? (uint32_t)((s.props[sl] >> sh) & 0xFFu) : 0u;
     }
     MT_DEV void pset(int sl, int k, uint32_t v) {
@@ -245,7 +283,8 @@ struct Wave {
         s.props[sl] = 0;
         if constexpr (W) {
             s.ph[sl] = s.pxl[sl] = s.pxh[sl] = 0;
-            for (int q = 0; q < 4; q++) s.pxx[4 * sl + q] = 0;
+            if (xk_p)
+                for (int q = 0; q < 4; q++) xk_p[4 * sl + q] = 0;
         }
     }
     MT_DEV void pcopy(int dst, int src) {
@@ -254,15 +293,17 @@ struct Wave {
             s.ph[dst] = s.ph[src];
             s.pxl[dst] = s.pxl[src];
             s.pxh[dst] = s.pxh[src];
-            for (int q = 0; q < 4; q++) s.pxx[4 * dst + q] = s.pxx[4 * src + q];
+            if (xk_p)
+                for (int q = 0; q < 4; q++) xk_p[4 * dst + q] = xk_p[4 * src + q];
         }
     }
     MT_DEV bool peq(int a, int b) const {
         if (s.props[a] != s.props[b]) return false;
         if constexpr (W) {
             if (s.ph[a] != s.ph[b] || s.pxl[a] != s.pxl[b] || s.pxh[a] != s.pxh[b]) return false;
-            for (int q = 0; q < 4; q++)
-                if (s.pxx[4 * a + q] != s.pxx[4 * b + q]) return false;
+            if (xk_p)
+                for (int q = 0; q < 4; q++)
+                    if (xk_p[4 * a + q] != xk_p[4 * b + q]) return false;
         }
         return true;
     }
@@ -714,7 +755,7 @@ struct Wave {
             s.rclient[t] = s.rclient[sl];
             s.ovl[t] = s.ovl[sl];
             if constexpr (W)
-                for (int q = 0; q < MT_OVX_WORDS; q++) s.ovx[MT_OVX_WORDS * t + q] = s.ovx[MT_OVX_WORDS * sl + q];
+                ovx_copy(t, sl);
             pcopy(t, sl);
             s.flags[t] = s.flags[sl];
             s.len[t] = s.len[sl] - (uint32_t)off;
@@ -1098,7 +1139,7 @@ struct Wave {
                 s.rclient[t] = lrm ? (CT)MT_LOAD_RCLIENT(op) : 0;
                 s.ovl[t] = 0;
                 if constexpr (W)
-                    for (int q = 0; q < MT_OVX_WORDS; q++) s.ovx[MT_OVX_WORDS * t + q] = 0;
+                    ovx_zero(t);
                 s.len[t] = (uint32_t)tlen;
                 s.toff[t] = top;
                 // a Marker (MT_F_MARKER): length 1, its arena byte is its ReferenceType
@@ -1609,7 +1650,7 @@ struct Wave {
         const int tlen = (int)((op.payload_len - plen) >> (wop ? 1 : 0));  // text code units
         const Pairs pr{pay + (op.payload_len - plen), np, wop};
         for (int q = 0; q < np; q++)
-            if (pr.key(q) >= pr.key_limit()) return fail(MT_DERR_LIMITS, S);
+            if (pr.key(q) >= pr.key_limit() || (W && pr.key(q) >= 16 && !xk_p)) return fail(MT_DERR_LIMITS, S);
         if (!noop) {
             if (op.pos1 < 0 || (type != MT_OP_INSERT && !load && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
             const int L = scan(op.ref_seq, C);  // cum for the op's view (no edit yet)
@@ -1812,9 +1853,18 @@ struct Wave {
         }
         const bool was_wide = (sc.wide & MT_WIDE_DOC) != 0;
         if constexpr (W) {
+            // the extension: staged when binning asks for it (every slot of the region: stored words
+            // for the document's segments, zeros for the rest)
+            xo_p = (sc.wide & MT_WIDE_XO) ? ext : nullptr;
+            xk_p = (sc.wide & MT_WIDE_XK) && ext ? ext + 4 * CAP : nullptr;
+            if (((sc.wide & MT_WIDE_XO) || (sc.wide & MT_WIDE_XK)) && !ext && lane == 0) s.err = MT_DERR_LIMITS;
+            const bool ov = was_wide && (sc.wide & MT_WIDE_XOV), kv = was_wide && (sc.wide & MT_WIDE_XKV);
+            for (int i = lane; i < CAP && (xo_p || xk_p); i += 64) {
+                for (int q = 0; q < 4 && xo_p; q++) xo_p[4 * i + q] = ov && i < n ? g.ovx[MT_OVX_WORDS * (so + i) + 4 + q] : 0ull;
+                for (int q = 0; q < 4 && xk_p; q++) xk_p[4 * i + q] = kv && i < n ? g.pxx[4 * (so + i) + q] : 0ull;
+            }
             for (int i = lane; i < n; i += 64) {
-                for (int q = 0; q < MT_OVX_WORDS; q++)
-                    s.ovx[MT_OVX_WORDS * i + q] = was_wide ? g.ovx[MT_OVX_WORDS * (so + i) + q] : 0ull;
+                for (int q = 0; q < 4; q++) s.ovx[4 * i + q] = was_wide ? g.ovx[MT_OVX_WORDS * (so + i) + q] : 0ull;
                 // (the short ids' high bytes; a narrow document's ids are below 64)
                 const uint32_t hi = was_wide ? g.chi[so + i] : 0u;
                 s.client[i] = (CT)(s.client[i] | ((hi & 0xFFu) << 8));
@@ -1822,7 +1872,6 @@ struct Wave {
                 s.ph[i] = was_wide ? g.ph[so + i] : 0ull;
                 s.pxl[i] = was_wide ? g.pxl[so + i] : 0ull;
                 s.pxh[i] = was_wide ? g.pxh[so + i] : 0ull;
-                for (int q = 0; q < 4; q++) s.pxx[4 * i + q] = was_wide ? g.pxx[4 * (so + i) + q] : 0ull;
             }
         }
         if (lane == 0) {
@@ -1999,14 +2048,25 @@ struct Wave {
             if (GW > 1 && s.lc.own >= 0) sc.wide = sc.wide | MT_WIDE_GROUPS;
         }
         if constexpr (W) {
+            int ovn = 0;  // the longest overlap list of ids >= 64 (binning's bound, mt_state.h MT_WIDE_OVN)
             for (int i = lane; i < nn; i += 64) {
                 const int sl = s.order[i];
-                for (int q = 0; q < MT_OVX_WORDS; q++) g.ovx[MT_OVX_WORDS * (so + i) + q] = s.ovx[MT_OVX_WORDS * sl + q];
+                for (int q = 0; q < 4; q++) g.ovx[MT_OVX_WORDS * (so + i) + q] = s.ovx[4 * sl + q];
                 g.chi[so + i] = (uint16_t)(((uint32_t)s.client[sl] >> 8) | (((uint32_t)s.rclient[sl] >> 8) << 8));
                 g.ph[so + i] = s.ph[sl];
                 g.pxl[so + i] = s.pxl[sl];
                 g.pxh[so + i] = s.pxh[sl];
-                for (int q = 0; q < 4; q++) g.pxx[4 * (so + i) + q] = s.pxx[4 * sl + q];
+                for (int q = 0; q < 4 && xo_p; q++) g.ovx[MT_OVX_WORDS * (so + i) + 4 + q] = xo_p[4 * sl + q];
+                for (int q = 0; q < 4 && xk_p; q++) g.pxx[4 * (so + i) + q] = xk_p[4 * sl + q];
+                int m = 0;
+                while (m < MT_OVX_IDS && mt_ovx_id2(&s.ovx[4 * sl], ovx_hi(sl), m)) m++;
+                ovn = max(ovn, m);
+            }
+            ovn = wave_max(ovn);
+            if (lane == 0) {
+                const uint32_t keep = s.wide & ~((0xFFu << MT_WIDE_OVN_SHIFT) | MT_WIDE_XOV);
+                g.sc[d].wide = keep | (xk_p ? MT_WIDE_XKV : 0u) | (xo_p && ovn > 16 ? MT_WIDE_XOV : 0u) |
+                               ((uint32_t)ovn << MT_WIDE_OVN_SHIFT);
             }
         }
         if constexpr (LOC) {
@@ -2166,6 +2226,7 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     LS& st = *reinterpret_cast<LS*>(ws + (size_t)w * sizeof(LS));
     Wave<CAP, true, LOC, W, GW> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                                    g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
+    if constexpr (W) wv.ext = st.ovh;  // (the extension: the workspace's own tail)
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -2186,21 +2247,24 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
 }
 
 // The wide form with the document staged in LDS (small wide documents: CAP <= 512, where its
-// ~112 B per slot still lets two or more waves share a CU)
+// ~112 B per slot still lets two or more waves share a CU); the extension (keys 16..31, overlap
+// ids past the 16th) of the documents that use it in an HBM region (wsx)
 template <int CAP>
 __global__ __launch_bounds__(64) void apply_kernel_wl(mt_gstate g, const mt_op_rec* __restrict__ ops,
                                                       const uint8_t* __restrict__ payload,
                                                       const uint32_t* __restrict__ row_ptr,
                                                       const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
-                                                      uint32_t op_lo, uint32_t op_cnt) {
+                                                      uint32_t op_lo, uint32_t op_cnt, uint64_t* __restrict__ wsx) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t w = blockIdx.x;
     if (w >= n_docs) return;
     const uint32_t d = doc_ids ? doc_ids[w] : w;
     using LS = Lds<CAP, false, true>;
-    LS& st = *reinterpret_cast<LS*>(smem);
+    LS& st = *reinterpret_cast<LS*>(smem);  // (launched without its extension members: LS::kExtBytes)
     Wave<CAP, false, false, true> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                                      g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
+    // the extension of the documents that stage it: an HBM region per wave, laid out as LS's tail
+    wv.ext = wsx ? wsx + (size_t)w * (LS::kExtBytes / sizeof(uint64_t)) : nullptr;
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -2295,13 +2359,17 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
 extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
                                            const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
                                            uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
-                                           hipStream_t stream) {
+                                           int xl, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     dim3 grid(n_docs), block(64);
     if (cap_class <= 512) {
+        // (the extension never takes LDS: with xl, ws holds it for the documents that stage it,
+        // mt_lds_bytes_wide per document)
 #define MT_LAUNCH_WL(CAPV)                                                                                   \
-        hipLaunchKernelGGL((mt::apply_kernel_wl<CAPV>), grid, block, sizeof(mt::Lds<CAPV, false, true>), stream, \
-                           *g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt);                       \
+        hipLaunchKernelGGL((mt::apply_kernel_wl<CAPV>), grid, block,                                         \
+                           mt::wl_lds_bytes<CAPV>(), stream,                                         \
+                           *g, ops, payload, row_ptr, doc_ids, n_docs, op_lo, op_cnt,                        \
+                           xl ? reinterpret_cast<uint64_t*>(ws) : nullptr);                                  \
         return hipGetLastError();
         if (cap_class <= 256) {
             MT_LAUNCH_WL(256)
@@ -2330,7 +2398,9 @@ extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, co
 }
 
 extern "C" size_t mt_lds_bytes_wide(int cap_class) {
-    if (cap_class <= 512) return 0;  // (staged in LDS: no workspace)
+    // (staged in LDS: the workspace holds only the extension, for launches that stage it)
+    if (cap_class <= 256) return mt::Lds<256, false, true>::kExtBytes;
+    if (cap_class <= 512) return mt::Lds<512, false, true>::kExtBytes;
     if (cap_class <= 1024) return sizeof(mt::Lds<1024, false, true>);
     switch (cap_class) {
         case 2048: return sizeof(mt::Lds<2048, false, true>);

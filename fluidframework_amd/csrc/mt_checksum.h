@@ -57,7 +57,14 @@ MT_HD static inline uint64_t mt_finish_checksum(uint64_t seg_sum, uint64_t tree_
 }
 
 // ---- readers of a document's HBM state, narrow or wide (mt_state.h) ------------------------------
+// form: 0 narrow; a wide document: 1, plus 2 when its stored keys 16..31 are valid (MT_WIDE_XKV) and
+// 4 when its stored overlap ids past the 16th are (MT_WIDE_XOV); a reader never looks at words a
+// document has not stored
+MT_HD static inline int mt_form(bool wide, uint32_t wbits) {
+    return wide ? 1 | ((wbits & MT_WIDE_XKV) ? 2 : 0) | ((wbits & MT_WIDE_XOV) ? 4 : 0) : 0;
+}
 // the two words (low bytes, high bytes) holding key k's value id of a wide segment at HBM index i
+// (k >= 16: forms with stored keys 16..31 only)
 MT_HD static inline void mt_gpwords(const mt_gstate& g, size_t i, int k, uint64_t& lo, uint64_t& hi) {
     if (k < 8) {
         lo = g.props[i];
@@ -72,45 +79,52 @@ MT_HD static inline void mt_gpwords(const mt_gstate& g, size_t i, int k, uint64_
     }
 }
 // segment at HBM index i (= doc * segcap + position): value id of key k
-MT_HD static inline uint32_t mt_gprop(const mt_gstate& g, bool wide, size_t i, int k) {
+MT_HD static inline uint32_t mt_gprop(const mt_gstate& g, int form, size_t i, int k) {
     const int sh = 8 * (k & 7);
-    if (!wide) return k < 8 ? (uint32_t)((g.props[i] >> sh) & 0xFFu) : 0u;
+    if (!form) return k < 8 ? (uint32_t)((g.props[i] >> sh) & 0xFFu) : 0u;
+    if (k >= 16 && !(form & 2)) return 0u;
     uint64_t lo, hi;
     mt_gpwords(g, i, k, lo, hi);
     return (uint32_t)((lo >> sh) & 0xFFu) | ((uint32_t)((hi >> sh) & 0xFFu) << 8);
 }
 // matchProperties' value comparison of two segments (properties.ts:62-93)
-MT_HD static inline bool mt_gprops_eq(const mt_gstate& g, bool wide, size_t a, size_t b) {
+MT_HD static inline bool mt_gprops_eq(const mt_gstate& g, int form, size_t a, size_t b) {
     if (g.props[a] != g.props[b]) return false;
-    if (!wide) return true;
+    if (!form) return true;
     if (g.ph[a] != g.ph[b] || g.pxl[a] != g.pxl[b] || g.pxh[a] != g.pxh[b]) return false;
-    for (int q = 0; q < 4; q++)
-        if (g.pxx[4 * a + q] != g.pxx[4 * b + q]) return false;
+    if (form & 2)
+        for (int q = 0; q < 4; q++)
+            if (g.pxx[4 * a + q] != g.pxx[4 * b + q]) return false;
     return true;
 }
-MT_HD static inline uint64_t mt_gprops_term(const mt_gstate& g, bool wide, size_t i) {
-    return wide ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i], g.pxx + 4 * i) : g.props[i];
+MT_HD static inline uint64_t mt_gprops_term(const mt_gstate& g, int form, size_t i) {
+    return form ? mt_props_term(g.props[i], g.ph[i], g.pxl[i], g.pxh[i], (form & 2) ? g.pxx + 4 * i : nullptr)
+                : g.props[i];
 }
 // A wide segment's overlapping removers >= 64: up to MT_OVX_IDS (32) u16 ids, ascending from the low
-// half-word of x[0], 0 = none (mt_state.h ovx, MT_OVX_WORDS words per segment)
+// half-word of lo[0]: ids 0..15 in the four words `lo`, ids 16..31 in the four words `hi` (null: none,
+// a document without its extension in use); 0 = none.  At rest both are one row of MT_OVX_WORDS words
+// per segment (mt_state.h ovx); the LDS engine stages them as two arrays (mt_apply.hip Lds).
 #define MT_OVX_WORDS 8
-MT_HD static inline uint32_t mt_ovx_id(const uint64_t* x, int q) {
-    return (uint32_t)(x[q >> 2] >> (16 * (q & 3))) & 0xFFFFu;
+MT_HD static inline uint32_t mt_ovx_id2(const uint64_t* lo, const uint64_t* hi, int q) {
+    const uint64_t* x = q < 16 ? lo : hi;
+    q &= 15;
+    return x ? (uint32_t)(x[q >> 2] >> (16 * (q & 3))) & 0xFFFFu : 0u;
 }
-MT_HD static inline bool mt_ovx_has(const uint64_t* x, uint32_t c) {
-    for (int q = 0; q < 4 * MT_OVX_WORDS; q++) {
-        const uint32_t v = mt_ovx_id(x, q);
+MT_HD static inline bool mt_ovx_has2(const uint64_t* lo, const uint64_t* hi, uint32_t c) {
+    for (int q = 0; q < MT_OVX_IDS; q++) {
+        const uint32_t v = mt_ovx_id2(lo, hi, q);
         if (!v) return false;
         if (v == c) return true;
     }
     return false;
 }
-MT_HD static inline uint64_t mt_ovx_hash(const uint64_t* x) {
+MT_HD static inline uint64_t mt_ovx_hash2(const uint64_t* lo, const uint64_t* hi) {
     uint64_t packed = 0, h = 0x9E3779B97F4A7C15ull;
     bool small = true;
     int n = 0;
-    for (; n < 4 * MT_OVX_WORDS; n++) {
-        const uint32_t v = mt_ovx_id(x, n);
+    for (; n < MT_OVX_IDS; n++) {
+        const uint32_t v = mt_ovx_id2(lo, hi, n);
         if (!v) break;
         if (v > 255u || n >= 8) small = false;
         else packed |= (uint64_t)v << (8 * n);
@@ -119,6 +133,11 @@ MT_HD static inline uint64_t mt_ovx_hash(const uint64_t* x) {
     if (!n) return 0;
     return small ? packed : (h ? h : 1ull);
 }
+// the at-rest list of the segment at HBM index i
+MT_HD static inline const uint64_t* mt_govx_lo(const mt_gstate& g, size_t i) { return g.ovx + MT_OVX_WORDS * i; }
+MT_HD static inline const uint64_t* mt_govx_hi(const mt_gstate& g, int form, size_t i) {
+    return (form & 4) ? g.ovx + MT_OVX_WORDS * i + 4 : nullptr;
+}
 // the short client ids of the segment at HBM index i (a wide document's ids >= 256 via chi)
 MT_HD static inline uint32_t mt_gclient(const mt_gstate& g, bool wide, size_t i) {
     return (uint32_t)g.client[i] | (wide && g.chi ? (uint32_t)(g.chi[i] & 0xFFu) << 8 : 0u);
@@ -126,8 +145,8 @@ MT_HD static inline uint32_t mt_gclient(const mt_gstate& g, bool wide, size_t i)
 MT_HD static inline uint32_t mt_grclient(const mt_gstate& g, bool wide, size_t i) {
     return (uint32_t)g.rclient[i] | (wide && g.chi ? (uint32_t)(g.chi[i] >> 8) << 8 : 0u);
 }
-MT_HD static inline uint64_t mt_govl_term(const mt_gstate& g, bool wide, size_t i) {
-    return wide ? mt_ovl_term(g.ovl[i], mt_ovx_hash(g.ovx + MT_OVX_WORDS * i)) : g.ovl[i];
+MT_HD static inline uint64_t mt_govl_term(const mt_gstate& g, int form, size_t i) {
+    return form ? mt_ovl_term(g.ovl[i], mt_ovx_hash2(mt_govx_lo(g, i), mt_govx_hi(g, form, i))) : g.ovl[i];
 }
 // code unit q of the text at arena unit offset `off` of document d (its current half)
 MT_HD static inline uint32_t mt_gtext(const mt_gstate& g, uint32_t d, const mt_doc_scalars& sc, uint32_t off) {

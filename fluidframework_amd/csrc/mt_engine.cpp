@@ -37,7 +37,7 @@ extern "C" hipError_t mt_launch_apply_big(int cap_class, const mt_gstate* g, con
                                           hipStream_t stream);
 extern "C" hipError_t mt_launch_apply_wide(int cap_class, const mt_gstate* g, const mt_op_rec* ops,
                                            const uint8_t* payload, const uint32_t* row_ptr, const uint32_t* doc_ids,
-                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws,
+                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, uint8_t* ws, int xl,
                                            hipStream_t stream);
 extern "C" size_t mt_lds_bytes_wide(int cap_class);
 extern "C" hipError_t mt_launch_apply_loc_big(int cap_class, int gw, const mt_gstate* g, const mt_op_rec* ops,
@@ -53,7 +53,7 @@ extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint3
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
                                     int first_wide, uint32_t* counts, uint32_t* ids, const mt_op_rec* ops,
-                                    unsigned long long* acc, hipStream_t st);
+                                    const uint8_t* payload, unsigned long long* acc, hipStream_t st);
 extern "C" hipError_t mt_launch_checksum(const mt_gstate* g, uint32_t n_docs, uint64_t* out, hipStream_t st);
 extern "C" hipError_t mt_launch_stacks(const mt_gstate* g, const mt_tile_query* q, uint32_t n, uint32_t cap,
                                        mt_stack_item* items, uint32_t* depth, hipStream_t st);
@@ -105,6 +105,9 @@ constexpr int kLocForms = 8;
 const int32_t kLocCaps[kLocForms] = {256, 512, 2048, 4096, 1024, 4096, 8192, 8192};
 const int32_t kLocGW[kLocForms] = {1, 1, 1, 1, MT_LOC_GW, MT_LOC_GW, 1, MT_LOC_GW};
 constexpr int kBuckets = kNumClasses + 1 + kWideClasses + 2 * kFirstLds + kLocForms;
+// binning's counters: one per bucket, then per wide bucket the documents that stage the wide form's
+// extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO) -- their launch takes an HBM region for it
+constexpr int kCounts = kBuckets + kWideClasses;
 // per-class statistics: the classes, the editing bucket, the LDS engine inside each register class,
 // the register engine's C64 form per class, the other editing forms
 constexpr int kStatClasses = kNumClasses + 1 + 2 * kFirstLds + kLocForms + kWideClasses;
@@ -459,13 +462,13 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) || (st = dalloc(e, &g.locbig, D)) ||
         (st = dalloc(e, &g.locgx, D)) ||
         // (the editing documents' and the wide documents' buckets after the capacity classes)
-        (st = dalloc(e, &e->d_counts, kBuckets)) || (st = dalloc(e, &e->d_acc, kBuckets)) ||
+        (st = dalloc(e, &e->d_counts, kCounts)) || (st = dalloc(e, &e->d_acc, kBuckets)) ||
         (st = dalloc(e, &e->d_ids, D * kBuckets))) {
         mt_engine_destroy(e);
         return st;
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&e->h_counts, kBuckets * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_counts, kCounts * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
         mt_engine_destroy(e);
         return MT_ERR_HIP;
@@ -940,10 +943,10 @@ static mt_status apply_launches(mt_engine* e, const mt_batch* b, uint32_t& nk) {
     const int lds_base = e->n_classes + 1 + (e->n_classes > kFirstWide ? e->n_classes - kFirstWide : 0);
     for (uint32_t t = 0; t < ticks; t++) {
         const uint32_t lo = t * per;
-        HIP_OK(hipMemsetAsync(e->d_counts, 0, kBuckets * sizeof(uint32_t), e->stream));
+        HIP_OK(hipMemsetAsync(e->d_counts, 0, kCounts * sizeof(uint32_t), e->stream));
         HIP_OK(mt_launch_bin(&e->g, b->row_ptr, b->n_docs, lo, per, e->d_classes, e->n_classes, e->first_lds,
-                             kFirstWide, e->d_counts, e->d_ids, b->ops, e->d_acc, e->stream));
-        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kBuckets * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             kFirstWide, e->d_counts, e->d_ids, b->ops, b->payload, e->d_acc, e->stream));
+        HIP_OK(hipMemcpyAsync(e->h_counts, e->d_counts, kCounts * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
         // the classes above 2048 segments keep each document's structure in an HBM workspace
@@ -954,9 +957,13 @@ static mt_status apply_launches(mt_engine* e, const mt_batch* b, uint32_t& nk) {
             ws_off[c] = need;
             need += (size_t)e->h_counts[c] * mt_lds_bytes(kClasses[c]);
         }
+        // (the LDS-staged wide classes take a region only when some document stages the extension)
+        const int n_bk = lds_base + 2 * e->first_lds + kLocForms;
         for (int c = kFirstWide; c < e->n_classes; c++) {
             wws_off[c] = need;
-            need += (size_t)e->h_counts[e->n_classes + 1 + (c - kFirstWide)] * mt_lds_bytes_wide(kClasses[c]);
+            const bool xl_any = e->h_counts[n_bk + (c - kFirstWide)] != 0;
+            if (kClasses[c] > 512 || xl_any)
+                need += (size_t)e->h_counts[e->n_classes + 1 + (c - kFirstWide)] * mt_lds_bytes_wide(kClasses[c]);
         }
         size_t lws_off[kLocForms] = {};
         for (int q = 0; q < kLocForms; q++) {
@@ -1055,8 +1062,11 @@ static mt_status apply_launches(mt_engine* e, const mt_batch* b, uint32_t& nk) {
                 e->kev.push_back(ev);
             }
             HIP_OK(hipEventRecord(e->kev[2 * nk], st));
+            // (the extension's region only when one of the bucket's documents stages it)
+            const bool xl = e->h_counts[lds_base + 2 * e->first_lds + kLocForms + (c - kFirstWide)] != 0;
             HIP_OK(mt_launch_apply_wide(kClasses[c], &e->g, b->ops, b->payload, b->row_ptr,
-                                        e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], st));
+                                        e->d_ids + (size_t)k * b->n_docs, cnt, lo, per, e->ws + wws_off[c], xl ? 1 : 0,
+                                        st));
             HIP_OK(hipEventRecord(e->kev[2 * nk + 1], st));
             e->kev_cls.push_back(kStatWide + (c - kFirstWide));
             nk++;
@@ -1516,10 +1526,10 @@ static mt_status synth_generate(mt_engine* e, const mt_synth_cfg* cfg, uint32_t 
     if (r == hipSuccess) r = hipMemsetAsync(pay_used, 0, (size_t)n * sizeof(uint32_t), e->stream);
     const uint32_t tick = 64;
     for (uint32_t lo = 0; r == hipSuccess && lo < per; lo += tick) {
-        r = hipMemsetAsync(e->d_counts, 0, kBuckets * sizeof(uint32_t), e->stream);
+        r = hipMemsetAsync(e->d_counts, 0, kCounts * sizeof(uint32_t), e->stream);
         if (r == hipSuccess)
             r = mt_launch_bin(&e->g, b->row_ptr, n, lo, tick, e->d_classes, std::min(e->n_classes, kLdsClasses), 0,
-                              kFirstWide, e->d_counts, e->d_ids, nullptr, nullptr, e->stream);
+                              kFirstWide, e->d_counts, e->d_ids, nullptr, nullptr, nullptr, e->stream);
         if (r == hipSuccess)
             r = hipMemcpyAsync(e->h_counts, e->d_counts, kNumClasses * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                e->stream);
@@ -1750,6 +1760,7 @@ struct HostDoc {
     uint32_t prop(int i, int k) const {
         const int sh = 8 * (k & 7);
         if (!wide) return k < 8 ? (uint32_t)((props[i] >> sh) & 0xFF) : 0u;
+        if (k >= 16 && !(sc.wide & MT_WIDE_XKV)) return 0u;  // (no keys 16..31 stored)
         const uint64_t lo = k < 8 ? props[i] : k < 16 ? pxl[i] : pxx[4 * (size_t)i + 2 * ((k - 16) >> 3)];
         const uint64_t hi = k < 8 ? ph[i] : k < 16 ? pxh[i] : pxx[4 * (size_t)i + 2 * ((k - 16) >> 3) + 1];
         return (uint32_t)((lo >> sh) & 0xFF) | ((uint32_t)((hi >> sh) & 0xFF) << 8);
@@ -1759,8 +1770,9 @@ struct HostDoc {
         for (int c = 0; c < 64; c++)
             if ((ovl[i] >> c) & 1) v.push_back(c);
         if (wide) {
+            const uint64_t* x = ovx.data() + (size_t)MT_OVX_WORDS * i;
             for (int q = 0; q < MT_OVX_IDS; q++) {
-                const int c = (int)mt_ovx_id(ovx.data() + (size_t)MT_OVX_WORDS * i, q);
+                const int c = (int)mt_ovx_id2(x, (sc.wide & MT_WIDE_XOV) ? x + 4 : nullptr, q);
                 if (!c) break;
                 v.push_back(c);
             }

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
     const uint32_t ucap = wdoc ? g.textcap / 2 : g.textcap;  // code units per arena half
     uint16_t* arena16 = reinterpret_cast<uint16_t*>(arena);
     uint32_t carry = 0;
+    bool key16 = false;  // a segment with a key >= 16: keys 16..31 in use (mt_state.h MT_WIDE_XK)
     for (int base = 0; base < ns && !err; base += 64) {
         const int i = base + lane;
         mt_load_seg sg{};
@@ -151,6 +152,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
                 g.pxl[so + i] = w4[2];
                 g.pxh[so + i] = w4[3];
                 for (int q = 0; q < 4; q++) g.pxx[4 * (so + i) + q] = w4[4 + q];
+                key16 = key16 || (w4[4] | w4[5] | w4[6] | w4[7]) != 0;
             }
             g.client[so + i] = sg.client;
             g.rclient[so + i] = rm ? sg.rclient : 0;
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
         }
     }
     const uint32_t lkeys = g.sc[d].label_keys;  // (declared keys outlive a load)
+    const bool xl = wave_ballot(key16) != 0;
     if (lane == 0) {
         mt_doc_scalars sc{};
         sc.win_op = -1;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
             sc.n_empty = ns == 0 ? 1u : 0u;
             sc.text_top = carry;
             sc.wide = (wdoc || lkeys != MT_NO_LABEL_KEYS ? MT_WIDE_LDS : 0u) | (lds ? MT_WIDE_C64 : 0u) |
-                      (wdoc ? MT_WIDE_DOC : 0u);
+                      (wdoc ? MT_WIDE_DOC : 0u) | (xl ? MT_WIDE_XK | MT_WIDE_XKV : 0u);
         }
         sc.cur_seq = cur_seq[w];
         sc.min_seq = min_seq[w];
@@ -216,8 +219,10 @@ __global__ __launch_bounds__(64) void mt_load_kernel(mt_gstate g, uint32_t n, co
 __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr, uint32_t n_docs, uint32_t op_lo,
                               uint32_t op_cnt, const int32_t* __restrict__ classes, int n_classes, int first_lds,
                               int first_wide, uint32_t* __restrict__ counts, uint32_t* __restrict__ ids,
-                              const mt_op_rec* __restrict__ ops, unsigned long long* __restrict__ acc) {
+                              const mt_op_rec* __restrict__ ops, const uint8_t* __restrict__ payload,
+                              unsigned long long* __restrict__ acc) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 8;
     int c = -1;
     unsigned long long bytes = 0;
     if (d < n_docs) {
@@ -237,6 +242,10 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             bool lds_only = false, editing = own >= 0;
             const uint32_t pend = own >= 0 ? g.loc[d].ghi - g.loc[d].glo : 0u;  // pending edits
             uint32_t nloc = 0, nregen = 0;  // (an editing document: its local edits / reconnects here)
+            // the wide form's extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO): a property key >= 16 in
+            // this launch, and removes by ids >= 64 that could grow an overlap list past 16
+            bool key16 = false;
+            uint32_t nrem_hi = 0;
             unsigned long long ob = 0;
             // one pass over this launch's records (each is read once: the loops below were separate)
             bool win = ops && sc.win_op < 0;
@@ -249,6 +258,16 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 nloc += o.seq == -1 ? 1u : 0u;
                 nregen += o.seq == MT_SEQ_REGEN ? 1u : 0u;
                 ob += 32ull + o.payload_len;
+                nrem_hi += (ty == MT_OP_REMOVE && o.client >= MT_MAX_CLIENTS) ? 1u : 0u;
+                if (o.type & MT_OP_WIDE) {
+                    const uint32_t np = MT_OP_NPAIRS(o);
+                    if (np && (!payload || o.payload_len < 3u * np)) {
+                        key16 = true;  // (unread pairs: the extension, to be safe)
+                    } else {
+                        const uint8_t* pp = payload + o.payload_off + (o.payload_len - 3u * np);
+                        for (uint32_t q = 0; q < np; q++) key16 = key16 || pp[3 * q] >= 16;
+                    }
+                }
                 if (!wdoc0) {
                     const uint32_t c = o.client;
                     const bool load = ty == MT_OP_LOAD;
@@ -321,6 +340,13 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                         }
                     }
                     c = n_classes + 1 + (c - first_wide);
+                    const bool xk = (sc.wide & MT_WIDE_XK) || key16;
+                    const bool xo = MT_WIDE_OVN(sc.wide) + nrem_hi > 16u;
+                    const uint32_t w0 = g.sc[d].wide;
+                    const uint32_t w1 = (w0 & ~MT_WIDE_XO) | (xk ? MT_WIDE_XK : 0u) | (xo ? MT_WIDE_XO : 0u);
+                    if (w1 != w0) g.sc[d].wide = w1;
+                    // (per wide bucket: how many of its documents stage the extension)
+                    if (xk || xo) atomicAdd(&counts[n_buckets + (c - (n_classes + 1))], 1u);
                 }
             }
             if (!wdoc && c < first_lds && (needs_lds || c64)) {
@@ -357,7 +383,6 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
         }
     }
     const int lane = (int)(threadIdx.x & 63u);
-    const int n_buckets = n_classes + 1 + (n_classes > first_wide ? n_classes - first_wide : 0) + 2 * first_lds + 8;
     for (int k = 0; k < n_buckets; k++) {
         const uint64_t m = wave_ballot(c == k);
         if (!m) continue;
@@ -394,13 +419,14 @@ __global__ void mt_fixup_kernel(mt_gstate g, const mt_op_rec* __restrict__ ops, 
     const int32_t R = o.ref_seq;
     const uint32_t C = o.client;
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+    const int form = mt_form(wdoc, sc.wide);
     int64_t len = 0;
     for (int i = 0; i < sc.nseg; i++) {  // nodeLength leaf branch (mergeTree.ts:1667-1697)
         // (an editing client's pending local edits carry seq / removedSeq -1, UnassignedSequenceNumber,
         // which no refSeq has seen)
         const bool seen = mt_gclient(g, wdoc, so + i) == C || (g.seq[so + i] != -1 && g.seq[so + i] <= R);
         const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
-                               : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
+                               : (wdoc && mt_ovx_has2(mt_govx_lo(g, so + i), mt_govx_hi(g, form, so + i), C));
         const bool hid = (g.flags[so + i] & MT_SF_REMOVED) &&
                          (mt_grclient(g, wdoc, so + i) == C || ov || (g.rseq[so + i] != -1 && g.rseq[so + i] <= R));
         if (seen && !hid) len += g.len[so + i];
@@ -416,6 +442,7 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
     const mt_doc_scalars sc = g.sc[d];
     const size_t so = (size_t)d * g.segcap;
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+    const int form = mt_form(wdoc, sc.wide);
     uint64_t seg_sum = 0;
     for (int i = lane; i < sc.nseg; i += 64) {
         uint64_t h = MT_FNV_INIT;
@@ -426,8 +453,8 @@ __global__ __launch_bounds__(64) void mt_checksum_kernel(mt_gstate g, uint32_t n
         const bool rm = f & MT_SF_REMOVED;
         seg_sum += mt_seg_hash((uint64_t)i, h, g.seq[so + i], mt_canon_client(mt_gclient(g, wdoc, so + i)),
                                rm ? g.rseq[so + i] : -1, rm ? (int32_t)mt_grclient(g, wdoc, so + i) : -1,
-                               mt_govl_term(g, wdoc, so + i),
-                               mt_gprops_term(g, wdoc, so + i), (f & MT_SF_PDEF) ? 1u : 0u);
+                               mt_govl_term(g, form, so + i),
+                               mt_gprops_term(g, form, so + i), (f & MT_SF_PDEF) ? 1u : 0u);
     }
     uint64_t tree_sum = 0;
     for (int L = 0; L < sc.nlev; L++) {
@@ -459,9 +486,9 @@ extern "C" hipError_t mt_launch_load(const mt_gstate* g, uint32_t n, const uint3
 extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr, uint32_t n_docs, uint32_t op_lo,
                                     uint32_t op_cnt, const int32_t* classes, int n_classes, int first_lds,
                                     int first_wide, uint32_t* counts, uint32_t* ids, const mt_op_rec* ops,
-                                    unsigned long long* acc, hipStream_t st) {
+                                    const uint8_t* payload, unsigned long long* acc, hipStream_t st) {
     hipLaunchKernelGGL(mt_bin_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, row_ptr, n_docs, op_lo, op_cnt,
-                       classes, n_classes, first_lds, first_wide, counts, ids, ops, acc);
+                       classes, n_classes, first_lds, first_wide, counts, ids, ops, payload, acc);
     return hipGetLastError();
 }
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st) {
@@ -493,9 +520,9 @@ MT_DEV void mt_leaf_block_of(const mt_gstate& g, uint32_t d, const mt_doc_scalar
 // The value id of label key `key` of segment i as the query sees it: a stale marker (MT_SF_STALE) outside
 // the search path's leaf block [blo, bhi) answers with the labels its block's caches still hold
 // (HierMergeBlock rightmostTiles / leftmostTiles / rangeStacks, rebuilt by blockUpdate only)
-MT_DEV uint32_t mt_label_vid(const mt_gstate& g, bool wdoc, size_t so, int i, uint32_t key, uint32_t lkeys, int blo,
+MT_DEV uint32_t mt_label_vid(const mt_gstate& g, int form, size_t so, int i, uint32_t key, uint32_t lkeys, int blo,
                              int bhi) {
-    uint32_t v = mt_gprop(g, wdoc, so + i, key);
+    uint32_t v = mt_gprop(g, form, so + i, key);
     if (lkeys != MT_NO_LABEL_KEYS && g.slab && (i < blo || i >= bhi) && (g.flags[so + i] & MT_SF_STALE)) {
         const uint32_t sl = g.slab[so + i];
         if (key == (lkeys & 0xFFu)) v = sl & 0xFFFFu;
@@ -535,7 +562,7 @@ __global__ __launch_bounds__(64) void mt_tiles_kernel(mt_gstate g, const mt_tile
     auto labeled = [&](int i) -> bool {  // refHasTileLabel (mergeTree.ts:581-597)
         if (qq.key >= MT_MAX_KEYS_WIDE || !(g.flags[so + i] & MT_SF_MARKER) || !(mt_gtext(g, d, sc, g.toff[so + i]) & 1u))
             return false;
-        const uint32_t v = mt_label_vid(g, wdoc, so, i, qq.key, sc.label_keys, blo, bhi);
+        const uint32_t v = mt_label_vid(g, mt_form(wdoc, sc.wide), so, i, qq.key, sc.label_keys, blo, bhi);
         return v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
     };
     auto local_len = [&](int i) -> int { return (g.flags[so + i] & MT_SF_REMOVED) ? 0 : (int)g.len[so + i]; };
@@ -644,6 +671,7 @@ __global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_po
     const int n = sc.nseg;
     const size_t so = (size_t)d * g.segcap;
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+    const int form = mt_form(wdoc, sc.wide);
     const bool local = qq.ref_seq == MT_POS_LOCAL;
     const int32_t R = qq.ref_seq;
     const uint32_t C = qq.client;
@@ -653,7 +681,7 @@ __global__ __launch_bounds__(64) void mt_resolve_kernel(mt_gstate g, const mt_po
         // (pending local edits: seq / removedSeq -1, UnassignedSequenceNumber, seen by no refSeq)
         const bool seen = mt_gclient(g, wdoc, so + i) == C || (g.seq[so + i] != -1 && g.seq[so + i] <= R);
         const bool ov = C < 64 ? ((g.ovl[so + i] >> C) & 1ull) != 0
-                               : (wdoc && mt_ovx_has(g.ovx + MT_OVX_WORDS * (so + i), C));
+                               : (wdoc && mt_ovx_has2(mt_govx_lo(g, so + i), mt_govx_hi(g, form, so + i), C));
         const bool hid = rm && (mt_grclient(g, wdoc, so + i) == C || ov || (g.rseq[so + i] != -1 && g.rseq[so + i] <= R));
         return (seen && !hid) ? (int)g.len[so + i] : 0;
     };
@@ -710,8 +738,10 @@ __global__ void mt_seginfo_kernel(mt_gstate g, const uint32_t* __restrict__ docs
         r.toff = g.toff[so];
         r.wide = wdoc ? 1u : 0u;
         r.overlap = g.ovl[so];
-        for (int q = 0; q < MT_OVX_IDS; q++) r.overlap_hi[q] = wdoc ? (uint16_t)mt_ovx_id(g.ovx + MT_OVX_WORDS * so, q) : 0;
-        for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) r.props[k] = (uint16_t)mt_gprop(g, wdoc, so, k);
+        const int form = mt_form(wdoc, sc.wide);
+        for (int q = 0; q < MT_OVX_IDS; q++)
+            r.overlap_hi[q] = wdoc ? (uint16_t)mt_ovx_id2(mt_govx_lo(g, so), mt_govx_hi(g, form, so), q) : 0;
+        for (int k = 0; k < MT_MAX_KEYS_WIDE; k++) r.props[k] = (uint16_t)mt_gprop(g, form, so, k);
     }
     out[w] = r;
 }
@@ -747,7 +777,7 @@ __global__ __launch_bounds__(64) void mt_stacks_kernel(mt_gstate g, const mt_til
         bool cand = false;
         if (i < n && ll > 0 && start <= pos && qq.key < MT_MAX_KEYS_WIDE && (g.flags[so + i] & MT_SF_MARKER)) {
             rt = mt_gtext(g, d, sc, g.toff[so + i]);
-            const uint32_t v = mt_label_vid(g, wdoc, so, i, qq.key, sc.label_keys, blo, bhi);
+            const uint32_t v = mt_label_vid(g, mt_form(wdoc, sc.wide), so, i, qq.key, sc.label_keys, blo, bhi);
             cand = (rt & 6u) && v != 0 && v < 256 && ((qq.vmask[v >> 5] >> (v & 31)) & 1u);
         }
         uint64_t m = wave_ballot(cand);
@@ -822,6 +852,7 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
     const int32_t msn = sc.min_seq;
     const size_t so = (size_t)d * g.segcap;
     const bool wdoc = (sc.wide & MT_WIDE_DOC) != 0;
+    const int form = mt_form(wdoc, sc.wide);
     uint32_t* out = specs + (size_t)w * cap * 3;
     int k = 0;
     bool have = false;
@@ -867,7 +898,7 @@ __global__ __launch_bounds__(64) void mt_snapshot_kernel(mt_gstate g, uint32_t d
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), j) << 32);
             if (have && !((pfl | fj) & MT_SF_MARKER) && !(pfl & MT_SF_NL) && (plen <= 256u || lj <= 256u) &&
                 ((pfl ^ fj) & MT_SF_PDEF) == 0 &&
-                pprops == pj && (!wdoc || mt_gprops_eq(g, true, so + ps, so + base + j))) {
+                pprops == pj && (!wdoc || mt_gprops_eq(g, form, so + ps, so + base + j))) {
                 pc = base + j - ps + 1;  // span from the run's first segment (elided ones inside it skipped by the reader)
                 plen += lj;
                 pfl = (pfl & ~MT_SF_NL) | (fj & MT_SF_NL);

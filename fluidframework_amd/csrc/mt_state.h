@@ -54,6 +54,22 @@ struct mt_doc_scalars {      // 84 bytes
 #define MT_WIDE_C64 4u  // has seen a client id above 32: 64-bit overlap sets (register engine: its C64 form)
 #define MT_WIDE_GROUPS 8u  // an editing document past 64 pending edits at once: the editing form with
                            // MT_LOC_GROUPS_WIDE group slots (its HBM-workspace form), for good
+// The wide form's extension: property keys 16..31 (pxx) and overlapping removers >= 64 past the 16th
+// per segment (ovx words 4..7).  It never takes LDS: a launch stages it in an HBM workspace region
+// per document (the LDS-staged classes) or in the document's HBM workspace (the others), and only
+// for the documents binning asks it for (mt_bin_kernel):
+//   MT_WIDE_XK  keys >= 16 in use, for good (a key >= 16 in a launch's ops, or in a loaded snapshot);
+//   MT_WIDE_XO  this launch may grow an overlap list past 16 ids: the longest list at the last store
+//               (MT_WIDE_OVN) plus the launch's removes by ids >= 64 exceeds 16 (set or cleared per launch);
+//   MT_WIDE_XKV / MT_WIDE_XOV  the at-rest pxx / ovx words 4..7 are valid (written by the last store):
+//               what readers test (mt_checksum.h mt_form).
+#define MT_WIDE_XK 16u
+#define MT_WIDE_XKV 32u
+#define MT_WIDE_XO 64u
+#define MT_WIDE_XOV 128u
+// bits 24..31: the longest overlap list of ids >= 64 of any segment at the document's last store
+#define MT_WIDE_OVN_SHIFT 24
+#define MT_WIDE_OVN(w) ((uint32_t)(w) >> MT_WIDE_OVN_SHIFT)
 
 // An editing client's document (client.ts:163-214, 588-625): its local
 // edits are pending until their acks.  Pending edit ordinals [glo, ghi) (at most 64 at once) index

@@ -39,6 +39,16 @@ MT_DEV int wave_sum(int v) {
     return v;
 }
 
+MT_DEV int wave_max(int v) {
+    v = max(v, __shfl_xor(v, 1, 64));
+    v = max(v, __shfl_xor(v, 2, 64));
+    v = max(v, __shfl_xor(v, 4, 64));
+    v = max(v, __shfl_xor(v, 8, 64));
+    v = max(v, __shfl_xor(v, 16, 64));
+    v = max(v, __shfl_xor(v, 32, 64));
+    return v;
+}
+
 MT_DEV int wave_min(int v) {
     v = min(v, __shfl_xor(v, 1, 64));
     v = min(v, __shfl_xor(v, 2, 64));

@@ -103,7 +103,7 @@ struct Lds {
     int32_t evn, evseq;     // delta events recorded (mt_events_enable) / seq of the message applying
     int32_t nb[MT_MAXLEV];
     uint32_t text_top, text_half;
-    int32_t gcref[64];      // generator: latest refSeq per client (deli clientSeqManager)
+    int32_t gcref[LOC ? 1 : 64];  // generator: latest refSeq per client (deli clientSeqManager)
     int32_t gstall;         // generator: client 1 holds its refSeq until this seq
     uint32_t gpay;          // generator: payload bytes used in this document's region
     // an editing client's document (LOC, mt_loc): per slot the pending group mask, the pending
@@ -111,7 +111,6 @@ struct Lds {
     typename std::conditional<(GW > 1), LocState<64 * GW>, mt_loc>::type lc;
     uint64_t gm[LOC ? CAP * GW : 1];
     uint64_t pk[LOC ? CAP : 1];
-    uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
     uint64_t ovx[W ? 4 * CAP : 1];  // (W) overlapping removers >= 64: ids 0..15 of the u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
@@ -122,6 +121,11 @@ struct Lds {
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
     // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
     uint32_t slab[LOC ? 1 : CAP];
+    // (LOC) the creation stamps by slot: the HBM-workspace forms keep them here, the LDS-staged ones
+    // launch without this tail (loc_lds_bytes) and keep them in HBM (mt_gstate.ctx; Wave::ctp) --
+    // read only where a segment's pending group is (acks), and 1 KB less LDS per document at 256
+    // slots is the eighth wave per CU
+    uint32_t ct[LOC ? CAP : 1];
     // (W) the extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO), last: ids 16..31 of the overlap lists
     // and keys 16..31 ([slot][4] each, mt_state.h pxx).  The HBM-workspace form keeps it here; the
     // LDS-staged form launches without these members (kExtBytes less LDS) and stages the extension
@@ -131,6 +135,12 @@ struct Lds {
     static constexpr size_t kExtBytes = W ? 2 * 4 * CAP * sizeof(uint64_t) : 0;
 };
 // (the extension is the struct's tail: a launch may leave it out of its LDS)
+// the LDS of the editing form staged in LDS: Lds without the stamps' tail (Lds::ct and after)
+template <int CAP>
+constexpr size_t loc_lds_bytes() {
+    using L = Lds<CAP, true>;
+    return offsetof(L, ct);
+}
 // the LDS of the wide form staged in LDS: Lds without the extension
 template <int CAP>
 constexpr size_t wl_lds_bytes() { return sizeof(Lds<CAP, false, true>) - Lds<CAP, false, true>::kExtBytes; }
@@ -186,6 +196,14 @@ struct Wave {
     uint64_t* ext = nullptr;
     uint64_t* xo_p = nullptr;
     uint64_t* xk_p = nullptr;
+    uint32_t* ctp = nullptr;  // (LOC) the creation stamps by slot (Lds::ct, or HBM: mt_gstate.ctx)
+    // (LOC) the stamps' writes are read by other lanes: through HBM in the LDS-staged forms
+    MT_DEV static void ct_publish() {
+        if (!G) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    }
     uint32_t rix = 0;       // index of the record being applied within its document
     mt_op_rec* rg = nullptr;  // (LOC) the document's regenerated-op buffer and its payload
     uint8_t* rgp = nullptr;
@@ -766,7 +784,8 @@ struct Wave {
                 s.pk[t] = s.pk[sl];
                 s.lsq[t] = s.lsq[sl];
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
-                s.ct[t] = s.lc.stamp;
+                ctp[t] = s.lc.stamp;
+                ct_publish();
             }
             const TC last = arena[s.toff[sl] + (uint32_t)off - 1];
             s.flags[sl] = (uint8_t)((s.flags[sl] & ~MT_SF_NL) | (last == '\n' ? MT_SF_NL : 0));
@@ -1158,9 +1177,11 @@ struct Wave {
                     s.pk[t] = 0;
                     s.lsq[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
                     s.lc.stamp = s.lc.stamp + 1;
-                    s.ct[t] = s.lc.stamp;
+                    const uint32_t stamp = s.lc.stamp;
+                    ctp[t] = stamp;
+                    ct_publish();
                     if (S == -1) {
-                        s.lc.gt[s.lc.ghi % GN] = s.ct[t];
+                        s.lc.gt[s.lc.ghi % GN] = stamp;
                         s.lc.gls[s.lc.ghi % GN] = s.lc.lseq;
                         s.lc.ghi = s.lc.ghi + 1;
                     }
@@ -1384,7 +1405,7 @@ struct Wave {
                     bool mem = false;
                     if (i < n) {
                         const int sl = s.order[i];
-                        mem = gm_has(sl, Lo) && s.ct[sl] < gt;
+                        mem = gm_has(sl, Lo) && ctp[sl] < gt;
                     }
                     uint64_t m = wave_ballot(mem);
                     while (m) {
@@ -1401,7 +1422,7 @@ struct Wave {
                         uint32_t v = 0xFFFFFFFFu;
                         if (i < n) {
                             const int sl = s.order[i];
-                            if (gm_has(sl, Lo)) v = s.ct[sl];
+                            if (gm_has(sl, Lo)) v = ctp[sl];
                         }
                         uint32_t mv = v;
                         for (int o = 32; o; o >>= 1) mv = min(mv, (uint32_t)__shfl_xor((int)mv, o, 64));
@@ -1411,7 +1432,7 @@ struct Wave {
                     int k = -1;
                     for (int base = 0; base < n && k < 0; base += 64) {
                         const int i = base + lane;
-                        const uint64_t hm = wave_ballot(i < n && gm_has(s.order[i], Lo) && s.ct[s.order[i]] == best);
+                        const uint64_t hm = wave_ballot(i < n && gm_has(s.order[i], Lo) && ctp[s.order[i]] == best);
                         if (hm) k = base + first_lane(hm);
                     }
                     if (k < 0) break;
@@ -1528,7 +1549,7 @@ struct Wave {
                         const uint32_t N = s.lc.ghi;
                         gm_set(sl, N);
                         s.lc.gls[N % GN] = Ls;
-                        s.lc.gt[N % GN] = s.ct[sl];
+                        s.lc.gt[N % GN] = ctp[sl];
                     }
                     sync();
                     s.lc.ghi = s.lc.ghi + 1;
@@ -1940,9 +1961,10 @@ struct Wave {
             }
             for (int i = lane; i < n; i += 64) {
                 s.pk[i] = has ? lr.pk[i] : 0ull;
-                s.ct[i] = has ? lr.ct[i] : 0u;
+                ctp[i] = has ? lr.ct[i] : 0u;
                 s.lsq[i] = has ? lr.lsq[i] : 0ull;
             }
+            ct_publish();
         }
         sync();
         arena = abase + (size_t)s.text_half * textcap;
@@ -2081,7 +2103,7 @@ struct Wave {
                         for (int w = 0; w < GW; w++) gmx[i * GW + w] = s.gm[sl * GW + w];
                     }
                     lr.pk[i] = s.pk[sl];
-                    lr.ct[i] = s.ct[sl];
+                    lr.ct[i] = ctp[sl];
                     lr.lsq[i] = s.lsq[sl];
                 }
                 if (lane == 0) {
@@ -2161,6 +2183,7 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     Lds<CAP, LOC>& lds = *reinterpret_cast<Lds<CAP, LOC>*>(smem);
     Wave<CAP, false, LOC> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                              GEN || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap, g.evcap);
+    if constexpr (LOC) wv.ctp = g.ctx + (size_t)d * MT_LOC_CAP;  // (launched without Lds::ct)
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -2227,6 +2250,7 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     Wave<CAP, true, LOC, W, GW> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                                    g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
     if constexpr (W) wv.ext = st.ovh;  // (the extension: the workspace's own tail)
+    if constexpr (LOC) wv.ctp = st.ct;
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
@@ -2419,11 +2443,12 @@ extern "C" hipError_t mt_launch_apply_loc(int cap_class, const mt_gstate* g, con
                                           uint32_t n_docs, uint32_t op_lo, uint32_t op_cnt, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     mt::GenArgs ga{};
-    // the editing form at 256 / 512 / 1024 slots: its LDS (~79 B per slot) allows 8 / 4 / 2 waves per CU
+    // the editing form at 256 / 512 / 1024 slots: its LDS (~78 B per slot, without the stamps'
+    // tail: loc_lds_bytes) allows 8 / 3 / 2 waves per CU
 #define MT_LAUNCH_LOC(CAPV)                                                                                  \
     case CAPV:                                                                                               \
         hipLaunchKernelGGL((mt::apply_kernel<CAPV, false, true>), dim3(n_docs), dim3(64),                     \
-                           sizeof(mt::Lds<CAPV, true>), stream, *g, const_cast<mt_op_rec*>(ops),             \
+                           mt::loc_lds_bytes<CAPV>(), stream, *g, const_cast<mt_op_rec*>(ops),               \
                            const_cast<uint8_t*>(payload), row_ptr, doc_ids, n_docs, op_lo, op_cnt, ga);     \
         return hipGetLastError();
     switch (cap_class) {

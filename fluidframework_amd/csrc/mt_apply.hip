@@ -110,8 +110,7 @@ struct Lds {
     // property counts (MT_PK_*) and the creation stamp
     typename std::conditional<(GW > 1), LocState<64 * GW>, mt_loc>::type lc;
     uint64_t gm[LOC ? CAP * GW : 1];
-    uint64_t pk[LOC ? CAP : 1];
-    uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
+    uint64_t pk[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
     uint64_t ovx[W ? 4 * CAP : 1];  // (W) overlapping removers >= 64: ids 0..15 of the u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
@@ -121,11 +120,12 @@ struct Lds {
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
     // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
     uint32_t slab[LOC ? 1 : CAP];
-    // (LOC) the creation stamps by slot: the HBM-workspace forms keep them here, the LDS-staged ones
-    // launch without this tail (loc_lds_bytes) and keep them in HBM (mt_gstate.ctx; Wave::ctp) --
-    // read only where a segment's pending group is (acks), and 1 KB less LDS per document at 256
-    // slots is the eighth wave per CU
+    // (LOC) the creation stamps and the localSeq pairs by slot: the HBM-workspace forms keep them here,
+    // the LDS-staged ones launch without this tail (loc_lds_bytes) and keep them in HBM
+    // (mt_gstate.ctx / lsqx; Wave::ctp / lsqp) -- read only at acks and reconnects, and 3 KB less LDS
+    // per document at 256 slots is the eighth and ninth wave per CU
     uint32_t ct[LOC ? CAP : 1];
+    uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
     // (W) the extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO), last: ids 16..31 of the overlap lists
     // and keys 16..31 ([slot][4] each, mt_state.h pxx).  The HBM-workspace form keeps it here; the
     // LDS-staged form launches without these members (kExtBytes less LDS) and stages the extension
@@ -197,7 +197,8 @@ struct Wave {
     uint64_t* xo_p = nullptr;
     uint64_t* xk_p = nullptr;
     uint32_t* ctp = nullptr;  // (LOC) the creation stamps by slot (Lds::ct, or HBM: mt_gstate.ctx)
-    // (LOC) the stamps' writes are read by other lanes: through HBM in the LDS-staged forms
+    uint64_t* lsqp = nullptr;  // (LOC) the localSeq pairs by slot (Lds::lsq, or HBM: mt_gstate.lsqx)
+    // (LOC) their writes are read by other lanes: through HBM in the LDS-staged forms
     MT_DEV static void ct_publish() {
         if (!G) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -782,7 +783,7 @@ struct Wave {
             if constexpr (LOC) {  // segmentGroups.copyTo + the property manager's counts (mergeTree.ts:555-560)
                 gm_copy(t, sl);
                 s.pk[t] = s.pk[sl];
-                s.lsq[t] = s.lsq[sl];
+                lsqp[t] = lsqp[sl];
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
                 ctp[t] = s.lc.stamp;
                 ct_publish();
@@ -1175,7 +1176,7 @@ struct Wave {
                     gm_zero(t);
                     if (S == -1) gm_set(t, s.lc.ghi);
                     s.pk[t] = 0;
-                    s.lsq[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
+                    lsqp[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
                     s.lc.stamp = s.lc.stamp + 1;
                     const uint32_t stamp = s.lc.stamp;
                     ctp[t] = stamp;
@@ -1250,7 +1251,7 @@ struct Wave {
                             s.rseq[sl] = S;
                             s.rclient[sl] = (CT)C;
                             s.flags[sl] |= MT_SF_OVW;  // (not among this op's removedSegments)
-                            if constexpr (LOC) s.lsq[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
+                            if constexpr (LOC) lsqp[sl] &= 0xFFFFFFFFull;  // localRemovedSeq = undefined
                         } else if (s.flags[sl] & MT_SF_REMOVED) {
                             over = !ovl_add(sl, C) || over;  // addOverlappingClient (first remover wins)
                         } else {
@@ -1258,7 +1259,7 @@ struct Wave {
                             s.rseq[sl] = S;
                             s.rclient[sl] = (CT)C;
                             if constexpr (LOC) {  // localRemovedSeq (mergeTree.ts:2637)
-                                s.lsq[sl] = (s.lsq[sl] & 0xFFFFFFFFull) | ((uint64_t)(local ? s.lc.lseq : 0u) << 32);
+                                lsqp[sl] = (lsqp[sl] & 0xFFFFFFFFull) | ((uint64_t)(local ? s.lc.lseq : 0u) << 32);
                             }
                         }
                     } else {  // SegmentPropertiesManager.addProperties (remote, no combining op)
@@ -1270,6 +1271,7 @@ struct Wave {
             }
         }
         if (wave_ballot(over)) return fail(MT_DERR_LIMITS, S);
+        if constexpr (LOC) ct_publish();  // (the localRemovedSeq writes, read by other lanes later)
         sync();
         if (is_remove && track()) {  // markRangeRemoved's post action: blockUpdate of every block mapRange enters
             block_starts();
@@ -1373,9 +1375,9 @@ struct Wave {
                 gm_clr(sl, N);
                 if (type == MT_OP_INSERT) {
                     s.seq[sl] = S;
-                    s.lsq[sl] &= ~0xFFFFFFFFull;
+                    lsqp[sl] &= ~0xFFFFFFFFull;
                 } else if (type == MT_OP_REMOVE) {
-                    s.lsq[sl] &= 0xFFFFFFFFull;
+                    lsqp[sl] &= 0xFFFFFFFFull;
                     if (s.rseq[sl] == -1) s.rseq[sl] = S;  // else a remote removal overwrote it
                 } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
                     uint64_t pk = s.pk[sl];
@@ -1385,6 +1387,7 @@ struct Wave {
                     s.pk[sl] = pk;
                 }
             }
+            ct_publish();
             sync();
             const int b = block_of_pos(k);
             add_lru(b, sl, S);
@@ -1490,7 +1493,7 @@ struct Wave {
                         int v = 0;
                         if (j < k) {
                             const int sj = s.order[j];
-                            const uint32_t lo = (uint32_t)s.lsq[sj], hi = (uint32_t)(s.lsq[sj] >> 32);
+                            const uint32_t lo = (uint32_t)lsqp[sj], hi = (uint32_t)(lsqp[sj] >> 32);
                             if ((lo == 0 || lo <= Ls) && (!(s.flags[sj] & MT_SF_REMOVED) || (hi != 0 && hi > Ls))) v = (int)s.len[sj];
                         }
                         pos += wave_sum(v);
@@ -1525,7 +1528,7 @@ struct Wave {
                         }
                         r.payload_len = len + 2u * (uint32_t)nkv;
                     } else if (op.type == MT_OP_REMOVE) {
-                        keep = (s.lsq[sl] >> 32) != 0;  // still locally removed
+                        keep = (lsqp[sl] >> 32) != 0;  // still locally removed
                         r.payload_len = 0;
                     } else {
                         r.flags = op.flags & MT_F_REWRITE;
@@ -1962,7 +1965,7 @@ struct Wave {
             for (int i = lane; i < n; i += 64) {
                 s.pk[i] = has ? lr.pk[i] : 0ull;
                 ctp[i] = has ? lr.ct[i] : 0u;
-                s.lsq[i] = has ? lr.lsq[i] : 0ull;
+                lsqp[i] = has ? lr.lsq[i] : 0ull;
             }
             ct_publish();
         }
@@ -2104,7 +2107,7 @@ struct Wave {
                     }
                     lr.pk[i] = s.pk[sl];
                     lr.ct[i] = ctp[sl];
-                    lr.lsq[i] = s.lsq[sl];
+                    lr.lsq[i] = lsqp[sl];
                 }
                 if (lane == 0) {
                     g.loc[d].own = s.lc.own;
@@ -2170,8 +2173,26 @@ MT_DEV bool loc_admit(const mt_gstate& g, const mt_op_rec* ops, uint32_t d, uint
     return true;
 }
 
+// The document arrays of mt_gstate are needed by load() and store() only.  Both get them as a copy
+// read through a pointer to the kernel's own argument block (g: the first argument, offset 0) that
+// the compiler cannot see through, so the pointers are loaded at those two sites and are not held
+// live across the op loop (where ~50 SGPR pairs were spilled into VGPR lanes: mt_apply_reg.hip
+// kernarg_gstate, the same remedy)
+MT_DEV mt_gstate kernarg_g() {
+    const char* p = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    mt_gstate g;
+    __builtin_memcpy(&g, p, sizeof g);
+    return g;
+}
+// (MT_LOC_WPE: the editing form's waves per SIMD at 256 slots, for A/B builds; 0 = the compiler's)
+#ifndef MT_LOC_WPE
+#define MT_LOC_WPE 0
+#endif
+constexpr int loc_wpe(int CAP, bool LOC) { return LOC && CAP <= 256 && MT_LOC_WPE > 0 ? MT_LOC_WPE : 1; }
 template <int CAP, bool GEN, bool LOC = false>
-__global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(loc_wpe(CAP, LOC))))
+void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
                                                    uint8_t* __restrict__ payload,
                                                    const uint32_t* __restrict__ row_ptr,
                                                    const uint32_t* __restrict__ doc_ids, uint32_t n_docs,
@@ -2183,18 +2204,21 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
     Lds<CAP, LOC>& lds = *reinterpret_cast<Lds<CAP, LOC>*>(smem);
     Wave<CAP, false, LOC> wv(lds, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                              GEN || !g.ev ? nullptr : g.ev + (size_t)d * g.evcap, g.evcap);
-    if constexpr (LOC) wv.ctp = g.ctx + (size_t)d * MT_LOC_CAP;  // (launched without Lds::ct)
+    if constexpr (LOC) {  // (launched without Lds::ct / lsq)
+        wv.ctp = g.ctx + (size_t)d * MT_LOC_CAP;
+        wv.lsqp = g.lsqx + (size_t)d * MT_LOC_CAP;
+    }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     if (LOC && !loc_admit<CAP>(g, ops, d, a, b)) return;
-    wv.load(g, d);
+    wv.load(kernarg_g(), d);
     if (LOC) {
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;
         wv.rgp = g.rgp + (size_t)d * MT_RG_BYTES;
     }
-    if (GEN) {
+    if constexpr (GEN) {
         lds.gcref[wv.lane] = gen.cref[(size_t)d * 64 + wv.lane];
         if (wv.lane == 0) {
             lds.gstall = gen.stall[d];
@@ -2227,7 +2251,7 @@ __global__ __launch_bounds__(64) void apply_kernel(mt_gstate g, mt_op_rec* __res
             wv.apply(op, payload);
         }
     }
-    wv.store(g, d);
+    wv.store(kernarg_g(), d);
 }
 
 // Documents above 2048 segments: the same engine with the document's structure in a per-wave
@@ -2250,13 +2274,16 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     Wave<CAP, true, LOC, W, GW> wv(st, g.text + (size_t)d * 2 * g.textcap, g.textcap,
                                    g.ev ? g.ev + (size_t)d * g.evcap : nullptr, g.evcap);
     if constexpr (W) wv.ext = st.ovh;  // (the extension: the workspace's own tail)
-    if constexpr (LOC) wv.ctp = st.ct;
+    if constexpr (LOC) {
+        wv.ctp = st.ct;
+        wv.lsqp = st.lsq;
+    }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     if (LOC && !loc_admit<CAP, GW>(g, ops, d, a, b)) return;
-    wv.load(g, d);
+    wv.load(kernarg_g(), d);
     if (LOC) {
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;
         wv.rgp = g.rgp + (size_t)d * MT_RG_BYTES;
@@ -2267,7 +2294,7 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
         if (LOC) wv.rix = i - r0;
         wv.apply(op, payload);
     }
-    wv.store(g, d);
+    wv.store(kernarg_g(), d);
 }
 
 // The wide form with the document staged in LDS (small wide documents: CAP <= 512, where its
@@ -2293,13 +2320,13 @@ __global__ __launch_bounds__(64) void apply_kernel_wl(mt_gstate g, const mt_op_r
     const uint32_t a = min(r1, r0 + op_lo);
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
-    wv.load(g, d);
+    wv.load(kernarg_g(), d);
     for (uint32_t i = a; i < b; i++) {
         if (st.err) break;
         const mt_op_rec op = ops[i];
         wv.apply(op, payload);
     }
-    wv.store(g, d);
+    wv.store(kernarg_g(), d);
 }
 
 }  // namespace mt

@@ -44,8 +44,11 @@ def main():
         cs = eng.checksums()
         same = ref is None or bool(np.array_equal(cs, ref))
         ref = cs if ref is None else ref
-        print(f'b={b}: {n_rec / el / 1e6:.1f} M records/s ({el * 1e3:.1f} ms), classes '
-              f'{[(hex(c), round(ms, 2), n) for c, ms, n, _ in cls]}, checksums agree {same}', flush=True)
+        # (a sum: the farm tiles 16 source documents, so an xor of the checksums would cancel)
+        digest = int(np.add.reduce(cs.astype(np.uint64), dtype=np.uint64))
+        used = [(hex(c), round(ms, 2), n) for c, ms, n, _ in cls if n]
+        print(f'b={b}: {n_rec / el / 1e6:.1f} M records/s ({el * 1e3:.1f} ms), classes {used}, '
+              f'checksums agree {same}, digest {digest:016x}', flush=True)
         dev.free()
         eng.close()
 

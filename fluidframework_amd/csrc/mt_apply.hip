@@ -2173,6 +2173,45 @@ MT_DEV bool loc_admit(const mt_gstate& g, const mt_op_rec* ops, uint32_t d, uint
     return true;
 }
 
+// The op records of a document in blocks of 8, double-buffered in two registers (lane l holds dword
+// l % 8 of record base + l / 8; the register engine's mtr::load_op_block): a record's fields are
+// readlanes of a register loaded up to 15 records earlier, so no record waits for its own load
+MT_DEV uint32_t op_block(const mt_op_rec* ops, uint32_t base, uint32_t end, int lane) {
+    const uint32_t r = min(base + (uint32_t)(lane >> 3), end - 1u);  // (end > base's first record)
+    return reinterpret_cast<const uint32_t*>(ops + r)[lane & 7];
+}
+MT_DEV mt_op_rec op_of_block(uint32_t blk, uint32_t j) {
+    const int l = (int)(j * 8);
+    mt_op_rec r;
+    r.seq = __builtin_amdgcn_readlane((int)blk, l + 0);
+    r.ref_seq = __builtin_amdgcn_readlane((int)blk, l + 1);
+    r.msn = __builtin_amdgcn_readlane((int)blk, l + 2);
+    const uint32_t w3 = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 3);
+    r.client = (uint16_t)(w3 & 0xFFFFu);
+    r.type = (uint8_t)((w3 >> 16) & 0xFFu);
+    r.flags = (uint8_t)(w3 >> 24);
+    r.pos1 = __builtin_amdgcn_readlane((int)blk, l + 4);
+    r.pos2 = __builtin_amdgcn_readlane((int)blk, l + 5);
+    r.payload_off = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 6);
+    r.payload_len = (uint32_t)__builtin_amdgcn_readlane((int)blk, l + 7);
+    return r;
+}
+// The records [a, b) of a document through op_block's two buffers: f(op, i) per record until it
+// returns false
+template <typename F>
+MT_DEV void for_each_op(const mt_op_rec* ops, uint32_t a, uint32_t b, int lane, F&& f) {
+    uint32_t blk0 = op_block(ops, a, b, lane);
+    uint32_t blk1 = op_block(ops, a + 8, b, lane);
+    for (uint32_t i = a; i < b; i++) {
+        const mt_op_rec op = op_of_block(blk0, (i - a) & 7u);
+        if (((i + 1 - a) & 7u) == 0) {
+            blk0 = blk1;
+            blk1 = op_block(ops, i + 9, b, lane);
+        }
+        if (!f(op, i)) break;
+    }
+}
+
 // The document arrays of mt_gstate are needed by load() and store() only.  Both get them as a copy
 // read through a pointer to the kernel's own argument block (g: the first argument, offset 0) that
 // the compiler cannot see through, so the pointers are loaded at those two sites and are not held
@@ -2244,12 +2283,12 @@ void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
             gen.pay_used[d] = lds.gpay;
         }
     } else {
-        for (uint32_t i = a; i < b; i++) {
-            if (lds.err) break;
-            const mt_op_rec op = ops[i];
+        for_each_op(ops, a, b, wv.lane, [&](const mt_op_rec& op, uint32_t i) {
+            if (lds.err) return false;
             wv.rix = i - r0;
             wv.apply(op, payload);
-        }
+            return true;
+        });
     }
     wv.store(kernarg_g(), d);
 }
@@ -2288,12 +2327,12 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
         wv.rg = g.rg + (size_t)d * MT_RG_RECS;
         wv.rgp = g.rgp + (size_t)d * MT_RG_BYTES;
     }
-    for (uint32_t i = a; i < b; i++) {
-        if (st.err) break;
-        const mt_op_rec op = ops[i];
+    for_each_op(ops, a, b, wv.lane, [&](const mt_op_rec& op, uint32_t i) {
+        if (st.err) return false;
         if (LOC) wv.rix = i - r0;
         wv.apply(op, payload);
-    }
+        return true;
+    });
     wv.store(kernarg_g(), d);
 }
 
@@ -2321,11 +2360,11 @@ __global__ __launch_bounds__(64) void apply_kernel_wl(mt_gstate g, const mt_op_r
     const uint32_t b = op_cnt ? min(r1, a + op_cnt) : r1;
     if (a >= b) return;
     wv.load(kernarg_g(), d);
-    for (uint32_t i = a; i < b; i++) {
-        if (st.err) break;
-        const mt_op_rec op = ops[i];
+    for_each_op(ops, a, b, wv.lane, [&](const mt_op_rec& op, uint32_t) {
+        if (st.err) return false;
         wv.apply(op, payload);
-    }
+        return true;
+    });
     wv.store(kernarg_g(), d);
 }
 

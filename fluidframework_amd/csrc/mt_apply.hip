@@ -874,70 +874,82 @@ struct Wave {
 
     // scourNode on leaf block b (mergeTree.ts:1289-1365).  Unlinks removed segments at or
     // below minSeq, appends acked segments into their predecessor, compacts the order array.
-    // Returns the block's new child count.
+    // Returns the block's new child count.  Two passes: the decisions first, child by child on
+    // scalars (the run's grown length and trailing newline are tracked, no text moves), then the
+    // appends, unlinks and callbacks in child order -- the text copies run with little else live
+    // (inlined into the decision loop, they set the editing form's register peak)
     MT_DEV int scour(int b) {
         const int st = s.bst[b];
         const int cnt = s.lbcnt[b];
         const int32_t minSeq = s.min_seq;
-        int kept = 0, prev = -1, prevk = -1;  // prevk: prev's leaf ordinal
-        uint16_t keep[kMaxNodes];
+        uint32_t unl = 0, app = 0;  // children unlinked / appended to the run before them (bit q)
+        int prev = -1;              // the run's head
+        uint32_t plen = 0;          // its length with the appends so far
+        bool pnl = false;           // its ENDS_WITH_NEWLINE after them
         for (int q = 0; q < cnt; q++) {
             const int sl = s.order[st + q];
             const uint8_t f = s.flags[sl];
             bool pending = false;
             if constexpr (LOC) pending = gm_any(sl);  // segmentGroups not empty: held (mergeTree.ts:1295)
             if (pending) {
-                keep[kept++] = (uint16_t)sl;
                 prev = -1;
             } else if (f & MT_SF_REMOVED) {
-                if (s.rseq[sl] > minSeq) {
-                    keep[kept++] = (uint16_t)sl;
-                } else {
-                    emit(MT_EV_UNLINK, MT_EVF_FIRST, st + kept, -1, s.len[sl]);  // mergeTree.ts:1310-1315
-                    free_slot(sl);  // UNLINK
-                }
+                if (!(s.rseq[sl] > minSeq)) unl |= 1u << q;
                 prev = -1;
             } else if (s.seq[sl] <= minSeq) {
-                bool app = false;
-                if (prev >= 0) {
-                    const uint32_t pl = s.len[prev], ql = s.len[sl];
-                    // TextSegment.canAppend: two text segments (a Marker never appends, nor is
-                    // appended to: Marker.canAppend, TextSegment.is, mergeTree.ts:793; textSegment.ts:63-68)
-                    app = !((s.flags[prev] | f) & MT_SF_MARKER) && !(s.flags[prev] & MT_SF_NL) &&
-                          (pl <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
-                          props_match(prev, sl) && ql > 0;
-                }
-                if (app) {
-                    append_text(prev, sl);
-                    emit(MT_EV_APPEND, MT_EVF_FIRST, prevk, -1, s.len[prev]);  // mergeTree.ts:1335-1340
-                    emit(MT_EV_APPEND, 0, st + kept, -1, s.len[sl]);
-                    free_slot(sl);  // APPEND: segment.parent = undefined
+                const uint32_t ql = s.len[sl];
+                // TextSegment.canAppend: two text segments (a Marker never appends, nor is appended
+                // to: Marker.canAppend, TextSegment.is, mergeTree.ts:793; textSegment.ts:63-68)
+                const bool a = prev >= 0 && !((s.flags[prev] | f) & MT_SF_MARKER) && !pnl &&
+                               (plen <= (uint32_t)kTextGranularity || ql <= (uint32_t)kTextGranularity) &&
+                               props_match(prev, sl) && ql > 0;
+                if (a) {
+                    app |= 1u << q;
+                    plen += ql;
                 } else {
-                    keep[kept++] = (uint16_t)sl;
-                    prev = s.len[sl] > 0 ? sl : -1;
-                    prevk = st + kept - 1;
+                    prev = ql > 0 ? sl : -1;
+                    plen = ql;
                 }
+                pnl = (f & MT_SF_NL) != 0;
             } else {
-                keep[kept++] = (uint16_t)sl;
                 prev = -1;
             }
         }
-        if (kept < cnt) {
-            sync();
-            if (lane < kept) s.order[st + lane] = keep[lane];
-            sync();
-            shift_left(s.order, st + cnt, s.n, cnt - kept);
-            s.n = s.n - (cnt - kept);
-            sync();
-            if (lane == 0) s.lbcnt[b] = (uint8_t)kept;
-            // later block starts move left
-            const int nb = s.nb[0];
-            for (int base = b + 1; base <= nb; base += 64) {
-                const int j = base + lane;
-                if (j <= nb) s.bst[j] -= (cnt - kept);
+        if (!(unl | app)) return cnt;
+        int kept = 0, hd = -1;  // children kept so far; the last of them (an append's head)
+        for (int q = 0; q < cnt; q++) {
+            const int sl = s.order[st + q];
+            if ((unl >> q) & 1u) {
+                emit(MT_EV_UNLINK, MT_EVF_FIRST, st + kept, -1, s.len[sl]);  // mergeTree.ts:1310-1315
+                free_slot(sl);  // UNLINK
+            } else if ((app >> q) & 1u) {
+                append_text(hd, sl);
+                emit(MT_EV_APPEND, MT_EVF_FIRST, st + kept - 1, -1, s.len[hd]);  // mergeTree.ts:1335-1340
+                emit(MT_EV_APPEND, 0, st + kept, -1, s.len[sl]);
+                free_slot(sl);  // APPEND: segment.parent = undefined
+            } else {
+                hd = sl;
+                kept++;
             }
-            sync();
         }
+        // the kept children close ranks (lane q: child q)
+        const uint32_t keepm = ((1u << cnt) - 1u) & ~(unl | app);
+        const bool mine = lane < cnt && ((keepm >> lane) & 1u);
+        const uint16_t v = mine ? s.order[st + lane] : (uint16_t)0;
+        sync();
+        if (mine) s.order[st + __popc(keepm & ((1u << lane) - 1u))] = v;
+        sync();
+        shift_left(s.order, st + cnt, s.n, cnt - kept);
+        s.n = s.n - (cnt - kept);
+        sync();
+        if (lane == 0) s.lbcnt[b] = (uint8_t)kept;
+        // later block starts move left
+        const int nb = s.nb[0];
+        for (int base = b + 1; base <= nb; base += 64) {
+            const int j = base + lane;
+            if (j <= nb) s.bst[j] -= (cnt - kept);
+        }
+        sync();
         return kept;
     }
 

@@ -109,8 +109,7 @@ struct Lds {
     // an editing client's document (LOC, mt_loc): per slot the pending group mask, the pending
     // property counts (MT_PK_*) and the creation stamp
     typename std::conditional<(GW > 1), LocState<64 * GW>, mt_loc>::type lc;
-    uint64_t gm[LOC ? CAP * GW : 1];
-    uint64_t pk[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
+    uint64_t gm[LOC ? CAP * GW : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
     uint64_t ovx[W ? 4 * CAP : 1];  // (W) overlapping removers >= 64: ids 0..15 of the u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
@@ -120,12 +119,14 @@ struct Lds {
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
     // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
     uint32_t slab[LOC ? 1 : CAP];
-    // (LOC) the creation stamps and the localSeq pairs by slot: the HBM-workspace forms keep them here,
-    // the LDS-staged ones launch without this tail (loc_lds_bytes) and keep them in HBM
-    // (mt_gstate.ctx / lsqx; Wave::ctp / lsqp) -- read only at acks and reconnects, and 3 KB less LDS
-    // per document at 256 slots is the eighth and ninth wave per CU
+    // (LOC) the creation stamps, the localSeq pairs and the pending property counts by slot: the
+    // HBM-workspace forms keep them here, the LDS-staged ones launch without this tail
+    // (loc_lds_bytes) and keep them in HBM (mt_gstate.ctx / lsqx / pkx; Wave::ctp / lsqp / pkp) --
+    // read only at annotates, acks and reconnects, and 5 KB less LDS per document at 256 slots is
+    // the eighth to tenth wave per CU
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
+    uint64_t pk[LOC ? CAP : 1];   // pending property counts (MT_PK_*)
     // (W) the extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO), last: ids 16..31 of the overlap lists
     // and keys 16..31 ([slot][4] each, mt_state.h pxx).  The HBM-workspace form keeps it here; the
     // LDS-staged form launches without these members (kExtBytes less LDS) and stages the extension
@@ -198,6 +199,7 @@ struct Wave {
     uint64_t* xk_p = nullptr;
     uint32_t* ctp = nullptr;  // (LOC) the creation stamps by slot (Lds::ct, or HBM: mt_gstate.ctx)
     uint64_t* lsqp = nullptr;  // (LOC) the localSeq pairs by slot (Lds::lsq, or HBM: mt_gstate.lsqx)
+    uint64_t* pkp = nullptr;   // (LOC) the pending property counts by slot (Lds::pk, or HBM: mt_gstate.pkx)
     // (LOC) their writes are read by other lanes: through HBM in the LDS-staged forms
     MT_DEV static void ct_publish() {
         if (!G) {
@@ -417,7 +419,7 @@ struct Wave {
                 const uint8_t f = s.flags[sl];
                 ln = s.len[sl];
                 uint64_t pk = 0;  // (LOC, a remote annotate: keys with pending local changes are skipped)
-                if constexpr (LOC) pk = (S != -1 && (f & MT_SF_PDEF)) ? s.pk[sl] : 0ull;
+                if constexpr (LOC) pk = (S != -1 && (f & MT_SF_PDEF)) ? pkp[sl] : 0ull;
                 ll = (f & MT_SF_REMOVED) ? 0 : (int)ln;
                 const int ce = s.cum[i], cs = cstart(i);
                 hit = ce > cs && cs < end && ce > start;
@@ -782,7 +784,7 @@ struct Wave {
             s.len[sl] = (uint32_t)off;
             if constexpr (LOC) {  // segmentGroups.copyTo + the property manager's counts (mergeTree.ts:555-560)
                 gm_copy(t, sl);
-                s.pk[t] = s.pk[sl];
+                pkp[t] = pkp[sl];
                 lsqp[t] = lsqp[sl];
                 s.lc.stamp = s.lc.stamp + 1;  // stamps start at 1: segments from before editing have 0
                 ctp[t] = s.lc.stamp;
@@ -1187,7 +1189,7 @@ struct Wave {
                 if constexpr (LOC) {  // a local insert is its edit's one pending segment (saveIfLocal)
                     gm_zero(t);
                     if (S == -1) gm_set(t, s.lc.ghi);
-                    s.pk[t] = 0;
+                    pkp[t] = 0;
                     lsqp[t] = S == -1 ? (uint64_t)s.lc.lseq : 0ull;
                     s.lc.stamp = s.lc.stamp + 1;
                     const uint32_t stamp = s.lc.stamp;
@@ -1346,11 +1348,11 @@ struct Wave {
     MT_DEV void annotate_loc(int sl, const uint8_t* pairs, int np, bool rewrite, bool local) {
         if constexpr (LOC) {
             uint64_t p = (s.flags[sl] & MT_SF_PDEF) ? s.props[sl] : 0;
-            uint64_t pk = (s.flags[sl] & MT_SF_PDEF) ? s.pk[sl] : 0;
+            uint64_t pk = (s.flags[sl] & MT_SF_PDEF) ? pkp[sl] : 0;
             s.flags[sl] |= MT_SF_PDEF;
             if (!local && MT_PK_RW(pk) > 0) {
                 s.props[sl] = p;
-                s.pk[sl] = pk;
+                pkp[sl] = pk;
                 return;
             }
             if (rewrite) {
@@ -1371,7 +1373,7 @@ struct Wave {
                 p = (p & ~(0xFFull << (8 * k))) | ((uint64_t)pairs[2 * q + 1] << (8 * k));
             }
             s.props[sl] = p;
-            s.pk[sl] = pk;
+            pkp[sl] = pk;
         }
     }
 
@@ -1392,11 +1394,11 @@ struct Wave {
                     lsqp[sl] &= 0xFFFFFFFFull;
                     if (s.rseq[sl] == -1) s.rseq[sl] = S;  // else a remote removal overwrote it
                 } else {  // ackPendingProperties (segmentPropertiesManager.ts:15-28)
-                    uint64_t pk = s.pk[sl];
+                    uint64_t pk = pkp[sl];
                     if (rewrite && MT_PK_RW(pk) > 0) pk -= 1ull << 56;
                     for (int q = 0; q < np; q++)
                         if (MT_PK_KEY(pk, pairs[2 * q]) > 0) pk -= 1ull << (7 * pairs[2 * q]);
-                    s.pk[sl] = pk;
+                    pkp[sl] = pk;
                 }
             }
             ct_publish();
@@ -1975,7 +1977,7 @@ struct Wave {
                 }
             }
             for (int i = lane; i < n; i += 64) {
-                s.pk[i] = has ? lr.pk[i] : 0ull;
+                pkp[i] = has ? lr.pk[i] : 0ull;
                 ctp[i] = has ? lr.ct[i] : 0u;
                 lsqp[i] = has ? lr.lsq[i] : 0ull;
             }
@@ -2117,7 +2119,7 @@ struct Wave {
                     } else {
                         for (int w = 0; w < GW; w++) gmx[i * GW + w] = s.gm[sl * GW + w];
                     }
-                    lr.pk[i] = s.pk[sl];
+                    lr.pk[i] = pkp[sl];
                     lr.ct[i] = ctp[sl];
                     lr.lsq[i] = lsqp[sl];
                 }
@@ -2258,6 +2260,7 @@ void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
     if constexpr (LOC) {  // (launched without Lds::ct / lsq)
         wv.ctp = g.ctx + (size_t)d * MT_LOC_CAP;
         wv.lsqp = g.lsqx + (size_t)d * MT_LOC_CAP;
+        wv.pkp = g.pkx + (size_t)d * MT_LOC_CAP;
     }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
@@ -2328,6 +2331,7 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
     if constexpr (LOC) {
         wv.ctp = st.ct;
         wv.lsqp = st.lsq;
+        wv.pkp = st.pk;
     }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);

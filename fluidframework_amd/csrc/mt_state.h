@@ -127,7 +127,8 @@ struct mt_gstate {
     uint32_t* slab;    // [doc][segcap] a stale marker's cached label value ids: tile key (low 16 bits),
                        // range key (high 16) -- allocated on the first mt_set_label_keys, else null
     uint32_t* ctx;     // [doc][MT_LOC_CAP] the LDS-staged editing form's creation stamps and localSeq
-    uint64_t* lsqx;    // pairs by slot during a launch (mt_apply.hip Lds::ct / lsq)
+    uint64_t* lsqx;    // pairs and pending property counts by slot during a launch (mt_apply.hip
+    uint64_t* pkx;     // Lds::ct / lsq / pk)
     uint32_t* slabx;   // [doc][segcap] the editing form's slot-indexed slab during a launch (its LDS
                        // has no room for it: mt_apply.hip Lds<.., LOC>); allocated with slab
     uint8_t* client;

@@ -52,6 +52,15 @@ struct LocState {
     uint32_t gls[GN];
     uint32_t rgn, rgpn;
 };
+// mt_loc's scalars: the editing forms with 64 group slots keep the groups' stamps and localSeqs
+// (mt_loc.gt / gls) in HBM, in the document's own mt_loc (Wave::gtp / glsp)
+struct LocLite {
+    int32_t own;
+    uint32_t glo, ghi;
+    uint32_t stamp;
+    uint32_t lseq;
+    uint32_t rgn, rgpn;
+};
 
 // An editing document's per-segment rows in HBM: its big-pool row once it has one, else its
 // MT_LOC_CAP-slot row (mt_state.h)
@@ -87,7 +96,7 @@ struct Lds {
     uint32_t len[CAP];
     uint32_t toff[CAP];
     int32_t cum[CAP];       // scratch: inclusive prefix of visible length per position
-    int32_t bst[LB + 1];    // scratch: leaf-block start positions
+    uint16_t bst[LB + 1];   // scratch: leaf-block start positions
     int32_t hseq[H];
     uint16_t hslot[H];
     uint16_t order[CAP];    // document order -> slot
@@ -108,8 +117,7 @@ struct Lds {
     uint32_t gpay;          // generator: payload bytes used in this document's region
     // an editing client's document (LOC, mt_loc): per slot the pending group mask, the pending
     // property counts (MT_PK_*) and the creation stamp
-    typename std::conditional<(GW > 1), LocState<64 * GW>, mt_loc>::type lc;
-    uint64_t gm[LOC ? CAP * GW : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
+    typename std::conditional<(GW > 1), LocState<64 * GW>, LocLite>::type lc;
     uint64_t ovx[W ? 4 * CAP : 1];  // (W) overlapping removers >= 64: ids 0..15 of the u16 lists (mt_checksum.h)
     uint64_t ph[W ? CAP : 1];
     uint64_t pxl[W ? CAP : 1];
@@ -119,14 +127,15 @@ struct Lds {
     // a stale marker's cached label value ids (mt_gstate.slab), by slot; the editing form keeps them
     // in HBM (mt_gstate.slabx): its LDS is at the two-waves-per-CU limit without them
     uint32_t slab[LOC ? 1 : CAP];
-    // (LOC) the creation stamps, the localSeq pairs and the pending property counts by slot: the
-    // HBM-workspace forms keep them here, the LDS-staged ones launch without this tail
-    // (loc_lds_bytes) and keep them in HBM (mt_gstate.ctx / lsqx / pkx; Wave::ctp / lsqp / pkp) --
-    // read only at annotates, acks and reconnects, and 5 KB less LDS per document at 256 slots is
-    // the eighth to tenth wave per CU
+    // (LOC) the creation stamps, the localSeq pairs, the pending property counts and the pending-group
+    // masks by slot: the HBM-workspace forms keep them here, the LDS-staged ones launch without this
+    // tail (loc_lds_bytes) and keep them in HBM (mt_gstate.ctx / lsqx / pkx / gmxs; Wave::ctp / lsqp
+    // / pkp / gmp) -- read at annotates, acks, reconnects and zamboni's pending test (one load per
+    // block), and 7 KB less LDS per document at 256 slots is the eighth to twelfth wave per CU
     uint32_t ct[LOC ? CAP : 1];
     uint64_t lsq[LOC ? CAP : 1];  // localSeq (low 32) / localRemovedSeq (high 32), 0: undefined
     uint64_t pk[LOC ? CAP : 1];   // pending property counts (MT_PK_*)
+    uint64_t gm[LOC ? CAP * GW : 1];  // pending-group masks (GW words per slot)
     // (W) the extension (mt_state.h MT_WIDE_XK / MT_WIDE_XO), last: ids 16..31 of the overlap lists
     // and keys 16..31 ([slot][4] each, mt_state.h pxx).  The HBM-workspace form keeps it here; the
     // LDS-staged form launches without these members (kExtBytes less LDS) and stages the extension
@@ -160,20 +169,20 @@ struct Wave {
     using CT = typename std::conditional<W, uint16_t, uint8_t>::type;  // a short client id (Lds::client)
     // (LOC) pending-group masks: GW words per slot; pending edit ordinal N is bit N % GN
     static constexpr uint32_t GN = 64u * GW;
-    MT_DEV uint64_t& gmw(int sl, uint32_t N) { return s.gm[sl * GW + (int)((N % GN) >> 6)]; }
+    MT_DEV uint64_t& gmw(int sl, uint32_t N) { return gmp[sl * GW + (int)((N % GN) >> 6)]; }
     MT_DEV bool gm_has(int sl, uint32_t N) { return (gmw(sl, N) >> (N & 63u)) & 1ull; }
     MT_DEV void gm_set(int sl, uint32_t N) { gmw(sl, N) |= 1ull << (N & 63u); }
     MT_DEV void gm_clr(int sl, uint32_t N) { gmw(sl, N) &= ~(1ull << (N & 63u)); }
     MT_DEV bool gm_any(int sl) {
         uint64_t v = 0;
-        for (int w = 0; w < GW; w++) v |= s.gm[sl * GW + w];
+        for (int w = 0; w < GW; w++) v |= gmp[sl * GW + w];
         return v != 0;
     }
     MT_DEV void gm_copy(int t, int sl) {
-        for (int w = 0; w < GW; w++) s.gm[t * GW + w] = s.gm[sl * GW + w];
+        for (int w = 0; w < GW; w++) gmp[t * GW + w] = gmp[sl * GW + w];
     }
     MT_DEV void gm_zero(int t) {
-        for (int w = 0; w < GW; w++) s.gm[t * GW + w] = 0ull;
+        for (int w = 0; w < GW; w++) gmp[t * GW + w] = 0ull;
     }
     using TC = typename std::conditional<W, uint16_t, uint8_t>::type;  // a text code unit in the arena
     MT_DEV static void sync() {
@@ -200,6 +209,9 @@ struct Wave {
     uint32_t* ctp = nullptr;  // (LOC) the creation stamps by slot (Lds::ct, or HBM: mt_gstate.ctx)
     uint64_t* lsqp = nullptr;  // (LOC) the localSeq pairs by slot (Lds::lsq, or HBM: mt_gstate.lsqx)
     uint64_t* pkp = nullptr;   // (LOC) the pending property counts by slot (Lds::pk, or HBM: mt_gstate.pkx)
+    uint64_t* gmp = nullptr;   // (LOC) the pending-group masks by slot (Lds::gm, or HBM: mt_gstate.gmxs)
+    uint32_t* gtp = nullptr;   // (LOC) the groups' creation stamps and localSeqs (LocState, or the
+    uint32_t* glsp = nullptr;  // document's mt_loc in HBM)
     // (LOC) their writes are read by other lanes: through HBM in the LDS-staged forms
     MT_DEV static void ct_publish() {
         if (!G) {
@@ -885,15 +897,17 @@ struct Wave {
         const int cnt = s.lbcnt[b];
         const int32_t minSeq = s.min_seq;
         uint32_t unl = 0, app = 0;  // children unlinked / appended to the run before them (bit q)
+        // (LOC) the children with a pending group (segmentGroups not empty: held, mergeTree.ts:1295),
+        // one lane per child: the masks may live in HBM
+        uint32_t pendm = 0;
+        if constexpr (LOC) pendm = (uint32_t)wave_ballot(lane < cnt && gm_any(s.order[st + lane]));
         int prev = -1;              // the run's head
         uint32_t plen = 0;          // its length with the appends so far
         bool pnl = false;           // its ENDS_WITH_NEWLINE after them
         for (int q = 0; q < cnt; q++) {
             const int sl = s.order[st + q];
             const uint8_t f = s.flags[sl];
-            bool pending = false;
-            if constexpr (LOC) pending = gm_any(sl);  // segmentGroups not empty: held (mergeTree.ts:1295)
-            if (pending) {
+            if ((pendm >> q) & 1u) {
                 prev = -1;
             } else if (f & MT_SF_REMOVED) {
                 if (!(s.rseq[sl] > minSeq)) unl |= 1u << q;
@@ -1196,8 +1210,9 @@ struct Wave {
                     ctp[t] = stamp;
                     ct_publish();
                     if (S == -1) {
-                        s.lc.gt[s.lc.ghi % GN] = stamp;
-                        s.lc.gls[s.lc.ghi % GN] = s.lc.lseq;
+                        gtp[s.lc.ghi % GN] = stamp;
+                        glsp[s.lc.ghi % GN] = s.lc.lseq;
+                        ct_publish();
                         s.lc.ghi = s.lc.ghi + 1;
                     }
                 }
@@ -1236,9 +1251,10 @@ struct Wave {
                 gN = s.lc.ghi;
                 sync();
                 if (lane == 0) {
-                    s.lc.gt[gN % GN] = s.lc.stamp + 1;  // every member existed before it
-                    s.lc.gls[gN % GN] = s.lc.lseq;
+                    gtp[gN % GN] = s.lc.stamp + 1;  // every member existed before it
+                    glsp[gN % GN] = s.lc.lseq;
                 }
+                ct_publish();
                 sync();
                 s.lc.ghi = s.lc.ghi + 1;
                 sync();
@@ -1413,7 +1429,7 @@ struct Wave {
             const int32_t S = op.seq;
             if (s.lc.glo < s.lc.ghi) {
                 const uint32_t Lo = s.lc.glo;
-                const uint32_t gt = s.lc.gt[Lo % GN];
+                const uint32_t gt = gtp[Lo % GN];
                 const bool rewrite = op.flags & MT_F_REWRITE;
                 block_starts();
                 const int n = s.n;
@@ -1478,7 +1494,7 @@ struct Wave {
             const int np = MT_OP_NPAIRS(op);
             const uint8_t* opairs = payload + op.payload_off + (op.payload_len - 2 * np);
             const uint32_t Lo = s.lc.glo;
-            const uint32_t Ls = s.lc.gls[Lo % GN];
+            const uint32_t Ls = glsp[Lo % GN];
             auto emit_rec = [&](const mt_op_rec& r) -> bool {
                 if (s.lc.rgn >= MT_RG_RECS || s.lc.rgpn + r.payload_len > MT_RG_BYTES) return fail(MT_DERR_CAPACITY, S), false;
                 if (lane == 0) rg[s.lc.rgn] = r;
@@ -1514,6 +1530,7 @@ struct Wave {
                     }
                     sync();
                     if (lane == 0) gm_clr(sl, Lo);
+                    ct_publish();
                     sync();
                     const uint32_t len = s.len[sl];
                     mt_op_rec r{};
@@ -1565,9 +1582,10 @@ struct Wave {
                     if (lane == 0) {
                         const uint32_t N = s.lc.ghi;
                         gm_set(sl, N);
-                        s.lc.gls[N % GN] = Ls;
-                        s.lc.gt[N % GN] = ctp[sl];
+                        glsp[N % GN] = Ls;
+                        gtp[N % GN] = ctp[sl];
                     }
+                    ct_publish();
                     sync();
                     s.lc.ghi = s.lc.ghi + 1;
                     sync();
@@ -1944,30 +1962,29 @@ struct Wave {
             const bool has = g.loc[d].own >= 0;
             const LocRow lr = loc_row(g, d);
             if constexpr (GW == 1) {
-                s.lc.gt[lane] = g.loc[d].gt[lane];
-                s.lc.gls[lane] = g.loc[d].gls[lane];
-                for (int i = lane; i < n; i += 64) s.gm[i] = has ? lr.gm[i] : 0ull;
+                // (the groups' stamps and localSeqs stay in the document's mt_loc: gtp / glsp)
+                for (int i = lane; i < n; i += 64) gmp[i] = has ? lr.gm[i] : 0ull;
             } else if (g.sc[d].wide & MT_WIDE_GROUPS) {
                 const uint32_t gx = g.locgx[d];
                 for (uint32_t j = lane; j < GN; j += 64) {
-                    s.lc.gt[j] = g.locx[gx].gt[j];
-                    s.lc.gls[j] = g.locx[gx].gls[j];
+                    gtp[j] = g.locx[gx].gt[j];
+                    glsp[j] = g.locx[gx].gls[j];
                 }
                 const uint64_t* gmx = g.gmx + (size_t)gx * MT_LOC_BIGCAP * GW;
-                for (int i = lane; i < n * GW; i += 64) s.gm[i] = gmx[i];
+                for (int i = lane; i < n * GW; i += 64) gmp[i] = gmx[i];
             } else {
                 // entering the wide-group form: ordinal N moves from bit / index N % 64 to N % GN
                 // (at most 64 pending, so N % 64 names one ordinal of [glo, ghi))
                 const uint32_t glo = g.loc[d].glo, np = g.loc[d].ghi - glo;
-                for (uint32_t j = lane; j < GN; j += 64) s.lc.gt[j] = s.lc.gls[j] = 0u;
+                for (uint32_t j = lane; j < GN; j += 64) gtp[j] = glsp[j] = 0u;
                 sync();
                 if ((uint32_t)lane < np) {
                     const uint32_t N = glo + (uint32_t)lane;
-                    s.lc.gt[N % GN] = g.loc[d].gt[N & 63u];
-                    s.lc.gls[N % GN] = g.loc[d].gls[N & 63u];
+                    gtp[N % GN] = g.loc[d].gt[N & 63u];
+                    glsp[N % GN] = g.loc[d].gls[N & 63u];
                 }
                 for (int i = lane; i < n; i += 64) {
-                    for (int w = 0; w < GW; w++) s.gm[i * GW + w] = 0ull;
+                    for (int w = 0; w < GW; w++) gmp[i * GW + w] = 0ull;
                     uint64_t m = has ? lr.gm[i] : 0ull;
                     while (m) {
                         const uint32_t b = (uint32_t)__builtin_ctzll(m);
@@ -2115,9 +2132,9 @@ struct Wave {
                 for (int i = lane; i < min(nn, lr.cap); i += 64) {
                     const int sl = s.order[i];
                     if constexpr (GW == 1) {
-                        lr.gm[i] = s.gm[sl];
+                        lr.gm[i] = gmp[sl];
                     } else {
-                        for (int w = 0; w < GW; w++) gmx[i * GW + w] = s.gm[sl * GW + w];
+                        for (int w = 0; w < GW; w++) gmx[i * GW + w] = gmp[sl * GW + w];
                     }
                     lr.pk[i] = pkp[sl];
                     lr.ct[i] = ctp[sl];
@@ -2132,14 +2149,11 @@ struct Wave {
                     g.loc[d].rgn = s.lc.rgn;
                     g.loc[d].rgpn = s.lc.rgpn;
                 }
-                if constexpr (GW == 1) {
-                    g.loc[d].gt[lane] = s.lc.gt[lane];
-                    g.loc[d].gls[lane] = s.lc.gls[lane];
-                } else {
+                if constexpr (GW > 1) {
                     const uint32_t gx = g.locgx[d];
                     for (uint32_t j = lane; j < GN; j += 64) {
-                        g.locx[gx].gt[j] = s.lc.gt[j];
-                        g.locx[gx].gls[j] = s.lc.gls[j];
+                        g.locx[gx].gt[j] = gtp[j];
+                        g.locx[gx].gls[j] = glsp[j];
                     }
                 }
             }
@@ -2261,6 +2275,9 @@ void apply_kernel(mt_gstate g, mt_op_rec* __restrict__ ops,
         wv.ctp = g.ctx + (size_t)d * MT_LOC_CAP;
         wv.lsqp = g.lsqx + (size_t)d * MT_LOC_CAP;
         wv.pkp = g.pkx + (size_t)d * MT_LOC_CAP;
+        wv.gmp = g.gmxs + (size_t)d * MT_LOC_CAP;
+        wv.gtp = g.loc[d].gt;
+        wv.glsp = g.loc[d].gls;
     }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);
@@ -2332,6 +2349,14 @@ __global__ __launch_bounds__(64) void apply_kernel_g(mt_gstate g, const mt_op_re
         wv.ctp = st.ct;
         wv.lsqp = st.lsq;
         wv.pkp = st.pk;
+        wv.gmp = st.gm;
+        if constexpr (GW > 1) {
+            wv.gtp = st.lc.gt;
+            wv.glsp = st.lc.gls;
+        } else {
+            wv.gtp = g.loc[d].gt;
+            wv.glsp = g.loc[d].gls;
+        }
     }
     const uint32_t r0 = row_ptr[d], r1 = row_ptr[d + 1];
     const uint32_t a = min(r1, r0 + op_lo);

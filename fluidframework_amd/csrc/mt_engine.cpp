@@ -458,7 +458,8 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         (st = dalloc(e, &g.text, D * 2 * g.textcap)) || (st = dalloc(e, &e->d_classes, kNumClasses * 4)) ||
         (st = dalloc(e, &g.gm, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pk, D * MT_LOC_CAP)) ||
         (st = dalloc(e, &g.ct, D * MT_LOC_CAP)) || (st = dalloc(e, &g.ctx, D * MT_LOC_CAP)) ||
-        (st = dalloc(e, &g.lsqx, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pkx, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
+        (st = dalloc(e, &g.lsqx, D * MT_LOC_CAP)) || (st = dalloc(e, &g.pkx, D * MT_LOC_CAP)) ||
+        (st = dalloc(e, &g.gmxs, D * MT_LOC_CAP)) || (st = dalloc(e, &g.loc, D)) ||
         (st = dalloc(e, &g.lsq, D * MT_LOC_CAP)) || (st = dalloc(e, &g.rg, D * MT_RG_RECS)) ||
         (st = dalloc(e, &g.rgp, D * MT_RG_BYTES)) || (st = dalloc(e, &g.locbig, D)) ||
         (st = dalloc(e, &g.locgx, D)) ||

@@ -128,7 +128,8 @@ struct mt_gstate {
                        // range key (high 16) -- allocated on the first mt_set_label_keys, else null
     uint32_t* ctx;     // [doc][MT_LOC_CAP] the LDS-staged editing form's creation stamps and localSeq
     uint64_t* lsqx;    // pairs and pending property counts by slot during a launch (mt_apply.hip
-    uint64_t* pkx;     // Lds::ct / lsq / pk)
+    uint64_t* pkx;     // Lds::ct / lsq / pk / gm)
+    uint64_t* gmxs;
     uint32_t* slabx;   // [doc][segcap] the editing form's slot-indexed slab during a launch (its LDS
                        // has no room for it: mt_apply.hip Lds<.., LOC>); allocated with slab
     uint8_t* client;

@@ -1436,6 +1436,20 @@ struct RWave {
                 ba = uni(ba);
                 be = uni(be);
                 t = uni(t);
+#ifdef MT_UNI_ELEM
+                // (the inserted element and the cut as scalars: 4-8 B less scratch in most classes)
+                e.seq = uni(e.seq);
+                e.rseq = uni(e.rseq);
+                e.li = uniu(e.li);
+                e.cf = uniu(e.cf);
+                e.ov = uniu(e.ov);
+                e.oh = uniu(e.oh);
+                e.cum = uni(e.cum);
+                cut.lli = uniu(cut.lli);
+                cut.lcf = uniu(cut.lcf);
+                cut.rli = uniu(cut.rli);
+                cut.pos = uni(cut.pos);
+#endif
                 const bool ok = insert_at(k, ba, be, e, S, cut, !placing);
                 if (placing) {
                     PROF_END(prof, P_INSERT, t1);

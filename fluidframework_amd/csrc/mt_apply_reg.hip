@@ -62,14 +62,21 @@ template <class T>
 MT_DEV MT_GLOB T* gp(T* p) { return (MT_GLOB T*)p; }
 typedef const MT_KARG mt_gstate KGState;
 typedef uint32_t EvWords __attribute__((ext_vector_type(4)));
-// one 64-byte event row through a global pointer: four 16-byte stores
-MT_DEV void put_event(MT_GLOB mt_event* p, const mt_event& e) {
-    static_assert(sizeof(mt_event) == 96, "mt_event");
-    EvWords w[6];
-    __builtin_memcpy(w, &e, sizeof w);
+// One 96-byte event row (mt_event, include/mtgpu.h) through a global pointer, six 16-byte stores
+// built from the field values: a row assembled as an mt_event first costs the 24 registers of the
+// struct at every call site (the event kernels' register peak and scratch came from exactly that).
+// pv01..pv67: pvals[0..7] two to a word (the register engine's eight keys; pvals[8..31] are zero).
+MT_DEV void put_event(MT_GLOB mt_event* p, int32_t seq, int op, unsigned flags, int leaf, int pos, uint32_t len,
+                      uint32_t pmask = 0, uint32_t pv01 = 0, uint32_t pv23 = 0, uint32_t pv45 = 0, uint32_t pv67 = 0) {
+    static_assert(sizeof(mt_event) == 96 && offsetof(mt_event, pvals) == 24, "mt_event");
     MT_GLOB EvWords* q = reinterpret_cast<MT_GLOB EvWords*>(p);
-#pragma unroll
-    for (int i = 0; i < 6; i++) q[i] = w[i];
+    const EvWords z = {0u, 0u, 0u, 0u};
+    q[0] = EvWords{(uint32_t)seq, ((uint32_t)op & 0xFFu) | ((flags & 0xFFu) << 8), (uint32_t)leaf, (uint32_t)pos};
+    q[1] = EvWords{len, pmask, pv01, pv23};
+    q[2] = EvWords{pv45, pv67, 0u, 0u};
+    q[3] = z;
+    q[4] = z;
+    q[5] = z;
 }
 
 MT_DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -332,14 +339,7 @@ struct RWave {
     // document then halts with MT_DERR_EVENTS after the op).
     MT_DEV void emit(int op, unsigned flags, int leaf, int pos, uint32_t len) {
         if (lane == 0 && evn < (int)evcap) {
-            mt_event e{};
-            e.seq = evseq;
-            e.op = (int8_t)op;
-            e.flags = (uint8_t)flags;
-            e.leaf = leaf;
-            e.pos = pos;
-            e.len = len;
-            put_event(evp + evn, e);
+            put_event(evp + evn, evseq, op, flags, leaf, pos, len);
         }
         evn = evn + 1;
     }
@@ -391,28 +391,28 @@ struct RWave {
             const bool live = (lvm >> j) & 1u;
             if ((hm >> j) & 1u) {
                 if (idx < (int)evcap) {
-                    mt_event e{};
-                    e.seq = evseq;
-                    e.op = (int8_t)(is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE);
-                    e.flags = (uint8_t)(idx == evn ? MT_EVF_FIRST : 0u);
-                    e.leaf = leaf;
-                    e.pos = pos;
-                    e.len = len_of(li[j]);
-                    if (!is_remove) {
+                    const int eop = is_remove ? MT_EV_REMOVE : MT_EV_ANNOTATE;
+                    const unsigned efl = idx == evn ? MT_EVF_FIRST : 0u;
+                    if (is_remove) {
+                        put_event(evp + idx, evseq, eop, efl, leaf, pos, len_of(li[j]));
+                    } else {
                         const uint64_t old = (cf[j] & F_PDEF) ? s.props[id_of(li[j])] : 0ull;
                         uint32_t oldnz = 0;
 #pragma unroll
                         for (int k = 0; k < 8; k++) oldnz |= ((old >> (8 * k)) & 0xFFu) ? (1u << k) : 0u;
                         const uint32_t pm = okeys | (rewrite ? (oldnz & ~onz) : 0u);
-                        e.pmask = pm;
+                        // the reported values: the old value of each reported key, null (0) where a
+                        // rewrite nulls a key the op names without a value
+                        const uint32_t rep = pm & ~(rewrite ? (okeys & ~onz) : 0u);
+                        uint32_t pw[4];
 #pragma unroll
-                        for (int k = 0; k < 8; k++) {
-                            const uint32_t ov = (uint32_t)(old >> (8 * k)) & 0xFFu;
-                            const bool nulled = rewrite && ((okeys >> k) & 1u) && !((onz >> k) & 1u);
-                            e.pvals[k] = ((pm >> k) & 1u) && !nulled ? (uint16_t)ov : (uint16_t)0;
+                        for (int h = 0; h < 4; h++) {
+                            const uint32_t v0 = ((rep >> (2 * h)) & 1u) ? (uint32_t)(old >> (16 * h)) & 0xFFu : 0u;
+                            const uint32_t v1 = ((rep >> (2 * h + 1)) & 1u) ? (uint32_t)(old >> (16 * h + 8)) & 0xFFu : 0u;
+                            pw[h] = v0 | (v1 << 16);
                         }
+                        put_event(evp + idx, evseq, eop, efl, leaf, pos, len_of(li[j]), pm, pw[0], pw[1], pw[2], pw[3]);
                     }
-                    put_event(evp + idx, e);
                 }
                 idx++;
             }
@@ -1021,33 +1021,11 @@ struct RWave {
                 const int kbp = __shfl(kb, hp, 64), aincp = __shfl(ainc, hp, 64);
                 const uint32_t lenp = (uint32_t)__shfl((int)ql, hp, 64);
                 const int o = evn + rinc - nrec;
-                if (tomb && o < (int)evcap) {
-                    mt_event ev{};
-                    ev.seq = evseq;
-                    ev.op = (int8_t)MT_EV_UNLINK;
-                    ev.flags = (uint8_t)MT_EVF_FIRST;
-                    ev.leaf = st + kb;
-                    ev.pos = -1;
-                    ev.len = ql;
-                    put_event(evp + o, ev);
-                }
+                if (tomb && o < (int)evcap) put_event(evp + o, evseq, MT_EV_UNLINK, MT_EVF_FIRST, st + kb, -1, ql);
                 if (app) {
-                    mt_event ev{};
-                    ev.seq = evseq;
-                    ev.op = (int8_t)MT_EV_APPEND;
-                    ev.pos = -1;
-                    if (o < (int)evcap) {
-                        ev.flags = (uint8_t)MT_EVF_FIRST;
-                        ev.leaf = st + kbp;
-                        ev.len = lenp + (uint32_t)(ainc - aincp);
-                        put_event(evp + o, ev);
-                    }
-                    if (o + 1 < (int)evcap) {
-                        ev.flags = 0;
-                        ev.leaf = st + kb;
-                        ev.len = ql;
-                        put_event(evp + o + 1, ev);
-                    }
+                    if (o < (int)evcap)
+                        put_event(evp + o, evseq, MT_EV_APPEND, MT_EVF_FIRST, st + kbp, -1, lenp + (uint32_t)(ainc - aincp));
+                    if (o + 1 < (int)evcap) put_event(evp + o + 1, evseq, MT_EV_APPEND, 0u, st + kb, -1, ql);
                 }
                 evn = evn + rtot;
             }

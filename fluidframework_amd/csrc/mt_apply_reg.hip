@@ -635,10 +635,12 @@ struct RWave {
             // profiles/r04_ab_split_htop_C3.log)
             Elem r = get(k - 1);
             r.li = cut.rli;
-            // (narrow form: slot k - 1 becomes the left part in the shift's own pass -- patching it
-            // first by dynamic index held two copies of the slot arrays live, C3/C4/C5 +0.4-0.7 %;
-            // the C64 form measured 9 % slower that way and patches first: profiles/r05_ab_patch_shift/)
-            if constexpr (W) {
+            // (narrow form up to K = 8: slot k - 1 becomes the left part in the shift's own pass --
+            // patching it first by dynamic index held two copies of the slot arrays live: C3/C4/C5
+            // +0.4-0.7 %, C4's <6> 1.81 -> 1.61x PMC traffic, C5's <2>/<3> 2.53/1.99 -> 2.33/1.70x.
+            // K >= 9 spilled more that way (<9>/<10>: 32/76 -> 44/88 B, 1.25/1.58 -> 1.37/1.77x) and
+            // the C64 form ran 9 % slower: they patch first. profiles/r05_ab_patch_shift/)
+            if constexpr (W || K >= 9) {
                 set_li_cf(k - 1, cut.lli, cut.lcf);
                 set_cum(k - 1, cut.pos);
                 shift_in<true>(k, r, false, 0, true);

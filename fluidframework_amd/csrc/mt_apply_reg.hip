@@ -439,39 +439,44 @@ struct RWave {
         const int jk = uni(k % K);
         return (uint32_t)__builtin_amdgcn_readlane((int)li[jk], k / K);
     }
+    // (per-register selects, not a uniform dynamic-index write: that is an s_set_gpr_idx move into a
+    // fresh copy of the whole register tuple, which the enclosing loops then copy back at their joins)
     MT_DEV void set_li_cf(int k, uint32_t lv, uint32_t cv) {
-        const int lk = k / K, jk = uni(k % K);
-        const bool me = lane == lk;
-        li[jk] = me ? lv : li[jk];
-        cf[jk] = me ? cv : cf[jk];
+        const int r = k - lane * K;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            li[j] = j == r ? lv : li[j];
+            cf[j] = j == r ? cv : cf[j];
+        }
     }
-
-    MT_DEV void set_cum(int k, int32_t v) {
-        const int lk = k / K, jk = uni(k % K);
-        cum[jk] = lane == lk ? v : cum[jk];
-    }
-    // insert e at slot p: slots >= p move one register right
-    // (PATCH: slot p - 1 takes plli / plcf / pcum in the same pass -- a boundary split's left part)
-    template <bool CUM, bool PATCH = false>
-    MT_DEV void shift_in(int p, const Elem& e, bool bs, int scv, bool live, uint32_t plli = 0, uint32_t plcf = 0,
-                         int32_t pcum = 0) {
+    // insert e at slot p: slots >= p move one register right.  dup (a boundary split of the segment
+    // at slot p - 1): slots >= p - 1 move right instead, so slot p receives a copy of the cut segment
+    // (patch_cut then gives the two parts their li / cf / cum).  Both forms are this one pass from one
+    // call site (insert_at): two call sites -- or a dynamic-index patch of slot p - 1 before the
+    // shift -- left the state in different registers on the two paths and the insert loop's join
+    // copied all of it (ISA: ~110 v_mov per join at K = 9)
+    template <bool CUM>
+    MT_DEV void shift_in(int p, const Elem& e, bool bs, int scv, bool live, bool dup = false) {
         mask_shift(p, bs, scv, live);
         const int32_t c_seq = shr1(seq[K - 1], 0), c_rseq = shr1(rseq[K - 1], 0);
         const uint32_t c_li = (uint32_t)shr1((int)li[K - 1], 0), c_cf = (uint32_t)shr1((int)cf[K - 1], 0);
         const uint32_t c_ov = (uint32_t)shr1((int)ov[K - 1], 0);
         const uint32_t c_oh = W ? (uint32_t)shr1((int)oh[K - 1], 0) : 0u;
         const int32_t c_cum = CUM ? shr1(cum[K - 1], 0) : 0;
+        // per lane: the register index of slot p in this lane, less one for dup (registers above it
+        // take their left neighbour), and the register taking e (none for dup)
+        const int r = p - lane * K;
+        const int rq = dup ? r - 1 : r;
+        const int ra = dup ? -K - 2 : r;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
-            const int i = idx(j);
-            const bool mv = i > p, at = i == p;
+            const bool mv = j > rq, at = j == ra;
             const int32_t pseq = j ? seq[j - 1] : c_seq, prseq = j ? rseq[j - 1] : c_rseq;
             const uint32_t pli = j ? li[j - 1] : c_li, pcf = j ? cf[j - 1] : c_cf, pov = j ? ov[j - 1] : c_ov;
             seq[j] = mv ? pseq : (at ? e.seq : seq[j]);
             rseq[j] = mv ? prseq : (at ? e.rseq : rseq[j]);
-            const bool lp = PATCH && i == p - 1;
-            li[j] = mv ? pli : (at ? e.li : (lp ? plli : li[j]));
-            cf[j] = mv ? pcf : (at ? e.cf : (lp ? plcf : cf[j]));
+            li[j] = mv ? pli : (at ? e.li : li[j]);
+            cf[j] = mv ? pcf : (at ? e.cf : cf[j]);
             ov[j] = mv ? pov : (at ? e.ov : ov[j]);
             if constexpr (W) {
                 const uint32_t poh = j ? oh[j - 1] : c_oh;
@@ -479,10 +484,26 @@ struct RWave {
             }
             if (CUM) {
                 const int32_t pcm = j ? cum[j - 1] : c_cum;
-                cum[j] = mv ? pcm : (at ? e.cum : (lp ? pcum : cum[j]));
+                cum[j] = mv ? pcm : (at ? e.cum : cum[j]);
             }
+            // register j is rewritten only after register j + 1 (its last reader): the new value can
+            // take the old one's register, so the state keeps its registers through the shift and
+            // the joins after it need no copies
+            __builtin_amdgcn_sched_barrier(0);
         }
         ns = ns + 1;
+    }
+    // after shift_in(p, .., dup): slot p - 1 becomes the cut's left part, slot p's li the right part's
+    // (in-place per-register selects: the state keeps its registers)
+    MT_DEV void patch_cut(int p, const Cut& c) {
+        const int r = p - lane * K;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const bool lp = j == r - 1, rp = j == r;
+            li[j] = lp ? c.lli : (rp ? c.rli : li[j]);
+            cf[j] = lp ? c.lcf : cf[j];
+            cum[j] = lp ? c.pos : cum[j];
+        }
     }
 
     // ------------------------------------------------------------ visibility
@@ -628,28 +649,13 @@ struct RWave {
     // (cut: a boundary split's right part, a copy of slot k - 1 patched after the shift; k > a)
     MT_DEV bool insert_at(int k, int a, int en, const Elem& e, int32_t sq, const Cut& cut, bool dup) {
         if (ns + 1 > CAP) return fail(MT_DERR_CAPACITY, sq), false;
-        const bool front = k == a;  // new first child: it takes over the block's marks
+        const bool front = !dup && k == a;  // new first child: it takes over the block's marks
         PROF_BEGIN(ti0, P_B_INS);
-        if (dup) {
-            // (fetching slot k - 1 and shifting it in measured faster than an in-register duplicate:
-            // profiles/r04_ab_split_htop_C3.log)
-            Elem r = get(k - 1);
-            r.li = cut.rli;
-            // (narrow form up to K = 8: slot k - 1 becomes the left part in the shift's own pass --
-            // patching it first by dynamic index held two copies of the slot arrays live: C3/C4/C5
-            // +0.4-0.7 %, C4's <6> 1.81 -> 1.61x PMC traffic, C5's <2>/<3> 2.53/1.99 -> 2.33/1.70x.
-            // K >= 9 spilled more that way (<9>/<10>: 32/76 -> 44/88 B, 1.25/1.58 -> 1.37/1.77x) and
-            // the C64 form ran 9 % slower: they patch first. profiles/r05_ab_patch_shift/)
-            if constexpr (W || K >= 9) {
-                set_li_cf(k - 1, cut.lli, cut.lcf);
-                set_cum(k - 1, cut.pos);
-                shift_in<true>(k, r, false, 0, true);
-            } else {
-                shift_in<true, true>(k, r, false, 0, true, cut.lli, cut.lcf, cut.pos);
-            }
-        } else {
-            shift_in<true>(k, e, front, front ? sc_of(a) : 0, true);
-        }
+        // (a split's right part is the cut slot shifted one register right with its li replaced, in
+        // the same pass that writes the left part: no readlane of the slot, no dynamic-index patch)
+        const int scv = front ? sc_of(a) : 0;
+        shift_in<true>(k, e, front, scv, true, dup);
+        if (dup) patch_cut(k, cut);
         if (front) {
             set_bs(k + 1, false);
             set_sc(k + 1, MT_SC_UNDEF);
@@ -1136,12 +1142,12 @@ struct RWave {
     // site: step 0 scours the popped segment's block; on underflow steps 1..m scour every
     // sibling under its parent (pack's scourNode loop), then repack.
     MT_DEV void zamboni() {
-        for (int it = 0; it < 2; it++) {
+        // (continues and returns folded into conditions: one exit per loop, see apply)
+        for (int it = 0; it < 2 && !err; it++) {
             if (heap_n == 0 || uni(s.hseq[1]) > min_seq) break;
             PROF_BEGIN(tz, P_ZPOP);
             const int id = heap_pop();
-            if (id == (int)kDead) continue;
-            const int k = slot_of_id(id);
+            const int k = id == (int)kDead ? -1 : slot_of_id(id);
             if (k < 0) continue;
             const int a = block_start(k), e = next_start(k);
             PROF_END(prof, P_ZPOP, tz);
@@ -1159,22 +1165,25 @@ struct RWave {
                 PROF_CNT(P_N_SCOUR, 1);
                 const int kept = scour(aa, ee);
                 PROF_END(prof, P_SCOUR, ts);
-                if (err) return;
-                if (step == 0) {
-                    set_sc(a, MT_SC_FALSE);
-                    if (!(kept < cnt && kept < kMaxNodes / 2 && nlev > 1)) break;
-                    P = parent_of(0, leaf_of(a), &fc);
-                    m = uni(s.ibcnt[0][P]);
-                    A = bs_slot(fc);
-                } else {
-                    total += kept;
+                bool more = !err;
+                if (more) {
+                    if (step == 0) {
+                        set_sc(a, MT_SC_FALSE);
+                        more = kept < cnt && kept < kMaxNodes / 2 && nlev > 1;
+                        if (more) {
+                            P = parent_of(0, leaf_of(a), &fc);
+                            m = uni(s.ibcnt[0][P]);
+                            A = bs_slot(fc);
+                        }
+                    } else {
+                        total += kept;
+                    }
                 }
-                if (step == m) break;
+                if (!more || step == m) break;
             }
             PROF_BEGIN(tr, P_REPACK);
-            if (P >= 0) repack_leaf(P, fc, m, total, A, ee);
+            if (P >= 0 && !err) repack_leaf(P, fc, m, total, A, ee);
             PROF_END(prof, P_REPACK, tr);
-            if (err) return;
         }
     }
 
@@ -1214,14 +1223,15 @@ struct RWave {
         // insertingWalk descends into the first block whose cumulative visible end >= pos
         // (breakTie is true for blocks, :2248-2277): that leaf block's last slot is the first
         // block-ending slot with cum >= pos
+        // (bitwise, not short-circuit, here and below: no exec-masked branch per register)
         const uint32_t bm = bs_bits();
         const int nxt = shl1((int)(bm & 1u), 0);
         int last = 0x7fffffff;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
             const int i = idx(j);
-            const bool ends = (j + 1 < K ? ((bm >> (j + 1)) & 1u) != 0 : nxt != 0) || i == ns - 1;
-            last = (i < ns && ends && cum[j] >= pos) ? i : last;
+            const bool ends = (j + 1 < K ? ((bm >> (j + 1)) & 1u) != 0 : nxt != 0) | (i == ns - 1);
+            last = ((i < ns) & ends & (cum[j] >= pos)) ? i : last;
         }
         last = first_hit(last);  // slots are blocked by lane: the first lane with a hit has the minimum
         if (last == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
@@ -1238,9 +1248,9 @@ struct RWave {
                 const int i = idx(j);
                 const int ce = cum[j];
                 const int csj = j ? cum[j - 1] : cs;
-                const bool rm_before = (cf[j] & F_RM) && rseq[j] <= R;
-                const bool h = ((lvm >> j) & 1u) && i >= a && i < e &&
-                               (ce > pos || (ce == pos && csj == pos && !rm_before));
+                const bool rm_before = ((cf[j] & F_RM) != 0) & (rseq[j] <= R);
+                const bool h = (((lvm >> j) & 1u) != 0) & (i >= a) & (i < e) &
+                               ((ce > pos) | ((ce == pos) & (csj == pos) & !rm_before));
                 best = h ? i : best;
             }
         }
@@ -1383,20 +1393,27 @@ struct RWave {
         const int tlen = (int)op.payload_len - 2 * np;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
         if constexpr (EV) evseq = S;
+        // (the checks set a code instead of returning: apply runs inlined in the op loop, and every
+        // early exit is one more edge the CFG structurizer routes the register state along)
+        int bad = 0;
+        const bool ins = op.type == MT_OP_INSERT;
         if (!noop) {
-            if (op.client == 0 || op.client > (W ? kC64Clients : kNarrowClients)) return fail(MT_DERR_LIMITS, S);
-            if (op.payload_len < (uint32_t)(2 * np) || !MT_OP_NO_TEXT_OK(op)) return fail(MT_DERR_BAD_OP, S);
-            for (int q = 0; q < np; q++)
-                if (pbyte(pay, tlen + 2 * q) >= MT_MAX_KEYS) return fail(MT_DERR_LIMITS, S);
-            const bool ins = op.type == MT_OP_INSERT;
-            if (op.pos1 < 0 || (!ins && op.pos2 < 0)) return fail(MT_DERR_BAD_OP, S);
+            uint32_t kmax = 0;
+            if (op.payload_len >= (uint32_t)(2 * np))
+                for (int q = 0; q < np; q++) kmax = max(kmax, pbyte(pay, tlen + 2 * q));
             // the window asserts (completeAndLogOp client.ts:461-464, updateSeqNumbers :826) are
             // decided before any edit: the document halts before the failing message.  (The
             // reference runs them after the op, so a failing insert outranks them: mt_fixup_kernel,
             // after the apply, from the halted state.)
-            if (!(cur_seq < S)) return fail(MT_DERR_SEQ_ORDER, S);
-            if (!(min_seq <= op.msn)) return fail(MT_DERR_MSN_ORDER, S);
-            if (!(op.msn <= S)) return fail(MT_DERR_MSN_ORDER, S);
+            bad = (op.client == 0 || op.client > (W ? kC64Clients : kNarrowClients)) ? MT_DERR_LIMITS
+                  : (op.payload_len < (uint32_t)(2 * np) || !MT_OP_NO_TEXT_OK(op)) ? MT_DERR_BAD_OP
+                  : (np > 0 && kmax >= MT_MAX_KEYS) ? MT_DERR_LIMITS
+                  : (op.pos1 < 0 || (!ins && op.pos2 < 0)) ? MT_DERR_BAD_OP
+                  : !(cur_seq < S) ? MT_DERR_SEQ_ORDER
+                  : (!(min_seq <= op.msn) || !(op.msn <= S)) ? MT_DERR_MSN_ORDER : 0;
+            if (bad) fail(bad, S);
+        }
+        if (!noop && !bad) {
             PROF_BEGIN(t0, P_SCAN);
             scan(op.ref_seq, op.client);
             PROF_END(prof, P_SCAN, t0);
@@ -1404,81 +1421,95 @@ struct RWave {
             // the new segment; every step ends in the one insert_at call site
             const int nsteps = ins ? (tlen > 0 ? 2 : 1) : 2;
             int kl = -1;  // (an insert) the slot of the segment the boundary split at pos cut
+            // (one exit: every failing step has set err -- a return or continue from inside the loop
+            // is a multi-exit region that the CFG structurizer lowers with a flow variable and
+            // copies of the register state on its edges)
             for (int step = 0; step < nsteps; step++) {
                 PROF_BEGIN2(t1, P_BOUND, P_INSERT);
                 const bool placing = ins && step == 1;
                 Elem e{};
                 Cut cut{};
                 int k = 0, ba = 0, be = 0, t = -1;
+                bool go;
                 if (!placing) {
-                    if (!split_prep(step == 0 ? op.pos1 : op.pos2, S, cut, k, ba, be)) {
-                        if (err) return;
-                        continue;
-                    }
-                    kl = k - 1;
+                    go = split_prep(step == 0 ? op.pos1 : op.pos2, S, cut, k, ba, be);
+                    if (go) kl = k - 1;
                 } else {
                     t = place_prep(op, pay, tlen, np, e, k, ba, be, uni(kl));
-                    if (t < 0) return;
+                    go = t >= 0;
                 }
-                // (uniform by construction; the phi that merges the two prep paths is not
-                // provably so, and its users would run on the VALU)
-                k = uni(k);
-                ba = uni(ba);
-                be = uni(be);
-                t = uni(t);
+                if (go) {
+                    // (uniform by construction; the phi that merges the two prep paths is not
+                    // provably so, and its users would run on the VALU)
+                    k = uni(k);
+                    ba = uni(ba);
+                    be = uni(be);
+                    t = uni(t);
 #ifdef MT_UNI_ELEM
-                // (the inserted element and the cut as scalars: 4-8 B less scratch in most classes)
-                e.seq = uni(e.seq);
-                e.rseq = uni(e.rseq);
-                e.li = uniu(e.li);
-                e.cf = uniu(e.cf);
-                e.ov = uniu(e.ov);
-                e.oh = uniu(e.oh);
-                e.cum = uni(e.cum);
-                cut.lli = uniu(cut.lli);
-                cut.lcf = uniu(cut.lcf);
-                cut.rli = uniu(cut.rli);
-                cut.pos = uni(cut.pos);
+                    // (the inserted element and the cut as scalars: 4-8 B less scratch in most classes)
+                    e.seq = uni(e.seq);
+                    e.rseq = uni(e.rseq);
+                    e.li = uniu(e.li);
+                    e.cf = uniu(e.cf);
+                    e.ov = uniu(e.ov);
+                    e.oh = uniu(e.oh);
+                    e.cum = uni(e.cum);
+                    cut.lli = uniu(cut.lli);
+                    cut.lcf = uniu(cut.lcf);
+                    cut.rli = uniu(cut.rli);
+                    cut.pos = uni(cut.pos);
 #endif
-                const bool ok = insert_at(k, ba, be, e, S, cut, !placing);
-                if (placing) {
-                    PROF_END(prof, P_INSERT, t1);
-                } else {
-                    PROF_END(prof, P_BOUND, t1);
+                    const bool ok = insert_at(k, ba, be, e, S, cut, !placing);
+                    if (placing) {
+                        PROF_END(prof, P_INSERT, t1);
+                    } else {
+                        PROF_END(prof, P_BOUND, t1);
+                    }
+                    if (ok && placing) {
+                        // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179): the new segment's block
+                        // after a possible split, the one holding slot k
+                        const bool lru = S > min_seq ? add_lru(block_start(k), t, S) : true;
+                        if (EV && lru)  // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988)
+                            emit(MT_EV_INSERT, MT_EVF_FIRST, live_before(k), local_before(k), (uint32_t)tlen);
+                    }
                 }
-                if (!ok) return;
-                if (placing && S > min_seq) {  // saveIfLocal -> addToLRUSet (mergeTree.ts:2164-2179)
-                    // the new segment's block after a possible split: the one holding slot k
-                    if (!add_lru(block_start(k), t, S)) return;
+                if (err) break;
+            }
+            if (!err) {
+                if (EV && ins && tlen == 0) emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
+                if (!ins) {
+                    PROF_BEGIN(t2, P_RANGE);
+                    range_action(op, pay, tlen, np);
+                    PROF_END(prof, P_RANGE, t2);
                 }
-                if (EV && placing)  // MergeTreeDeltaType.INSERT (mergeTree.ts:1981-1988)
-                    emit(MT_EV_INSERT, MT_EVF_FIRST, live_before(k), local_before(k), (uint32_t)tlen);
             }
-            if (EV && ins && tlen == 0) emit(MT_EV_INSERT, MT_EVF_FIRST, -1, -1, 0);  // an empty text with props: never linked
-            if (!ins) {
-                PROF_BEGIN(t2, P_RANGE);
-                range_action(op, pay, tlen, np);
-                PROF_END(prof, P_RANGE, t2);
-            }
-            if (err) return;
         }
         const int32_t msn = op.msn;
-        for (int ph = 0; ph < 2; ph++) {
-            if (ph == 0) {
-                if (noop) continue;
-            } else {
-                if (op.flags & MT_F_GROUP_MORE) break;
-                // (a non-op message's asserts, all before its edits: the document halts before it)
-                if (!(cur_seq <= S)) return fail(MT_DERR_SEQ_ORDER, S);                   // client.ts:824
-                if (!(msn <= S) || !(min_seq <= msn)) return fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
-                cur_seq = S;
-                if (!(msn > min_seq)) break;
-                min_seq = msn;
+        // zamboni after the op, then updateSeqNumbers and zamboni again when the msn moved: one call
+        // site, one exit (err)
+#pragma clang loop unroll(disable)
+        for (int ph = 0; ph < 2 && !err; ph++) {
+            bool run = !noop;
+            if (ph == 1) {
+                run = false;
+                if (!(op.flags & MT_F_GROUP_MORE)) {
+                    // (a non-op message's asserts, all before its edits: the document halts before it)
+                    if (!(cur_seq <= S)) {
+                        fail(MT_DERR_SEQ_ORDER, S);  // client.ts:824
+                    } else if (!(msn <= S) || !(min_seq <= msn)) {
+                        fail(MT_DERR_MSN_ORDER, S);  // :826, mergeTree.ts:1722
+                    } else {
+                        cur_seq = S;
+                        run = msn > min_seq;
+                        if (run) min_seq = msn;
+                    }
+                }
             }
-            PROF_BEGIN(t3, P_ZAMBONI);
-            zamboni();
-            PROF_END(prof, P_ZAMBONI, t3);
-            if (err) return;
+            if (run) {
+                PROF_BEGIN(t3, P_ZAMBONI);
+                zamboni();
+                PROF_END(prof, P_ZAMBONI, t3);
+            }
         }
         if (EV && evn > (int)evcap) fail(MT_DERR_EVENTS, S);  // halt rather than drop callbacks
     }

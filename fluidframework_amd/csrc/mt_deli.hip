@@ -43,7 +43,11 @@ struct DeliState {
     int32_t* bref;
     uint8_t* bfl;
     uint32_t big_cap; // rows in the big pool
-    uint32_t* ctl;    // [0] rows in use, [1] documents queued for the wide form in this call
+    // [0] rows handed out fresh (a count that may pass big_cap: the attempts), [1] documents queued
+    // for the wide form in this call, [2] rows on the free list (as int: the kernel's pops may take it
+    // below zero, which reads as empty; the host repairs it before it pushes)
+    uint32_t* ctl;
+    uint32_t* free_rows;  // [big_cap]: rows given back by restored documents, a stack of ctl[2]
     uint32_t* queue;  // [max_docs]: those documents
     int32_t* resume;  // per queued document: its first message the wide form tickets
 };
@@ -301,14 +305,19 @@ __global__ __launch_bounds__(64) void deli_wide_kernel(DeliState g, const int4* 
         const int m0 = g.resume[d];
         uint32_t row = g.big[d];
         if (row == kNoRow) {
+            // a row from the free list (each pop that finds it non-empty takes a distinct entry: only
+            // pops run during the kernel), else a fresh one
             uint32_t r = 0;
-            if (lane == 0) r = atomicAdd(&g.ctl[0], 1u);
+            if (lane == 0) {
+                const int fr = atomicSub(reinterpret_cast<int*>(&g.ctl[2]), 1);
+                r = fr > 0 ? g.free_rows[fr - 1] : atomicAdd(&g.ctl[0], 1u);
+            }
             r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
             if (r >= g.big_cap) {  // no row left: the document halts at the message that needed one
                 if (lane == 0) {
                     int4 sc = g.sc[d];
                     if (!sc.w) {
-                        sc.w = MT_DELI_ERR_CLIENT;
+                        sc.w = MT_DELI_ERR_CAPACITY;
                         g.err_at[d] = m0;
                     }
                     g.sc[d] = sc;
@@ -357,7 +366,10 @@ __global__ void restore_all_kernel(DeliState g, uint32_t n_docs, mt_deli_checkpo
         g.sc[d] = make_int4(ck.seq, ck.msn, ck.last_sent_msn, 0);
         g.err_at[d] = -1;
         g.big[d] = kNoRow;  // (every document restored: the big pool starts over)
-        if (d == 0) g.ctl[0] = 0u;
+        if (d == 0) {
+            g.ctl[0] = 0u;
+            g.ctl[2] = 0u;
+        }
     }
 }
 
@@ -448,11 +460,34 @@ static uint32_t deli_big_rows(uint32_t max_docs) { return std::max<uint32_t>(64u
 
 namespace {
 // the constructor's msn (lambda.ts:166-167): min refSeq over the checkpoint's clients, or seq
-int32_t ckpt_msn(const mt_deli_checkpoint& ck) {
+template <class CK>
+int32_t ckpt_msn(const CK& ck) {
+    constexpr int NC = sizeof(ck.clients) / sizeof(ck.clients[0]);
     int32_t m = INT_MAX;
-    for (int c = 0; c < MT_MAX_CLIENTS; c++)
+    for (int c = 0; c < NC; c++)
         if (ck.clients[c].joined) m = std::min(m, ck.clients[c].ref_seq);
     return m == INT_MAX ? ck.seq : m;
+}
+uint8_t client_flags(const mt_deli_client& c) {
+    return (uint8_t)((c.joined ? mtd::CL_JOINED : 0) | (c.nack ? mtd::CL_NACK : 0));
+}
+// the rows of the big pool held by documents [doc0, doc0 + n) go back to its free list (their
+// documents are about to be restored); the stream is idle
+mt_status release_rows(mt_deli* dl, uint32_t doc0, uint32_t n) {
+    std::vector<uint32_t> big(n);
+    DL_HIP(hipMemcpy(big.data(), dl->g.big + doc0, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> rows;
+    for (uint32_t r : big)
+        if (r != mtd::kNoRow) rows.push_back(r);
+    if (rows.empty()) return MT_OK;
+    int32_t nfree = 0;
+    DL_HIP(hipMemcpy(&nfree, dl->g.ctl + 2, sizeof nfree, hipMemcpyDeviceToHost));
+    nfree = std::max(nfree, 0);  // (pops past empty left it below zero)
+    if ((uint64_t)nfree + rows.size() > dl->g.big_cap) return MT_ERR_STATE;  // (a row freed twice)
+    DL_HIP(hipMemcpy(dl->g.free_rows + nfree, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    nfree += (int32_t)rows.size();
+    DL_HIP(hipMemcpy(dl->g.ctl + 2, &nfree, sizeof nfree, hipMemcpyHostToDevice));
+    return MT_OK;
 }
 // the common form over every document, then the wide form over the documents it queued (past client
 // 63: promoted now or earlier), on one stream
@@ -503,6 +538,7 @@ mt_status mt_deli_create(int32_t device, uint32_t max_docs, mt_deli** out) {
               hipMalloc(&dl->g.bcsn, nb * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dl->g.bref, nb * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&dl->g.bfl, nb) == hipSuccess &&
+              hipMalloc(&dl->g.free_rows, dl->g.big_cap * sizeof(uint32_t)) == hipSuccess &&
               hipMemset(dl->g.big, 0xFF, max_docs * sizeof(uint32_t)) == hipSuccess &&
               hipMemset(dl->g.ctl, 0, 4 * sizeof(uint32_t)) == hipSuccess;
     if (!ok) {
@@ -524,7 +560,7 @@ mt_status mt_deli_destroy(mt_deli* dl) {
     if (dl->stream) hipStreamSynchronize(dl->stream);
     for (void* p : {(void*)dl->g.sc, (void*)dl->g.err_at, (void*)dl->g.csn, (void*)dl->g.ref, (void*)dl->g.fl,
                     (void*)dl->g.big, (void*)dl->g.resume, (void*)dl->g.queue, (void*)dl->g.ctl, (void*)dl->g.bcsn,
-                    (void*)dl->g.bref, (void*)dl->g.bfl})
+                    (void*)dl->g.bref, (void*)dl->g.bfl, (void*)dl->g.free_rows})
         if (p) hipFree(p);
     if (dl->e0) hipEventDestroy(dl->e0);
     if (dl->e1) hipEventDestroy(dl->e1);
@@ -537,6 +573,8 @@ mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_
     if (!dl || doc0 > dl->max_docs || n > dl->max_docs - doc0) return MT_ERR_ARG;
     if (n == 0) return MT_OK;
     DL_HIP(hipSetDevice(dl->device));
+    DL_HIP(hipStreamSynchronize(dl->stream));
+    if (const mt_status rs = release_rows(dl, doc0, n)) return rs;
     std::vector<int4> sc(n);
     std::vector<int32_t> err_at(n, -1), csn((size_t)n * MT_MAX_CLIENTS, 0), ref((size_t)n * MT_MAX_CLIENTS, 0);
     std::vector<uint8_t> fl((size_t)n * MT_MAX_CLIENTS, 0);
@@ -551,7 +589,7 @@ mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_
             const size_t k = (size_t)i * MT_MAX_CLIENTS + c;
             csn[k] = ck.clients[c].csn;
             ref[k] = ck.clients[c].ref_seq;
-            fl[k] = (uint8_t)((ck.clients[c].joined ? mtd::CL_JOINED : 0) | (ck.clients[c].nack ? mtd::CL_NACK : 0));
+            fl[k] = client_flags(ck.clients[c]);
         }
     }
     const size_t c0 = (size_t)doc0 * MT_MAX_CLIENTS, nc = (size_t)n * MT_MAX_CLIENTS;
@@ -561,8 +599,7 @@ mt_status mt_deli_restore(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_
     DL_HIP(hipMemcpyAsync(dl->g.csn + c0, csn.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, dl->stream));
     DL_HIP(hipMemcpyAsync(dl->g.ref + c0, ref.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, dl->stream));
     DL_HIP(hipMemcpyAsync(dl->g.fl + c0, fl.data(), nc, hipMemcpyHostToDevice, dl->stream));
-    // (a restored document is back in the common form; a row it held in the big pool is not reused
-    // until mt_deli_restore_all)
+    // (a restored document is back in the common form; the row it held is on the free list now)
     DL_HIP(hipMemsetAsync(dl->g.big + doc0, 0xFF, n * sizeof(uint32_t), dl->stream));
     DL_HIP(hipStreamSynchronize(dl->stream));
     return MT_OK;
@@ -699,20 +736,106 @@ static mt_status read_clients(mt_deli* dl, uint32_t doc, uint32_t c0, uint32_t n
     return MT_OK;
 }
 
-extern "C" {
-
-mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out) {
+template <class CK>
+static mt_status get_checkpoint(mt_deli* dl, uint32_t doc, CK* out) {
+    constexpr uint32_t NC = sizeof(out->clients) / sizeof(out->clients[0]);
     if (!dl || !out || doc >= dl->max_docs) return MT_ERR_ARG;
     DL_HIP(hipSetDevice(dl->device));
     int4 sc;
+    uint32_t row = mtd::kNoRow;
     DL_HIP(hipStreamSynchronize(dl->stream));
     DL_HIP(hipMemcpy(&sc, dl->g.sc + doc, sizeof sc, hipMemcpyDeviceToHost));
+    DL_HIP(hipMemcpy(&row, dl->g.big + doc, sizeof row, hipMemcpyDeviceToHost));
+    // a promoted document whose clients past 63 hold state does not fit the narrow checkpoint: refuse
+    // rather than drop them (a restore from it would lose them and derive another msn)
+    if (NC <= MT_MAX_CLIENTS && row != mtd::kNoRow) {
+        std::vector<uint8_t> fl(MT_DELI_MAX_CLIENTS - MT_MAX_CLIENTS);
+        DL_HIP(hipMemcpy(fl.data(), dl->g.bfl + (size_t)row * MT_DELI_MAX_CLIENTS + MT_MAX_CLIENTS, fl.size(),
+                         hipMemcpyDeviceToHost));
+        for (uint8_t f : fl)
+            if (f) return MT_ERR_WIDE;
+    }
     memset(out, 0, sizeof *out);
     out->seq = sc.x;
     out->msn = sc.y;
     out->last_sent_msn = sc.z;
     out->err = sc.w;
-    return read_clients(dl, doc, 0, MT_MAX_CLIENTS, out->clients);
+    return read_clients(dl, doc, 0, NC, out->clients);
+}
+
+extern "C" {
+
+mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out) {
+    return get_checkpoint(dl, doc, out);
+}
+
+mt_status mt_deli_get_checkpoint_wide(mt_deli* dl, uint32_t doc, mt_deli_checkpoint_wide* out) {
+    return get_checkpoint(dl, doc, out);
+}
+
+mt_status mt_deli_restore_wide(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_checkpoint_wide* ckpts) {
+    if (!dl || !ckpts || doc0 > dl->max_docs || n > dl->max_docs - doc0) return MT_ERR_ARG;
+    if (n == 0) return MT_OK;
+    DL_HIP(hipSetDevice(dl->device));
+    DL_HIP(hipStreamSynchronize(dl->stream));
+    // the documents needing a row (a client >= 64 joined or nacked), and whether the pool holds them
+    // once the rows of [doc0, doc0 + n) are back on the free list
+    std::vector<uint32_t> wide;
+    for (uint32_t i = 0; i < n; i++)
+        for (int c = MT_MAX_CLIENTS; c < MT_DELI_MAX_CLIENTS; c++)
+            if (ckpts[i].clients[c].joined || ckpts[i].clients[c].nack) {
+                wide.push_back(i);
+                break;
+            }
+    std::vector<uint32_t> held(n);
+    DL_HIP(hipMemcpy(held.data(), dl->g.big + doc0, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint32_t ctl[3] = {0, 0, 0};
+    DL_HIP(hipMemcpy(ctl, dl->g.ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    const uint32_t fresh = std::min(ctl[0], dl->g.big_cap);
+    const uint32_t nfree = (uint32_t)std::max((int32_t)ctl[2], 0);
+    const uint32_t freed = (uint32_t)std::count_if(held.begin(), held.end(), [](uint32_t r) { return r != mtd::kNoRow; });
+    if (wide.size() > (size_t)(dl->g.big_cap - fresh) + nfree + freed) return MT_ERR_NOMEM;
+    // the narrow part (clients 0..63, scalars) through mt_deli_restore, which also frees the rows
+    std::vector<mt_deli_checkpoint> narrow(n);
+    for (uint32_t i = 0; i < n; i++) {
+        mt_deli_checkpoint& k = narrow[i];
+        k.seq = ckpts[i].seq;
+        k.msn = 0;
+        k.last_sent_msn = ckpts[i].last_sent_msn;
+        k.err = 0;
+        memcpy(k.clients, ckpts[i].clients, sizeof k.clients);
+    }
+    if (const mt_status st = mt_deli_restore(dl, doc0, n, narrow.data())) return st;
+    if (wide.empty()) return MT_OK;
+    // rows for the wide documents: free list first (mt_deli_restore just pushed), then fresh ones
+    DL_HIP(hipMemcpy(ctl, dl->g.ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    int32_t top = std::max((int32_t)ctl[2], 0);
+    uint32_t next = std::min(ctl[0], dl->g.big_cap);
+    std::vector<uint32_t> stack((size_t)top);
+    if (top) DL_HIP(hipMemcpy(stack.data(), dl->g.free_rows, top * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<int32_t> csn(MT_DELI_MAX_CLIENTS), ref(MT_DELI_MAX_CLIENTS);
+    std::vector<uint8_t> fl(MT_DELI_MAX_CLIENTS);
+    for (uint32_t i : wide) {
+        const uint32_t row = top > 0 ? stack[--top] : next++;  // (capacity checked above)
+        const mt_deli_checkpoint_wide& ck = ckpts[i];
+        for (int c = 0; c < MT_DELI_MAX_CLIENTS; c++) {
+            csn[c] = ck.clients[c].csn;
+            ref[c] = ck.clients[c].ref_seq;
+            fl[c] = client_flags(ck.clients[c]);
+        }
+        const size_t o = (size_t)row * MT_DELI_MAX_CLIENTS;
+        DL_HIP(hipMemcpy(dl->g.bcsn + o, csn.data(), MT_DELI_MAX_CLIENTS * sizeof(int32_t), hipMemcpyHostToDevice));
+        DL_HIP(hipMemcpy(dl->g.bref + o, ref.data(), MT_DELI_MAX_CLIENTS * sizeof(int32_t), hipMemcpyHostToDevice));
+        DL_HIP(hipMemcpy(dl->g.bfl + o, fl.data(), MT_DELI_MAX_CLIENTS, hipMemcpyHostToDevice));
+        DL_HIP(hipMemcpy(dl->g.big + doc0 + i, &row, sizeof row, hipMemcpyHostToDevice));
+        // the constructor's msn over every client (lambda.ts:166-167)
+        const int4 sc = make_int4(ck.seq, ckpt_msn(ck), ck.last_sent_msn, 0);
+        DL_HIP(hipMemcpy(dl->g.sc + doc0 + i, &sc, sizeof sc, hipMemcpyHostToDevice));
+    }
+    ctl[0] = std::max(ctl[0], next);
+    ctl[2] = (uint32_t)top;
+    DL_HIP(hipMemcpy(dl->g.ctl, ctl, sizeof ctl, hipMemcpyHostToDevice));  // ([1] is per call: rewritten as read)
+    return MT_OK;
 }
 
 mt_status mt_deli_get_clients(mt_deli* dl, uint32_t doc, uint32_t first, uint32_t n, mt_deli_client* out) {

@@ -360,23 +360,33 @@ static mt_status assign_loc_rows(mt_engine* e, const uint32_t* ids, uint32_t cnt
     return MT_OK;
 }
 
-// A document that starts over (mt_docs_load) gives its pool rows back: the next document that needs
-// such a form reuses them before the pools grow (its 1024-slot row is copied in then, as for a new row)
-static mt_status release_loc_rows(mt_engine* e, uint32_t d) {
-    if (d >= e->h_locbig.size()) return MT_OK;
-    const uint32_t none = MT_NO_ROW;
-    if (e->h_locbig[d] != MT_NO_ROW) {
-        e->free_big.push_back(e->h_locbig[d]);
-        e->h_locbig[d] = MT_NO_ROW;
-        HIP_OK(hipMemcpyAsync(e->g.locbig + d, &none, 4, hipMemcpyHostToDevice, e->stream));
-        HIP_OK(hipStreamSynchronize(e->stream));
+// Documents that start over (mt_docs_load) give their pool rows back: the next document that needs
+// such a form reuses them before the pools grow (its 1024-slot row is copied in then, as for a new
+// row).  The host mirrors are updated per document; the device tables get one copy of the changed
+// span each and one synchronization (not two round trips per document).
+static mt_status release_loc_rows(mt_engine* e, const uint32_t* docs, uint32_t n) {
+    uint32_t lo[2] = {UINT32_MAX, UINT32_MAX}, hi[2] = {0, 0};
+    std::vector<uint32_t>* mirror[2] = {&e->h_locbig, &e->h_locgx};
+    std::vector<uint32_t>* freel[2] = {&e->free_big, &e->free_gx};
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t d = docs[i];
+        for (int k = 0; k < 2; k++) {
+            if (d >= mirror[k]->size() || (*mirror[k])[d] == MT_NO_ROW) continue;
+            freel[k]->push_back((*mirror[k])[d]);
+            (*mirror[k])[d] = MT_NO_ROW;
+            lo[k] = std::min(lo[k], d);
+            hi[k] = std::max(hi[k], d + 1);
+        }
     }
-    if (e->h_locgx[d] != MT_NO_ROW) {
-        e->free_gx.push_back(e->h_locgx[d]);
-        e->h_locgx[d] = MT_NO_ROW;
-        HIP_OK(hipMemcpyAsync(e->g.locgx + d, &none, 4, hipMemcpyHostToDevice, e->stream));
-        HIP_OK(hipStreamSynchronize(e->stream));
+    uint32_t* dev[2] = {e->g.locbig, e->g.locgx};
+    bool any = false;
+    for (int k = 0; k < 2; k++) {
+        if (lo[k] >= hi[k]) continue;
+        HIP_OK(hipMemcpyAsync(dev[k] + lo[k], mirror[k]->data() + lo[k], 4ull * (hi[k] - lo[k]), hipMemcpyHostToDevice,
+                              e->stream));
+        any = true;
     }
+    if (any) HIP_OK(hipStreamSynchronize(e->stream));
     return MT_OK;
 }
 
@@ -629,10 +639,7 @@ mt_status mt_docs_load(mt_engine* e, uint32_t n, const uint32_t* doc_ids, const 
         wide = wide || wide_load_seg(sg);
     }
     HIP_OK(hipSetDevice(e->cfg.device));
-    for (uint32_t i = 0; i < n; i++) {
-        const mt_status rs = release_loc_rows(e, doc_ids[i]);
-        if (rs) return rs;
-    }
+    if (const mt_status rs = release_loc_rows(e, doc_ids, n)) return rs;
     HIP_OK(hipSetDevice(e->cfg.device));
     if (wide) {
         const mt_status ws = ensure_wide(e);
@@ -1411,14 +1418,19 @@ mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* p
                 }
             if (!msgs) continue;
             uint32_t t = 0;
+            uint64_t prev = 0;  // 1 + the last record a message of this document carried
             for (uint64_t i = msg_row_ptr[d]; i < msg_row_ptr[d + 1]; i++) {
                 const mt_raw_msg& x = msgs[i];
                 if (x.op_index) {
                     const uint64_t rec = x.op_index - 1;
-                    if (rec < doc_row_ptr[d] || rec >= doc_row_ptr[d + 1]) {
-                        bad = true;  // (a message carries a record of its own document)
+                    // (a message carries a record of its own document, each record once and in stream
+                    // order: a record behind the previous one would put its message in an earlier tick
+                    // than the message before it, and deli would ticket the stream out of order)
+                    if (rec < doc_row_ptr[d] || rec >= doc_row_ptr[d + 1] || x.op_index <= prev) {
+                        bad = true;
                         return;
                     }
+                    prev = x.op_index;
                     t = tick_of(d, rec);
                 }
                 if (!write) {

@@ -248,7 +248,9 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
             uint32_t nrem_hi = 0;
             unsigned long long ob = 0;
             // one pass over this launch's records (each is read once: the loops below were separate)
-            bool win = ops && sc.win_op < 0;
+            // (only a document with no recorded failure and no sticky error: -2 marks a record the
+            // fixup consumed, and a halted document's window is never replayed again)
+            bool win = ops && sc.win_op == -1 && sc.err == 0;
             int32_t cur = sc.cur_seq, mn = sc.min_seq;
             for (uint32_t i = a; ops && i < b; i++) {
                 const mt_op_rec o = ops[i];

@@ -43,7 +43,8 @@ struct mt_doc_scalars {      // 84 bytes
     uint32_t wide;           // MT_WIDE_LDS: a client id above 32 was seen (the document stays on the LDS
                              // engine); MT_WIDE_DOC: the wide representation (include/mtgpu.h "limits")
     int32_t win_op;          // batch index of the first op failing a window assert (binning's
-                             // replay of the window), -1 if none: mt_fixup_kernel's input
+                             // replay of the window), -1 if none, -2 once mt_fixup_kernel
+                             // (its reader) consumed it
     uint32_t label_keys;     // key ids of "referenceTileLabels" (bits 0-7) and "referenceRangeLabels"
                              // (bits 8-15), 0xFF: none; MT_NO_LABEL_KEYS: block caches not tracked
 };

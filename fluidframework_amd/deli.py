@@ -19,7 +19,9 @@ OP, NOOP, NOOP_DATA, JOIN, LEAVE, SERVER_NOOP, NOCLIENT, CONTROL = range(8)
 DROPPED, SENT, LATER, NEVER, NACK_GAP, NACK_CLIENT, NACK_REFSEQ, HALTED = range(8)
 STATUS_NAMES = ['dropped', 'sent', 'later', 'never', 'nack-gap', 'nack-client', 'nack-refseq', 'halted']
 DELI_ERRORS = {0: None, 1: 'client id out of range', 2: 'unknown message kind',
-               3: 'assert(referenceSequenceNumber >= minimumSequenceNumber) (lambda.ts:426-428)'}
+               3: 'assert(referenceSequenceNumber >= minimumSequenceNumber) (lambda.ts:426-428)',
+               4: 'capacity: no big-pool row left for a document past client 63'}
+ERR_CAPACITY = 4  # mt_deli_err MT_DELI_ERR_CAPACITY
 MAX_CLIENTS = 512  # include/mtgpu.h MT_DELI_MAX_CLIENTS (up to 63: eight documents per wave; then the wide form)
 CKPT_CLIENTS = 64  # mt_deli_checkpoint's client slots
 
@@ -37,6 +39,11 @@ class _Client(ctypes.Structure):
 class _Checkpoint(ctypes.Structure):
     _fields_ = [('seq', ctypes.c_int32), ('msn', ctypes.c_int32), ('last_sent_msn', ctypes.c_int32),
                 ('err', ctypes.c_int32), ('clients', _Client * CKPT_CLIENTS)]
+
+
+class _CheckpointWide(ctypes.Structure):  # mt_deli_checkpoint_wide: every client slot
+    _fields_ = [('seq', ctypes.c_int32), ('msn', ctypes.c_int32), ('last_sent_msn', ctypes.c_int32),
+                ('err', ctypes.c_int32), ('clients', _Client * MAX_CLIENTS)]
 
 
 _bound = False
@@ -58,23 +65,27 @@ def _lib():
         L.mt_deli_sync.argtypes = [vp]
         L.mt_deli_last_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.mt_deli_get_checkpoint.argtypes = [vp, u32, vp]
+        L.mt_deli_get_checkpoint_wide.argtypes = [vp, u32, vp]
+        L.mt_deli_restore_wide.argtypes = [vp, u32, u32, vp]
         L.mt_deli_get_clients.argtypes = [vp, u32, u32, u32, vp]
         L.mt_deli_doc_error.argtypes = [vp, u32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.mt_batch_device_ptrs.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]
         for name in ('mt_deli_create', 'mt_deli_destroy', 'mt_deli_restore', 'mt_deli_restore_all', 'mt_deli_ticket',
                      'mt_deli_ticket_device', 'mt_deli_raw_from_ops', 'mt_deli_raw_stream', 'mt_deli_sync', 'mt_deli_last_ms',
-                     'mt_deli_get_checkpoint', 'mt_deli_get_clients', 'mt_deli_doc_error', 'mt_batch_device_ptrs'):
+                     'mt_deli_get_checkpoint', 'mt_deli_get_clients', 'mt_deli_doc_error', 'mt_batch_device_ptrs',
+                     'mt_deli_get_checkpoint_wide', 'mt_deli_restore_wide'):
             getattr(L, name).restype = ctypes.c_int
         _bound = True
     return L
 
 
-def make_checkpoint(seq=0, clients=None, last_sent_msn=0):
-    """IDeliState -> mt_deli_checkpoint.  clients: {short id: (csn, ref_seq, nack)}."""
-    ck = _Checkpoint()
+def make_checkpoint(seq=0, clients=None, last_sent_msn=0, wide=False):
+    """IDeliState -> mt_deli_checkpoint (wide: mt_deli_checkpoint_wide, client ids up to MAX_CLIENTS - 1).
+    clients: {short id: (csn, ref_seq, nack)}."""
+    ck = _CheckpointWide() if wide else _Checkpoint()
     ck.seq, ck.last_sent_msn = seq, last_sent_msn
     for c, (csn, ref, nack) in (clients or {}).items():
-        if not 0 <= c < CKPT_CLIENTS:
+        if not 0 <= c < (MAX_CLIENTS if wide else CKPT_CLIENTS):
             raise MtError(f'client id {c} out of range of a checkpoint')
         ck.clients[c].csn, ck.clients[c].ref_seq = csn, ref
         ck.clients[c].joined, ck.clients[c].nack = 1, int(bool(nack))
@@ -102,9 +113,16 @@ class DeliSequencer:
 
     def restore(self, checkpoints, doc0=0):
         """new DeliLambda(..., lastCheckpoint) for documents doc0.. (lambda.ts:112-171);
-        checkpoints: list of dicts {seq, clients: {id: (csn, ref, nack)}, last_sent_msn}."""
-        arr = (_Checkpoint * len(checkpoints))(*[make_checkpoint(**ck) for ck in checkpoints])
-        _check(_lib().mt_deli_restore(self.h, doc0, len(checkpoints), ctypes.cast(arr, ctypes.c_void_p)),
+        checkpoints: list of dicts {seq, clients: {id: (csn, ref, nack)}, last_sent_msn}.  A checkpoint
+        with a client id >= 64 goes through the wide form (mt_deli_restore_wide: a big-pool row)."""
+        cks = [{k: v for k, v in ck.items() if k in ('seq', 'clients', 'last_sent_msn')} for ck in checkpoints]
+        if any(c >= CKPT_CLIENTS for ck in cks for c in (ck.get('clients') or {})):
+            arr = (_CheckpointWide * len(cks))(*[make_checkpoint(wide=True, **ck) for ck in cks])
+            _check(_lib().mt_deli_restore_wide(self.h, doc0, len(cks), ctypes.cast(arr, ctypes.c_void_p)),
+                   'mt_deli_restore_wide')
+            return
+        arr = (_Checkpoint * len(cks))(*[make_checkpoint(**ck) for ck in cks])
+        _check(_lib().mt_deli_restore(self.h, doc0, len(cks), ctypes.cast(arr, ctypes.c_void_p)),
                'mt_deli_restore')
 
     def restore_all(self, n_docs=None, **checkpoint):
@@ -147,13 +165,19 @@ class DeliSequencer:
     def checkpoint(self, doc):
         """generateDeliCheckpoint (lambda.ts:754-764), device-representable part: every joined client
         (ids up to MAX_CLIENTS - 1, mt_deli_get_clients)."""
-        ck = _Checkpoint()
-        _check(_lib().mt_deli_get_checkpoint(self.h, doc, ctypes.byref(ck)), 'mt_deli_get_checkpoint')
-        cl = (_Client * MAX_CLIENTS)()
-        _check(_lib().mt_deli_get_clients(self.h, doc, 0, MAX_CLIENTS, ctypes.cast(cl, ctypes.c_void_p)),
-               'mt_deli_get_clients')
+        ck = _CheckpointWide()
+        _check(_lib().mt_deli_get_checkpoint_wide(self.h, doc, ctypes.byref(ck)), 'mt_deli_get_checkpoint_wide')
+        cl = ck.clients
         return {'seq': ck.seq, 'msn': ck.msn, 'last_sent_msn': ck.last_sent_msn, 'err': ck.err,
                 'clients': {c: (cl[c].csn, cl[c].ref_seq, bool(cl[c].nack)) for c in range(MAX_CLIENTS) if cl[c].joined}}
+
+    def checkpoint_narrow(self, doc):
+        """mt_deli_get_checkpoint: the 64-client form; raises (MT_ERR_WIDE) for a document past client 63."""
+        ck = _Checkpoint()
+        _check(_lib().mt_deli_get_checkpoint(self.h, doc, ctypes.byref(ck)), 'mt_deli_get_checkpoint')
+        return {'seq': ck.seq, 'msn': ck.msn, 'last_sent_msn': ck.last_sent_msn, 'err': ck.err,
+                'clients': {c: (ck.clients[c].csn, ck.clients[c].ref_seq, bool(ck.clients[c].nack))
+                            for c in range(CKPT_CLIENTS) if ck.clients[c].joined}}
 
     def error(self, doc):
         err, idx = ctypes.c_int32(), ctypes.c_int32()

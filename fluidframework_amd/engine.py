@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('MTGPU_LIB') or os.path.join(HERE, 'libmtgpu.so')
 
 MT_ERRORS = {0: 'ok', 1: 'bad argument', 2: 'HIP error', 3: 'out of device memory', 4: 'bad state',
-             5: 'document error'}
+             5: 'document error', 6: 'RCCL error', 7: 'document past the form of the call (wide)'}
 DOC_ERRORS = {0: None,
               1: "Incoming remote op sequence# <= local collabWindow's currentSequence#",
               2: "Incoming remote op minSequence# < local collabWindow's minSequence#",

@@ -153,7 +153,9 @@ typedef enum mt_status {
     MT_ERR_NOMEM = 3,
     MT_ERR_STATE = 4,
     MT_ERR_DOC = 5,         /* at least one document has a sticky error (see mt_doc_error) */
-    MT_ERR_COMM = 6         /* an RCCL call failed (mt_comm_*) */
+    MT_ERR_COMM = 6,        /* an RCCL call failed (mt_comm_*) */
+    MT_ERR_WIDE = 7         /* the call's form cannot express the document (a deli checkpoint of a
+                               document past client 63: mt_deli_get_checkpoint_wide) */
 } mt_status;
 
 /* per-document sticky error codes (mirror the reference's assert/throw sites) */
@@ -625,16 +627,19 @@ typedef struct mt_ticket {  /* 16 bytes */
 /* Client ids: a document holds short ids 0..MT_DELI_MAX_CLIENTS-1.  Up to id 63 it is ticketed eight
  * documents per wave; its first message from a client >= 64 promotes it, for good, to the wide form
  * (one document per wave, its clients in a row of the deli's big pool: one row per 16 documents of
- * max_docs, at least 64; mt_deli_restore_all empties the pool).  The reference keeps a Map and a heap
- * (clientSeqManager.ts:70-143, joins at lambda.ts:280-306): no limit. */
+ * max_docs, at least 64).  mt_deli_restore / mt_deli_restore_wide give a restored document's row back
+ * to the pool (a free list the next promotion takes first), mt_deli_restore_all empties the pool.  The
+ * reference keeps a Map and a heap (clientSeqManager.ts:70-143, joins at lambda.ts:280-306): no limit. */
 #define MT_DELI_MAX_CLIENTS 512
 
 /* per-document sticky deli errors (the reference lambda throws / has no representation) */
 typedef enum mt_deli_err {
     MT_DELI_OK = 0,
-    MT_DELI_ERR_CLIENT = 1, /* short client id >= MT_DELI_MAX_CLIENTS, or no big-pool row left      */
+    MT_DELI_ERR_CLIENT = 1, /* short client id >= MT_DELI_MAX_CLIENTS                               */
     MT_DELI_ERR_KIND = 2,   /* unknown mt_raw_kind                                                  */
-    MT_DELI_ERR_ASSERT = 3  /* assert(refSeq >= msn) lambda.ts:426-428 (a client no-op with ref -1) */
+    MT_DELI_ERR_ASSERT = 3, /* assert(refSeq >= msn) lambda.ts:426-428 (a client no-op with ref -1) */
+    MT_DELI_ERR_CAPACITY = 4 /* a client >= 64 needed a big-pool row and none was left (a capacity
+                               limit of this engine, not an error of the stream)                    */
 } mt_deli_err;
 
 typedef struct mt_deli_client {
@@ -652,6 +657,14 @@ typedef struct mt_deli_checkpoint {  /* IDeliState (lambda.ts:754-764), device-r
     int32_t err;            /* mt_deli_err (read back; ignored on restore)                          */
     mt_deli_client clients[MT_MAX_CLIENTS];
 } mt_deli_checkpoint;
+
+typedef struct mt_deli_checkpoint_wide {  /* the same with every client slot (documents past client 63) */
+    int32_t seq;
+    int32_t msn;
+    int32_t last_sent_msn;
+    int32_t err;
+    mt_deli_client clients[MT_DELI_MAX_CLIENTS];
+} mt_deli_checkpoint_wide;
 
 typedef struct mt_deli mt_deli;
 mt_status mt_deli_create(int32_t device, uint32_t max_docs, mt_deli** out);
@@ -688,7 +701,14 @@ mt_status mt_deli_raw_stream(mt_deli* dl, const mt_op_rec* d_ops, const uint32_t
 mt_status mt_deli_sync(mt_deli* dl);
 /* Kernel time of the last mt_deli_ticket / mt_deli_ticket_device (HIP events around the launch). */
 mt_status mt_deli_last_ms(mt_deli* dl, float* kernel_ms);
-mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);  /* (clients < 64) */
+/* generateDeliCheckpoint (lambda.ts:754-764).  A document holding a client >= 64 (joined or nacked)
+ * does not fit mt_deli_checkpoint: the call returns MT_ERR_WIDE and writes nothing -- read it
+ * with mt_deli_get_checkpoint_wide, which serves every document (clients past 63 zero when unpromoted). */
+mt_status mt_deli_get_checkpoint(mt_deli* dl, uint32_t doc, mt_deli_checkpoint* out);
+mt_status mt_deli_get_checkpoint_wide(mt_deli* dl, uint32_t doc, mt_deli_checkpoint_wide* out);
+/* mt_deli_restore from wide checkpoints: a document with any client >= 64 joined or nacked takes a row of
+ * the big pool (its free list first); MT_ERR_NOMEM and nothing restored when the pool cannot hold them. */
+mt_status mt_deli_restore_wide(mt_deli* dl, uint32_t doc0, uint32_t n, const mt_deli_checkpoint_wide* ckpts);
 /* clients [first, first + n) of a document (any id < MT_DELI_MAX_CLIENTS; not joined: zeros) */
 mt_status mt_deli_get_clients(mt_deli* dl, uint32_t doc, uint32_t first, uint32_t n, mt_deli_client* out);
 /* err = mt_deli_err, index = position of the failing message inside the document's stream */

@@ -9,6 +9,8 @@ import pytest
 from deli_streams import FIELDS, SPEC, oracle_tickets, random_streams, to_batch
 from oracle import deli as od
 
+ERR_CAPACITY = 4  # include/mtgpu.h MT_DELI_ERR_CAPACITY (an engine limit: the oracle has none)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -105,8 +107,9 @@ def test_documents_past_64_clients_against_oracle(seed, n_clients, n_msgs):
 
 def test_big_pool_exhausted_halts_the_document():
     """The big pool holds max(64, max_docs / 16) documents past client 63: with 80 such documents the
-    80 - 64 promoted last halt at the message that needed a row (MT_DELI_ERR_CLIENT, the rest of
-    their tickets HALTED); the others are ticketed as the restatement does."""
+    80 - 64 promoted last halt at the message that needed a row (MT_DELI_ERR_CAPACITY -- an engine
+    limit, told apart from a bad client id -- the rest of their tickets HALTED); the others are
+    ticketed as the restatement does."""
     streams = []
     for d in range(80):
         s = [(od.JOIN, c, -1, -1) for c in range(60, 70)] + [(od.OP, 65, 1, 10), (od.OP, 61, 1, 11)]
@@ -120,10 +123,69 @@ def test_big_pool_exhausted_halts_the_document():
     for d in range(80):
         g, w = got[rp[d]:rp[d + 1]], want[rp[d]:rp[d + 1]]
         if d in halted:
-            assert dl.error(d) == (od.ERR_CLIENT, 4)  # the join of client 64
+            assert dl.error(d) == (ERR_CAPACITY, 4)  # the join of client 64
             assert np.array_equal(g[:4], w[:4]) and np.all(g[4:, 3] == od.HALTED), d
         else:
             assert np.array_equal(g, w), d
+
+
+def test_big_pool_rows_come_back_on_restore():
+    """Restoring a promoted document gives its big-pool row back (a free list the next promotion takes
+    first): 64 documents fill the pool, 16 of them are restored, and 16 new documents then promote
+    without MT_DELI_ERR_CAPACITY; a row is never shared (every document's tickets as the restatement's)."""
+    def wide_stream(d):
+        return [(od.JOIN, c, -1, -1) for c in range(60, 70)] + [(od.OP, 65, 1, 10 + d % 3), (od.OP, 61, 1, 11)]
+    n = 128  # max(64, n / 16) = 64 rows
+    first = [wide_stream(d) if d < 64 else [] for d in range(n)]
+    dl = _seq(n)
+    dl.ticket(*to_batch(first))
+    _, first_docs = oracle_tickets(first)
+    assert all(dl.error(d)[0] == 0 for d in range(64))
+    dl.restore([{'seq': 0, 'clients': {}, 'last_sent_msn': 0}] * 16, doc0=8)  # documents 8..23 back to new
+    assert all(dl.checkpoint(d)['clients'] == {} for d in range(8, 24))
+    second = [wide_stream(d) if 64 <= d < 80 else [] for d in range(n)]
+    want, docs = oracle_tickets(second)
+    got = _tickets(dl.ticket(*to_batch(second)))
+    assert np.array_equal(got, want)
+    assert all(dl.error(d)[0] == 0 for d in range(n))
+    for d in list(range(64, 80)) + [0, 7, 24, 63]:  # the new rows, and rows the restore left alone
+        assert dl.checkpoint(d)['clients'] == (docs[d] if d >= 64 else first_docs[d]).checkpoint()['clients'], d
+    # one more promotion finds the pool full again
+    third = [wide_stream(d) if d == 100 else [] for d in range(n)]
+    dl.ticket(*to_batch(third))
+    assert dl.error(100) == (ERR_CAPACITY, 4)
+
+
+@pytest.mark.parametrize('seed,n_clients', [(31, 96), (32, 300)])
+def test_wide_checkpoint_round_trip(seed, n_clients):
+    """generateDeliCheckpoint / restore of documents past client 63: the narrow checkpoint call refuses
+    them (MT_ERR_WIDE, nothing dropped), the wide one carries every client, and a deli restored from it
+    tickets the rest of the stream as the restatement does (the msn derived over all clients)."""
+    from fluidframework_amd.engine import MtError
+    streams = random_streams(24, 1200, seed=seed, n_clients=n_clients)
+    half = [s[:len(s) // 2] for s in streams]
+    rest = [s[len(s) // 2:] for s in streams]
+    dl = _seq(len(streams))
+    dl.ticket(*to_batch(half))
+    _, docs = oracle_tickets(half)
+    cks = []
+    for d in range(len(streams)):
+        ck, o = dl.checkpoint(d), docs[d].checkpoint()
+        assert ck['clients'] == o['clients'] and (ck['seq'], ck['msn']) == (o['seq'], o['msn']), d
+        if max(o['clients'], default=0) >= 64:
+            with pytest.raises(MtError, match='wide'):
+                dl.checkpoint_narrow(d)
+        else:
+            assert dl.checkpoint_narrow(d)['clients'] == o['clients'], d
+        cks.append({'seq': ck['seq'], 'clients': ck['clients'], 'last_sent_msn': ck['last_sent_msn']})
+    assert any(max(c['clients'], default=0) >= 64 for c in cks)
+    want, _ = oracle_tickets(rest, checkpoints=cks)
+    dl2 = _seq(len(streams))
+    dl2.restore(cks)
+    for d in range(len(streams)):
+        got_ck = dl2.checkpoint(d)
+        assert got_ck['clients'] == cks[d]['clients'] and got_ck['msn'] == od.DeliDoc(**cks[d]).msn, d
+    assert np.array_equal(_tickets(dl2.ticket(*to_batch(rest))), want)
 
 
 def test_restore_from_checkpoints():

@@ -145,6 +145,40 @@ def test_malformed_logs_are_refused():
         TickLog.from_batch(OpBatch(batch.ops, batch.payload, rp), 32, pinned=False)
 
 
+def test_messages_out_of_record_order_are_refused():
+    """A document's messages must carry its records in stream order, each once: a message pointing at a
+    record before the previous message's would land in an earlier tick than that message and deli
+    would ticket the stream out of order, so the layout refuses it (MT_ERR_ARG)."""
+    from fluidframework_amd.deli import OP, RAW_DTYPE
+    from fluidframework_amd.engine import MtError
+    from fluidframework_amd.ticks import TickLog
+    batch, _ = load_golden('synth_c2')
+    D = batch.n_docs
+
+    def stream(swap=None, dup=None):
+        msgs, mrp = [], [0]
+        for d in range(D):
+            recs = list(range(int(batch.row_ptr[d]), int(batch.row_ptr[d + 1])))
+            if d == 1 and swap is not None and len(recs) > swap + 1:
+                recs[swap], recs[swap + 1] = recs[swap + 1], recs[swap]
+            if d == 1 and dup is not None and len(recs) > dup + 1:
+                recs[dup + 1] = recs[dup]
+            msgs += [(i, 0, 1, OP, i + 1) for i in recs]
+            mrp.append(mrp[-1] + len(recs))
+        raw = np.zeros(len(msgs), dtype=RAW_DTYPE)
+        for k, f in enumerate(('csn', 'ref_seq', 'client', 'kind', 'op_index')):
+            raw[f] = [x[k] for x in msgs]
+        return raw, np.array(mrp, dtype=np.uint32)
+
+    assert int(batch.row_ptr[2] - batch.row_ptr[1]) > 20
+    raw, mrp = stream()
+    TickLog.from_batch(batch, 16, msgs=raw, msg_row_ptr=mrp, pinned=False)  # in order: accepted
+    for kw in ({'swap': 3}, {'swap': 15}, {'dup': 7}):  # inside one tick, across ticks 0/1, a repeat
+        raw, mrp = stream(**kw)
+        with pytest.raises(MtError):
+            TickLog.from_batch(batch, 16, msgs=raw, msg_row_ptr=mrp, pinned=False)
+
+
 def test_layout_on_all_host_cores():
     """Past 4096 documents the layout runs on several host threads (document ranges): the same
     result, checked vectorised -- every record at its tick-major place, every payload byte moved."""

@@ -46,6 +46,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
 PMC_ROUND = 'r05'
+SQ_ROUND = 'r06'   # profiles/<round>_sq_counters_C3_pass{1,2}.txt (tools/sq_pass.sh): the issue roofline
+# instruction issue peaks (MI355X_MICROARCH.md "Wave scheduling"): 256 CUs x 4 SIMDs, a wave64 VALU
+# instruction every 2 cycles per SIMD at 2.4 GHz; one scalar (SALU) instruction per CU per cycle
+VALU_PEAK = 1024 * 2.4e9 / 2
+SALU_PEAK = 256 * 2.4e9
 CAL_ROUND = 'r04'  # profiles/<round>_js_calibration_<config>.json: r of the JS baseline (oracle/tsref/calibrate.py)
 
 CONFIG_NAMES = {'C2': 'BASELINE.json configs[1]', 'C3': 'BASELINE.json configs[2]', 'C4': 'BASELINE.json configs[3]',
@@ -72,6 +77,53 @@ def pmc_traffic(kernel, config):
         hit = [v for n, v in ks.items() if n.startswith(kernel[:-1] + ', ')]
         k = hit[0] if len(hit) == 1 else None
     return int(k['hbm_bytes_per_launch']) if k else None
+
+
+def mangled_stem(kernel):
+    """'mtr::reg_apply_kernel<9>' -> '3mtr16reg_apply_kernelILi9E' (the Itanium-mangled prefix rocprof prints)."""
+    ns, _, rest = kernel.partition('::')
+    name, _, targ = rest.partition('<')
+    k = targ.split(',')[0].strip(' >')
+    return f'{len(ns)}{ns}{len(name)}{name}ILi{k}E'
+
+
+def sq_counters(kernel, config='C3'):
+    """Per-dispatch SQ counters of `kernel` from the committed SQ passes (both files merged), or None."""
+    stem, got = mangled_stem(kernel), {}
+    for pss in (1, 2):
+        path = os.path.join(PROFILES, f'{SQ_ROUND}_sq_counters_{config}_pass{pss}.txt')
+        try:
+            lines = open(path).read().split('\n')
+        except OSError:
+            return None
+        cur = None
+        for ln in lines:
+            if ln and not ln.startswith(' '):
+                cur = ln.split(',')[0]
+            elif cur and stem in cur and 'per dispatch' in ln:
+                f = ln.split()
+                got[f[0]] = float(f[-1])
+    return got or None
+
+
+def issue_roofline(kernel, ops_per_launch, avg_launch_ms, config='C3'):
+    """The dominant kernel against the instruction-issue peaks: VALU / SALU / LDS instructions per op
+    from the committed SQ passes of the same kernel (per dispatch / (waves x ops per wave), each wave
+    applying ops_per_launch ops), times its ops/s in this run (ops per launch / the live launch time)."""
+    c = sq_counters(kernel, config)
+    if not c or not c.get('SQ_WAVES') or not avg_launch_ms:
+        return None
+    ops = c['SQ_WAVES'] * ops_per_launch
+    valu, salu = c.get('SQ_INSTS_VALU', 0) / ops, c.get('SQ_INSTS_SALU', 0) / ops
+    ops_s = ops / (avg_launch_ms * 1e-3)
+    return {'bound': 'issue', 'valu_per_op': round(valu, 1), 'salu_per_op': round(salu, 1),
+            'lds_per_op': round(c.get('SQ_INSTS_LDS', 0) / ops, 1),
+            'valu_frac': round(valu * ops_s / VALU_PEAK, 4), 'salu_frac': round(salu * ops_s / SALU_PEAK, 4),
+            'wait_frac': round(c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES'], 4)
+            if c.get('SQ_WAIT_ANY') and c.get('SQ_WAVE_CYCLES') else None,
+            'peaks': {'valu_instr_per_s': VALU_PEAK, 'salu_instr_per_s': SALU_PEAK},
+            'source': f'profiles/{SQ_ROUND}_sq_counters_{config}_pass{{1,2}}.txt (per dispatch / SQ_WAVES x '
+                      f'{ops_per_launch} ops); ops/s = ops per launch / avg_launch_ms of this run'}
 
 
 def parse():
@@ -366,6 +418,7 @@ def main():
                 'avg_launch_ms': round(avg_launch_ms, 4), 'alg_bytes_per_launch': int(bytes_per_launch),
                 'class_ms_serialized': {class_label(c): round(v[0], 2) for c, v in sorted(rcls.items()) if v[1]},
                 'classes': class_table(rcls, args.config, kname_of),
+                'issue': issue_roofline(kname, args.ops_per_launch, avg_launch_ms, args.config),
                 'b_infinity': {'bytes_per_step_rank0': int(min_bytes),
                                'frac': round(min_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
                                'note': 'SURVEY.md 8(d): state read + written once per step, every op once; '

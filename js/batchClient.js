@@ -14,7 +14,14 @@
 // throw.
 // Delta / maintenance callbacks (mergeTreeDeltaCallback.ts:15-73): setting a client's
 // mergeTreeDeltaCallback or mergeTreeMaintenanceCallback makes the engine record them
-// (mt_events_enable); they are delivered, in firing order, after the batch that fired them.
+// (mt_events_enable); they are delivered, in firing order, after the batch that fired them --
+// or, with `new BatchEngine({ syncCallbacks: true })`, before applyMsg / the local edit that fired them
+// returns: a client with callbacks then flushes per message (per member of a GROUP op, b = 1 for its
+// document), so a listener reading getText() / getLength() / getPosition(deltaSegment.segment) inside
+// its callback sees what the reference's listener sees (mergeTree.ts:1981-1988: the op applied; the
+// text and lengths are those zamboni leaves unchanged; a delta segment's position is the one at
+// callback time).  Maintenance callbacks (SPLIT / APPEND / UNLINK) are delivered the same way, after
+// the message (a SPLIT's listener reads the text with the op applied).
 // Segments are identified by position: deltaSegments[i].segment = {ordinal, position,
 // cachedLength} (ordinal among the linked leaves at callback time; position in the local view,
 // op callbacks only) -- include/mtgpu.h "delta / maintenance events".
@@ -55,6 +62,8 @@ class BatchEngine {
         this.eventsPerDoc = opts.eventsPerDoc || (1 << 16);
         this.labelDecl = [];  // [doc, tile key, range key] to declare before the next submit
         this.gen = 0;         // bumped by every submit: segment descriptors are valid within one generation
+        this.syncCallbacks = !!opts.syncCallbacks;  // deliver callbacks before the firing call returns
+        this.delivering = false;
     }
 
     _enableEvents() {
@@ -69,9 +78,20 @@ class BatchEngine {
         if (!this.recording) return;
         const [rows, rpBuf] = native.eventsDrain(this.handle, this.maxDocs);
         const rp = new Uint32Array(rpBuf.buffer, rpBuf.byteOffset, this.maxDocs + 1);
-        for (let d = 0; d < this.clients.length; d++) {
-            if (rp[d + 1] > rp[d]) this.clients[d]._deliver(rows, rp[d], rp[d + 1]);
+        this.delivering = true;
+        try {
+            for (let d = 0; d < this.clients.length; d++) {
+                if (rp[d + 1] > rp[d]) this.clients[d]._deliver(rows, rp[d], rp[d + 1]);
+            }
+        } finally {
+            this.delivering = false;
         }
+        // (ops a listener queued while the callbacks ran: applied now, their callbacks delivered in turn)
+        if (this.syncCallbacks && this.pending) this.flush();
+    }
+    /** syncCallbacks: a client with callbacks applies what it queued before the firing call returns. */
+    _syncPoint(client) {
+        if (this.syncCallbacks && this.recording && !this.delivering && (client._delta || client._maintenance)) this.flush();
     }
 
     createClient() {
@@ -154,6 +174,7 @@ class BatchClient {
         this._delta = undefined;
         this._maintenance = undefined;
         this.expect = [];               // opArgs of the ops whose delta callback is still to come
+        this.cbSegs = new WeakSet();    // the delta segments of the callbacks being delivered
     }
 
     get mergeTreeDeltaCallback() { return this._delta; }
@@ -169,7 +190,10 @@ class BatchClient {
             if (flags & 1) cbs.push({ seq: rows.readInt32LE(o), operation: op, deltaSegments: [] });
             if (flags & 2) continue;  // a callback without delta segments
             const segment = { ordinal: rows.readInt32LE(o + 8), cachedLength: rows.readUInt32LE(o + 16) };
-            if (op >= 0) segment.position = rows.readInt32LE(o + 12);
+            if (op >= 0) {
+                segment.position = rows.readInt32LE(o + 12);
+                this.cbSegs.add(segment);  // getPosition answers with the position at callback time
+            }
             const delta = { segment };
             if (op === ANNOTATE && !(flags & 4)) {  // (MT_EVF_NOPD: propertyDeltas undefined)
                 const mask = rows.readUInt32LE(o + 20);
@@ -332,6 +356,7 @@ class BatchClient {
         this.queue.push(r);
         if (this.engine.recording) this.expect.push({ op });  // a local edit's callback: no sequencedMessage
         this.engine.pending += 1;
+        this.engine._syncPoint(this);
         return op;
     }
     /** TestClient.insertTextLocal (testClient.ts:133-143) -> insertSegmentLocal: the insert op. */
@@ -415,8 +440,13 @@ class BatchClient {
             if (this.engine.recording && r.type !== NOOP && !ack) {
                 this.expect.push({ op: m, groupOp: op.type === GROUP ? op : undefined, sequencedMessage: msg });
             }
+            this.engine.pending += 1;
+            // (syncCallbacks: each member applied and its callback delivered in turn, as the reference
+            // fires one callback per member inside the GROUP's apply)
+            this.engine._syncPoint(this);
         });
-        this.engine.pending += members.length;
+        // (after the members, as updateSeqNumbers follows the op: client.ts:818; a listener reading
+        // getCurrentSeq() inside the callback sees the previous one, as the reference's does)
         this.currentSeq = msg.sequenceNumber;
         this.minSeq = Math.max(this.minSeq, msg.minimumSequenceNumber);
     }
@@ -633,6 +663,9 @@ class BatchClient {
     }
     /** Client.getPosition (client.ts:290-292): the local-view position of the segment (by ordinal). */
     getPosition(segment) {
+        // a delta segment of the callback being delivered: its position at callback time (the reference's
+        // getPosition inside the listener; the ordinal may have moved since, e.g. by zamboni)
+        if (this.cbSegs.has(segment)) return segment.position;
         const r = this._resolve(POS_OF_ORDINAL, segment.ordinal);
         return r.ordinal >= 0 ? r.position : 0;
     }

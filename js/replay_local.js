@@ -31,8 +31,13 @@ const withEvents = process.argv[3] === "events";
 const withSeqDelta = process.argv[3] === "seqdelta";
 // "read": the read surface over each document's final state, in replay_ref.js's read form
 const withRead = process.argv[3] === "read";
+// "seqreads": what a listener reads inside each delta callback (getText, getLength, getPosition of the
+// delta segments), callbacks delivered synchronously (BatchEngine syncCallbacks), in replay_ref.js's
+// seqreads form; argv[4]: the first documents only
+const withReads = process.argv[3] === "seqreads";
+const nReads = withReads && process.argv[4] ? parseInt(process.argv[4], 10) : Infinity;
 const { SequenceEvents } = require("./sequenceDeltaEvent.js");
-const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16 });
+const eng = new BatchEngine({ maxDocs: log.nDocs, opsPerLaunch: 16, syncCallbacks: withReads });
 const sortKeys = (pd) => {
     const o = {};
     for (const k of Object.keys(pd).sort((a, b) => parseInt(a.slice(1), 10) - parseInt(b.slice(1), 10))) o[k] = pd[k];
@@ -54,6 +59,11 @@ for (let d = 0; d < log.nDocs; d++) {
             args.deltaSegments.map((x) => seg(x, args.operation === 2 && x.propertyDeltas ? sortKeys(x.propertyDeltas) : null))]);
         c.mergeTreeMaintenanceCallback = (args) => c.events.push([args.sequenceNumber, args.operation,
             args.deltaSegments.map((x) => seg(x, null))]);
+    }
+    if (withReads && d < nReads) {
+        c.mergeTreeDeltaCallback = (opArgs, args) => c.events.push([
+            opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, c.getText(), c.getLength(),
+            args.deltaSegments.map((x) => c.getPosition(x.segment))]);
     }
     if (withSeqDelta) {
         const seqEvents = new SequenceEvents(c);
@@ -143,6 +153,7 @@ const out = clients.map((c, d) => {
     try { state = c.getState(); } catch (e) { err = String(e.message || e); }
     const line = c.regen.length ? { doc: d, err, state, regen: c.regen } : { doc: d, err, state };
     if (withEvents || withSeqDelta) line.events = c.events;
+    if (withReads) return JSON.stringify({ doc: d, err, reads: c.events });
     return JSON.stringify(line);
 });
 process.stdout.write(out.join("\n") + "\n");

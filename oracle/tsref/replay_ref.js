@@ -494,6 +494,53 @@ function main() {
         process.stdout.write(out.join("\n") + "\n");
         return;
     }
+    if (mode === "seqreads") {
+        // what a listener reads INSIDE each delta callback of the document's client (an editing client
+        // for a local_* log, else the observer): SharedString.getText() (the client's view at its
+        // collab window: textHelper.getText(currentSeq, clientId), sequence.ts), getLength(), and
+        // getPosition(segment) of every delta segment -- one record per callback [seq (-1: local
+        // edit), text, length, [position, ...]]
+        const out = [];
+        const d1 = Math.min(log.nDocs, process.argv[4] ? parseInt(process.argv[4], 10) : log.nDocs);
+        for (let d = 0; d < d1; d++) {
+            const items = [...messages(log, d)];
+            const own = items.find((x) => x.local);
+            const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+            const c = new Client(specToSegment, logger);
+            c.startOrUpdateCollaboration(own ? "c" + own.client : "observer");
+            const helper = c.createTextHelper();
+            const seqRef = { seq: 0 };
+            const reads = [];
+            c.mergeTreeDeltaCallback = (opArgs, deltaArgs) => {
+                const w = c.getCollabWindow();
+                reads.push([seqRef.seq, helper.getText(w.currentSeq, w.clientId), c.getLength(),
+                    deltaArgs.deltaSegments.map((s) => c.getPosition(s.segment))]);
+            };
+            let err = null;
+            try {
+                for (const it of items) {
+                    if (it.regen) {
+                        seqRef.seq = -2;
+                        c.regeneratePendingOp(it.op, c.mergeTree.pendingSegments.first());
+                    } else if (it.local) {
+                        seqRef.seq = -1;
+                        const op = it.op;
+                        if (op.type === 0) c.insertSegmentLocal(op.pos1, specToSegment(op.seg));
+                        else if (op.type === 1) c.removeRangeLocal(op.pos1, op.pos2);
+                        else c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp);
+                    } else {
+                        seqRef.seq = it.sequenceNumber;
+                        c.applyMsg(it);
+                    }
+                }
+            } catch (e) {
+                err = String(e.message || e);
+            }
+            out.push(JSON.stringify({ doc: d, err, reads }));
+        }
+        process.stdout.write(out.join("\n") + "\n");
+        return;
+    }
     if (mode === "read") {
         // the client's read surface over its final state (client.ts:275-311, 838-847, 1004-1040):
         // getContainingSegment / getPropertiesAtPosition / getRangeExtentsOfPosition at a spread of

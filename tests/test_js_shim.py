@@ -375,6 +375,52 @@ def test_batchclient_sequence_delta_events_match_reference(name):
                 g['sha256'], (name, g['doc'])
 
 
+SEQREADS_LOGS = {'seqdelta': None, 'local_lag': 6, 'local_rounds': 6, 'local_markers': 4, 'scenarios': 12}
+
+
+def _seqreads_gold():
+    with open(os.path.join(GOLDEN, 'seqreads.expected.jsonl')) as f:
+        return [json.loads(x) for x in f if x.strip()]
+
+
+def test_seqreads_fixture_covers_the_spec():
+    """seqreads.expected.jsonl (tests/golden/make_seqreads.py, the transpiled reference): every document of
+    seqdelta.mtlog (sequenceDeltaEvent.spec.ts re-expressed) in full, with local and remote callbacks, and
+    reads that change between callbacks."""
+    gold = _seqreads_gold()
+    assert {g['log'] for g in gold} == set(SEQREADS_LOGS)
+    spec = [g for g in gold if g['log'] == 'seqdelta']
+    assert len(spec) == 59 and all(g['err'] is None and g['n'] == len(g['reads']) for g in spec)
+    seqs = {r[0] for g in spec for r in g['reads']}
+    assert -1 in seqs and any(x > 0 for x in seqs)
+    assert any(len({r[1] for r in g['reads']}) > 2 for g in spec)
+    assert any(len(r[3]) > 1 for g in spec for r in g['reads'])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', sorted(SEQREADS_LOGS))
+def test_batchclient_sync_callbacks_read_reference_state(name):
+    """BatchEngine({syncCallbacks: true}): a listener reading getText() / getLength() / getPosition(segment)
+    of its delta segments INSIDE the callback reads what the reference's listener reads inside the
+    reference's callback (tests/golden/seqreads.expected.jsonl)."""
+    import hashlib
+    assert _addon()
+    n = SEQREADS_LOGS[name]
+    out = subprocess.run([NODE, os.path.join(REPO, 'js', 'replay_local.js'), os.path.join(GOLDEN, name + '.mtlog'),
+                          'seqreads'] + ([str(n)] if n else []), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {r['doc']: r for r in (json.loads(x) for x in out.stdout.strip().split('\n'))}
+    gold = [g for g in _seqreads_gold() if g['log'] == name]
+    assert gold
+    for g in gold:
+        reads = got[g['doc']]['reads']
+        if 'reads' in g:
+            assert reads == g['reads'], (name, g['doc'])
+        else:
+            assert len(reads) == g['n'] and hashlib.sha256(json.dumps(reads, separators=(',', ':')).encode()).hexdigest() \
+                == g['sha256'], (name, g['doc'])
+
+
 READ_LOGS = ['scenarios', 'markers', 'synth_markers', 'wide', 'synth_c1', 'local_lag', 'local_markers',
              'local_reconnect']
 

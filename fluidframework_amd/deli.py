@@ -22,7 +22,8 @@ DELI_ERRORS = {0: None, 1: 'client id out of range', 2: 'unknown message kind',
                3: 'assert(referenceSequenceNumber >= minimumSequenceNumber) (lambda.ts:426-428)',
                4: 'capacity: no big-pool row left for a document past client 63'}
 ERR_CAPACITY = 4  # mt_deli_err MT_DELI_ERR_CAPACITY
-MAX_CLIENTS = 512  # include/mtgpu.h MT_DELI_MAX_CLIENTS (up to 63: eight documents per wave; then the wide form)
+MAX_CLIENTS = 4096  # include/mtgpu.h MT_DELI_MAX_CLIENTS (up to 63: eight documents per wave; to 511 the wide
+# form; then the huge form)
 CKPT_CLIENTS = 64  # mt_deli_checkpoint's client slots
 
 RAW_DTYPE = np.dtype([('csn', '<i4'), ('ref_seq', '<i4'), ('client', '<u2'), ('kind', 'u1'), ('pad', 'u1'),

@@ -626,11 +626,14 @@ typedef struct mt_ticket {  /* 16 bytes */
 
 /* Client ids: a document holds short ids 0..MT_DELI_MAX_CLIENTS-1.  Up to id 63 it is ticketed eight
  * documents per wave; its first message from a client >= 64 promotes it, for good, to the wide form
- * (one document per wave, its clients in a row of the deli's big pool: one row per 16 documents of
- * max_docs, at least 64).  mt_deli_restore / mt_deli_restore_wide give a restored document's row back
- * to the pool (a free list the next promotion takes first), mt_deli_restore_all empties the pool.  The
- * reference keeps a Map and a heap (clientSeqManager.ts:70-143, joins at lambda.ts:280-306): no limit. */
-#define MT_DELI_MAX_CLIENTS 512
+ * (one document per wave, its clients in a row of the deli's big pool, MT_DELI_BIG_CLIENTS per row:
+ * one row per 16 documents of max_docs, at least 64), and its first from a client >= 512 to the huge
+ * form (a row of MT_DELI_MAX_CLIENTS clients in the huge pool: one row per 256 documents, at least 8).
+ * mt_deli_restore / mt_deli_restore_wide give a restored document's rows back to the pools (free lists
+ * the next promotion takes first), mt_deli_restore_all empties them.  The reference keeps a Map and a
+ * heap (clientSeqManager.ts:70-143, joins at lambda.ts:280-306): no limit. */
+#define MT_DELI_BIG_CLIENTS 512
+#define MT_DELI_MAX_CLIENTS 4096
 
 /* per-document sticky deli errors (the reference lambda throws / has no representation) */
 typedef enum mt_deli_err {

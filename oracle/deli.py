@@ -26,7 +26,7 @@ OP, NOOP, NOOP_DATA, JOIN, LEAVE, SERVER_NOOP, NOCLIENT, CONTROL = range(8)
 DROPPED, SENT, LATER, NEVER, NACK_GAP, NACK_CLIENT, NACK_REFSEQ, HALTED = range(8)
 # mt_deli_err
 ERR_CLIENT, ERR_KIND, ERR_ASSERT = 1, 2, 3
-MAX_CLIENTS = 512  # include/mtgpu.h MT_DELI_MAX_CLIENTS (the engine's limit; the lambda has none)
+MAX_CLIENTS = 4096  # include/mtgpu.h MT_DELI_MAX_CLIENTS (the engine's limit; the lambda has none)
 
 
 class Client:

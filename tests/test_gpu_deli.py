@@ -72,17 +72,18 @@ def test_batches_continue_the_state():
         assert np.array_equal(got, want[rp[d]:rp[d + 1]]), d
 
 
-@pytest.mark.parametrize('seed,n_clients,n_msgs', [(11, 96, 1500), (12, 300, 2500)])
+@pytest.mark.parametrize('seed,n_clients,n_msgs', [(11, 96, 1500), (12, 300, 2500), (13, 700, 3000), (14, 2500, 4000)])
 def test_documents_past_64_clients_against_oracle(seed, n_clients, n_msgs):
-    """Documents whose joined clients pass 63 (96, 300 client ids): their first message from a client
-    >= 64 promotes them to the wide form (one document per wave, 512 clients), mid-stream; tickets and
-    checkpoints (every client) equal the restatement's, in one launch and in two (the promotion and
-    the big-pool state carry across calls)."""
+    """Documents whose joined clients pass 63 (96, 300 client ids) or 511 (700, 2500): their first message
+    from a client >= 64 promotes them to the wide form (one document per wave, 512 clients), and from a
+    client >= 512 on to the huge form (4096), mid-stream; tickets and checkpoints (every client) equal the
+    restatement's, in one launch and in two (the promotions and the pools' state carry across calls)."""
     streams = random_streams(48, n_msgs, seed=seed, n_clients=n_clients)
     streams[1] = []
     want, docs = oracle_tickets(streams)
-    assert max(c for s in streams for (_, c, _, _) in s) >= 64
-    dl = _seq(len(streams))
+    assert max(c for s in streams for (_, c, _, _) in s) >= (512 if n_clients > 512 else 64)
+    # (a deli sized for 16K documents: its huge pool holds 64 of them, more than these streams promote)
+    dl = _seq(16384)
     got = _tickets(dl.ticket(*to_batch(streams)))
     bad = np.nonzero(np.any(got != want, axis=1))[0]
     assert not len(bad), f'{len(bad)} tickets differ, first {int(bad[0])}: got {got[bad[0]]} want {want[bad[0]]}'
@@ -92,7 +93,7 @@ def test_documents_past_64_clients_against_oracle(seed, n_clients, n_msgs):
                                                                          o['err']), d
         assert ck['clients'] == o['clients'], d
     # the same streams in two launches
-    dl2 = _seq(len(streams))
+    dl2 = _seq(16384)
     a = [s[:len(s) // 3] for s in streams]
     b = [s[len(s) // 3:] for s in streams]
     ta, tb = _tickets(dl2.ticket(*to_batch(a))), _tickets(dl2.ticket(*to_batch(b)))
@@ -129,6 +130,28 @@ def test_big_pool_exhausted_halts_the_document():
             assert np.array_equal(g, w), d
 
 
+def test_huge_pool_exhausted_halts_the_document():
+    """The huge pool holds max(8, max_docs / 256) documents past client 511: of 12 documents that join
+    client 600, the 4 promoted last halt at that join (MT_DELI_ERR_CAPACITY); the rest, promoted through
+    the big pool to the huge one, are ticketed as the restatement does."""
+    streams = [[(od.JOIN, c, -1, -1) for c in (5, 70, 600)] + [(od.OP, 600, 1, 3), (od.OP, 70, 1, 4)]
+               for _ in range(12)]
+    want, docs = oracle_tickets(streams)
+    dl = _seq(len(streams))
+    got = _tickets(dl.ticket(*to_batch(streams)))
+    _, rp = to_batch(streams)
+    halted = [d for d in range(12) if dl.error(d)[0]]
+    assert len(halted) == 4, halted
+    for d in range(12):
+        g, w = got[rp[d]:rp[d + 1]], want[rp[d]:rp[d + 1]]
+        if d in halted:
+            assert dl.error(d) == (ERR_CAPACITY, 2)  # the join of client 600
+            assert np.array_equal(g[:2], w[:2]) and np.all(g[2:, 3] == od.HALTED), d
+        else:
+            assert np.array_equal(g, w), d
+            assert dl.checkpoint(d)['clients'] == docs[d].checkpoint()['clients'], d
+
+
 def test_big_pool_rows_come_back_on_restore():
     """Restoring a promoted document gives its big-pool row back (a free list the next promotion takes
     first): 64 documents fill the pool, 16 of them are restored, and 16 new documents then promote
@@ -156,7 +179,7 @@ def test_big_pool_rows_come_back_on_restore():
     assert dl.error(100) == (ERR_CAPACITY, 4)
 
 
-@pytest.mark.parametrize('seed,n_clients', [(31, 96), (32, 300)])
+@pytest.mark.parametrize('seed,n_clients', [(31, 96), (32, 300), (33, 700)])
 def test_wide_checkpoint_round_trip(seed, n_clients):
     """generateDeliCheckpoint / restore of documents past client 63: the narrow checkpoint call refuses
     them (MT_ERR_WIDE, nothing dropped), the wide one carries every client, and a deli restored from it
@@ -165,7 +188,7 @@ def test_wide_checkpoint_round_trip(seed, n_clients):
     streams = random_streams(24, 1200, seed=seed, n_clients=n_clients)
     half = [s[:len(s) // 2] for s in streams]
     rest = [s[len(s) // 2:] for s in streams]
-    dl = _seq(len(streams))
+    dl = _seq(8192)
     dl.ticket(*to_batch(half))
     _, docs = oracle_tickets(half)
     cks = []
@@ -180,7 +203,7 @@ def test_wide_checkpoint_round_trip(seed, n_clients):
         cks.append({'seq': ck['seq'], 'clients': ck['clients'], 'last_sent_msn': ck['last_sent_msn']})
     assert any(max(c['clients'], default=0) >= 64 for c in cks)
     want, _ = oracle_tickets(rest, checkpoints=cks)
-    dl2 = _seq(len(streams))
+    dl2 = _seq(8192)
     dl2.restore(cks)
     for d in range(len(streams)):
         got_ck = dl2.checkpoint(d)

@@ -904,7 +904,9 @@ struct RWave {
     // the following children whose bits are set in runm.  Only the text content is state, so
     // the run is made contiguous once (or found contiguous) instead of pair by pair.  Lane q of
     // (vli, vcf, vslot) holds the block's live child of rank q.
-    MT_DEV void append_run(int p, uint32_t runm, uint32_t vli, uint32_t vcf, int vslot) {
+    // The head's new li / cf are returned (hli, hcf), not written to the register state here: scour
+    // writes every head back after its run loop, so the loop carries no register state.
+    MT_DEV void append_run(int p, uint32_t runm, uint32_t vli, uint32_t vcf, uint32_t& hli, uint32_t& hcf) {
         const uint32_t pli = (uint32_t)__builtin_amdgcn_readlane((int)vli, p);
         const uint32_t pid_ = id_of(pli);
         const uint32_t lastq = 31u - (uint32_t)__builtin_clz(runm);
@@ -942,7 +944,8 @@ struct RWave {
         const uint32_t pcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, p);
         const uint32_t lcf = (uint32_t)__builtin_amdgcn_readlane((int)vcf, (int)lastq);
         const uint32_t anynl = __ballot(in_run && (vcf & F_HASNL)) ? F_HASNL : 0u;
-        set_li_cf(__builtin_amdgcn_readlane(vslot, p), total | (pid_ << kLenBits), (pcf & ~F_NL) | (lcf & F_NL) | anynl);
+        hli = total | (pid_ << kLenBits);
+        hcf = (pcf & ~F_NL) | (lcf & F_NL) | anynl;
     }
 
     // scourNode on the leaf block whose slots are [a, e) (mergeTree.ts:1289-1365); returns the
@@ -970,11 +973,17 @@ struct RWave {
         }
         wave_sync();
         const bool mine = lane < cnt;
-        const int32_t vsq = mine ? (int32_t)s.zr[lane] : 0;
-        const uint32_t vli = mine ? s.zr[kMaxNodes + lane] : 0u;
-        uint32_t vcf = mine ? s.zr[2 * kMaxNodes + lane] : 0u;
-        const int vslot = mine ? (int)s.zr[3 * kMaxNodes + lane] : 0;
-        const uint64_t vpr = mine ? s.props[id_of(vli)] : 0ull;
+        // (every lane reads -- lane q < 8 its child's words, the others words of the scratch area
+        // behind them -- and the values are selected after: no exec-masked branch per read)
+        const int zq = lane & (kMaxNodes - 1);
+        const uint32_t r0 = s.zr[zq], r1 = s.zr[kMaxNodes + zq], r2 = s.zr[2 * kMaxNodes + zq],
+                       r3 = s.zr[3 * kMaxNodes + zq];
+        const int32_t vsq = mine ? (int32_t)r0 : 0;
+        const uint32_t vli = mine ? r1 : 0u;
+        uint32_t vcf = mine ? r2 : 0u;
+        const int vslot = mine ? (int)r3 : 0;
+        const uint64_t pr = s.props[mine ? id_of(vli) : 0u];
+        const uint64_t vpr = mine ? pr : 0ull;
         if (__ballot(mine && (vcf & F_NLQ))) {  // the children's pending ENDS_WITH_NEWLINE, in one load
             arena_sync();
             if (mine && (vcf & F_NLQ)) {
@@ -1050,13 +1059,32 @@ struct RWave {
         }
         PROF_CNT(P_N_UNLINK, __popc(unlink));
         uint64_t runs = __ballot(vtgt >= 0);
-        while (runs) {
-            const int p = __builtin_amdgcn_readlane(vtgt, first_lane(runs));
-            const uint64_t runm = __ballot(vtgt == p);
-            runs &= ~runm;
-            PROF_CNT(P_N_APPEND, __popcll(runm));
-            append_run(p, (uint32_t)runm, vli, vcf, vslot);
-            if (err) return cnt;
+        if (runs) {
+            // the runs' text work; each head's new li / cf parked in its child lane (nli / ncf) ...
+            uint32_t nli = vli, ncf = vcf, heads = 0;
+            while (runs) {
+                const int p = __builtin_amdgcn_readlane(vtgt, first_lane(runs));
+                const uint64_t runm = __ballot(vtgt == p);
+                runs &= ~runm;
+                PROF_CNT(P_N_APPEND, __popcll(runm));
+                uint32_t hli = 0, hcf = 0;
+                append_run(p, (uint32_t)runm, vli, vcf, hli, hcf);
+                if (err) return cnt;
+                nli = lane == p ? hli : nli;
+                ncf = lane == p ? hcf : ncf;
+                heads |= 1u << p;
+            }
+            // ... and written back in one pass: register j of a lane holds the block's child of rank
+            // q (its prefix count), which reads its new values from lane q (no state in the loop above)
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                const int q = rbase + __popc(lb & ((1u << j) - 1u));
+                const bool hit = ((lb >> j) & 1u) && q < 32 && ((heads >> q) & 1u);
+                const uint32_t xl = (uint32_t)__builtin_amdgcn_ds_bpermute(q << 2, (int)nli);
+                const uint32_t xc = (uint32_t)__builtin_amdgcn_ds_bpermute(q << 2, (int)ncf);
+                li[j] = hit ? xl : li[j];
+                cf[j] = hit ? xc : cf[j];
+            }
         }
         // unlink: the slots become dead in place (their block marks stay)
         const bool gone = mine && ((unlink >> lane) & 1u);
@@ -1221,21 +1249,19 @@ struct RWave {
             be = next_start(kl);
         } else {
         // insertingWalk descends into the first block whose cumulative visible end >= pos
-        // (breakTie is true for blocks, :2248-2277): that leaf block's last slot is the first
-        // block-ending slot with cum >= pos
+        // (breakTie is true for blocks, :2248-2277).  cum is monotone over the slots, so that is the
+        // block holding the first slot with cum >= pos: every block before it ends at a slot before
+        // that one, at a cumulative end < pos
         // (bitwise, not short-circuit, here and below: no exec-masked branch per register)
-        const uint32_t bm = bs_bits();
-        const int nxt = shl1((int)(bm & 1u), 0);
-        int last = 0x7fffffff;
+        int first = 0x7fffffff;
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
             const int i = idx(j);
-            const bool ends = (j + 1 < K ? ((bm >> (j + 1)) & 1u) != 0 : nxt != 0) | (i == ns - 1);
-            last = ((i < ns) & ends & (cum[j] >= pos)) ? i : last;
+            first = ((i < ns) & (cum[j] >= pos)) ? i : first;
         }
-        last = first_hit(last);  // slots are blocked by lane: the first lane with a hit has the minimum
-        if (last == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
-        const int a = block_start(last), e = last + 1;
+        first = first_hit(first);  // slots are blocked by lane: the first lane with a hit has the minimum
+        if (first == 0x7fffffff) return fail(MT_DERR_INSERT_FAILED, S), -1;
+        const int a = block_start(first), e = next_start(first);
         ba = a;
         be = e;
         // leaf placement: first child with pos < len, or pos == len == 0 and breakTie; else the
@@ -1388,7 +1414,7 @@ struct RWave {
     MT_DEV void apply(const mt_op_rec op, const uint8_t* payload) {
         const int np = MT_OP_NPAIRS(op);
         const int32_t S = op.seq;
-        if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);
+        if (op.type > MT_OP_NOOP) return fail(MT_DERR_BAD_OP, S);  // (err: the op loop stops)
         const uint8_t* pay = payload + op.payload_off;
         const int tlen = (int)op.payload_len - 2 * np;
         const bool noop = MT_OP_IS_NOOP(op);  // incl. an empty-string insert (client.ts:403-407)
@@ -1968,8 +1994,11 @@ MT_DEV KGState& kernarg_gstate() {
 // at 3 waves is spill-free (158 VGPRs; 176 B of scratch at 4) and faster (C3's 448 class 50.6 -> 43.9 ms,
 // its traffic 13.3x -> 1.19x its algorithmic bytes); K = 2 at 6 and K = 3 at 5 waves keep 24 / 28 B of
 // scratch instead of 60 / 104 B (C5 traffic 3.9x -> 2.6x and 12.0x -> 2.0x) for 1 % of C5's rate.
+// Round 6 (after the one-pass shift cut the register peaks: K = 7 at four waves 64 B of scratch, K = 2
+// at seven 24 B, K = 3 at six 40 B): K = 7 at four +0.8 % on C3, K = 2 / 3 at seven / six +2.8 % on C5;
+// K = 8 / 9 at four (124 / 144 B) -3.2 % on C3 (profiles/r06_ab/ab4_*)
 constexpr int wpe_default(int K) {
-    return K <= 2 ? 6 : K == 3 ? 5 : K <= 4 ? 5 : K <= 6 ? 4 : K <= 10 ? 3 : 2;
+    return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2;
 }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV
@@ -1997,7 +2026,10 @@ MT_DEV void reg_apply(uint8_t* text, uint32_t textcap, const mt_op_rec* __restri
     // software pipeline: op i's payload was loaded at the end of op i-1's apply and op i+1's is
     // issued at the end of op i's, so every wait for a prefetch finds it a whole op old (a prefetch
     // issued at the top of the loop was waited for at once: the copy into the current-op register,
-    // and any arena read of the op, drain vmcnt to 0)
+    // and any arena read of the op, drain vmcnt to 0).  (Round 6 tried both an explicit vmcnt(0) at
+    // the end of each op and requesting op i+1's payload in the middle of op i, where its last
+    // reader is done: neutral, and 0.90x -- the mid-op request raised K = 9's scratch from 24 to
+    // 212 B; profiles/r06_ab/ab4_*.)
     uint32_t blk0 = load_op_block(ops, a, b, wv.lane);
     uint32_t blk1 = load_op_block(ops, a + 8, b, wv.lane);
     uint32_t pb = load_payload(payload, (uint32_t)__builtin_amdgcn_readlane((int)blk0, 6),

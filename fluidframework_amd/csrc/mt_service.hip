@@ -378,6 +378,11 @@ __global__ void mt_bin_kernel(mt_gstate g, const uint32_t* __restrict__ row_ptr,
                 // accounting"): persistent state in + out, op records, payload
                 unsigned long long st = (unsigned long long)MT_SEG_STATE_BYTES * sc.nseg + 2ull * sc.nb[0] +
                                         6ull * sc.heap_n + sizeof(mt_doc_scalars);
+                // an editing document's per-segment rows (group mask words, pending property counts,
+                // creation stamp, localSeq pair: mt_gstate gm / pk / ct / lsq), which its form reads and
+                // writes by slot during the launch: counted as state in + out like the rest
+                if (editing)
+                    st += (unsigned long long)(20u + 8u * ((sc.wide & MT_WIDE_GROUPS) ? MT_LOC_GW : 1u)) * sc.nseg;
                 for (int L = 1; L < sc.nlev; L++) st += (unsigned long long)sc.nb[L];
                 if (!ops) ob = 32ull * (b - a);  // (with records: summed in the pass above)
                 bytes = 2ull * st + ob;

@@ -1450,7 +1450,11 @@ struct RWave {
             // (one exit: every failing step has set err -- a return or continue from inside the loop
             // is a multi-exit region that the CFG structurizer lowers with a flow variable and
             // copies of the register state on its edges)
-            for (int step = 0; step < nsteps; step++) {
+            // nsteps <= 2: unrolled, the two steps keep their own register assignment instead of
+            // joining the whole state at a loop back edge (C3 +4.0%, C4 +3.8%, C5 +5.7%:
+            // profiles/r06_ab/ab6_step_unroll_*)
+#pragma unroll
+            for (int step = 0; step < 2 && step < nsteps; step++) {
                 PROF_BEGIN2(t1, P_BOUND, P_INSERT);
                 const bool placing = ins && step == 1;
                 Elem e{};
@@ -1996,9 +2000,11 @@ MT_DEV KGState& kernarg_gstate() {
 // scratch instead of 60 / 104 B (C5 traffic 3.9x -> 2.6x and 12.0x -> 2.0x) for 1 % of C5's rate.
 // Round 6 (after the one-pass shift cut the register peaks: K = 7 at four waves 64 B of scratch, K = 2
 // at seven 24 B, K = 3 at six 40 B): K = 7 at four +0.8 % on C3, K = 2 / 3 at seven / six +2.8 % on C5;
-// K = 8 / 9 at four (124 / 144 B) -3.2 % on C3 (profiles/r06_ab/ab4_*)
+// K = 8 / 9 at four (124 / 144 B) -3.2 % on C3 (profiles/r06_ab/ab4_*).  With the step loop unrolled:
+// K = 11 at three (120 B) +2.9 % on C3 (its 704 class 54.2 -> 47.3 ms); K = 7 at three (spill-free)
+// -3.3 % on C4 (profiles/r06_ab/ab6_*); K = 12 at three would take 356 B
 constexpr int wpe_default(int K) {
-    return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 10 ? 3 : 2;
+    return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 11 ? 3 : 2;
 }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV

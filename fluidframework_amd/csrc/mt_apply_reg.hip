@@ -1171,6 +1171,7 @@ struct RWave {
     // sibling under its parent (pack's scourNode loop), then repack.
     MT_DEV void zamboni() {
         // (continues and returns folded into conditions: one exit per loop, see apply)
+#pragma unroll
         for (int it = 0; it < 2 && !err; it++) {
             if (heap_n == 0 || uni(s.hseq[1]) > min_seq) break;
             PROF_BEGIN(tz, P_ZPOP);
@@ -1517,7 +1518,8 @@ struct RWave {
         const int32_t msn = op.msn;
         // zamboni after the op, then updateSeqNumbers and zamboni again when the msn moved: one call
         // site, one exit (err)
-#pragma clang loop unroll(disable)
+        // (unrolled, as the zamboni passes and the steps: C3 +2.2 %, C5 +3.1 %, profiles/r06_ab/ab7_*)
+#pragma unroll
         for (int ph = 0; ph < 2 && !err; ph++) {
             bool run = !noop;
             if (ph == 1) {
@@ -2002,9 +2004,11 @@ MT_DEV KGState& kernarg_gstate() {
 // at seven 24 B, K = 3 at six 40 B): K = 7 at four +0.8 % on C3, K = 2 / 3 at seven / six +2.8 % on C5;
 // K = 8 / 9 at four (124 / 144 B) -3.2 % on C3 (profiles/r06_ab/ab4_*).  With the step loop unrolled:
 // K = 11 at three (120 B) +2.9 % on C3 (its 704 class 54.2 -> 47.3 ms); K = 7 at three (spill-free)
-// -3.3 % on C4 (profiles/r06_ab/ab6_*); K = 12 at three would take 356 B
+// -3.3 % on C4 (profiles/r06_ab/ab6_*); K = 12 at three would take 356 B.  With the zamboni passes
+// unrolled too: K = 8 at four (60 B) +0.6 % C3 (its 512 class 45.7 -> 44.0 ms), K = 12 at three (116 B)
+// -1.1 % (profiles/r06_ab/ab8_*)
 constexpr int wpe_default(int K) {
-    return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 7 ? 4 : K <= 11 ? 3 : 2;
+    return K <= 2 ? 7 : K == 3 ? 6 : K <= 4 ? 5 : K <= 8 ? 4 : K <= 11 ? 3 : 2;
 }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV

@@ -145,6 +145,10 @@ def parse():
     p.add_argument('--hbm-only', action='store_true',
                    help='tooling (A/Bs, profiles): skip the host-fed steps; value is then the HBM-resident figure')
     p.add_argument('--no-tickets', action='store_true', help='C5: the host-fed steps do not copy the tickets back')
+    p.add_argument('--first-tick', type=int, default=0,
+                   help='a ramp of short first ticks in the host-fed feed (mt_log_to_ticks_ramp: tick t holds '
+                        'min(b, N << t) ops per document; 0: none -- the ramp measured slower on C3 and C5, '
+                        'profiles/r06_ab/ab9_*)')
     p.add_argument('--no-slow-paths', action='store_true',
                    help='skip the N=1 side lines for the paths off the narrow register engine (C3 with delta '
                         'events recorded, C3 with 48 clients, the editing-client farm at 100K documents)')
@@ -242,14 +246,16 @@ def main():
     # b ops of every document per tick, what a serving node receives -- and mt_submit_ticks copies
     # tick k + 1 on a copy stream while tick k applies.  Laying the log out is log generation (not
     # timed); the upload, deli and the apply are.
+    # (--first-tick: a ramp of short first ticks, so the apply starts after a short copy)
+    first_tick = max(1, min(args.first_tick, args.ops_per_launch)) if args.first_tick > 0 else None
     t0 = time.time()
     host = dev.to_host() if not args.hbm_only else None
     if args.hbm_only:
         log = None
     elif deli is None:
-        log = TickLog.from_batch(host, args.ops_per_launch)
+        log = TickLog.from_batch(host, args.ops_per_launch, first=first_tick)
     else:
-        log = TickLog.from_batch(host, args.ops_per_launch, msgs=d_msgs.download(RAW_DTYPE, n_msgs),
+        log = TickLog.from_batch(host, args.ops_per_launch, first=first_tick, msgs=d_msgs.download(RAW_DTYPE, n_msgs),
                                  msg_row_ptr=d_mrow.download(np.uint32, n_docs + 1), tickets=not args.no_tickets)
     del host
     layout_s = time.time() - t0
@@ -342,7 +348,8 @@ def main():
         assert np.all(t['status'] == 1), 'deli nacked or dropped a message of the synthetic stream'
         assert tk_ok is not False, 'a ticket of the host-fed steps is not SENT'
     upload = None if log is None else {
-              'bytes_per_step': log.upload_bytes(), 'ticks': log.n_ticks, 'layout_s': round(layout_s, 2),
+              'bytes_per_step': log.upload_bytes(), 'ticks': log.n_ticks, 'first_tick_ops_per_doc': first_tick or args.ops_per_launch,
+              'layout_s': round(layout_s, 2),
               'note': 'page-locked host memory, tick-major (mt_log_to_ticks), payload compacted per tick; '
                       'copied on a copy stream into a ring of 3 device slots while the previous tick applies'
                       + ('; tickets copied back per tick' if deli is not None and not args.no_tickets else '')}

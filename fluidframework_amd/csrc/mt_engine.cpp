@@ -176,6 +176,7 @@ struct mt_engine {
     // (fork/join around the tick) so the small classes and every class's tail overlap;
     // MTGPU_SERIAL=1 keeps them on the engine stream, one after another
     bool concurrent = true;
+    bool desc_order = true;  // class kernels launched largest capacity first (see apply_launches)
     hipStream_t side[kNumClasses] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kNumClasses] = {};
     uint64_t gen = 0;  // bumped by every call that can change document state (snap_cache's key)
@@ -196,7 +197,7 @@ struct mt_engine {
         mt_ticket* tk = nullptr;
         uint64_t ops_cap = 0, pay_cap = 0, msg_cap = 0;
         hipEvent_t ready = nullptr, applied = nullptr, drained = nullptr, ticketed = nullptr;
-    } ring[3];
+    } ring[6];
     hipStream_t h2d = nullptr, d2h = nullptr;
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
@@ -498,6 +499,8 @@ mt_status mt_engine_create(const mt_cfg* cfg, mt_engine** out) {
         e->reg_default = e->use_reg;
         const char* sv = getenv("MTGPU_SERIAL");
         e->concurrent = !(sv && strcmp(sv, "1") == 0);
+        const char* ov = getenv("MTGPU_CLASS_ORDER");  // (A/B: "asc" launches the classes smallest first)
+        e->desc_order = !(ov && strcmp(ov, "asc") == 0);
     }
     if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess) {
         mt_engine_destroy(e);
@@ -994,7 +997,11 @@ static mt_status apply_launches(mt_engine* e, const mt_batch* b, uint32_t& nk) {
         }
         if (e->concurrent) HIP_OK(hipEventRecord(e->fork_ev, e->stream));
         bool joined[kNumClasses] = {};
-        for (int c = 0; c < e->n_classes; c++) {  // (h_counts[n_classes]: the editing bucket, below)
+        // largest capacity first: a class's waves last longer the more segments its documents hold, and
+        // the few documents of the upper classes would otherwise start once the bulk classes' waves had
+        // all been dispatched -- the tick's tail.  Started first they run beside the bulk.
+        for (int i = 0; i < e->n_classes; i++) {  // (h_counts[n_classes]: the editing bucket, below)
+            const int c = e->desc_order ? e->n_classes - 1 - i : i;
             const uint32_t cnt = e->h_counts[c];
             if (!cnt) continue;
             hipStream_t st = e->stream;
@@ -1165,7 +1172,9 @@ extern "C" mt_status mt_deli_ticket_on_stream(mt_deli* dl, int32_t device, hipSt
                                               mt_op_rec* d_ops, uint64_t n_ops);
 
 namespace {
-constexpr int kRing = 3;  // device slots of mt_submit_ticks: two ticks in flight while one applies
+// device slots of mt_submit_ticks: the copy stream runs up to kRing - 1 ticks ahead of the apply (a
+// C5 tick is ~0.3 GB of records, messages and tickets: six slots are 2 GB of 288)
+constexpr int kRing = 6;
 
 // slot buffers of at least the given sizes (called with nothing in flight on the engine)
 mt_status ring_reserve(mt_engine* e, uint64_t n_ops, uint64_t pay, uint64_t n_msgs) {
@@ -1241,13 +1250,15 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
     }
     HIP_OK(hipSetDevice(e->cfg.device));
     if (n == 0) return MT_OK;
+    const auto t_start = std::chrono::steady_clock::now();
     HIP_OK(hipStreamSynchronize(e->stream));
+    const auto t_synced = std::chrono::steady_clock::now();
     mt_status st = ring_reserve(e, mo, mp, mm);
     if (st) return st;
+    const auto t_reserved = std::chrono::steady_clock::now();
     mt_batch bs[kRing];
     // (MTGPU_TICK_TRACE=1: the host's time in the checks and in the apply loop, to stderr)
-    double t_check = 0, t_apply = 0, t_copy = 0, t_wait = 0;
-    const auto t_start = std::chrono::steady_clock::now();
+    double t_check = 0, t_apply = 0, t_copy = 0, t_wait = 0, wait_k[64] = {}, check_k[64] = {};
     // tick k: checked on the host, then copied into its slot.  Every dependency between the copies and
     // the apply is kept by the host, not by a stream waiting on another stream's event: the streams
     // share the device's few hardware queues (GPU_MAX_HW_QUEUES), where such a wait holds up every
@@ -1266,7 +1277,9 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
             return MT_ERR_ARG;
         const int flags = scan_records(t.ops, t.n_ops, t.payload_bytes);
         if (flags & 1) return MT_ERR_ARG;
-        t_check += std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+        const double ck = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+        t_check += ck;
+        if (k < 64) check_k[k] = ck;
         b = mt_batch();
         b.ops = s.ops;
         b.payload = s.pay;
@@ -1299,13 +1312,18 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
         if (k >= limit) return;
         if ((refused = stage(k))) limit = k;
     };
-    for (uint32_t k = 0; k + 1 < kRing; k++) stage_or_stop(k);
+    // ticks 0 and 1 before the first apply (tick 1's check runs under tick 0's copy), then up to two per
+    // tick (a check is ~1/3 of a copy: the copy stream stays busy, the host gets back to the next bin)
+    uint32_t ns = 0;
+    for (; ns < 2; ns++) stage_or_stop(ns);
     for (uint32_t k = 0; k < limit && !st; k++) {
         auto& s = e->ring[k % kRing];
         const mt_tick& t = ticks[k];
         const auto w0 = std::chrono::steady_clock::now();
         HIP_OK(hipEventSynchronize(s.ready));
-        t_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+        const double wk = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+        t_wait += wk;
+        if (k < 64) wait_k[k] = wk;
         if (t.n_msgs) {
             if ((st = mt_deli_ticket_on_stream(dl, e->cfg.device, e->stream, s.msgs, s.mrp, D, s.tk, s.ops, t.n_ops)))
                 break;
@@ -1320,9 +1338,9 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
         if ((st = apply_launches(e, &bs[k % kRing], nk))) break;
         t_apply += std::chrono::duration<double>(std::chrono::steady_clock::now() - a0).count();
         HIP_OK(hipEventRecord(s.applied, e->stream));
-        // the next tick's copy goes out while this one applies (its slot's tick, k - 1, is done: this
-        // tick's bin followed it on the engine stream)
-        stage_or_stop(k + kRing - 1);
+        // the next ticks' copies go out while this one applies (a slot is reused by tick k + kRing - 1 at
+        // the latest; its tick, k - 1, is done: this tick's bin followed it on the engine stream)
+        for (int j = 0; j < 2 && ns <= k + kRing - 1; j++, ns++) stage_or_stop(ns);
     }
     // (on an error the ticks in flight still land before the slots can be reused or freed)
     const mt_status se = apply_end(e, nk);
@@ -1333,6 +1351,15 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
                 "%.2f ms, apply loop %.2f ms, GPU wall %.2f ms\n", n,
                 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
                 1e3 * t_check, 1e3 * t_copy, 1e3 * t_wait, 1e3 * t_apply, e->last_wall_ms);
+    if (const char* tv = getenv("MTGPU_TICK_TRACE"); tv && tv[0] == '1') {
+        fprintf(stderr, "  stream sync %.2f ms, ring %.2f ms; waits per tick (ms):",
+                1e3 * std::chrono::duration<double>(t_synced - t_start).count(),
+                1e3 * std::chrono::duration<double>(t_reserved - t_synced).count());
+        for (uint32_t k = 0; k < std::min<uint32_t>(n, 64); k++) fprintf(stderr, " %.2f", 1e3 * wait_k[k]);
+        fprintf(stderr, "; checks:");
+        for (uint32_t k = 0; k < std::min<uint32_t>(n, 64); k++) fprintf(stderr, " %.2f", 1e3 * check_k[k]);
+        fprintf(stderr, "\n");
+    }
     return st ? st : se ? se : refused;
 }
 }  // namespace
@@ -1364,18 +1391,45 @@ mt_status mt_submit_ticks_deli(mt_engine* e, mt_deli* dl, const mt_tick* ticks, 
 mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
                           const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, const mt_raw_msg* msgs,
                           uint64_t n_msgs, const uint32_t* msg_row_ptr, mt_tick_layout* out) {
-    if (!out || per == 0 || (n_ops && !ops) || (payload_bytes && !payload) || (n_msgs && (!msgs || !msg_row_ptr)))
+    return mt_log_to_ticks_ramp(ops, n_ops, payload, payload_bytes, doc_row_ptr, n_docs, per, per, msgs, n_msgs,
+                                msg_row_ptr, out);
+}
+
+mt_status mt_log_to_ticks_ramp(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
+                               const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, uint32_t first,
+                               const mt_raw_msg* msgs, uint64_t n_msgs, const uint32_t* msg_row_ptr,
+                               mt_tick_layout* out) {
+    if (!out || per == 0 || first == 0 || first > per || (n_ops && !ops) || (payload_bytes && !payload) ||
+        (n_msgs && (!msgs || !msg_row_ptr)))
         return MT_ERR_ARG;
     uint32_t mx = 0;
     if (!row_ptr_ok(doc_row_ptr, n_docs, n_ops, &mx) || (msgs && !row_ptr_ok(msg_row_ptr, n_docs, n_msgs, nullptr)))
         return MT_ERR_ARG;
-    const uint32_t T = std::max<uint32_t>(1, (mx + per - 1) / per);
+    // a ramp: tick t holds min(per, first << t) records of each document (first, 2 first, 4 first, ...,
+    // then per): RT ramp ticks of [0, rs), then ticks of per
+    uint32_t RT = 0;
+    uint64_t rs = 0;
+    while (((uint64_t)first << RT) < per) rs += (uint64_t)first << RT++;
+    const uint32_t T = mx <= rs ? std::max<uint32_t>(1, [&] {
+        uint32_t t = 0;
+        for (uint64_t c = 0; c < mx; t++) c += (uint64_t)first << t;
+        return t;
+    }()) : RT + (uint32_t)((mx - rs + per - 1) / per);
     // documents in nt contiguous ranges; per range and tick: records, payload bytes, messages
     const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
     const unsigned R = n_docs < 4096 ? 1u : nt;
     std::vector<uint64_t> cnt((size_t)R * T * 3, 0);
     std::atomic<bool> bad{false};
-    auto tick_of = [&](uint32_t d, uint64_t rec) { return (uint32_t)((rec - doc_row_ptr[d]) / per); };
+    auto tick_of = [&](uint32_t d, uint64_t rec) {
+        const uint64_t l = rec - doc_row_ptr[d];
+        if (l >= rs) return RT + (uint32_t)((l - rs) / per);
+        uint32_t t = 0;  // (l < rs: inside the ramp, first * (2^(t+1) - 1) > l)
+        while (((uint64_t)first << (t + 1)) - first <= l) t++;
+        return t;
+    };
+    auto tick_start = [&](uint32_t t) {
+        return t <= RT ? ((uint64_t)first << t) - first : rs + (uint64_t)(t - RT) * per;
+    };
     // the tick of message i of document d (its record's, else the previous record's, else 0)
     auto run = [&](unsigned r, bool write, const std::vector<uint64_t>* base) {
         const uint32_t d0 = (uint32_t)((uint64_t)n_docs * r / R), d1 = (uint32_t)((uint64_t)n_docs * (r + 1) / R);
@@ -1441,8 +1495,8 @@ mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* p
                 if (x.op_index) {
                     // the record's index inside its tick
                     const uint64_t rec = x.op_index - 1;
-                    const uint64_t first = doc_row_ptr[d] + (uint64_t)t * per;  // the document's first record of tick t
-                    y.op_index = (uint32_t)(start[t] - out->tick_ops[t] + (rec - first) + 1);
+                    const uint64_t f = doc_row_ptr[d] + tick_start(t);  // the document's first record of tick t
+                    y.op_index = (uint32_t)(start[t] - out->tick_ops[t] + (rec - f) + 1);
                 }
                 out->msgs[m[t]++] = y;
             }

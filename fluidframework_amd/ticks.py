@@ -43,7 +43,8 @@ def _lib():
         L.mt_submit_ticks.argtypes = [vp, vp, u32]
         L.mt_submit_ticks_deli.argtypes = [vp, vp, vp, u32]
         L.mt_log_to_ticks.argtypes = [vp, u64, vp, u64, vp, u32, u32, vp, u64, vp, ctypes.POINTER(_Layout)]
-        for name in ('mt_submit_ticks', 'mt_submit_ticks_deli', 'mt_log_to_ticks'):
+        L.mt_log_to_ticks_ramp.argtypes = [vp, u64, vp, u64, vp, u32, u32, u32, vp, u64, vp, ctypes.POINTER(_Layout)]
+        for name in ('mt_submit_ticks', 'mt_submit_ticks_deli', 'mt_log_to_ticks', 'mt_log_to_ticks_ramp'):
             getattr(L, name).restype = ctypes.c_int
         _bound = True
     return L
@@ -53,7 +54,9 @@ class TickLog:
     """A tick-major feed of `n_docs` documents in host memory (page-locked by default).
 
     `TickLog.from_batch(batch, per)` lays a document-major OpBatch out tick-major: tick t holds
-    records [t*per, (t+1)*per) of every document, payload compacted per tick.  With `msgs` /
+    records [t*per, (t+1)*per) of every document, payload compacted per tick (`first`: a ramp, tick t
+    holds min(per, first << t) records -- mt_log_to_ticks_ramp, short first ticks for the copies the
+    apply waits for at the start).  With `msgs` /
     `msg_row_ptr` (deli RAW_DTYPE rows in the mt_deli_raw_stream layout, op_index = 1 + the record's
     index in the batch) each tick also carries its raw messages for mt_submit_ticks_deli;
     `tickets=True` gives every tick a host buffer its tickets come back to (`tickets_of(t)`)."""
@@ -84,22 +87,22 @@ class TickLog:
         self._ticks = None
 
     @classmethod
-    def from_batch(cls, batch: OpBatch, per, msgs=None, msg_row_ptr=None, pinned=True, tickets=False):
+    def from_batch(cls, batch: OpBatch, per, msgs=None, msg_row_ptr=None, pinned=True, tickets=False, first=None):
         L = _lib()
         lay = _Layout()
         n_msgs = 0 if msgs is None else len(msgs)
         mp = None if msgs is None else _ptr(np.ascontiguousarray(msgs))
         mr = None if msgs is None else _ptr(np.ascontiguousarray(msg_row_ptr, dtype=np.uint32))
         args = (_ptr(batch.ops), batch.n_ops, _ptr(batch.payload), len(batch.payload), _ptr(batch.row_ptr),
-                batch.n_docs, per, mp, n_msgs, mr)
-        _check(L.mt_log_to_ticks(*args, ctypes.byref(lay)), 'mt_log_to_ticks')
+                batch.n_docs, per, per if first is None else first, mp, n_msgs, mr)
+        _check(L.mt_log_to_ticks_ramp(*args, ctypes.byref(lay)), 'mt_log_to_ticks_ramp')
         self = cls(batch.n_docs, batch.n_ops, lay.payload_bytes, lay.n_ticks, n_msgs, pinned, tickets)
         lay.ops, lay.payload, lay.row_ptrs = self.ops.ctypes.data, self.payload.ctypes.data, self.row_ptrs.ctypes.data
         lay.tick_ops, lay.tick_payload = self.tick_ops.ctypes.data, self.tick_payload.ctypes.data
         if n_msgs:
             lay.msgs, lay.msg_row_ptrs = self.msgs.ctypes.data, self.msg_row_ptrs.ctypes.data
             lay.tick_msgs = self.tick_msgs.ctypes.data
-        _check(L.mt_log_to_ticks(*args, ctypes.byref(lay)), 'mt_log_to_ticks')
+        _check(L.mt_log_to_ticks_ramp(*args, ctypes.byref(lay)), 'mt_log_to_ticks_ramp')
         return self
 
     def ticks(self):

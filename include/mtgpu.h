@@ -775,6 +775,14 @@ typedef struct mt_tick_layout {
 mt_status mt_log_to_ticks(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
                           const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, const mt_raw_msg* msgs,
                           uint64_t n_msgs, const uint32_t* msg_row_ptr, mt_tick_layout* out);
+/* The same with a ramp of short first ticks: tick t holds min(per, first << t) records of each document
+ * (first, 2 first, 4 first, ... then per; 1 <= first <= per).  A feed starts applying once its first
+ * tick has landed and the copy runs ahead of the apply only once the ticks' apply outlasts their copy:
+ * the ramp cuts the copies the apply waits for at the start. */
+mt_status mt_log_to_ticks_ramp(const mt_op_rec* ops, uint64_t n_ops, const uint8_t* payload, uint64_t payload_bytes,
+                               const uint32_t* doc_row_ptr, uint32_t n_docs, uint32_t per, uint32_t first,
+                               const mt_raw_msg* msgs, uint64_t n_msgs, const uint32_t* msg_row_ptr,
+                               mt_tick_layout* out);
 
 #ifdef __cplusplus
 }

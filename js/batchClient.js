@@ -356,7 +356,7 @@ class BatchClient {
         this.queue.push(r);
         if (this.engine.recording) this.expect.push({ op });  // a local edit's callback: no sequencedMessage
         this.engine.pending += 1;
-        this.engine._syncPoint(this);
+        if (this.engine._syncPoint) this.engine._syncPoint(this);  // (a host-only stub engine has none)
         return op;
     }
     /** TestClient.insertTextLocal (testClient.ts:133-143) -> insertSegmentLocal: the insert op. */
@@ -443,7 +443,7 @@ class BatchClient {
             this.engine.pending += 1;
             // (syncCallbacks: each member applied and its callback delivered in turn, as the reference
             // fires one callback per member inside the GROUP's apply)
-            this.engine._syncPoint(this);
+            if (this.engine._syncPoint) this.engine._syncPoint(this);  // (a host-only stub engine has none)
         });
         // (after the members, as updateSeqNumbers follows the op: client.ts:818; a listener reading
         // getCurrentSeq() inside the callback sees the previous one, as the reference's does)

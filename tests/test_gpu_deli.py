@@ -352,9 +352,9 @@ def test_c5_tick_feed_through_deli(oracle_lib):
     eng.reset()
     eng.apply_staged(dev)
     want_cs = eng.checksums()
-    for b in (32, 16):
-        log = TickLog.from_batch(host, 32, msgs=raw, msg_row_ptr=rp, tickets=True)
-        assert log.n_ticks == 8
+    for b, first in ((32, None), (16, None), (32, 8)):
+        log = TickLog.from_batch(host, 32, msgs=raw, msg_row_ptr=rp, tickets=True, first=first)
+        assert log.n_ticks == (8 if first is None else 10)  # (ramp 8, 16, then 32s)
         e2 = MergeEngine(n, ops_per_launch=b)
         dl.restore_all(seq=0, clients={})
         e2.apply_ticks(log, deli=dl)

@@ -57,17 +57,18 @@ def test_fullshape_bit_exact(name, b):
     assert all(eng.error(d) == (0, 0) for d in range(0, batch.n_docs, 7))
 
 
-@pytest.mark.parametrize('per,b', [(32, 32), (64, 32), (5, 0)])
+@pytest.mark.parametrize('per,b,first', [(32, 32, None), (64, 32, None), (5, 0, None), (32, 32, 8), (32, 32, 1)])
 @pytest.mark.parametrize('name', ['full_c4', 'fuzz_1k'])
-def test_tick_feed_equals_reference(name, per, b):
-    """mt_submit_ticks (the tick-major feed: tick k + 1 copied from page-locked host memory into a
+def test_tick_feed_equals_reference(name, per, b, first):
+    """mt_submit_ticks (the tick-major feed: later ticks copied from page-locked host memory into a
     ring of device slots while tick k applies) ends in the reference's states, as mt_submit does:
-    ticks of 32 ops per document applied as one launch, ticks of 64 as two launches of 32, and
-    ticks of 5 in one launch each."""
+    ticks of 32 ops per document applied as one launch, ticks of 64 as two launches of 32, ticks of
+    5 in one launch each (hundreds of ticks: the ring wraps many times), and a short first tick
+    (mt_log_to_ticks_ramp)."""
     from fluidframework_amd.engine import MergeEngine
     from fluidframework_amd.ticks import TickLog
     batch, fx = load_fullshape(name)
-    log = TickLog.from_batch(batch, per)
+    log = TickLog.from_batch(batch, per, first=first)
     eng = MergeEngine(batch.n_docs, ops_per_launch=b)
     eng.apply_ticks(log)
     got = ['%016x' % c for c in eng.checksums()]

@@ -24,10 +24,27 @@ def _doc_records(log, d):
     return recs, pays
 
 
-def _check_layout(batch, log, per):
+def _tick_span(t, per, first):
+    """[lo, hi) of a document's records in tick t (mt_log_to_ticks_ramp: tick u holds min(per, first << u))."""
+    lo = 0
+    for u in range(t):
+        lo += min(per, first << u)
+    return lo, lo + min(per, first << t)
+
+
+def _n_ticks(mx, per, first):
+    t = c = 0
+    while c < mx:
+        c += min(per, first << t)
+        t += 1
+    return max(1, t)
+
+
+def _check_layout(batch, log, per, first=None):
     from fluidframework_amd.oplog import OP_DTYPE
+    first = per if first is None else first
     lens = np.diff(batch.row_ptr.astype(np.int64))
-    assert log.n_ticks == max(1, -(-int(lens.max()) // per))
+    assert log.n_ticks == _n_ticks(int(lens.max()), per, first)
     assert int(log.tick_ops[-1]) == batch.n_ops
     used = int(batch.ops['payload_len'].astype(np.int64).sum())
     assert int(log.tick_payload[-1]) == used  # compacted: no unused payload bytes travel
@@ -42,10 +59,11 @@ def _check_layout(batch, log, per):
                     assert r[f] == s[f], (d, k, f)
             off = int(s['payload_off'])
             assert p == bytes(batch.payload[off:off + int(s['payload_len'])])
-        # tick t holds records [t*per, (t+1)*per) of the document
+        # tick t holds records [t*per, (t+1)*per) of the document (tick 0: [0, first))
         for t in range(log.n_ticks):
             rp = log.row_ptrs[t * (batch.n_docs + 1):(t + 1) * (batch.n_docs + 1)]
-            assert int(rp[d + 1] - rp[d]) == max(0, min(per, len(src) - t * per))
+            lo, hi = _tick_span(t, per, first)
+            assert int(rp[d + 1] - rp[d]) == max(0, min(hi, len(src)) - lo)
 
 
 @pytest.mark.parametrize('per', [1, 5, 32, 4096])
@@ -54,6 +72,25 @@ def test_layout_of_golden_logs(per):
     batch, _ = load_golden('synth_c3')
     log = TickLog.from_batch(batch, per, pinned=False)
     _check_layout(batch, log, per)
+
+
+@pytest.mark.parametrize('per,first', [(32, 8), (32, 1), (5, 4), (4096, 100), (32, 3), (1000, 1)])
+def test_ramp_layout_of_golden_logs(per, first):
+    """A ramp of short first ticks (mt_log_to_ticks_ramp): the same records in the same order, tick t
+    cut to min(per, first << t) records per document."""
+    from fluidframework_amd.ticks import TickLog
+    batch, _ = load_golden('synth_c3')
+    log = TickLog.from_batch(batch, per, pinned=False, first=first)
+    _check_layout(batch, log, per, first)
+
+
+def test_ramp_first_tick_is_checked():
+    from fluidframework_amd.engine import MtError
+    from fluidframework_amd.ticks import TickLog
+    batch, _ = load_golden('synth_c2')
+    for first in (0, 33):
+        with pytest.raises(MtError):
+            TickLog.from_batch(batch, 32, pinned=False, first=first)
 
 
 def test_layout_of_ragged_documents():
@@ -78,9 +115,9 @@ def test_layout_of_ragged_documents():
     payload = rng.integers(0, 256, size=cur + 1).astype(np.uint8)
     row_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
     batch = OpBatch(ops, payload, row_ptr)
-    for per in (1, 7, 32, 200):
-        log = TickLog.from_batch(batch, per, pinned=False)
-        _check_layout(batch, log, per)
+    for per, first in ((1, 1), (7, 7), (32, 32), (200, 200), (32, 3), (7, 1)):
+        log = TickLog.from_batch(batch, per, pinned=False, first=first)
+        _check_layout(batch, log, per, first)
         assert int(log.tick_payload[-1]) == total
 
 
@@ -107,8 +144,14 @@ def test_raw_messages_follow_their_records():
     for k, f in enumerate(('csn', 'ref_seq', 'client', 'kind', 'op_index')):
         raw[f] = [x[k] for x in msgs]
     mrp = np.array(mrp, dtype=np.uint32)
-    per = 16
-    log = TickLog.from_batch(batch, per, msgs=raw, msg_row_ptr=mrp, pinned=False)
+    for per, first in ((16, 16), (16, 5)):
+        log = TickLog.from_batch(batch, per, msgs=raw, msg_row_ptr=mrp, pinned=False, first=first)
+        _check_messages(batch, log, raw, mrp)
+
+
+def _check_messages(batch, log, raw, mrp):
+    from fluidframework_amd.deli import RAW_DTYPE
+    D = batch.n_docs
     assert int(log.tick_msgs[-1]) == len(raw)
     for d in range(D):
         got = []

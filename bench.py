@@ -45,7 +45,7 @@ METRIC = 'sequenced merge-tree ops applied/sec (node) at 100K docs; % HBM roofli
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch from the rocprofv3 PMC passes (tools/rocprof.sh -> tools/pmc_traffic.py)
 PROFILES = os.path.join(HERE, 'profiles')
-PMC_ROUND = 'r05'
+PMC_ROUND = 'r06'
 SQ_ROUND = 'r06'   # profiles/<round>_sq_counters_C3_pass{1,2}.txt (tools/sq_pass.sh): the issue roofline
 # instruction issue peaks (MI355X_MICROARCH.md "Wave scheduling"): 256 CUs x 4 SIMDs, a wave64 VALU
 # instruction every 2 cycles per SIMD at 2.4 GHz; one scalar (SALU) instruction per CU per cycle

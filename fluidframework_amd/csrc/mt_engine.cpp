@@ -67,6 +67,8 @@ extern "C" hipError_t mt_launch_seginfo(const mt_gstate* g, const uint32_t* docs
 extern "C" hipError_t mt_launch_events_pack(const mt_gstate* g, uint32_t n_docs, const uint64_t* off, mt_event* out,
                                             hipStream_t st);
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st);
+extern "C" hipError_t mt_launch_scan_records(const mt_op_rec* ops, uint64_t n_ops, uint64_t payload_bytes,
+                                             uint32_t* flags, hipStream_t st);
 extern "C" hipError_t mt_launch_snapshot(const mt_gstate* g, uint32_t d0, uint32_t n_docs, uint32_t cap,
                                          uint32_t* specs, uint32_t* counts, hipStream_t st);
 extern "C" hipError_t mt_launch_gen(int cap_class, const mt_gstate* g, const mt_synth_cfg* cfg, uint32_t doc_id_base,
@@ -199,6 +201,7 @@ struct mt_engine {
         hipEvent_t ready = nullptr, applied = nullptr, drained = nullptr, ticketed = nullptr;
     } ring[6];
     hipStream_t h2d = nullptr, d2h = nullptr;
+    uint32_t* d_scan = nullptr;  // the first tick's record check on the device (mt_scan_records_kernel)
     struct {  // mt_get_snapshots: the JSON of the last sizing call
         bool valid = false;
         uint64_t gen = 0;
@@ -546,6 +549,7 @@ mt_status mt_engine_destroy(mt_engine* e) {
             (void)hipStreamSynchronize(s);
             (void)hipStreamDestroy(s);
         }
+    if (e->d_scan) (void)hipFree(e->d_scan);
     for (auto& s : e->ring) {
         for (void* p : {(void*)s.ops, (void*)s.pay, (void*)s.rp, (void*)s.msgs, (void*)s.mrp, (void*)s.tk})
             if (p) (void)hipFree(p);
@@ -1184,6 +1188,7 @@ mt_status ring_reserve(mt_engine* e, uint64_t n_ops, uint64_t pay, uint64_t n_ms
     if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
     if (!e->h2d && hipStreamCreateWithPriority(&e->h2d, hipStreamNonBlocking, hi_pri) != hipSuccess) return MT_ERR_HIP;
     if (!e->d2h && hipStreamCreateWithPriority(&e->d2h, hipStreamNonBlocking, hi_pri) != hipSuccess) return MT_ERR_HIP;
+    if (!e->d_scan) HIP_OK(hipMalloc(&e->d_scan, sizeof(uint32_t)));
     const size_t rp = ((size_t)e->cfg.max_docs + 1) * sizeof(uint32_t);
     for (auto& s : e->ring) {
         if (!s.ready) {
@@ -1275,7 +1280,9 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
         const auto c0 = std::chrono::steady_clock::now();
         if (!row_ptr_ok(t.doc_row_ptr, D, t.n_ops, &mx) || (t.n_msgs && !row_ptr_ok(t.msg_row_ptr, D, t.n_msgs, nullptr)))
             return MT_ERR_ARG;
-        const int flags = scan_records(t.ops, t.n_ops, t.payload_bytes);
+        // (tick 0: its records are checked on the device once they have landed, in the apply loop --
+        // the host check would sit between the start and the first copy)
+        const int flags = k == 0 ? 0 : scan_records(t.ops, t.n_ops, t.payload_bytes);
         if (flags & 1) return MT_ERR_ARG;
         const double ck = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
         t_check += ck;
@@ -1324,6 +1331,18 @@ mt_status submit_ticks(mt_engine* e, mt_deli* dl, const mt_tick* ticks, uint32_t
         const double wk = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
         t_wait += wk;
         if (k < 64) wait_k[k] = wk;
+        if (k == 0) {
+            uint32_t f = 0;
+            HIP_OK(mt_launch_scan_records(s.ops, t.n_ops, t.payload_bytes, e->d_scan, e->stream));
+            HIP_OK(hipMemcpyAsync(&f, e->d_scan, sizeof f, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipStreamSynchronize(e->stream));
+            if (f & 1) {  // refused before anything of it ran: no tick applies
+                refused = MT_ERR_ARG;
+                limit = 0;
+                break;
+            }
+            bs[0].wide = (f & 2) != 0;
+        }
         if (t.n_msgs) {
             if ((st = mt_deli_ticket_on_stream(dl, e->cfg.device, e->stream, s.msgs, s.mrp, D, s.tk, s.ops, t.n_ops)))
                 break;

@@ -498,6 +498,37 @@ extern "C" hipError_t mt_launch_bin(const mt_gstate* g, const uint32_t* row_ptr,
                        classes, n_classes, first_lds, first_wide, counts, ids, ops, payload, acc);
     return hipGetLastError();
 }
+// The host's record check (mt_engine.cpp scan_records) on the device, for a feed's first tick, whose
+// host check would otherwise sit between the start and the first copy: bit 0 of *flags a payload
+// out of bounds, bit 1 a record that needs the wide document form (wide_rec).  Reads the records
+// only (no payload, no document state): a refused tick leaves every document as it was.
+__global__ __launch_bounds__(256) void mt_scan_records_kernel(const mt_op_rec* __restrict__ ops, uint64_t n_ops,
+                                                              uint64_t payload_bytes, uint32_t* __restrict__ flags) {
+    uint32_t f = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += (uint64_t)gridDim.x * blockDim.x) {
+        const mt_op_rec o = ops[i];
+        if ((uint64_t)o.payload_off + o.payload_len > payload_bytes) f |= 1u;
+        bool wide = (o.type & MT_OP_WIDE) != 0;
+        if (MT_OP_TYPE(o) == MT_OP_LOAD) {
+            const uint32_t c0 = MT_LOAD_CLIENT(o), c1 = MT_LOAD_RCLIENT(o);
+            wide = wide || (c0 != MT_CLIENT_NONCOLLAB && c0 >= MT_MAX_CLIENTS) || (o.pos2 >= 0 && c1 >= MT_MAX_CLIENTS);
+        } else {
+            wide = wide || (!MT_OP_IS_NOOP(o) && o.client >= MT_MAX_CLIENTS);
+        }
+        if (wide) f |= 2u;
+    }
+    // one atomic per wave (vector memory atomics)
+    const uint64_t bad = __ballot(f & 1u), wide = __ballot(f & 2u);
+    if ((threadIdx.x & 63) == 0 && (bad || wide)) atomicOr(flags, (bad ? 1u : 0u) | (wide ? 2u : 0u));
+}
+extern "C" hipError_t mt_launch_scan_records(const mt_op_rec* ops, uint64_t n_ops, uint64_t payload_bytes,
+                                             uint32_t* flags, hipStream_t st) {
+    hipError_t r = hipMemsetAsync(flags, 0, sizeof(uint32_t), st);
+    if (r != hipSuccess || n_ops == 0) return r;
+    const uint64_t blocks = (n_ops + 255) / 256 < 4096 ? (n_ops + 255) / 256 : 4096;
+    hipLaunchKernelGGL(mt_scan_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, ops, n_ops, payload_bytes, flags);
+    return hipGetLastError();
+}
 extern "C" hipError_t mt_launch_fixup(const mt_gstate* g, const mt_op_rec* ops, uint32_t n_docs, hipStream_t st) {
     if (n_docs == 0) return hipSuccess;
     hipLaunchKernelGGL(mt_fixup_kernel, dim3((n_docs + 255) / 256), dim3(256), 0, st, *g, ops, n_docs);

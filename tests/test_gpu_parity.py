@@ -38,6 +38,26 @@ def test_golden_bit_exact(name, b):
         assert '%016x' % cs[d] == r['checksum']
 
 
+@pytest.mark.parametrize('name', WIDE_SETS + ['scenarios'])
+def test_tick_feed_golden(name):
+    """The golden sets through the tick feed (mt_submit_ticks, 16 ops per document per tick): the
+    wide sets' first ticks hold wide records, which the device-side check of the first tick must
+    report (the wide form's workspace is set up from it) -- the reference's states."""
+    from fluidframework_amd.engine import MergeEngine
+    from fluidframework_amd.ticks import TickLog
+    batch, exp = load_golden(name)
+    log = TickLog.from_batch(batch, 16)
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    eng.apply_ticks(log)
+    cs = eng.checksums()
+    for r in exp:
+        d = r['doc']
+        assert eng.error(d) == (0, 0), (name, d, eng.error(d))
+        assert '%016x' % cs[d] == r['checksum'], (name, d)
+    eng.close()
+    log.free()
+
+
 @pytest.mark.parametrize('b', [0, 32, 5])
 @pytest.mark.parametrize('name', FULLSHAPE_SETS)
 def test_fullshape_bit_exact(name, b):
@@ -101,6 +121,34 @@ def test_tick_feed_stops_at_a_malformed_tick():
     eng = MergeEngine(batch.n_docs, ops_per_launch=16)
     with pytest.raises(MtError):
         eng.apply_ticks(log)
+    assert np.array_equal(eng.checksums(), ref.checksums())
+
+
+@pytest.mark.parametrize('where', ['first', 'last'])
+def test_tick_feed_refuses_a_malformed_first_tick(where):
+    """The first tick's records are checked on the device once they have landed
+    (mt_scan_records_kernel, not on the host before the copy): a payload out of bounds there -- at
+    its first or its last record -- refuses the feed with nothing applied; the same feed repaired then
+    applies as before (wide records in the first tick: tests/test_wide_ids.py)."""
+    from fluidframework_amd.engine import MergeEngine, MtError
+    from fluidframework_amd.ticks import TickLog
+    batch, fx = load_golden('synth_c2')
+    log = TickLog.from_batch(batch, 16)
+    t0 = log.tick_batch(0)
+    i = 0 if where == 'first' else len(t0.ops) - 1
+    keep = t0.ops[i].copy()
+    t0.ops['payload_off'][i] = int(log.tick_payload[1] - log.tick_payload[0])  # one past the tick's payload
+    t0.ops['payload_len'][i] = 1
+    eng = MergeEngine(batch.n_docs, ops_per_launch=16)
+    empty = eng.checksums()
+    with pytest.raises(MtError):
+        eng.apply_ticks(log)
+    assert np.array_equal(eng.checksums(), empty)
+    t0.ops[i] = keep
+    eng.reset()
+    eng.apply_ticks(log)
+    ref = MergeEngine(batch.n_docs, ops_per_launch=16)
+    ref.apply(batch)
     assert np.array_equal(eng.checksums(), ref.checksums())
 
 

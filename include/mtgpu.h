@@ -742,8 +742,9 @@ typedef struct mt_tick {
     mt_ticket* tickets;           /* optional: one ticket per message, copied back to the host         */
 } mt_tick;
 /* Apply ticks[0 .. n_ticks) in order.  Each tick is checked on the host while earlier ticks apply
- * (row pointers, payload bounds, as mt_batch_upload does); a malformed tick returns MT_ERR_ARG with
- * the ticks before it applied, as a loop of applyMsg stops at the message that throws.
+ * (row pointers, payload bounds, as mt_batch_upload does) -- the first tick's records on the device
+ * once they have landed, before anything of it runs; a malformed tick returns MT_ERR_ARG with the
+ * ticks before it applied, as a loop of applyMsg stops at the message that throws.
  * mt_last_apply_stats / mt_last_apply_class_stats then cover the whole call. */
 mt_status mt_submit_ticks(mt_engine* eng, const mt_tick* ticks, uint32_t n_ticks);
 /* The same with each tick's raw messages ticketed by `dl` on the engine's stream first (deli -> apply

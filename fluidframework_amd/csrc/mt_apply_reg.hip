@@ -2007,9 +2007,10 @@ MT_DEV KGState& kernarg_gstate() {
 // -3.3 % on C4 (profiles/r06_ab/ab6_*); K = 12 at three would take 356 B.  With the zamboni passes
 // unrolled too: K = 8 at four (60 B) +0.6 % C3 (its 512 class 45.7 -> 44.0 ms), K = 12 at three (116 B)
 // -1.1 % (profiles/r06_ab/ab8_*); K = 3 at seven (48 B) +1.8 % on C5, K = 2 at eight +0.9 % (both: +1.1 %),
-// K = 2 / 3 at six / five (spill-free) -3.1 % (profiles/r06_ab/ab11_*)
+// K = 2 / 3 at six / five (spill-free) -3.1 % (profiles/r06_ab/ab11_*); K = 5 at five (68 B) its C4 class
+// 65.0 -> 60.9 ms, K = 4 at six neutral (profiles/r06_ab/ab12_*)
 constexpr int wpe_default(int K) {
-    return K <= 3 ? 7 : K <= 4 ? 5 : K <= 8 ? 4 : K <= 11 ? 3 : 2;
+    return K <= 3 ? 7 : K <= 5 ? 5 : K <= 8 ? 4 : K <= 11 ? 3 : 2;
 }
 // MT_WPE_OV={w0,w1,...,w16} overrides classes one by one (0 = the default), for A/B builds.
 #ifndef MT_WPE_OV

@@ -2103,7 +2103,9 @@ constexpr int wpe_c64_ov[17] = MT_WPE_C64_OV;
 // K >= 13 runs one wave per SIMD: at two it spilled 590-660 B per lane in round 4's code, at one the
 // excess lives in AGPRs (C3W 137.3 -> 184.5 M ops/s, profiles/r04_ab_c64_occupancy_C3W.log).  (The
 // event kernels measured the other way: one wave at K >= 11 0.89x, r04_ab_events_onewave_C3.jsonl.)
-constexpr int wpe_c64_default(int K) { return K <= 4 ? 5 : K <= 6 ? 4 : K <= 9 ? 3 : K <= 12 ? 2 : 1; }
+// Round 6, after the unrolled op path cut the register peaks: K >= 13 at two waves takes 60 B, K = 10
+// at three 60 B -- C3W 223.5 -> 258.7 M ops/s (profiles/r06_ab/ab13_side_occupancy/).
+constexpr int wpe_c64_default(int K) { return K <= 4 ? 5 : K <= 6 ? 4 : K <= 10 ? 3 : 2; }
 constexpr int wpe_c64(int K) { return K < 17 && wpe_c64_ov[K] > 0 ? wpe_c64_ov[K] : wpe_c64_default(K); }
 template <int K>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) void reg_apply_kernel(
@@ -2118,8 +2120,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(wpe(K)))) vo
 // The event-recording kernels need ~35 VGPRs more (the event rows' placement and property deltas):
 // at the plain kernels' occupancy they would spill 180-560 B per lane from K = 2 on, so they run one
 // or two waves lower, spill-free up to K = 9 (K = 10 / 11: 100 / 180 B at two waves).
-// MT_WPE_EV_OV overrides them like MT_WPE_OV.
-constexpr int wpe_ev_default(int K) { return K <= 2 ? 4 : K <= 5 ? 3 : 2; }
+// MT_WPE_EV_OV overrides them like MT_WPE_OV.  Round 6 (the unrolled op path): K = 6..8 three waves
+// spill-free, K = 9 / 10 / 11 at three 64 / 72 / 144 B -- C3 with events 231.7 -> 260.8 M ops/s (K <= 10),
+// 258.7 -> 269.9 M (K = 11; K = 12 at three loses its class, 37.5 -> 42.7 ms)
+// (profiles/r06_ab/ab13_side_occupancy/).
+constexpr int wpe_ev_default(int K) { return K <= 2 ? 4 : K <= 11 ? 3 : 2; }
 #ifndef MT_WPE_EV_OV
 #define MT_WPE_EV_OV {0}
 #endif
